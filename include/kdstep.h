@@ -1,0 +1,105 @@
+/*
+ * kdstep.h — C-ABI of the MI355X-native online-KD training step (gfx950).
+ *
+ * Drop-in boundary for the reference's per-step hot path
+ *   OnlineKnowledgeDistillationLLavaOneVision.training_step / forward
+ *   (distillation/knowledge_distillation7b_double_trouble/phase1/
+ *    OnlineKnowledgeDistillationLLavaOneVision.py:123-131, :206-271)
+ * and the third-party HF arithmetic it calls into (SigLIP, Qwen2, LLaVA-OV pack,
+ * causal-LM CE).  The reference has no FFI of its own (it is pure Python); every
+ * entry point below replaces a PyTorch/transformers call site that is cited next
+ * to it.  Conventions:
+ *
+ *  - Every function returns an int status (kd_status).  0 = OK.  On failure a
+ *    thread-local message is available from kd_last_error().
+ *  - All pointers are DEVICE pointers unless the parameter name ends in _host.
+ *    The caller (PyTorch) owns every buffer; the library never allocates or frees
+ *    caller memory.  Workspaces are sized with the matching *_workspace_size().
+ *  - `stream` is a hipStream_t passed as void*.  All calls are asynchronous and
+ *    stream-ordered: no hidden device synchronisation.
+ *  - bf16 tensors are raw 16-bit storage (uint16_t / __bf16); fp32 is float.
+ *  - Leading dimensions (ld*) are in ELEMENTS.
+ */
+#ifndef KDSTEP_H
+#define KDSTEP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    KD_OK = 0,
+    KD_ERR_SHAPE = 1,        /* inconsistent / unsupported shape                       */
+    KD_ERR_DTYPE = 2,        /* unsupported dtype enum                                 */
+    KD_ERR_ALIGN = 3,        /* pointer / leading dimension misaligned (16 B needed)   */
+    KD_ERR_ARCH = 4,         /* device is not gfx950                                   */
+    KD_ERR_LABEL_RANGE = 5,  /* a label is outside [0, V) where the reference gathers  */
+    KD_ERR_LAUNCH = 6,       /* HIP launch / runtime error                             */
+    KD_ERR_ARG = 7,          /* null pointer or invalid enum / parameter               */
+    KD_ERR_WORKSPACE = 8     /* workspace too small                                    */
+} kd_status;
+
+/* ---------------------------------------------------------------- library ---- */
+int kd_abi_version(void);                 /* returns KD_ABI_VERSION                  */
+const char* kd_last_error(void);          /* thread-local, never NULL                */
+int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
+
+#define KD_ABI_VERSION 1
+
+/* ------------------------------------------------------------- KD losses ---- */
+/* Variants of the logit loss.  Each replaces one reference function:
+ *  KD_LOSS_LOCA         compute_loca_loss, DT:141-194 (T=0.8) and LB:208-261 (T=1):
+ *                       KL(calibrated teacher || clamp(p_S,1e-8)), mean over B*L*V,
+ *                       x T^2, with the global last-write-wins column overrides.
+ *  KD_LOSS_KL           compute_vision_loss's KL term, DT:330-343:
+ *                       kl_div(log_softmax(s/T), softmax(t/T), 'mean') * T^2.
+ *  KD_LOSS_KL_LOGTARGET FB compute_loss, FB:205-219 (and LB compute_loss LB:177-190):
+ *                       kl_div(log_softmax(s/T), softmax(t/T), 'mean', log_target=True)*T^2
+ *                       = mean(exp(p_T) * (p_T - log p_S)) * T^2.
+ *  KD_LOSS_NONE         no teacher term (student CE only; BD SFT step, BD:90-109).
+ * The student CE is the in-model causal-LM loss (shift by one, ignore -100, mean over
+ * valid labels), HF ForCausalLMLoss; the teacher CE (computed and discarded by the
+ * reference at DT:228) is reported as a side output when teacher logits are given. */
+typedef enum {
+    KD_LOSS_NONE = 0,
+    KD_LOSS_LOCA = 1,
+    KD_LOSS_KL = 2,
+    KD_LOSS_KL_LOGTARGET = 3
+} kd_loss_variant;
+
+typedef struct {
+    int32_t variant;        /* kd_loss_variant                                         */
+    float temperature;      /* T (self.T: DT 0.8, LB 1.0, FB 0.8)                       */
+    float alpha;            /* LoCa alpha (compute_loca_loss default 0.8)               */
+    float kd_weight;        /* weight of the (T^2-scaled) KD term in the total          */
+    float ce_weight;        /* weight of the student CE in the total                    */
+    float grad_scale;       /* dlogits multiplier (upstream dL/dtotal, e.g. 1/accum)    */
+    float clamp_min;        /* LoCa clamp of p_S before log (1e-8, DT:161-162)           */
+    int32_t teacher_ce;     /* 1: also compute the teacher's (unused) CE side output    */
+} kd_loss_params;
+
+/* loss_out (device float[4]): [0] KD term (mean, incl. T^2, unweighted)
+ *                             [1] student CE   [2] teacher CE   [3] total
+ * dlogits: d(total)/d(student_logits) * grad_scale, bf16 [B*L, ld_d] (may be NULL).
+ * labels: int64 [B, L] (row-major).  LoCa requires every label in [0, V_s): a label
+ * outside raises KD_ERR_LABEL_RANGE from kd_loss_check() (the reference raises
+ * RuntimeError from gather, DT:166).  teacher may be NULL for KD_LOSS_NONE.
+ * V_t >= V_s: the teacher is sliced to its first V_s columns (DT:155). */
+size_t kd_loss_workspace_size(int B, int L, int V_s);
+int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t,
+                    const void* student_logits, int64_t ld_s, int V_s,
+                    const int64_t* labels, int B, int L,
+                    kd_loss_params params,
+                    float* loss_out, void* dlogits, int64_t ld_d,
+                    void* workspace, size_t workspace_bytes, void* stream);
+/* Synchronises `stream` and reports a device-side error recorded in `workspace` by the
+ * last kd_loss_fwd_bwd (KD_ERR_LABEL_RANGE), else KD_OK. */
+int kd_loss_check(const void* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KDSTEP_H */

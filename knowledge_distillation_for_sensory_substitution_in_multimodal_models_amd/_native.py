@@ -1,0 +1,99 @@
+"""ctypes binding of the C-ABI library libkdstep.so (include/kdstep.h).
+
+This is the exact binding a maintainer of the reference would add: plain pointers,
+sizes and an int status per call.  A non-zero status raises RuntimeError with the
+library's thread-local message (mirroring the reference's RuntimeError behaviour).
+
+There is NO fallback: if the library is missing the import of any op fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("KDSTEP_LIB", _PKG / "libkdstep.so"))
+HEADER = _PKG.parent / "include" / "kdstep.h"
+
+KD_OK = 0
+STATUS_NAMES = {
+    0: "KD_OK", 1: "KD_ERR_SHAPE", 2: "KD_ERR_DTYPE", 3: "KD_ERR_ALIGN", 4: "KD_ERR_ARCH",
+    5: "KD_ERR_LABEL_RANGE", 6: "KD_ERR_LAUNCH", 7: "KD_ERR_ARG", 8: "KD_ERR_WORKSPACE",
+}
+
+# kd_loss_variant
+KD_LOSS_NONE, KD_LOSS_LOCA, KD_LOSS_KL, KD_LOSS_KL_LOGTARGET = 0, 1, 2, 3
+
+
+class KdLossParams(C.Structure):
+    _fields_ = [
+        ("variant", C.c_int32),
+        ("temperature", C.c_float),
+        ("alpha", C.c_float),
+        ("kd_weight", C.c_float),
+        ("ce_weight", C.c_float),
+        ("grad_scale", C.c_float),
+        ("clamp_min", C.c_float),
+        ("teacher_ce", C.c_int32),
+    ]
+
+
+class KdError(RuntimeError):
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn}: {STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_vp, _i32, _i64, _sz, _f32 = C.c_void_p, C.c_int, C.c_int64, C.c_size_t, C.c_float
+
+# name -> (restype, argtypes).  Kept in the same order as include/kdstep.h.
+SIGNATURES = {
+    "kd_abi_version": (_i32, []),
+    "kd_last_error": (C.c_char_p, []),
+    "kd_device_is_gfx950": (_i32, [_i32]),
+    "kd_loss_workspace_size": (_sz, [_i32, _i32, _i32]),
+    "kd_loss_fwd_bwd": (_i32, [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _i32, _i32, KdLossParams,
+                               _vp, _vp, _i64, _vp, _sz, _vp]),
+    "kd_loss_check": (_i32, [_vp, _vp]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libkdstep.so once.  Raises if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(
+                f"libkdstep.so not found at {LIB_PATH}; run `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (hipcc --offload-arch=gfx950)")
+        l = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        if l.kd_abi_version() != 1:
+            raise ImportError("libkdstep.so ABI version mismatch")
+        _lib = l
+    return _lib
+
+
+def check(fn: str, status: int) -> None:
+    if status != KD_OK:
+        msg = lib().kd_last_error().decode(errors="replace")
+        raise KdError(fn, status, msg)
+
+
+def call(fn: str, *args) -> None:
+    check(fn, getattr(lib(), fn)(*args))
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/kdstep.h (for the export test)."""
+    import re
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(kd_[a-z0-9_]+)\s*\(", txt, flags=re.M)
+    return sorted(set(names))

@@ -1,0 +1,94 @@
+// Shared helpers for the gfx950 kernels behind include/kdstep.h.
+// Wave = 64 lanes everywhere (CDNA4); never use warp-32 idioms here.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <cmath>
+
+#include "../../include/kdstep.h"
+
+namespace kd {
+
+// ------------------------------------------------------------------ errors ----
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define KD_CHECK_ARG(cond, msg)                                   \
+    do {                                                          \
+        if (!(cond)) return ::kd::fail(KD_ERR_ARG, (msg));        \
+    } while (0)
+#define KD_CHECK_SHAPE(cond, msg)                                 \
+    do {                                                          \
+        if (!(cond)) return ::kd::fail(KD_ERR_SHAPE, (msg));      \
+    } while (0)
+#define KD_CHECK_ALIGN(ptr, bytes, msg)                                          \
+    do {                                                                         \
+        if (((uintptr_t)(ptr)) % (bytes) != 0) return ::kd::fail(KD_ERR_ALIGN, (msg)); \
+    } while (0)
+#define KD_LAUNCH_CHECK(what)                                                    \
+    do {                                                                         \
+        hipError_t e__ = hipGetLastError();                                      \
+        if (e__ != hipSuccess)                                                   \
+            return ::kd::fail(KD_ERR_LAUNCH, std::string(what) + ": " + hipGetErrorString(e__)); \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------------- types ----
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+// ------------------------------------------------------------- reductions ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide sum over NW waves using a caller-provided LDS scratch of >= NW floats.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) scratch[w] = v;
+    __syncthreads();
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r += scratch[i];
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) scratch[w] = v;
+    __syncthreads();
+    float r = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r = fmaxf(r, scratch[i]);
+    return r;
+}
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace kd

@@ -1,0 +1,498 @@
+// Fused KD-loss forward+backward over [B*L, V] bf16 logits (HBM-bound).
+//
+// Replaces, in one launch sequence, the reference's per-step logit losses:
+//   compute_loca_loss      DT:141-194 / LB:208-261   (KD_LOSS_LOCA)
+//   compute_vision_loss KL DT:330-343                 (KD_LOSS_KL)
+//   compute_loss KL(log_target=True) FB:205-219       (KD_LOSS_KL_LOGTARGET)
+//   the in-model student CE (HF ForCausalLMLoss: shift by one, ignore -100, mean)
+// and the autograd backward of all of them w.r.t. the student logits.
+//
+// Kernels (one row = one (b, l) position; one 256-thread workgroup per row,
+// grid-strided over rows):
+//   k_row_stats : one pass over teacher+student rows -> max / sum-exp at T and 1,
+//                 teacher top-2 (LoCa "klogits", DT:170-171), gathers at the label;
+//                 LoCa: records the LAST row-major position per label id and per
+//                 klogit id (atomicMax) — the global last-write-wins semantics of
+//                 `loca[:, :, labels] = X` (DT:184-185; SURVEY §4 KAT 1).
+//   k_ovr_mask  : bitmask of overridden vocab columns (LoCa only).
+//   k_loss_grad : pass A sums the KD term and the row scalar S, pass B writes
+//                 dlogits (re-read of the row is served by L2 / Infinity Cache).
+//   k_finalize  : deterministic fp64 reduction of the per-row partials.
+#include "common.h"
+
+namespace kd {
+namespace {
+
+constexpr int NT = 256;  // threads per workgroup
+constexpr int NW = NT / 64;
+
+struct RowStats {
+    float mt, zt;     // teacher max over [0,V_s) and sum exp((t-mt)/T)
+    float mtf, ztf;   // teacher max over [0,V_t) and sum exp(t-mtf)  (teacher CE)
+    float ms, zs;     // student max and sum exp((s-ms)/T)
+    float zs1;        // student sum exp(s-ms)
+    float ce;         // student CE of this row (0 if no valid shifted label)
+    float tce;        // teacher CE of this row
+    float ovx, ovy;   // LoCa override values X = 1 - s(1-p_gt), Y = s p_k
+    int i1, i2;       // teacher top-1 / top-2 index over [0,V_s)
+    int lab;          // label at this position (LoCa gather index)
+    int lab_next;     // shifted CE label (-100 => ignored)
+    int valid;        // 1 if lab_next is a CE target
+};
+static_assert(sizeof(RowStats) == 64, "RowStats layout");
+
+struct Layout {
+    size_t stats, lab_last, klo_last, mask, part_kl, err, total;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+inline Layout make_layout(int B, int L, int V) {
+    Layout lo{};
+    const size_t rows = (size_t)B * L;
+    size_t off = 0;
+    lo.err = off;      off = align16(off + 16);   // error word first: kd_loss_check reads ws[0]
+    lo.stats = off;    off = align16(off + rows * sizeof(RowStats));
+    lo.lab_last = off; off = align16(off + (size_t)V * 4);
+    lo.klo_last = off; off = align16(off + (size_t)V * 4);
+    lo.mask = off;     off = align16(off + (size_t)((V + 63) / 64) * 8);
+    lo.part_kl = off;  off = align16(off + rows * 4);
+    lo.total = off;
+    return lo;
+}
+
+// top-2 with deterministic tie-break: larger value first, lower index on ties.
+__device__ __forceinline__ bool better(float a, int ia, float b, int ib) {
+    return a > b || (a == b && ia < ib);
+}
+__device__ __forceinline__ void top2_push(float v, int i, float& v1, int& i1, float& v2, int& i2) {
+    if (better(v, i, v1, i1)) {
+        v2 = v1; i2 = i1; v1 = v; i1 = i;
+    } else if (better(v, i, v2, i2)) {
+        v2 = v; i2 = i;
+    }
+}
+
+// merge an online (max, sum-exp-at-invT) pair
+__device__ __forceinline__ void lse_merge(float& m, float& z, float m2, float z2, float invT) {
+    if (m2 == -INFINITY) return;
+    if (m == -INFINITY) { m = m2; z = z2; return; }
+    if (m2 > m) { z = z * __expf((m - m2) * invT) + z2; m = m2; }
+    else        { z = z + z2 * __expf((m2 - m) * invT); }
+}
+
+__global__ void __launch_bounds__(NT)
+k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
+            const bf16* __restrict__ S_, int64_t ld_s, int V_s,
+            const int64_t* __restrict__ labels, int L, int rows,
+            int variant, float invT, float alpha, int want_tce,
+            RowStats* __restrict__ stats, int* __restrict__ lab_last,
+            int* __restrict__ klo_last, int* __restrict__ err) {
+    __shared__ float sm[NW * 8];
+    __shared__ int si[NW * 2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const bool has_t = (T_ != nullptr);
+    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+        const bf16* srow = S_ + (int64_t)r * ld_s;
+        const bf16* trow = has_t ? T_ + (int64_t)r * ld_t : nullptr;
+        // ---- student: max / sum-exp at T and at 1 (same max)
+        float ms = -INFINITY, zs = 0.f, zs1 = 0.f;
+        for (int v = tid * 8; v < V_s; v += NT * 8) {
+            bf16x8 x = *(const bf16x8*)(srow + v);
+            float f[8], cm = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { f[j] = (float)x[j]; cm = fmaxf(cm, f[j]); }
+            if (cm > ms) {
+                if (ms != -INFINITY) { zs *= __expf((ms - cm) * invT); zs1 *= __expf(ms - cm); }
+                ms = cm;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { zs += __expf((f[j] - ms) * invT); zs1 += __expf(f[j] - ms); }
+        }
+        // ---- teacher: max/sum over V_s at T, top-2 over V_s; max/sum over V_t at 1
+        float mt = -INFINITY, zt = 0.f, mtf = -INFINITY, ztf = 0.f;
+        float v1 = -INFINITY, v2 = -INFINITY;
+        int i1 = 0x7fffffff, i2 = 0x7fffffff;
+        if (has_t) {
+            for (int v = tid * 8; v < V_t; v += NT * 8) {
+                bf16x8 x = *(const bf16x8*)(trow + v);
+                float f[8], cm = -INFINITY, cmf = -INFINITY;
+                const bool in_s = v < V_s;  // V_s % 8 == 0: chunks never straddle
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { f[j] = (float)x[j]; cmf = fmaxf(cmf, f[j]); }
+                if (in_s) cm = cmf;
+                if (want_tce) {
+                    if (cmf > mtf) { if (mtf != -INFINITY) ztf *= __expf(mtf - cmf); mtf = cmf; }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) ztf += __expf(f[j] - mtf);
+                }
+                if (in_s) {
+                    if (cm > mt) { if (mt != -INFINITY) zt *= __expf((mt - cm) * invT); mt = cm; }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        zt += __expf((f[j] - mt) * invT);
+                        top2_push(f[j], v + j, v1, i1, v2, i2);
+                    }
+                }
+            }
+        }
+        // ---- wave reductions
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            float oms = __shfl_xor(ms, o, 64), ozs = __shfl_xor(zs, o, 64), ozs1 = __shfl_xor(zs1, o, 64);
+            float m1 = ms, zz1 = zs1;
+            lse_merge(ms, zs, oms, ozs, invT);
+            lse_merge(m1, zz1, oms, ozs1, 1.f);
+            zs1 = zz1;
+            float omt = __shfl_xor(mt, o, 64), ozt = __shfl_xor(zt, o, 64);
+            lse_merge(mt, zt, omt, ozt, invT);
+            float omtf = __shfl_xor(mtf, o, 64), oztf = __shfl_xor(ztf, o, 64);
+            lse_merge(mtf, ztf, omtf, oztf, 1.f);
+            float ov1 = __shfl_xor(v1, o, 64), ov2 = __shfl_xor(v2, o, 64);
+            int oi1 = __shfl_xor(i1, o, 64), oi2 = __shfl_xor(i2, o, 64);
+            top2_push(ov1, oi1, v1, i1, v2, i2);
+            top2_push(ov2, oi2, v1, i1, v2, i2);
+        }
+        __syncthreads();
+        if (lane == 0) {
+            sm[w * 8 + 0] = ms; sm[w * 8 + 1] = zs; sm[w * 8 + 2] = zs1;
+            sm[w * 8 + 3] = mt; sm[w * 8 + 4] = zt; sm[w * 8 + 5] = mtf; sm[w * 8 + 6] = ztf;
+            sm[w * 8 + 7] = v1; si[w * 2 + 0] = i1; si[w * 2 + 1] = i2;
+        }
+        // v2 of each wave kept in a second LDS slot set
+        __shared__ float sv2[NW];
+        if (lane == 0) sv2[w] = v2;
+        __syncthreads();
+        if (tid == 0) {
+            float Ms = sm[0], Zs = sm[1], Zs1 = sm[2], Mt = sm[3], Zt = sm[4], Mtf = sm[5], Ztf = sm[6];
+            float V1 = sm[7], V2 = sv2[0];
+            int I1 = si[0], I2 = si[1];
+            for (int k = 1; k < NW; ++k) {
+                float m1 = Ms, z1 = Zs1;
+                lse_merge(Ms, Zs, sm[k * 8 + 0], sm[k * 8 + 1], invT);
+                lse_merge(m1, z1, sm[k * 8 + 0], sm[k * 8 + 2], 1.f);
+                Zs1 = z1;
+                lse_merge(Mt, Zt, sm[k * 8 + 3], sm[k * 8 + 4], invT);
+                lse_merge(Mtf, Ztf, sm[k * 8 + 5], sm[k * 8 + 6], 1.f);
+                top2_push(sm[k * 8 + 7], si[k * 2 + 0], V1, I1, V2, I2);
+                top2_push(sv2[k], si[k * 2 + 1], V1, I1, V2, I2);
+            }
+            RowStats st;
+            st.ms = Ms; st.zs = Zs; st.zs1 = Zs1;
+            st.mt = Mt; st.zt = Zt; st.mtf = Mtf; st.ztf = Ztf;
+            st.i1 = I1; st.i2 = I2;
+            const int b = r / L, l = r - b * L;
+            const int64_t lab = labels[r];
+            const int64_t labn = (l + 1 < L) ? labels[r + 1] : -100;
+            st.lab = (int)lab;
+            st.lab_next = (int)labn;
+            // student / teacher CE on the shifted label
+            const bool labn_ok = (labn == -100) || (labn >= 0 && labn < V_s);
+            if (!labn_ok) atomicOr(err, 1);
+            st.valid = (labn >= 0 && labn < V_s) ? 1 : 0;
+            st.ce = 0.f; st.tce = 0.f;
+            if (st.valid) {
+                const float sl = (float)srow[labn];
+                st.ce = logf(Zs1) + Ms - sl;
+                if (has_t && want_tce) st.tce = logf(Ztf) + Mtf - (float)trow[labn];
+            }
+            st.ovx = 0.f; st.ovy = 0.f;
+            if (variant == KD_LOSS_LOCA) {
+                if (lab < 0 || lab >= V_s) {
+                    atomicOr(err, 1);  // reference: gather index out of bounds (DT:166)
+                } else {
+                    // p_gt, p_k (DT:166, :174), sigma, s (DT:177-180)
+                    const float p_gt = __expf(((float)trow[lab] - Mt) * invT) / Zt;
+                    const float p_k = __expf((V2 - Mt) * invT) / Zt;
+                    const float sigma = 1.f / (1.f - p_gt + p_k);
+                    const float sc = alpha * sigma;
+                    // X = 1 - s*(sum(p_T) - p_gt) with sum(p_T) = 1 (DT:184)
+                    st.ovx = 1.f - sc * (1.f - p_gt);
+                    st.ovy = sc * p_k;  // DT:185
+                    atomicMax(&lab_last[lab], r);
+                    atomicMax(&klo_last[I2], r);
+                }
+            }
+            stats[r] = st;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_ovr_mask(const int* __restrict__ lab_last, const int* __restrict__ klo_last,
+                           int V, unsigned long long* __restrict__ mask) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool on = (v < V) && (lab_last[v] >= 0 || klo_last[v] >= 0);
+    const unsigned long long bits = __ballot(on);
+    if ((threadIdx.x & 63) == 0 && v < V + 63) mask[v >> 6] = bits;
+}
+
+template <int VARIANT>
+__device__ __forceinline__ void
+loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
+            const bf16* __restrict__ S_, int64_t ld_s, int V,
+            int rows, float invT, float clamp_min,
+            const RowStats* __restrict__ stats,
+            const int* __restrict__ lab_last, const int* __restrict__ klo_last,
+            const unsigned long long* __restrict__ mask_g,
+            float kd_coef,   // kd_weight * T / N * grad_scale
+            float ce_coef,   // ce_weight / n_valid * grad_scale   (host-computed count)
+            bf16* __restrict__ D_, int64_t ld_d, float* __restrict__ part_kl,
+            unsigned long long* smask, float* red) {
+    const int tid = threadIdx.x;
+    const int nwords = (V + 63) / 64;
+    if (VARIANT == KD_LOSS_LOCA) {
+        for (int i = tid; i < nwords; i += NT) smask[i] = mask_g[i];
+        __syncthreads();
+    }
+    const float log_clamp = logf(clamp_min);
+    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+        const RowStats st = stats[r];
+        const bf16* srow = S_ + (int64_t)r * ld_s;
+        const bf16* trow = (VARIANT != KD_LOSS_NONE) ? T_ + (int64_t)r * ld_t : nullptr;
+        const float log_zs = logf(st.zs);
+        const float inv_zt = (VARIANT != KD_LOSS_NONE) ? 1.f / st.zt : 0.f;
+        const float log_zt = (VARIANT != KD_LOSS_NONE) ? logf(st.zt) : 0.f;
+        float Ssum = 0.f;
+        if (VARIANT != KD_LOSS_NONE) {
+            // ---- pass A: KD term and S
+            float term = 0.f, sacc = 0.f;
+            for (int v = tid * 8; v < V; v += NT * 8) {
+                bf16x8 xt = *(const bf16x8*)(trow + v);
+                bf16x8 xs = *(const bf16x8*)(srow + v);
+                unsigned int mbits = 0;
+                if (VARIANT == KD_LOSS_LOCA) mbits = (unsigned)(smask[v >> 6] >> (v & 63)) & 0xffu;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float lt = ((float)xt[j] - st.mt) * invT;  // log-space teacher (unnormalised)
+                    const float pT = __expf(lt) * inv_zt;
+                    const float lps = ((float)xs[j] - st.ms) * invT - log_zs;
+                    if (VARIANT == KD_LOSS_LOCA) {
+                        float q = pT, logq = lt - log_zt;
+                        if (mbits & (1u << j)) {
+                            const int kl = klo_last[v + j];
+                            q = (kl >= 0) ? stats[kl].ovy : stats[lab_last[v + j]].ovx;
+                            logq = logf(q);
+                        }
+                        const float ps = __expf(lps);
+                        const bool unc = ps >= clamp_min;
+                        const float logc = unc ? lps : log_clamp;
+                        term += (q > 0.f ? q * logq : 0.f) - q * logc;
+                        sacc += unc ? q : 0.f;
+                    } else if (VARIANT == KD_LOSS_KL) {
+                        term += (pT > 0.f ? pT * (lt - log_zt) : 0.f) - pT * lps;
+                        sacc += pT;
+                    } else {  // KL_LOGTARGET quirk: exp(p_T) * (p_T - log p_S)
+                        const float e = __expf(pT);
+                        term += e * (pT - lps);
+                        sacc += e;
+                    }
+                }
+            }
+            term = block_sum<NW>(term, red);
+            Ssum = block_sum<NW>(sacc, red);
+            if (tid == 0) part_kl[r] = term;
+        } else {
+            if (tid == 0) part_kl[r] = 0.f;
+        }
+        if (D_ != nullptr) {
+            // ---- pass B: dlogits
+            const float log_zs1 = logf(st.zs1);
+            const float cec = st.valid ? ce_coef : 0.f;
+            bf16* drow = D_ + (int64_t)r * ld_d;
+            for (int v = tid * 8; v < V; v += NT * 8) {
+                bf16x8 xs = *(const bf16x8*)(srow + v);
+                bf16x8 xt;
+                if (VARIANT != KD_LOSS_NONE) xt = *(const bf16x8*)(trow + v);
+                unsigned int mbits = 0;
+                if (VARIANT == KD_LOSS_LOCA) mbits = (unsigned)(smask[v >> 6] >> (v & 63)) & 0xffu;
+                bf16x8 out;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float sv = (float)xs[j];
+                    float g = 0.f;
+                    if (VARIANT != KD_LOSS_NONE) {
+                        const float lt = ((float)xt[j] - st.mt) * invT;
+                        const float pT = __expf(lt) * inv_zt;
+                        const float ps = __expf((sv - st.ms) * invT - log_zs);
+                        float gq;
+                        if (VARIANT == KD_LOSS_LOCA) {
+                            float q = pT;
+                            if (mbits & (1u << j)) {
+                                const int kl = klo_last[v + j];
+                                q = (kl >= 0) ? stats[kl].ovy : stats[lab_last[v + j]].ovx;
+                            }
+                            gq = (ps >= clamp_min) ? q : 0.f;
+                        } else if (VARIANT == KD_LOSS_KL) {
+                            gq = pT;
+                        } else {
+                            gq = __expf(pT);
+                        }
+                        g = kd_coef * (ps * Ssum - gq);
+                    }
+                    if (cec != 0.f) {
+                        const float p1 = __expf(sv - st.ms - log_zs1);
+                        g += cec * (p1 - ((v + j) == st.lab_next ? 1.f : 0.f));
+                    }
+                    out[j] = (bf16)g;
+                }
+                *(bf16x8*)(drow + v) = out;
+            }
+        }
+    }
+}
+
+__global__ void k_finalize(const RowStats* __restrict__ stats, const float* __restrict__ part_kl,
+                           int rows, double kl_scale, float kd_weight, float ce_weight,
+                           float* __restrict__ out) {
+    __shared__ double red[4][NW];
+    double kl = 0, ce = 0, tce = 0, nv = 0;
+    for (int r = threadIdx.x; r < rows; r += NT) {
+        kl += part_kl[r];
+        const RowStats& st = stats[r];
+        ce += st.ce; tce += st.tce; nv += st.valid;
+    }
+    kl = wave_sum_d(kl); ce = wave_sum_d(ce); tce = wave_sum_d(tce); nv = wave_sum_d(nv);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = kl; red[1][w] = ce; red[2][w] = tce; red[3][w] = nv; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0, b = 0, c = 0, n = 0;
+        for (int i = 0; i < NW; ++i) { a += red[0][i]; b += red[1][i]; c += red[2][i]; n += red[3][i]; }
+        const double kd = a * kl_scale;
+        // HF CE: mean over valid targets (NaN when there are none, as torch's mean of empty)
+        const double ce_m = b / n, tce_m = c / n;
+        out[0] = (float)kd;
+        out[1] = (float)ce_m;
+        out[2] = (float)tce_m;
+        out[3] = (float)(kd_weight * kd + ce_weight * ce_m);
+    }
+}
+
+// count of valid shifted labels, computed on device into a float (for the CE mean)
+__global__ void k_count_valid(const int64_t* __restrict__ labels, int B, int L, int V, float* out) {
+    __shared__ float red[NW];
+    float c = 0.f;
+    for (int r = threadIdx.x; r < B * L; r += NT) {
+        const int l = r % L;
+        if (l + 1 < L) {
+            const int64_t x = labels[r + 1];
+            c += (x >= 0 && x < V) ? 1.f : 0.f;
+        }
+    }
+    c = block_sum<NW>(c, red);
+    if (threadIdx.x == 0) *out = c;
+}
+
+template <int VARIANT>
+__global__ void __launch_bounds__(NT)
+k_loss_grad(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
+            int V, int rows, float invT, float clamp_min, const RowStats* __restrict__ stats,
+            const int* __restrict__ lab_last, const int* __restrict__ klo_last,
+            const unsigned long long* __restrict__ mask_g, float kd_coef, float ce_coef_num,
+            const float* __restrict__ n_valid, bf16* __restrict__ D_, int64_t ld_d,
+            float* __restrict__ part_kl) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long smask[];
+    __shared__ float red[NW];
+    // the CE mean's denominator lives on the device (no host sync)
+    const float nv = *n_valid;
+    const float ce_coef = nv > 0.f ? ce_coef_num / nv : 0.f;
+    loss_grad_body<VARIANT>(T_, ld_t, S_, ld_s, V, rows, invT, clamp_min, stats, lab_last, klo_last,
+                            mask_g, kd_coef, ce_coef, D_, ld_d, part_kl, smask, red);
+}
+
+}  // namespace
+
+int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* student, int64_t ld_s,
+                   int V_s, const int64_t* labels, int B, int L, kd_loss_params p, float* loss_out,
+                   void* dlogits, int64_t ld_d, void* ws, size_t ws_bytes, void* stream_) {
+    hipStream_t stream = as_stream(stream_);
+    const int variant = p.variant;
+    KD_CHECK_ARG(variant >= KD_LOSS_NONE && variant <= KD_LOSS_KL_LOGTARGET, "kd_loss: bad variant");
+    KD_CHECK_ARG(student && labels && loss_out && ws, "kd_loss: null pointer");
+    KD_CHECK_ARG(variant == KD_LOSS_NONE || teacher, "kd_loss: teacher logits required");
+    KD_CHECK_SHAPE(B > 0 && L > 0 && V_s > 0, "kd_loss: empty shape");
+    KD_CHECK_SHAPE(V_s % 8 == 0 && ld_s % 8 == 0 && ld_s >= V_s, "kd_loss: V_s/ld_s must be multiples of 8");
+    KD_CHECK_ALIGN(student, 16, "kd_loss: student logits must be 16-B aligned");
+    if (teacher) {
+        KD_CHECK_SHAPE(V_t >= V_s && V_t % 8 == 0 && ld_t % 8 == 0 && ld_t >= V_t,
+                       "kd_loss: teacher V_t/ld_t must be multiples of 8 and V_t >= V_s");
+        KD_CHECK_ALIGN(teacher, 16, "kd_loss: teacher logits must be 16-B aligned");
+    }
+    if (dlogits) {
+        KD_CHECK_SHAPE(ld_d % 8 == 0 && ld_d >= V_s, "kd_loss: ld_d must be a multiple of 8");
+        KD_CHECK_ALIGN(dlogits, 16, "kd_loss: dlogits must be 16-B aligned");
+    }
+    KD_CHECK_ARG(p.temperature > 0.f, "kd_loss: temperature must be > 0");
+    const Layout lo = make_layout(B, L, V_s);
+    if (ws_bytes < lo.total) return fail(KD_ERR_WORKSPACE, "kd_loss: workspace too small");
+    char* w = (char*)ws;
+    RowStats* stats = (RowStats*)(w + lo.stats);
+    int* lab_last = (int*)(w + lo.lab_last);
+    int* klo_last = (int*)(w + lo.klo_last);
+    unsigned long long* mask = (unsigned long long*)(w + lo.mask);
+    float* part_kl = (float*)(w + lo.part_kl);
+    int* err = (int*)(w + lo.err);
+    float* nvalid = (float*)(w + lo.err + 4);
+    const int rows = B * L;
+    const float invT = 1.f / p.temperature;
+    const bf16* T_ = (const bf16*)(variant == KD_LOSS_NONE ? nullptr : teacher);
+    const bf16* S_ = (const bf16*)student;
+
+    if (hipMemsetAsync(err, 0, 16, stream) != hipSuccess) return fail(KD_ERR_LAUNCH, "kd_loss: memset");
+    if (variant == KD_LOSS_LOCA) {
+        if (hipMemsetAsync(lab_last, 0xff, (size_t)V_s * 4, stream) != hipSuccess ||
+            hipMemsetAsync(klo_last, 0xff, (size_t)V_s * 4, stream) != hipSuccess)
+            return fail(KD_ERR_LAUNCH, "kd_loss: memset tables");
+    }
+    const int grid = rows < 2048 ? rows : 2048;
+    hipLaunchKernelGGL(k_row_stats, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
+                       V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
+                       lab_last, klo_last, err);
+    KD_LAUNCH_CHECK("k_row_stats");
+    if (variant == KD_LOSS_LOCA) {
+        const int nb = (V_s + 255) / 256;
+        hipLaunchKernelGGL(k_ovr_mask, dim3(nb), dim3(256), 0, stream, lab_last, klo_last, V_s, mask);
+        KD_LAUNCH_CHECK("k_ovr_mask");
+    }
+    hipLaunchKernelGGL(k_count_valid, dim3(1), dim3(NT), 0, stream, labels, B, L, V_s, nvalid);
+    KD_LAUNCH_CHECK("k_count_valid");
+    const double N = (double)rows * (double)V_s;
+    const float T = p.temperature;
+    const float kd_coef = (float)((double)p.kd_weight * T / N * p.grad_scale);
+    const float ce_num = p.ce_weight * p.grad_scale;
+    const size_t smem = variant == KD_LOSS_LOCA ? (size_t)((V_s + 63) / 64) * 8 : 0;
+    if (smem > 150 * 1024) return fail(KD_ERR_SHAPE, "kd_loss: vocab too large for LDS mask");
+    bf16* D_ = (bf16*)dlogits;
+#define KD_LAUNCH_LG(VAR)                                                                          \
+    hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(grid), dim3(NT), smem, stream, T_, ld_t, S_, ld_s, \
+                       V_s, rows, invT, p.clamp_min, stats, lab_last, klo_last, mask, kd_coef,     \
+                       ce_num, nvalid, D_, ld_d, part_kl)
+    switch (variant) {
+        case KD_LOSS_NONE: KD_LAUNCH_LG(KD_LOSS_NONE); break;
+        case KD_LOSS_LOCA: KD_LAUNCH_LG(KD_LOSS_LOCA); break;
+        case KD_LOSS_KL: KD_LAUNCH_LG(KD_LOSS_KL); break;
+        default: KD_LAUNCH_LG(KD_LOSS_KL_LOGTARGET); break;
+    }
+#undef KD_LAUNCH_LG
+    KD_LAUNCH_CHECK("k_loss_grad");
+    const double kl_scale = (variant == KD_LOSS_NONE) ? 0.0 : (double)T * T / N;
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(NT), 0, stream, stats, part_kl, rows, kl_scale,
+                       p.kd_weight, p.ce_weight, loss_out);
+    KD_LAUNCH_CHECK("k_finalize");
+    return KD_OK;
+}
+
+size_t kd_loss_ws(int B, int L, int V) { return make_layout(B, L, V).total; }
+
+int kd_loss_check_impl(const void* ws_, void* stream_) {
+    int h = 0;  // error word is at workspace offset 0
+    KD_CHECK_ARG(ws_ != nullptr, "kd_loss_check: null workspace");
+    if (hipStreamSynchronize(as_stream(stream_)) != hipSuccess) return fail(KD_ERR_LAUNCH, "kd_loss_check: sync");
+    if (hipMemcpy(&h, ws_, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(KD_ERR_LAUNCH, "kd_loss_check: copy");
+    if (h) return fail(KD_ERR_LABEL_RANGE, "kd_loss: label outside [0, V) (LoCa gathers at every label; "
+                                            "CE targets must be -100 or in range)");
+    return KD_OK;
+}
+
+}  // namespace kd

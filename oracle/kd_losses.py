@@ -1,0 +1,195 @@
+"""ORACLE — test infrastructure only, never the product path.
+
+CPU restatement of the reference's per-step loss arithmetic
+(shayekh00/Knowledge_Distillation_for_Sensory_Substitution_in_Multimodal_Models):
+
+  loca_kd_term        compute_loca_loss      DT:141-194, LB:208-261
+  kl_mean_term        compute_vision_loss KL DT:330-343
+  kl_logtarget_term   compute_loss KL        FB:205-219 (log_target=True quirk)
+  nt_xent             contrastive_loss       DT:393-416, FB:288-311
+  causal_lm_ce        in-model CE of LlavaOnevisionForConditionalGeneration (labels given,
+                      no attention mask) = transformers ForCausalLMLoss (shift by one,
+                      ignore_index=-100, mean over valid targets)
+  *_total             the per-variant combinations of forward(): DT:250-260, LB:164-165,
+                      FB:161-165/227, BD:90-101
+
+Pinned against the reference itself: tests/golden/make_golden.py imports the
+reference modules in this container and records their outputs on seeded inputs
+(tests/golden/*.npz); tests/test_oracle_golden.py checks this file against them.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  Formulation notes (SURVEY §4 known-answer tests):
+  KAT 1  `loca[:, :, labels] = X` with labels [B,L] writes, in EVERY row, column v the
+         value X at the LAST row-major position whose label is v; the klogits write
+         (DT:185) is applied second and wins.  Restated here as explicit tables.
+  KAT 2  a label outside [0, V) makes the reference's gather raise; so does this.
+  KAT 3  kl_div(log_target=True) with a probability target = mean(exp(p)(p - log q)).
+  KAT 4  reduction='mean' divides by B*L*V.
+  KAT 5  clamp(p_S, 1e-8) zeroes the gradient where p_S < 1e-8 (autograd of clamp).
+  KAT 6  torch.topk tie order on CPU is not lowest-index-first; fixtures are tie-free,
+         this oracle breaks ties by lowest index (as the HIP kernel does).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _softmax_T(logits: torch.Tensor, T: float) -> torch.Tensor:
+    z = logits / T
+    z = z - z.amax(dim=-1, keepdim=True)
+    e = torch.exp(z)
+    return e / e.sum(dim=-1, keepdim=True)
+
+
+def _log_softmax_T(logits: torch.Tensor, T: float) -> torch.Tensor:
+    z = logits / T
+    return z - torch.logsumexp(z, dim=-1, keepdim=True)
+
+
+def top2_second_index(probs: torch.Tensor) -> torch.Tensor:
+    """Index of the second most probable class (DT:170-171), ties -> lowest index."""
+    v = probs.detach()
+    n = v.shape[-1]
+    idx = torch.arange(n, device=v.device).expand_as(v)
+    # sort by (-value, index): stable sort on -value keeps index order among ties
+    order = torch.sort(-v, dim=-1, stable=True).indices
+    del idx
+    return order[..., 1]
+
+
+def last_position_table(ids: np.ndarray, V: int) -> np.ndarray:
+    """last[v] = largest flattened (row-major) position p with ids.flat[p] == v, else -1."""
+    flat = ids.reshape(-1).astype(np.int64)
+    last = np.full(V, -1, dtype=np.int64)
+    np.maximum.at(last, flat, np.arange(flat.size, dtype=np.int64))
+    return last
+
+
+def loca_kd_term(teacher_logits, student_logits, labels, T: float, alpha: float = 0.8,
+                 clamp_min: float = 1e-8):
+    """KD part of compute_loca_loss (DT:141-194): returns loca_loss WITHOUT the CE.
+
+    loss = mean_{b,l,v}( q log q - q log clamp(p_S) ) * T^2 with q the calibrated teacher.
+    """
+    V = student_logits.shape[-1]
+    t = teacher_logits[..., :V]                                   # DT:155
+    if labels.min().item() < 0 or labels.max().item() >= V:       # KAT 2 (DT:166)
+        raise RuntimeError("index out of bounds: LoCa gathers the teacher prob at every label")
+    p_t = _softmax_T(t, T)                                        # DT:158
+    p_s = _softmax_T(student_logits, T)                           # DT:159
+    c_s = torch.clamp(p_s, min=clamp_min)                         # DT:161-162
+    p_gt = torch.gather(p_t, -1, labels.unsqueeze(-1)).squeeze(-1)            # DT:166
+    k = top2_second_index(p_t)                                                 # DT:170-171
+    p_k = torch.gather(p_t, -1, k.unsqueeze(-1)).squeeze(-1)                   # DT:174
+    s = alpha / (1.0 - p_gt + p_k)                                             # DT:177-180
+    X = 1.0 - s * (p_t.sum(-1) - p_gt)                                          # DT:184 rhs
+    Y = s * p_k                                                                 # DT:185 rhs
+    # KAT 1: global last-write-wins column overrides, labels first then klogits
+    lab_last = last_position_table(labels.cpu().numpy(), V)
+    klo_last = last_position_table(k.cpu().numpy(), V)
+    q = p_t.clone()
+    Xf, Yf = X.reshape(-1), Y.reshape(-1)
+    cols_l = np.nonzero(lab_last >= 0)[0]
+    cols_k = np.nonzero(klo_last >= 0)[0]
+    if cols_l.size:
+        q[..., torch.from_numpy(cols_l)] = Xf[torch.from_numpy(lab_last[cols_l])].to(q.dtype)
+    if cols_k.size:
+        q[..., torch.from_numpy(cols_k)] = Yf[torch.from_numpy(klo_last[cols_k])].to(q.dtype)
+    xlogx = torch.where(q > 0, q * torch.log(torch.where(q > 0, q, torch.ones_like(q))), torch.zeros_like(q))
+    return (xlogx - q * torch.log(c_s)).mean() * (T ** 2)          # DT:188-192 (KAT 4)
+
+
+def kl_mean_term(teacher_logits, student_logits, T: float):
+    """kl_div(log_softmax(s/T), softmax(t/T), reduction='mean') * T^2 (DT:330-343)."""
+    V = student_logits.shape[-1]
+    p_t = _softmax_T(teacher_logits[..., :V], T)
+    lq = _log_softmax_T(student_logits, T)
+    xlogx = torch.where(p_t > 0, p_t * torch.log(torch.where(p_t > 0, p_t, torch.ones_like(p_t))),
+                        torch.zeros_like(p_t))
+    return (xlogx - p_t * lq).mean() * (T ** 2)
+
+
+def kl_logtarget_term(teacher_logits, student_logits, T: float):
+    """FB:205-219 quirk (KAT 3): target is a probability but log_target=True."""
+    V = student_logits.shape[-1]
+    p_t = _softmax_T(teacher_logits[..., :V], T)
+    lq = _log_softmax_T(student_logits, T)
+    return (torch.exp(p_t) * (p_t - lq)).mean() * (T ** 2)
+
+
+def causal_lm_ce(logits, labels, ignore_index: int = -100):
+    """HF causal-LM loss: logits[:, :-1] predict labels[:, 1:], mean over valid targets."""
+    V = logits.shape[-1]
+    lg = logits[:, :-1, :].reshape(-1, V).float() if logits.dtype != torch.float64 else logits[:, :-1, :].reshape(-1, V)
+    tg = labels[:, 1:].reshape(-1)
+    valid = tg != ignore_index
+    if ((tg[valid] < 0) | (tg[valid] >= V)).any():
+        raise RuntimeError("CE target out of range")
+    lse = torch.logsumexp(lg, dim=-1)
+    picked = torch.gather(lg, -1, torch.where(valid, tg, torch.zeros_like(tg)).unsqueeze(-1)).squeeze(-1)
+    nll = (lse - picked)[valid]
+    return nll.sum() / valid.sum()
+
+
+def l2_normalize(x, eps: float = 1e-12):
+    """F.normalize(p=2, dim=-1): x / max(||x||, eps)."""
+    n = torch.sqrt((x * x).sum(-1, keepdim=True))
+    return x / torch.clamp(n, min=eps)
+
+
+def nt_xent(student_features, teacher_features, temperature: float = 0.07):
+    """contrastive_loss (DT:393-416): normalise, S T^T / tau, CE against arange."""
+    s = l2_normalize(student_features)
+    t = l2_normalize(teacher_features)
+    logits = s @ t.T / temperature
+    n = logits.shape[0]
+    lse = torch.logsumexp(logits, dim=-1)
+    return (lse - logits[torch.arange(n), torch.arange(n)]).mean()
+
+
+def pooled_features(post_ln_out):
+    """DT:243-248: mean over tokens then L2-normalise.  post_ln_out: [2B, 729, 1152]."""
+    return l2_normalize(post_ln_out.mean(dim=1))
+
+
+# ---------------------------------------------------------------- totals ----
+# The hard-coded hyper-parameters of each reference module.
+DT_HPARAMS = dict(T=0.8, gamma=0.8, soft_target_loss_weight=0.1, ce_loss_weight=0.5, alpha=0.8)  # DT:67-71
+LB_HPARAMS = dict(T=1.0, soft_target_loss_weight=0.5, ce_loss_weight=0.5, alpha=0.8)             # LB:73-75
+FB_HPARAMS = dict(T=0.8, soft_target_loss_weight=0.1, ce_loss_weight=0.8)                       # FB:72-74
+
+
+def dt_total(phase: int, teacher_logits, student_logits, labels, s_feat=None, t_feat=None):
+    """forward() of the double-trouble module, DT:250-260."""
+    h = DT_HPARAMS
+    ce = causal_lm_ce(student_logits, labels)
+    if phase == 1:   # compute_vision_loss DT:316-354: 0.1 KL T^2 + 0.5 NT-Xent (no CE)
+        kl = kl_mean_term(teacher_logits, student_logits, h["T"])
+        return h["soft_target_loss_weight"] * kl + h["ce_loss_weight"] * nt_xent(s_feat, t_feat)
+    loca = loca_kd_term(teacher_logits, student_logits, labels, h["T"], h["alpha"]) + ce
+    if phase == 2:
+        return loca
+    if phase == 3:   # KAT 8: gamma (loca + CE) + (1 - gamma) CE
+        return h["gamma"] * loca + (1 - h["gamma"]) * ce
+    raise ValueError(phase)
+
+
+def lb_total(teacher_logits, student_logits, labels):
+    """LB forward: compute_loca_loss at T=1 (LB:164-165, :208-261)."""
+    h = LB_HPARAMS
+    return loca_kd_term(teacher_logits, student_logits, labels, h["T"], h["alpha"]) + causal_lm_ce(student_logits, labels)
+
+
+def fb_total(teacher_logits, student_logits, labels, s_feat, t_feat):
+    """FB forward + compute_loss: 0.1 KLq T^2 + 0.8 CE + NT-Xent (FB:161-165, :205-227)."""
+    h = FB_HPARAMS
+    kl = kl_logtarget_term(teacher_logits, student_logits, h["T"])
+    return (h["soft_target_loss_weight"] * kl + h["ce_loss_weight"] * causal_lm_ce(student_logits, labels)
+            + nt_xent(s_feat, t_feat))
+
+
+def bd_total(student_logits, labels):
+    """BD training_step: the student's CE only (BD:90-101)."""
+    return causal_lm_ce(student_logits, labels)
