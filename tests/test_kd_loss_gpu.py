@@ -52,7 +52,8 @@ def test_kd_loss_kernel_matches_reference(name, dev):
     t, s, labels = kd_inputs(meta, exp)
     loss, g = _run(meta, t, s, labels, dev)
     assert loss[1] == pytest.approx(float(exp["ce"]), rel=1e-5)
-    assert loss[2] == pytest.approx(float(exp["teacher_ce"]), rel=1e-5)
+    if meta["variant"] != "ce":  # BD SFT has no teacher (teacher CE side output absent)
+        assert loss[2] == pytest.approx(float(exp["teacher_ce"]), rel=1e-5)
     assert loss[0] == pytest.approx(float(exp["kd_term"]), rel=1e-4, abs=1e-12)
     assert loss[3] == pytest.approx(float(exp["total"]), rel=1e-4)
     np.testing.assert_allclose(g.abs().sum(1).double().numpy(), exp["g_rowabs"], rtol=5e-3, atol=1e-12)
