@@ -99,6 +99,42 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t,
  * last kd_loss_fwd_bwd (KD_ERR_LABEL_RANGE), else KD_OK. */
 int kd_loss_check(const void* workspace, void* stream);
 
+/* ------------------------------------------------------------------ GEMM ---- */
+/* C[M,N] = epilogue(alpha * sum_k A[m,k] B[n,k]), bf16 operands, fp32 accumulation
+ * (MFMA 16x16x32).  Replaces every torch.nn.functional.linear of the step (SigLIP,
+ * projector, Qwen2, lm_head: HF5 siglip :250-322, llava_onevision :131-150,
+ * qwen2 :35-140, llava_onevision :762) and their autograd dgrad / wgrad.
+ *  a_layout K_MAJOR : A[m][k] at A + m*lda + k        MN_MAJOR : A stored [k][m]
+ *  b_layout K_MAJOR : B[n][k] at B + n*ldb + k        MN_MAJOR : B stored [k][n]
+ * epilogue, in order: v = alpha*(*alpha_dev if set)*acc + bias[n]; aux[m][n] = v (bf16);
+ *   v = act(v); v += residual[m][n]; C = v or C += v (accumulate).
+ * Requirements: 16-B aligned A/B; ld % 8 == 0; K % 8 == 0 for K-major operands,
+ * rows % 8 == 0 for MN-major ones.  Any M/N/K otherwise (tails read as zeros). */
+typedef enum { KD_LAYOUT_K_MAJOR = 0, KD_LAYOUT_MN_MAJOR = 1 } kd_layout;
+typedef enum { KD_DTYPE_BF16 = 0, KD_DTYPE_F32 = 1 } kd_dtype;
+typedef enum { KD_ACT_NONE = 0, KD_ACT_GELU_TANH = 1, KD_ACT_GELU_ERF = 2, KD_ACT_SILU = 3 } kd_act;
+
+typedef struct {
+    int32_t M, N, K;
+    int32_t a_layout, b_layout;
+    const void* A; int64_t lda;
+    const void* B; int64_t ldb;
+    void* C; int64_t ldc;
+    int32_t c_dtype;          /* kd_dtype                                   */
+    int32_t accumulate;       /* 1: C += result                             */
+    float alpha;
+    const float* alpha_dev;   /* optional device scalar multiplied into alpha */
+    const void* bias;         /* optional [N]                               */
+    int32_t bias_dtype;       /* kd_dtype of bias                           */
+    int32_t act;              /* kd_act                                     */
+    const void* residual;     /* optional bf16 [M][N] added after act       */
+    int64_t ldr;
+    void* aux;                /* optional bf16 [M][N] pre-activation output */
+    int64_t ld_aux;
+} kd_gemm_desc;
+
+int kd_gemm(const kd_gemm_desc* desc, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,27 @@ class KdLossParams(C.Structure):
     ]
 
 
+# kd_layout / kd_dtype / kd_act
+KD_LAYOUT_K_MAJOR, KD_LAYOUT_MN_MAJOR = 0, 1
+KD_DTYPE_BF16, KD_DTYPE_F32 = 0, 1
+KD_ACT_NONE, KD_ACT_GELU_TANH, KD_ACT_GELU_ERF, KD_ACT_SILU = 0, 1, 2, 3
+
+
+class KdGemmDesc(C.Structure):
+    _fields_ = [
+        ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32),
+        ("a_layout", C.c_int32), ("b_layout", C.c_int32),
+        ("A", C.c_void_p), ("lda", C.c_int64),
+        ("B", C.c_void_p), ("ldb", C.c_int64),
+        ("C", C.c_void_p), ("ldc", C.c_int64),
+        ("c_dtype", C.c_int32), ("accumulate", C.c_int32),
+        ("alpha", C.c_float), ("alpha_dev", C.c_void_p),
+        ("bias", C.c_void_p), ("bias_dtype", C.c_int32), ("act", C.c_int32),
+        ("residual", C.c_void_p), ("ldr", C.c_int64),
+        ("aux", C.c_void_p), ("ld_aux", C.c_int64),
+    ]
+
+
 class KdError(RuntimeError):
     def __init__(self, fn: str, code: int, msg: str):
         super().__init__(f"{fn}: {STATUS_NAMES.get(code, code)}: {msg}")
@@ -56,6 +77,7 @@ SIGNATURES = {
     "kd_loss_fwd_bwd": (_i32, [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _i32, _i32, KdLossParams,
                                _vp, _vp, _i64, _vp, _sz, _vp]),
     "kd_loss_check": (_i32, [_vp, _vp]),
+    "kd_gemm": (_i32, [C.POINTER(KdGemmDesc), _vp]),
 }
 
 _lib = None

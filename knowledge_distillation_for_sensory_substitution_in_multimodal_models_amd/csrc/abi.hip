@@ -19,6 +19,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
                    void* dlogits, int64_t ld_d, void* ws, size_t ws_bytes, void* stream);
 size_t kd_loss_ws(int B, int L, int V);
 int kd_loss_check_impl(const void* ws, void* stream);
+int launch_gemm(const kd_gemm_desc* d, void* stream);
 
 }  // namespace kd
 
@@ -45,5 +46,7 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t, const voi
 }
 
 int kd_loss_check(const void* workspace, void* stream) { return kd::kd_loss_check_impl(workspace, stream); }
+
+int kd_gemm(const kd_gemm_desc* desc, void* stream) { return kd::launch_gemm(desc, stream); }
 
 }  // extern "C"

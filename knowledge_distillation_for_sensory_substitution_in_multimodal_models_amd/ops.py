@@ -5,6 +5,8 @@ FLOP runs in libkdstep.so.  There is no CPU or torch fallback for any op.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _native as N
@@ -80,3 +82,58 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
     if check:
         N.call("kd_loss_check", _ptr(ws), _stream())
     return loss, dl
+
+
+# --------------------------------------------------------------------- GEMM ----
+ACTS = {None: N.KD_ACT_NONE, "none": N.KD_ACT_NONE, "gelu_tanh": N.KD_ACT_GELU_TANH,
+        "gelu_erf": N.KD_ACT_GELU_ERF, "silu": N.KD_ACT_SILU}
+_DT = {torch.bfloat16: N.KD_DTYPE_BF16, torch.float32: N.KD_DTYPE_F32}
+
+
+def _operand(x: torch.Tensor, name: str):
+    """(ptr, ld, layout, rows, k) of a 2-D bf16 operand; MN-major if it is a transposed view."""
+    _require(x, torch.bfloat16, name)
+    if x.dim() != 2:
+        raise RuntimeError(f"{name}: expected 2-D")
+    r, k = x.shape
+    if x.stride(1) == 1 and (x.stride(0) >= k or r == 1):
+        return x.data_ptr(), max(x.stride(0), k), N.KD_LAYOUT_K_MAJOR
+    if x.stride(0) == 1 and (x.stride(1) >= r or k == 1):
+        return x.data_ptr(), max(x.stride(1), r), N.KD_LAYOUT_MN_MAJOR
+    raise RuntimeError(f"{name}: needs a unit stride in one dimension")
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
+         residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
+         out_dtype=torch.bfloat16) -> torch.Tensor:
+    """out[M, N] = epilogue(alpha * a[M, K] @ b[N, K]^T).
+
+    `a`/`b` may be K-contiguous tensors or transposed views (x.t() of a contiguous tensor):
+    the kernel reads either layout directly (no transpose copies).
+    """
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise RuntimeError(f"gemm: K mismatch {K} vs {K2}")
+    pa, lda, la = _operand(a, "gemm.a")
+    pb, ldb, lb = _operand(b, "gemm.b")
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    if out.stride(1) != 1:
+        raise RuntimeError("gemm: out must have a contiguous last dim")
+    d = N.KdGemmDesc()
+    d.M, d.N, d.K, d.a_layout, d.b_layout = M, N, K, la, lb
+    d.A, d.lda, d.B, d.ldb = pa, lda, pb, ldb
+    d.C, d.ldc, d.c_dtype, d.accumulate = out.data_ptr(), out.stride(0), _DT[out.dtype], int(accumulate)
+    d.alpha, d.alpha_dev = float(alpha), _ptr(alpha_dev)
+    if bias is not None:
+        d.bias, d.bias_dtype = bias.data_ptr(), _DT[bias.dtype]
+    d.act = ACTS[act]
+    if residual is not None:
+        _require(residual, torch.bfloat16, "gemm.residual")
+        d.residual, d.ldr = residual.data_ptr(), residual.stride(0)
+    if aux is not None:
+        _require(aux, torch.bfloat16, "gemm.aux")
+        d.aux, d.ld_aux = aux.data_ptr(), aux.stride(0)
+    N.call("kd_gemm", C.byref(d), _stream())
+    return out
