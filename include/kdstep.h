@@ -135,6 +135,81 @@ typedef struct {
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream);
 
+/* ------------------------------------------------------------- attention ---- */
+/* Fused flash attention (scores = q k^T * hd^-0.5, fp32 softmax), replacing the SDPA /
+ * eager attention transformers dispatches for Qwen2 (causal GQA, HF5 qwen2 :80-140) and
+ * SigLIP (non-causal MHA, HF5 siglip :250-307).
+ * q [B,H,S,hdp], k/v [B,HKV,S,hdp] bf16 with head dim zero-padded to hdp in {64,96,128};
+ * o [B,S,H,hd] bf16 (token-major), lse [B,H,S] fp32 (may be NULL in forward-only use). */
+typedef struct {
+    const void* q; const void* k; const void* v;
+    void* o; float* lse;
+    int32_t B, H, HKV, S, hd, hdp, causal;
+} kd_attn_desc;
+int kd_attn_fwd(const kd_attn_desc* desc, void* stream);
+
+/* Backward: dO [B,S,H,hd]; delta workspace [B,H,S] fp32; dq fp32 [B,H,S,hdp] (scaled,
+ * overwritten); dk/dv bf16 [B,HKV,S,hdp]. */
+typedef struct {
+    const void* q; const void* k; const void* v; const void* o; const void* dO;
+    const float* lse; float* delta; float* dq; void* dk; void* dv;
+    int32_t B, H, HKV, S, hd, hdp, causal;
+} kd_attn_bwd_desc;
+int kd_attn_bwd(const kd_attn_bwd_desc* desc, void* stream);
+
+/* ------------------------------------------------------------ layer ops ---- */
+/* LayerNorm (rms = 0; nn.LayerNorm, SigLIP, HF5 siglip :325-357, :567) or RMSNorm
+ * (rms = 1; Qwen2RMSNorm, HF5 qwen2 :35-55) over rows of D (D % 8 == 0, D <= 4096).
+ * mean/rstd fp32 [R] saved for backward (mean unused for RMS, may be NULL). */
+int kd_norm_fwd(int rms, const void* x, int64_t ldx, const void* weight, const void* bias, void* y, int64_t ldy,
+                float* mean, float* rstd, int R, int D, float eps, void* stream);
+/* dx (bf16, or += when dx_accum) and fp32 dweight/dbias (+= when accum_w); D <= 2048. */
+size_t kd_norm_bwd_workspace_size(int R, int D);
+int kd_norm_bwd(int rms, const void* x, int64_t ldx, const void* weight, const void* dy, int64_t lddy,
+                const float* mean, const float* rstd, void* dx, int64_t lddx, int dx_accum,
+                float* dweight, float* dbias, int accum_w, void* workspace, size_t workspace_bytes,
+                int R, int D, void* stream);
+/* q/k/v split of a fused projection output qkv [B*S, (nq+2nkv)*hd] into padded head-major
+ * q/k/v (+ RoPE rotate_half with fp32 cos/sin tables [S, hd/2] when non-NULL; HF5 qwen2
+ * apply_rotary_pos_emb) and its transpose for the backward (dq fp32). */
+int kd_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, const float* cos_t, const float* sin_t,
+                 int B, int S, int nq, int nkv, int hd, int hdp, void* stream);
+int kd_qkv_merge(const float* dq, const void* dk, const void* dv, void* dqkv, int64_t ld, const float* cos_t,
+                 const float* sin_t, int B, int S, int nq, int nkv, int hd, int hdp, void* stream);
+/* SwiGLU of Qwen2MLP: h = silu(gate) * up with gu = [gate | up] (width 2I). */
+int kd_swiglu_fwd(const void* gu, int64_t ldg, void* h, int64_t ldh, int M, int I, void* stream);
+int kd_swiglu_bwd(const void* gu, int64_t ldg, const void* dh, int64_t ldh, void* dgu, int64_t ldd, int M, int I,
+                  void* stream);
+/* dx = dy * act'(pre) for kd_act (gelu_pytorch_tanh: SigLIP MLP; gelu: projector). */
+int kd_act_bwd(const void* pre, const void* dy, void* dx, int64_t n, int act, void* stream);
+/* SigLIP patch embedding as im2col: pixels [NI,3,img,img] (kd_dtype) -> [NI*(img/ps)^2, Kp]
+ * bf16 with k = c*ps*ps + kh*ps + kw, zero padded to Kp (HF5 siglip :116-186). */
+int kd_patchify(const void* pixels, int pixel_dtype, void* out, int NI, int img, int ps, int Kp, void* stream);
+/* inputs_embeds assembly = embed_tokens(ids) + masked_scatter of the packed image features
+ * (HF5 llava_onevision :280-343, :510-513).  src[t] >= 0: feature row; -1: image_newline;
+ * -2: token embedding.  err (device int) is OR-ed with 1 on an id outside [0, vocab). */
+int kd_embed_assemble(const int64_t* ids, const int32_t* src, const void* table, const void* feats,
+                      const void* newline, void* out, int M, int H, int vocab, int32_t* err, void* stream);
+int kd_embed_bwd(const int64_t* ids, const int32_t* src, const void* dout, float* dtable, void* dfeats,
+                 float* dnewline, int M, int H, void* stream);
+/* bias gradient: out[n] (+)= sum_m dy[m][n] (fp32). */
+int kd_colsum(const void* dy, int64_t ld, int M, int N, float* out, int accumulate, void* stream);
+/* hook feature pooling (DT:243-244): out[g][d] = mean_p x[g*P+p][d] (fp32), and its backward. */
+int kd_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float* out, void* stream);
+int kd_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, void* stream);
+/* NT-Xent (DT:246-248 + contrastive_loss DT:393-416): loss_out[0] = weight * loss,
+ * loss_out[1] = loss; dfs = d(weight*loss)/d(fs) * grad_scale (may be NULL). n <= 64. */
+int kd_ntxent(const float* fs, const float* ft, int n, int D, float tau, float weight, float* loss_out,
+              float* dfs, float grad_scale, void* stream);
+/* torch.optim.AdamW step (DT:198-201) on flat fp32 master params with a bf16 working copy;
+ * gscale (device, optional) multiplies the gradient first. */
+int kd_adamw(float* param, void* param_bf16, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+             float lr, float beta1, float beta2, float eps, float weight_decay, int step, const float* gscale,
+             void* stream);
+/* out[0] += sum x^2 (gradient norm). */
+int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
+int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,20 @@ class KdGemmDesc(C.Structure):
     ]
 
 
+class KdAttnDesc(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("k", C.c_void_p), ("v", C.c_void_p), ("o", C.c_void_p), ("lse", C.c_void_p),
+                ("B", C.c_int32), ("H", C.c_int32), ("HKV", C.c_int32), ("S", C.c_int32), ("hd", C.c_int32),
+                ("hdp", C.c_int32), ("causal", C.c_int32)]
+
+
+class KdAttnBwdDesc(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("k", C.c_void_p), ("v", C.c_void_p), ("o", C.c_void_p), ("dO", C.c_void_p),
+                ("lse", C.c_void_p), ("delta", C.c_void_p), ("dq", C.c_void_p), ("dk", C.c_void_p),
+                ("dv", C.c_void_p),
+                ("B", C.c_int32), ("H", C.c_int32), ("HKV", C.c_int32), ("S", C.c_int32), ("hd", C.c_int32),
+                ("hdp", C.c_int32), ("causal", C.c_int32)]
+
+
 class KdError(RuntimeError):
     def __init__(self, fn: str, code: int, msg: str):
         super().__init__(f"{fn}: {STATUS_NAMES.get(code, code)}: {msg}")
@@ -78,6 +92,27 @@ SIGNATURES = {
                                _vp, _vp, _i64, _vp, _sz, _vp]),
     "kd_loss_check": (_i32, [_vp, _vp]),
     "kd_gemm": (_i32, [C.POINTER(KdGemmDesc), _vp]),
+    "kd_attn_fwd": (_i32, [C.POINTER(KdAttnDesc), _vp]),
+    "kd_attn_bwd": (_i32, [C.POINTER(KdAttnBwdDesc), _vp]),
+    "kd_norm_fwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _f32, _vp]),
+    "kd_norm_bwd_workspace_size": (_sz, [_i32, _i32]),
+    "kd_norm_bwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _sz,
+                           _i32, _i32, _vp]),
+    "kd_qkv_split": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "kd_qkv_merge": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "kd_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _i32, _i32, _vp]),
+    "kd_swiglu_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _vp]),
+    "kd_act_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
+    "kd_patchify": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp]),
+    "kd_embed_assemble": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    "kd_embed_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
+    "kd_colsum": (_i32, [_vp, _i64, _i32, _i32, _vp, _i32, _vp]),
+    "kd_row_group_mean": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp]),
+    "kd_row_group_mean_bwd": (_i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp]),
+    "kd_ntxent": (_i32, [_vp, _vp, _i32, _i32, _f32, _f32, _vp, _vp, _f32, _vp]),
+    "kd_adamw": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
+    "kd_sumsq": (_i32, [_vp, _i64, _vp, _vp]),
+    "kd_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
 }
 
 _lib = None

@@ -20,6 +20,36 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
 size_t kd_loss_ws(int B, int L, int V);
 int kd_loss_check_impl(const void* ws, void* stream);
 int launch_gemm(const kd_gemm_desc* d, void* stream);
+int launch_attn_fwd(const kd_attn_desc* d, void* stream);
+int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream);
+int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy,
+                    float* mean, float* rstd, int R, int D, float eps, void* stream);
+size_t norm_bwd_ws(int R, int D);
+int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
+                    const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w,
+                    void* ws, size_t ws_bytes, int R, int D, void* stream);
+int launch_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, const float* cos_t, const float* sin_t,
+                     int B, int S, int nq, int nkv, int hd, int hdp, void* stream);
+int launch_qkv_merge(const float* dq, const void* dk, const void* dv, void* dqkv, int64_t ld, const float* cos_t,
+                     const float* sin_t, int B, int S, int nq, int nkv, int hd, int hdp, void* stream);
+int launch_swiglu_fwd(const void* gu, int64_t ldg, void* h, int64_t ldh, int M, int I, void* stream);
+int launch_swiglu_bwd(const void* gu, int64_t ldg, const void* dh, int64_t ldh, void* dgu, int64_t ldd, int M, int I,
+                      void* stream);
+int launch_act_bwd(const void* pre, const void* dy, void* dx, int64_t n, int act, void* stream);
+int launch_patchify(const void* px, int px_dtype, void* out, int NI, int img, int ps, int Kp, void* stream);
+int launch_embed_assemble(const int64_t* ids, const int* src, const void* table, const void* feats, const void* newline,
+                          void* out, int M, int H, int vocab, int* err, void* stream);
+int launch_embed_bwd(const int64_t* ids, const int* src, const void* dout, float* dtable, void* dfeats, float* dnewline,
+                     int M, int H, void* stream);
+int launch_colsum(const void* dy, int64_t ld, int M, int N, float* out, int accumulate, void* stream);
+int launch_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float* out, void* stream);
+int launch_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, void* stream);
+int launch_ntxent(const float* fs, const float* ft, int n, int D, float tau, float weight, float* loss_out, float* dfs,
+                  float grad_scale, void* stream);
+int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                 float eps, float wd, int step, const float* gscale, void* stream);
+int launch_sumsq(const float* x, int64_t n, float* out, void* stream);
+int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 
 }  // namespace kd
 
@@ -48,5 +78,63 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t, const voi
 int kd_loss_check(const void* workspace, void* stream) { return kd::kd_loss_check_impl(workspace, stream); }
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream) { return kd::launch_gemm(desc, stream); }
+int kd_attn_fwd(const kd_attn_desc* d, void* s) { return kd::launch_attn_fwd(d, s); }
+int kd_attn_bwd(const kd_attn_bwd_desc* d, void* s) { return kd::launch_attn_bwd(d, s); }
+int kd_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy, float* mean,
+                float* rstd, int R, int D, float eps, void* s) {
+    return kd::launch_norm_fwd(rms, x, ldx, w, b, y, ldy, mean, rstd, R, D, eps, s);
+}
+size_t kd_norm_bwd_workspace_size(int R, int D) { return kd::norm_bwd_ws(R, D); }
+int kd_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
+                const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w, void* ws,
+                size_t wsb, int R, int D, void* s) {
+    return kd::launch_norm_bwd(rms, x, ldx, w, dy, lddy, mean, rstd, dx, lddx, dx_accum, dw, db, accum_w, ws, wsb, R, D, s);
+}
+int kd_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, const float* c, const float* sn, int B, int S,
+                 int nq, int nkv, int hd, int hdp, void* s) {
+    return kd::launch_qkv_split(qkv, ld, q, k, v, c, sn, B, S, nq, nkv, hd, hdp, s);
+}
+int kd_qkv_merge(const float* dq, const void* dk, const void* dv, void* dqkv, int64_t ld, const float* c, const float* sn,
+                 int B, int S, int nq, int nkv, int hd, int hdp, void* s) {
+    return kd::launch_qkv_merge(dq, dk, dv, dqkv, ld, c, sn, B, S, nq, nkv, hd, hdp, s);
+}
+int kd_swiglu_fwd(const void* gu, int64_t ldg, void* h, int64_t ldh, int M, int I, void* s) {
+    return kd::launch_swiglu_fwd(gu, ldg, h, ldh, M, I, s);
+}
+int kd_swiglu_bwd(const void* gu, int64_t ldg, const void* dh, int64_t ldh, void* dgu, int64_t ldd, int M, int I, void* s) {
+    return kd::launch_swiglu_bwd(gu, ldg, dh, ldh, dgu, ldd, M, I, s);
+}
+int kd_act_bwd(const void* pre, const void* dy, void* dx, int64_t n, int act, void* s) {
+    return kd::launch_act_bwd(pre, dy, dx, n, act, s);
+}
+int kd_patchify(const void* px, int dt, void* out, int NI, int img, int ps, int Kp, void* s) {
+    return kd::launch_patchify(px, dt, out, NI, img, ps, Kp, s);
+}
+int kd_embed_assemble(const int64_t* ids, const int32_t* src, const void* table, const void* feats, const void* nl,
+                      void* out, int M, int H, int vocab, int32_t* err, void* s) {
+    return kd::launch_embed_assemble(ids, src, table, feats, nl, out, M, H, vocab, err, s);
+}
+int kd_embed_bwd(const int64_t* ids, const int32_t* src, const void* dout, float* dtable, void* dfeats, float* dnl, int M,
+                 int H, void* s) {
+    return kd::launch_embed_bwd(ids, src, dout, dtable, dfeats, dnl, M, H, s);
+}
+int kd_colsum(const void* dy, int64_t ld, int M, int N, float* out, int acc, void* s) {
+    return kd::launch_colsum(dy, ld, M, N, out, acc, s);
+}
+int kd_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float* out, void* s) {
+    return kd::launch_row_group_mean(x, ld, G, P, D, out, s);
+}
+int kd_row_group_mean_bwd(const float* dp, int G, int P, int D, void* dx, int64_t ld, void* s) {
+    return kd::launch_row_group_mean_bwd(dp, G, P, D, dx, ld, s);
+}
+int kd_ntxent(const float* fs, const float* ft, int n, int D, float tau, float w, float* lo, float* dfs, float gs, void* s) {
+    return kd::launch_ntxent(fs, ft, n, D, tau, w, lo, dfs, gs, s);
+}
+int kd_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+             float wd, int step, const float* gscale, void* s) {
+    return kd::launch_adamw(p, pb, g, m, v, n, lr, b1, b2, eps, wd, step, gscale, s);
+}
+int kd_sumsq(const float* x, int64_t n, float* out, void* s) { return kd::launch_sumsq(x, n, out, s); }
+int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* s) { return kd::launch_cast_f32_bf16(x, y, n, s); }
 
 }  // extern "C"

@@ -1,0 +1,767 @@
+// Memory-bound layer kernels of the KD step (vectorised 16-B bf16 access, fp32 math).
+//
+// Each replaces a PyTorch / transformers op reached from the reference's forward
+// (DT:206-271) or its autograd backward:
+//   layernorm_fwd/bwd   nn.LayerNorm eps 1e-6 (SigLIP layer_norm1/2, post_layernorm;
+//                       HF5 siglip :325-357, :567) + the post-LN hook's token mean (DT:243)
+//   rmsnorm_fwd/bwd     Qwen2RMSNorm eps 1e-6 (HF5 qwen2 :35-55)
+//   qkv_split / merge   q/k/v view+transpose + RoPE theta=1e6 rotate_half (HF5 qwen2 :60-140)
+//   swiglu_fwd/bwd      down(silu(gate) * up) (HF5 qwen2 Qwen2MLP)
+//   act_bwd             gelu_pytorch_tanh (SigLIP MLP) / gelu erf (projector) derivatives
+//   patchify            Conv2d(3,1152,14,stride 14) as im2col (HF5 siglip :116-186)
+//   embed_assemble/bwd  embed_tokens + masked_scatter of packed image features
+//                       (HF5 llava_onevision :280-343, :510-513)
+//   colsum              bias gradients
+//   row_group_mean      hook_out.mean(dim=1) (DT:243-244)
+//   ntxent_fwd_bwd      normalize + contrastive_loss (DT:246-248, :393-416)
+//   adamw               torch.optim.AdamW (DT:198-201) on flat fp32 master weights
+//   sumsq               gradient norm
+#include "common.h"
+
+namespace kd {
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ void load8(const bf16* p, float* f) {
+    bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+}
+__device__ __forceinline__ void store8(bf16* p, const float* f) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16)f[j];
+    *(bf16x8*)p = v;
+}
+
+// -------------------------------------------------------------- LayerNorm ----
+// one wave per row, D % 8 == 0, D <= 64 * 8 * 8
+template <bool RMS>
+__global__ void __launch_bounds__(NT) k_norm_fwd(const bf16* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
+                                                 const bf16* __restrict__ bias, bf16* __restrict__ y, int64_t ldy,
+                                                 float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                 int R, int D, float eps) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= R) return;
+    const bf16* xr = x + (int64_t)row * ldx;
+    float f[8][8];
+    const int nch = D / 8;
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int c = lane + it * 64;
+        if (c < nch) {
+            load8(xr + c * 8, f[it]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s += f[it][j]; ss += f[it][j] * f[it][j]; }
+        }
+    }
+    s = wave_sum(s);
+    float mean = RMS ? 0.f : s / D;
+    float var;
+    if (RMS) {
+        var = wave_sum(ss) / D;
+    } else {
+        // two-pass variance for accuracy
+        float v2 = 0.f;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int c = lane + it * 64;
+            if (c < nch)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { const float dd = f[it][j] - mean; v2 += dd * dd; }
+        }
+        var = wave_sum(v2) / D;
+    }
+    const float rstd = rsqrtf(var + eps);
+    bf16* yr = y + (int64_t)row * ldy;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int c = lane + it * 64;
+        if (c < nch) {
+            float wv[8], o[8];
+            load8(w + c * 8, wv);
+            if (!RMS) {
+                float bv[8];
+                load8(bias + c * 8, bv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = (f[it][j] - mean) * rstd * wv[j] + bv[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = f[it][j] * rstd * wv[j];
+            }
+            store8(yr + c * 8, o);
+        }
+    }
+    if (lane == 0) {
+        if (mean_out) mean_out[row] = mean;
+        if (rstd_out) rstd_out[row] = rstd;
+    }
+}
+
+// dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat))   (LayerNorm)
+// dx = rstd * (w*dy - xhat * mean(w*dy*xhat))                (RMSNorm, xhat = x*rstd)
+// dw/db partial sums over the rows a workgroup handles -> fp32 [gridDim.x, D].
+// One wave per row, two passes over the row (the second re-reads x/dy from L2).
+constexpr int BWD_IT = 4;  // D <= 64 lanes * 8 * BWD_IT = 2048
+template <bool RMS>
+__global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
+                                                 const bf16* __restrict__ dy, int64_t lddy,
+                                                 const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                 bf16* __restrict__ dx, int64_t lddx, int dx_accum,
+                                                 float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                 int R, int D, int rows_per_block) {
+    extern __shared__ __attribute__((aligned(16))) float sacc[];  // [2][D] per workgroup
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int nch = D / 8;
+    for (int i = threadIdx.x; i < 2 * D; i += NT) sacc[i] = 0.f;
+    __syncthreads();
+    float pw[BWD_IT][8], pb[BWD_IT][8];
+#pragma unroll
+    for (int it = 0; it < BWD_IT; ++it)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { pw[it][j] = 0.f; pb[it][j] = 0.f; }
+    const int r_begin = blockIdx.x * rows_per_block;
+    const int r_end = min(R, r_begin + rows_per_block);
+    for (int row = r_begin + wv; row < r_end; row += 4) {
+        const bf16* xr = x + (int64_t)row * ldx;
+        const bf16* gr = dy + (int64_t)row * lddy;
+        const float mean = RMS ? 0.f : mean_in[row], rstd = rstd_in[row];
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int it = 0; it < BWD_IT; ++it) {
+            const int c = lane + it * 64;
+            if (c < nch) {
+                float xv[8], dv[8], wv8[8];
+                load8(xr + c * 8, xv);
+                load8(gr + c * 8, dv);
+                load8(w + c * 8, wv8);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float xh = (xv[j] - mean) * rstd;
+                    const float g = dv[j] * wv8[j];
+                    a1 += g;
+                    a2 += g * xh;
+                    pw[it][j] += dv[j] * xh;
+                    pb[it][j] += dv[j];
+                }
+            }
+        }
+        a1 = wave_sum(a1) / D;
+        a2 = wave_sum(a2) / D;
+        bf16* dxr = dx + (int64_t)row * lddx;
+#pragma unroll
+        for (int it = 0; it < BWD_IT; ++it) {
+            const int c = lane + it * 64;
+            if (c < nch) {
+                float xv[8], dv[8], wv8[8], o[8];
+                load8(xr + c * 8, xv);
+                load8(gr + c * 8, dv);
+                load8(w + c * 8, wv8);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float xh = (xv[j] - mean) * rstd;
+                    o[j] = rstd * (dv[j] * wv8[j] - (RMS ? 0.f : a1) - xh * a2);
+                }
+                if (dx_accum) {
+                    float prev[8];
+                    load8(dxr + c * 8, prev);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o[j] += prev[j];
+                }
+                store8(dxr + c * 8, o);
+            }
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < BWD_IT; ++it) {
+        const int c = lane + it * 64;
+        if (c < nch)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                atomicAdd(&sacc[c * 8 + j], pw[it][j]);
+                atomicAdd(&sacc[D + c * 8 + j], pb[it][j]);
+            }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < D; i += NT) {
+        if (dw_part) dw_part[(int64_t)blockIdx.x * D + i] = sacc[i];
+        if (db_part) db_part[(int64_t)blockIdx.x * D + i] = sacc[D + i];
+    }
+}
+
+// out[d] (+)= sum_p part[p][d]
+__global__ void k_reduce_parts(const float* __restrict__ part, int P, int D, float* __restrict__ out, int accum) {
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= D) return;
+    float s = 0.f;
+    for (int p = 0; p < P; ++p) s += part[(int64_t)p * D + d];
+    out[d] = accum ? out[d] + s : s;
+}
+
+// ------------------------------------------------------------------ q/k/v ----
+// qkv [M = B*S, (nq + 2 nkv) * hd] -> q [B,nq,S,HDP], k/v [B,nkv,S,HDP] (zero pad),
+// with RoPE (rotate_half convention) on q and k when cos/sin tables are given.
+__global__ void k_qkv_split(const bf16* __restrict__ qkv, int64_t ld, bf16* __restrict__ q, bf16* __restrict__ k,
+                            bf16* __restrict__ v, const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                            int B, int S, int nq, int nkv, int hd, int hdp) {
+    // one thread per (token, head, pair i < hdp/2)
+    const int heads = nq + 2 * nkv;
+    const int half = hdp / 2, hh = hd / 2;
+    const int64_t total = (int64_t)B * S * heads * half;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx % half);
+        const int64_t th = idx / half;
+        const int head = (int)(th % heads);
+        const int64_t tok = th / heads;
+        const int s = (int)(tok % S), b = (int)(tok / S);
+        bf16* dst;
+        int hidx;
+        if (head < nq) { dst = q; hidx = head; }
+        else if (head < nq + nkv) { dst = k; hidx = head - nq; }
+        else { dst = v; hidx = head - nq - nkv; }
+        const int nh = head < nq ? nq : nkv;
+        bf16* drow = dst + (((int64_t)b * nh + hidx) * S + s) * hdp;
+        // element pair (i, i + hd/2) for i < hd/2; padding columns hd.. zeroed
+        if (i < hh) {
+            const bf16* srow = qkv + tok * ld + (int64_t)head * hd;
+            float x1 = (float)srow[i], x2 = (float)srow[i + hh];
+            if (cos_t && head < nq + nkv) {
+                const float c = cos_t[(int64_t)s * hh + i], sn = sin_t[(int64_t)s * hh + i];
+                const float y1 = x1 * c - x2 * sn, y2 = x2 * c + x1 * sn;
+                x1 = y1; x2 = y2;
+            }
+            drow[i] = (bf16)x1;
+            drow[i + hh] = (bf16)x2;
+        } else {
+            // zero the padding [hd, hdp): thread i in [hh, half) covers 2 columns
+            const int c0 = hd + 2 * (i - hh);
+            if (c0 < hdp) drow[c0] = (bf16)0.f;
+            if (c0 + 1 < hdp) drow[c0 + 1] = (bf16)0.f;
+        }
+    }
+}
+
+// inverse: dq (fp32, [B,nq,S,HDP]), dk/dv (bf16 [B,nkv,S,HDP]) -> dqkv [M, (nq+2nkv)*hd]
+__global__ void k_qkv_merge(const float* __restrict__ dq, const bf16* __restrict__ dk, const bf16* __restrict__ dv,
+                            bf16* __restrict__ dqkv, int64_t ld, const float* __restrict__ cos_t,
+                            const float* __restrict__ sin_t, int B, int S, int nq, int nkv, int hd, int hdp) {
+    const int heads = nq + 2 * nkv, hh = hd / 2;
+    const int64_t total = (int64_t)B * S * heads * hh;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx % hh);
+        const int64_t th = idx / hh;
+        const int head = (int)(th % heads);
+        const int64_t tok = th / heads;
+        const int s = (int)(tok % S), b = (int)(tok / S);
+        float g1, g2;
+        if (head < nq) {
+            const float* r = dq + (((int64_t)b * nq + head) * S + s) * hdp;
+            g1 = r[i]; g2 = r[i + hh];
+        } else {
+            const bool isk = head < nq + nkv;
+            const int hidx = isk ? head - nq : head - nq - nkv;
+            const bf16* r = (isk ? dk : dv) + (((int64_t)b * nkv + hidx) * S + s) * hdp;
+            g1 = (float)r[i]; g2 = (float)r[i + hh];
+        }
+        if (cos_t && head < nq + nkv) {  // transpose of the rotation
+            const float c = cos_t[(int64_t)s * hh + i], sn = sin_t[(int64_t)s * hh + i];
+            const float y1 = g1 * c + g2 * sn, y2 = g2 * c - g1 * sn;
+            g1 = y1; g2 = y2;
+        }
+        bf16* d = dqkv + tok * ld + (int64_t)head * hd;
+        d[i] = (bf16)g1;
+        d[i + hh] = (bf16)g2;
+    }
+}
+
+// ------------------------------------------------------------------ SwiGLU ----
+// gu [M, 2I] = [gate | up] -> h [M, I] = silu(gate) * up
+__global__ void k_swiglu_fwd(const bf16* __restrict__ gu, int64_t ldg, bf16* __restrict__ h, int64_t ldh, int M, int I) {
+    const int n8 = I / 8;
+    const int64_t total = (int64_t)M * n8;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = idx / n8;
+        const int c = (int)(idx % n8) * 8;
+        float g[8], u[8], o[8];
+        load8(gu + m * ldg + c, g);
+        load8(gu + m * ldg + I + c, u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
+        store8(h + m * ldh + c, o);
+    }
+}
+
+__global__ void k_swiglu_bwd(const bf16* __restrict__ gu, int64_t ldg, const bf16* __restrict__ dh, int64_t ldh,
+                             bf16* __restrict__ dgu, int64_t ldd, int M, int I) {
+    const int n8 = I / 8;
+    const int64_t total = (int64_t)M * n8;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = idx / n8;
+        const int c = (int)(idx % n8) * 8;
+        float g[8], u[8], d[8], og[8], ou[8];
+        load8(gu + m * ldg + c, g);
+        load8(gu + m * ldg + I + c, u);
+        load8(dh + m * ldh + c, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float sg = 1.f / (1.f + __expf(-g[j]));
+            const float silu = g[j] * sg;
+            ou[j] = d[j] * silu;
+            og[j] = d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg));
+        }
+        store8(dgu + m * ldd + c, og);
+        store8(dgu + m * ldd + I + c, ou);
+    }
+}
+
+// dx = dy * act'(pre)
+__global__ void k_act_bwd(const bf16* __restrict__ pre, const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                          int64_t n, int act) {
+    const int64_t n8 = n / 8;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n8; idx += (int64_t)gridDim.x * blockDim.x) {
+        float x[8], d[8], o[8];
+        load8(pre + idx * 8, x);
+        load8(dy + idx * 8, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float dv;
+            if (act == KD_ACT_GELU_TANH) {
+                const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+                const float u = k0 * (x[j] + k1 * x[j] * x[j] * x[j]);
+                const float t = tanhf(u);
+                dv = 0.5f * (1.f + t) + 0.5f * x[j] * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x[j] * x[j]);
+            } else if (act == KD_ACT_GELU_ERF) {
+                const float cdf = 0.5f * (1.f + erff(x[j] * 0.7071067811865476f));
+                const float pdf = 0.3989422804014327f * __expf(-0.5f * x[j] * x[j]);
+                dv = cdf + x[j] * pdf;
+            } else {  // silu
+                const float sg = 1.f / (1.f + __expf(-x[j]));
+                dv = sg * (1.f + x[j] * (1.f - sg));
+            }
+            o[j] = d[j] * dv;
+        }
+        store8(dx + idx * 8, o);
+    }
+}
+
+// -------------------------------------------------------------- patchify ----
+// pixels [NI, 3, IMG, IMG] (fp32 or bf16) -> rows [NI * P*P, Kp] bf16, k = c*ps*ps + kh*ps + kw
+template <typename T>
+__global__ void k_patchify(const T* __restrict__ px, bf16* __restrict__ out, int NI, int img, int ps, int Kp) {
+    const int P = img / ps, K = 3 * ps * ps;
+    const int64_t rows = (int64_t)NI * P * P;
+    const int64_t total = rows * Kp;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(idx % Kp);
+        const int64_t r = idx / Kp;
+        float v = 0.f;
+        if (k < K) {
+            const int c = k / (ps * ps), kh = (k / ps) % ps, kw = k % ps;
+            const int pidx = (int)(r % (P * P));
+            const int64_t n = r / (P * P);
+            const int py = pidx / P, pxx = pidx % P;
+            v = (float)px[((n * 3 + c) * img + (int64_t)py * ps + kh) * img + (int64_t)pxx * ps + kw];
+        }
+        out[idx] = (bf16)v;
+    }
+}
+
+// --------------------------------------------------------- embed assemble ----
+// src[t] >= 0 : image feature row src[t]; -1 : image newline; -2 : token embedding of ids[t]
+__global__ void k_embed_assemble(const int64_t* __restrict__ ids, const int* __restrict__ src, const bf16* __restrict__ table,
+                                 const bf16* __restrict__ feats, const bf16* __restrict__ newline, bf16* __restrict__ out,
+                                 int M, int H, int vocab, int* __restrict__ err) {
+    const int t = blockIdx.x;
+    if (t >= M) return;
+    const int s = src[t];
+    const bf16* from;
+    if (s >= 0) from = feats + (int64_t)s * H;
+    else if (s == -1) from = newline;
+    else {
+        const int64_t id = ids[t];
+        if (id < 0 || id >= vocab) { if (threadIdx.x == 0) atomicOr(err, 1); return; }
+        from = table + id * H;
+    }
+    for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8) *(bf16x8*)(out + (int64_t)t * H + c) = *(const bf16x8*)(from + c);
+}
+
+__global__ void k_embed_bwd(const int64_t* __restrict__ ids, const int* __restrict__ src, const bf16* __restrict__ dout,
+                            float* __restrict__ dtable, bf16* __restrict__ dfeats, float* __restrict__ dnewline, int M, int H) {
+    const int t = blockIdx.x;
+    if (t >= M) return;
+    const int s = src[t];
+    const bf16* g = dout + (int64_t)t * H;
+    if (s >= 0) {
+        if (dfeats)
+            for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8)
+                *(bf16x8*)(dfeats + (int64_t)s * H + c) = *(const bf16x8*)(g + c);
+    } else if (s == -1) {
+        if (dnewline)
+            for (int c = threadIdx.x; c < H; c += blockDim.x) atomicAdd(dnewline + c, (float)g[c]);
+    } else if (dtable) {
+        float* row = dtable + ids[t] * H;
+        for (int c = threadIdx.x; c < H; c += blockDim.x) atomicAdd(row + c, (float)g[c]);
+    }
+}
+
+// ---------------------------------------------------------------- colsum ----
+// out[n] (+)= sum_m dy[m][n] ; grid.x over 256-column groups of 8 (2048 cols), grid.y row chunks
+__global__ void k_colsum(const bf16* __restrict__ dy, int64_t ld, int M, int N, float* __restrict__ out, int rows_per) {
+    const int c = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (c >= N) return;
+    const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = r0; r < r1; ++r) {
+        float f[8];
+        load8(dy + (int64_t)r * ld + c, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(out + c + j, s[j]);
+}
+
+// ------------------------------------------------------- row-group mean ----
+// out[g][d] = mean_{p < P} x[g*P + p][d] (fp32)
+__global__ void k_row_group_mean(const bf16* __restrict__ x, int64_t ld, int G, int P, int D, float* __restrict__ out) {
+    const int gi = blockIdx.y;
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= D || gi >= G) return;
+    float s = 0.f;
+    for (int p = 0; p < P; ++p) s += (float)x[((int64_t)gi * P + p) * ld + d];
+    out[(int64_t)gi * D + d] = s / P;
+}
+
+// dx[g*P+p][d] = dpool[g][d] / P (broadcast)
+__global__ void k_row_group_mean_bwd(const float* __restrict__ dpool, int G, int P, int D, bf16* __restrict__ dx, int64_t ld) {
+    const int64_t total = (int64_t)G * P * D;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int d = (int)(idx % D);
+        const int64_t r = idx / D;
+        const int g = (int)(r / P);
+        dx[r * ld + d] = (bf16)(dpool[(int64_t)g * D + d] / P);
+    }
+}
+
+// ---------------------------------------------------------------- NT-Xent ----
+// one workgroup; n <= 64 features of dim D.  fs/ft pooled (pre-normalisation) student /
+// teacher features.  DT:246-248 normalises once, contrastive_loss normalises again
+// (idempotent up to rounding; both applied).  loss = CE(S T^T / tau, arange).
+__global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, const float* __restrict__ ft, int n, int D,
+                                               float tau, float weight, float* __restrict__ loss_out,
+                                               float* __restrict__ dfs, float grad_scale) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // s_hat[n][D], t_hat[n][D], logits[n][n], norms
+    float* sh = sm;
+    float* th = sh + n * D;
+    float* lg = th + n * D;
+    float* nrm = lg + n * n;  // [4n]: |fs|, |s1|, |ft|, |t1|
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // norms (two normalisations, each x / max(|x|, 1e-12))
+    for (int r = w; r < 2 * n; r += 4) {
+        const float* src = r < n ? fs + (int64_t)r * D : ft + (int64_t)(r - n) * D;
+        float s2 = 0.f;
+        for (int d = lane; d < D; d += 64) s2 += src[d] * src[d];
+        s2 = wave_sum(s2);
+        const float n1 = fmaxf(sqrtf(s2), 1e-12f);
+        float s3 = 0.f;
+        for (int d = lane; d < D; d += 64) { const float y = src[d] / n1; s3 += y * y; }
+        s3 = wave_sum(s3);
+        const float n2 = fmaxf(sqrtf(s3), 1e-12f);
+        float* dst = r < n ? sh + r * D : th + (r - n) * D;
+        for (int d = lane; d < D; d += 64) dst[d] = src[d] / n1 / n2;
+        if (lane == 0) {
+            if (r < n) { nrm[r] = n1; nrm[n + r] = n2; }
+            else { nrm[2 * n + r - n] = n1; nrm[3 * n + r - n] = n2; }
+        }
+    }
+    __syncthreads();
+    for (int e = w; e < n * n; e += 4) {
+        const int i = e / n, j = e % n;
+        float s = 0.f;
+        for (int d = lane; d < D; d += 64) s += sh[i * D + d] * th[j * D + d];
+        s = wave_sum(s);
+        if (lane == 0) lg[e] = s / tau;
+    }
+    __syncthreads();
+    // softmax rows, loss, dlogits (in place: lg <- (softmax - onehot) / n * weight)
+    __shared__ float lrow[64];
+    if (tid < n) {
+        float m = -INFINITY;
+        for (int j = 0; j < n; ++j) m = fmaxf(m, lg[tid * n + j]);
+        float z = 0.f;
+        for (int j = 0; j < n; ++j) z += __expf(lg[tid * n + j] - m);
+        lrow[tid] = logf(z) + m - lg[tid * n + tid];
+        for (int j = 0; j < n; ++j) {
+            const float pj = __expf(lg[tid * n + j] - m) / z;
+            lg[tid * n + j] = (pj - (j == tid ? 1.f : 0.f)) / n * weight * grad_scale;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float L = 0.f;
+        for (int i = 0; i < n; ++i) L += lrow[i];
+        loss_out[0] = L / n * weight;
+        loss_out[1] = L / n;
+    }
+    if (!dfs) return;
+    // d s_hat_i = sum_j dlg_ij t_hat_j / tau ; then back through the two normalisations
+    for (int i = w; i < n; i += 4) {
+        // y = s_hat = u / n2, u = x / n1.  dL/du = (g - y (y.g)) / n2 ; dL/dx = (dL/du - u (u.dL/du)) / n1
+        float yg = 0.f;
+        for (int d = lane; d < D; d += 64) {
+            float g = 0.f;
+            for (int j = 0; j < n; ++j) g += lg[i * n + j] * th[j * D + d];
+            g /= tau;
+            dfs[(int64_t)i * D + d] = g;  // scratch
+            yg += g * sh[i * D + d];
+        }
+        yg = wave_sum(yg);
+        const float n1 = nrm[i], n2 = nrm[n + i];
+        float uq = 0.f;
+        for (int d = lane; d < D; d += 64) {
+            const float y = sh[i * D + d];
+            const float gu = (dfs[(int64_t)i * D + d] - y * yg) / n2;
+            dfs[(int64_t)i * D + d] = gu;
+            uq += gu * (y * n2);  // u = y * n2
+        }
+        uq = wave_sum(uq);
+        for (int d = lane; d < D; d += 64) {
+            const float u = sh[i * D + d] * n2;
+            dfs[(int64_t)i * D + d] = (dfs[(int64_t)i * D + d] - u * uq) / n1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- AdamW ----
+// torch.optim.AdamW semantics: p -= lr*wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+// p -= lr * (m / (1-b1^t)) / (sqrt(v / (1-b2^t)) + eps).  Master fp32, working copy bf16.
+__global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const float* __restrict__ g, float* __restrict__ m,
+                        float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                        float bc1, float bc2, const float* __restrict__ gscale) {
+    const float gs = gscale ? *gscale : 1.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i] * gs;
+        float pi = p[i] * (1.f - lr * wd);
+        const float mi = b1 * m[i] + (1.f - b1) * gi;
+        const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+        p[i] = pi;
+        pb[i] = (bf16)pi;
+    }
+}
+
+__global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) s += x[i] * x[i];
+    s = block_sum<4>(s, red);
+    if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+__global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16* __restrict__ y, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = (bf16)x[i];
+}
+
+inline int grid_for(int64_t work, int per_block = 256, int cap = 8192) {
+    int64_t g = (work + per_block - 1) / per_block;
+    return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers ----
+int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy,
+                    float* mean, float* rstd, int R, int D, float eps, void* stream) {
+    KD_CHECK_ARG(x && w && y && (rms || b), "norm_fwd: null pointer");
+    KD_CHECK_SHAPE(D % 8 == 0 && D <= 4096 && ldx % 8 == 0 && ldy % 8 == 0, "norm_fwd: D must be a multiple of 8, <= 4096");
+    const dim3 grid((R + 3) / 4);
+    if (rms) hipLaunchKernelGGL(k_norm_fwd<true>, grid, dim3(NT), 0, as_stream(stream), (const bf16*)x, ldx, (const bf16*)w,
+                                nullptr, (bf16*)y, ldy, mean, rstd, R, D, eps);
+    else hipLaunchKernelGGL(k_norm_fwd<false>, grid, dim3(NT), 0, as_stream(stream), (const bf16*)x, ldx, (const bf16*)w,
+                            (const bf16*)b, (bf16*)y, ldy, mean, rstd, R, D, eps);
+    KD_LAUNCH_CHECK("k_norm_fwd");
+    return KD_OK;
+}
+
+size_t norm_bwd_ws(int R, int D) {
+    const int nb = R < 512 ? (R + 3) / 4 : 128;
+    return (size_t)nb * D * 4 * 2;
+}
+
+int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
+                    const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w,
+                    void* ws, size_t ws_bytes, int R, int D, void* stream) {
+    KD_CHECK_ARG(x && w && dy && rstd && dx && (rms || mean), "norm_bwd: null pointer");
+    KD_CHECK_SHAPE(D % 8 == 0 && D <= 2048, "norm_bwd: D must be a multiple of 8, <= 2048");
+    const int nb = R < 512 ? (R + 3) / 4 : 128;
+    const int rows_per = (R + nb - 1) / nb;
+    if (ws_bytes < (size_t)nb * D * 8) return fail(KD_ERR_WORKSPACE, "norm_bwd: workspace");
+    float* dwp = (float*)ws;
+    float* dbp = dwp + (size_t)nb * D;
+    hipStream_t st = as_stream(stream);
+    const size_t smem = 2 * D * 4;
+    if (rms) hipLaunchKernelGGL(k_norm_bwd<true>, dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx, (const bf16*)w,
+                                (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,
+                                nullptr, R, D, rows_per);
+    else hipLaunchKernelGGL(k_norm_bwd<false>, dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx, (const bf16*)w,
+                            (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,
+                            db ? dbp : nullptr, R, D, rows_per);
+    KD_LAUNCH_CHECK("k_norm_bwd");
+    if (dw) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 255) / 256), dim3(256), 0, st, dwp, nb, D, dw, accum_w);
+    if (db) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 255) / 256), dim3(256), 0, st, dbp, nb, D, db, accum_w);
+    KD_LAUNCH_CHECK("k_reduce_parts");
+    return KD_OK;
+}
+
+int launch_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, const float* cos_t, const float* sin_t,
+                     int B, int S, int nq, int nkv, int hd, int hdp, void* stream) {
+    KD_CHECK_ARG(qkv && q && k && v, "qkv_split: null pointer");
+    KD_CHECK_SHAPE(hd % 2 == 0 && hdp >= hd && hdp % 2 == 0, "qkv_split: head dims");
+    const int64_t work = (int64_t)B * S * (nq + 2 * nkv) * (hdp / 2);
+    hipLaunchKernelGGL(k_qkv_split, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), (const bf16*)qkv, ld, (bf16*)q,
+                       (bf16*)k, (bf16*)v, cos_t, sin_t, B, S, nq, nkv, hd, hdp);
+    KD_LAUNCH_CHECK("k_qkv_split");
+    return KD_OK;
+}
+
+int launch_qkv_merge(const float* dq, const void* dk, const void* dv, void* dqkv, int64_t ld, const float* cos_t,
+                     const float* sin_t, int B, int S, int nq, int nkv, int hd, int hdp, void* stream) {
+    KD_CHECK_ARG(dq && dk && dv && dqkv, "qkv_merge: null pointer");
+    const int64_t work = (int64_t)B * S * (nq + 2 * nkv) * (hd / 2);
+    hipLaunchKernelGGL(k_qkv_merge, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), dq, (const bf16*)dk,
+                       (const bf16*)dv, (bf16*)dqkv, ld, cos_t, sin_t, B, S, nq, nkv, hd, hdp);
+    KD_LAUNCH_CHECK("k_qkv_merge");
+    return KD_OK;
+}
+
+int launch_swiglu_fwd(const void* gu, int64_t ldg, void* h, int64_t ldh, int M, int I, void* stream) {
+    KD_CHECK_ARG(gu && h, "swiglu_fwd: null pointer");
+    KD_CHECK_SHAPE(I % 8 == 0 && ldg % 8 == 0 && ldh % 8 == 0, "swiglu_fwd: I % 8");
+    hipLaunchKernelGGL(k_swiglu_fwd, dim3(grid_for((int64_t)M * I / 8)), dim3(256), 0, as_stream(stream), (const bf16*)gu,
+                       ldg, (bf16*)h, ldh, M, I);
+    KD_LAUNCH_CHECK("k_swiglu_fwd");
+    return KD_OK;
+}
+
+int launch_swiglu_bwd(const void* gu, int64_t ldg, const void* dh, int64_t ldh, void* dgu, int64_t ldd, int M, int I,
+                      void* stream) {
+    KD_CHECK_ARG(gu && dh && dgu, "swiglu_bwd: null pointer");
+    KD_CHECK_SHAPE(I % 8 == 0, "swiglu_bwd: I % 8");
+    hipLaunchKernelGGL(k_swiglu_bwd, dim3(grid_for((int64_t)M * I / 8)), dim3(256), 0, as_stream(stream), (const bf16*)gu,
+                       ldg, (const bf16*)dh, ldh, (bf16*)dgu, ldd, M, I);
+    KD_LAUNCH_CHECK("k_swiglu_bwd");
+    return KD_OK;
+}
+
+int launch_act_bwd(const void* pre, const void* dy, void* dx, int64_t n, int act, void* stream) {
+    KD_CHECK_ARG(pre && dy && dx, "act_bwd: null pointer");
+    KD_CHECK_SHAPE(n % 8 == 0, "act_bwd: n % 8");
+    KD_CHECK_ARG(act >= KD_ACT_GELU_TANH && act <= KD_ACT_SILU, "act_bwd: act");
+    hipLaunchKernelGGL(k_act_bwd, dim3(grid_for(n / 8)), dim3(256), 0, as_stream(stream), (const bf16*)pre,
+                       (const bf16*)dy, (bf16*)dx, n, act);
+    KD_LAUNCH_CHECK("k_act_bwd");
+    return KD_OK;
+}
+
+int launch_patchify(const void* px, int px_dtype, void* out, int NI, int img, int ps, int Kp, void* stream) {
+    KD_CHECK_ARG(px && out, "patchify: null pointer");
+    KD_CHECK_SHAPE(img % ps == 0 && Kp >= 3 * ps * ps, "patchify: shape");
+    const int64_t work = (int64_t)NI * (img / ps) * (img / ps) * Kp;
+    if (px_dtype == KD_DTYPE_F32)
+        hipLaunchKernelGGL(k_patchify<float>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), (const float*)px,
+                           (bf16*)out, NI, img, ps, Kp);
+    else
+        hipLaunchKernelGGL(k_patchify<bf16>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), (const bf16*)px,
+                           (bf16*)out, NI, img, ps, Kp);
+    KD_LAUNCH_CHECK("k_patchify");
+    return KD_OK;
+}
+
+int launch_embed_assemble(const int64_t* ids, const int* src, const void* table, const void* feats, const void* newline,
+                          void* out, int M, int H, int vocab, int* err, void* stream) {
+    KD_CHECK_ARG(ids && src && table && out && err, "embed_assemble: null pointer");
+    KD_CHECK_SHAPE(H % 8 == 0, "embed_assemble: H % 8");
+    hipLaunchKernelGGL(k_embed_assemble, dim3(M), dim3(128), 0, as_stream(stream), ids, src, (const bf16*)table,
+                       (const bf16*)feats, (const bf16*)newline, (bf16*)out, M, H, vocab, err);
+    KD_LAUNCH_CHECK("k_embed_assemble");
+    return KD_OK;
+}
+
+int launch_embed_bwd(const int64_t* ids, const int* src, const void* dout, float* dtable, void* dfeats, float* dnewline,
+                     int M, int H, void* stream) {
+    KD_CHECK_ARG(ids && src && dout, "embed_bwd: null pointer");
+    hipLaunchKernelGGL(k_embed_bwd, dim3(M), dim3(128), 0, as_stream(stream), ids, src, (const bf16*)dout, dtable,
+                       (bf16*)dfeats, dnewline, M, H);
+    KD_LAUNCH_CHECK("k_embed_bwd");
+    return KD_OK;
+}
+
+int launch_colsum(const void* dy, int64_t ld, int M, int N, float* out, int accumulate, void* stream) {
+    KD_CHECK_ARG(dy && out, "colsum: null pointer");
+    KD_CHECK_SHAPE(N % 8 == 0 && ld % 8 == 0, "colsum: N % 8");
+    hipStream_t st = as_stream(stream);
+    if (!accumulate && hipMemsetAsync(out, 0, (size_t)N * 4, st) != hipSuccess) return fail(KD_ERR_LAUNCH, "colsum memset");
+    const int rows_per = 64;
+    dim3 grid((N / 8 + 255) / 256, (M + rows_per - 1) / rows_per);
+    hipLaunchKernelGGL(k_colsum, grid, dim3(256), 0, st, (const bf16*)dy, ld, M, N, out, rows_per);
+    KD_LAUNCH_CHECK("k_colsum");
+    return KD_OK;
+}
+
+int launch_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float* out, void* stream) {
+    KD_CHECK_ARG(x && out, "row_group_mean: null pointer");
+    hipLaunchKernelGGL(k_row_group_mean, dim3((D + 255) / 256, G), dim3(256), 0, as_stream(stream), (const bf16*)x, ld, G, P,
+                       D, out);
+    KD_LAUNCH_CHECK("k_row_group_mean");
+    return KD_OK;
+}
+
+int launch_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, void* stream) {
+    KD_CHECK_ARG(dpool && dx, "row_group_mean_bwd: null pointer");
+    hipLaunchKernelGGL(k_row_group_mean_bwd, dim3(grid_for((int64_t)G * P * D)), dim3(256), 0, as_stream(stream), dpool, G,
+                       P, D, (bf16*)dx, ld);
+    KD_LAUNCH_CHECK("k_row_group_mean_bwd");
+    return KD_OK;
+}
+
+int launch_ntxent(const float* fs, const float* ft, int n, int D, float tau, float weight, float* loss_out, float* dfs,
+                  float grad_scale, void* stream) {
+    KD_CHECK_ARG(fs && ft && loss_out, "ntxent: null pointer");
+    KD_CHECK_SHAPE(n >= 1 && n <= 64, "ntxent: 1 <= n <= 64");
+    const size_t smem = ((size_t)2 * n * D + n * n + 4 * n) * 4;
+    KD_CHECK_SHAPE(smem <= 160 * 1024, "ntxent: n * D too large for LDS");
+    hipLaunchKernelGGL(k_ntxent, dim3(1), dim3(NT), smem, as_stream(stream), fs, ft, n, D, tau, weight, loss_out, dfs,
+                       grad_scale);
+    KD_LAUNCH_CHECK("k_ntxent");
+    return KD_OK;
+}
+
+int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                 float eps, float wd, int step, const float* gscale, void* stream) {
+    KD_CHECK_ARG(p && pb && g && m && v && step >= 1, "adamw: bad argument");
+    const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+    hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 256, 16384)), dim3(256), 0, as_stream(stream), p, (bf16*)pb, g, m, v, n,
+                       lr, b1, b2, eps, wd, bc1, bc2, gscale);
+    KD_LAUNCH_CHECK("k_adamw");
+    return KD_OK;
+}
+
+int launch_sumsq(const float* x, int64_t n, float* out, void* stream) {
+    KD_CHECK_ARG(x && out, "sumsq: null pointer");
+    hipLaunchKernelGGL(k_sumsq, dim3(grid_for(n, 256, 2048)), dim3(256), 0, as_stream(stream), x, n, out);
+    KD_LAUNCH_CHECK("k_sumsq");
+    return KD_OK;
+}
+
+int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream) {
+    KD_CHECK_ARG(x && y, "cast: null pointer");
+    hipLaunchKernelGGL(k_cast_f32_bf16, dim3(grid_for(n, 256, 16384)), dim3(256), 0, as_stream(stream), x, (bf16*)y, n);
+    KD_LAUNCH_CHECK("k_cast_f32_bf16");
+    return KD_OK;
+}
+
+}  // namespace kd

@@ -9,7 +9,7 @@ import ctypes as C
 
 import torch
 
-from . import _native as N
+from . import _native as NV
 
 _WS: dict = {}
 
@@ -38,8 +38,8 @@ def _require(t: torch.Tensor, dtype, name: str):
 
 
 # ------------------------------------------------------------------ KD loss ----
-VARIANTS = {"none": N.KD_LOSS_NONE, "loca": N.KD_LOSS_LOCA, "kl": N.KD_LOSS_KL,
-            "kl_logtarget": N.KD_LOSS_KL_LOGTARGET}
+VARIANTS = {"none": NV.KD_LOSS_NONE, "loca": NV.KD_LOSS_LOCA, "kl": NV.KD_LOSS_KL,
+            "kl_logtarget": NV.KD_LOSS_KL_LOGTARGET}
 
 
 def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor | None,
@@ -66,28 +66,28 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
             raise RuntimeError("teacher_logits: rows must be uniformly strided")
         V_t, ld_t = teacher_logits.shape[2], teacher_logits.stride(1)
     else:
-        if v != N.KD_LOSS_NONE:
+        if v != NV.KD_LOSS_NONE:
             raise RuntimeError(f"kd_loss variant {variant} needs teacher logits")
         V_t, ld_t = 0, 0
     dev = student_logits.device
     loss = torch.empty(4, dtype=torch.float32, device=dev)
     dl = torch.empty((B, L, V_s), dtype=torch.bfloat16, device=dev) if want_grad else None
-    nbytes = N.lib().kd_loss_workspace_size(B, L, V_s)
+    nbytes = NV.lib().kd_loss_workspace_size(B, L, V_s)
     ws = _workspace("kd_loss", nbytes, dev)
-    prm = N.KdLossParams(v, float(temperature), float(alpha), float(kd_weight), float(ce_weight),
+    prm = NV.KdLossParams(v, float(temperature), float(alpha), float(kd_weight), float(ce_weight),
                          float(grad_scale), float(clamp_min), 1 if teacher_ce else 0)
-    N.call("kd_loss_fwd_bwd", _ptr(teacher_logits), ld_t, V_t, _ptr(student_logits),
+    NV.call("kd_loss_fwd_bwd", _ptr(teacher_logits), ld_t, V_t, _ptr(student_logits),
            student_logits.stride(1), V_s, _ptr(labels), B, L, prm, _ptr(loss), _ptr(dl),
            V_s, _ptr(ws), ws.numel(), _stream())
     if check:
-        N.call("kd_loss_check", _ptr(ws), _stream())
+        NV.call("kd_loss_check", _ptr(ws), _stream())
     return loss, dl
 
 
 # --------------------------------------------------------------------- GEMM ----
-ACTS = {None: N.KD_ACT_NONE, "none": N.KD_ACT_NONE, "gelu_tanh": N.KD_ACT_GELU_TANH,
-        "gelu_erf": N.KD_ACT_GELU_ERF, "silu": N.KD_ACT_SILU}
-_DT = {torch.bfloat16: N.KD_DTYPE_BF16, torch.float32: N.KD_DTYPE_F32}
+ACTS = {None: NV.KD_ACT_NONE, "none": NV.KD_ACT_NONE, "gelu_tanh": NV.KD_ACT_GELU_TANH,
+        "gelu_erf": NV.KD_ACT_GELU_ERF, "silu": NV.KD_ACT_SILU}
+_DT = {torch.bfloat16: NV.KD_DTYPE_BF16, torch.float32: NV.KD_DTYPE_F32}
 
 
 def _operand(x: torch.Tensor, name: str):
@@ -97,9 +97,9 @@ def _operand(x: torch.Tensor, name: str):
         raise RuntimeError(f"{name}: expected 2-D")
     r, k = x.shape
     if x.stride(1) == 1 and (x.stride(0) >= k or r == 1):
-        return x.data_ptr(), max(x.stride(0), k), N.KD_LAYOUT_K_MAJOR
+        return x.data_ptr(), max(x.stride(0), k), NV.KD_LAYOUT_K_MAJOR
     if x.stride(0) == 1 and (x.stride(1) >= r or k == 1):
-        return x.data_ptr(), max(x.stride(1), r), N.KD_LAYOUT_MN_MAJOR
+        return x.data_ptr(), max(x.stride(1), r), NV.KD_LAYOUT_MN_MAJOR
     raise RuntimeError(f"{name}: needs a unit stride in one dimension")
 
 
@@ -121,7 +121,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     if out.stride(1) != 1:
         raise RuntimeError("gemm: out must have a contiguous last dim")
-    d = N.KdGemmDesc()
+    d = NV.KdGemmDesc()
     d.M, d.N, d.K, d.a_layout, d.b_layout = M, N, K, la, lb
     d.A, d.lda, d.B, d.ldb = pa, lda, pb, ldb
     d.C, d.ldc, d.c_dtype, d.accumulate = out.data_ptr(), out.stride(0), _DT[out.dtype], int(accumulate)
@@ -135,5 +135,174 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     if aux is not None:
         _require(aux, torch.bfloat16, "gemm.aux")
         d.aux, d.ld_aux = aux.data_ptr(), aux.stride(0)
-    N.call("kd_gemm", C.byref(d), _stream())
+    NV.call("kd_gemm", C.byref(d), _stream())
     return out
+
+
+# ---------------------------------------------------------------- attention ----
+def attn_fwd(q, k, v, hd: int, causal: bool, want_lse: bool = True):
+    """q [B,H,S,hdp], k/v [B,HKV,S,hdp] bf16 -> (o [B,S,H,hd] bf16, lse [B,H,S] fp32 | None)."""
+    B, H, S, hdp = q.shape
+    HKV = k.shape[1]
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _require(t, torch.bfloat16, n)
+        if not t.is_contiguous():
+            raise RuntimeError(f"attn_fwd: {n} must be contiguous")
+    o = torch.empty((B, S, H, hd), dtype=torch.bfloat16, device=q.device)
+    lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device) if want_lse else None
+    d = NV.KdAttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), _ptr(lse), B, H, HKV, S, hd, hdp,
+                      int(causal))
+    NV.call("kd_attn_fwd", C.byref(d), _stream())
+    return o, lse
+
+
+def attn_bwd(q, k, v, o, do, lse, hd: int, causal: bool):
+    """Returns (dq fp32 [B,H,S,hdp] scaled, dk, dv bf16 [B,HKV,S,hdp])."""
+    B, H, S, hdp = q.shape
+    HKV = k.shape[1]
+    dev = q.device
+    do = do.contiguous()
+    delta = _workspace("attn_delta", B * H * S * 4, dev)
+    dq = torch.empty((B, H, S, hdp), dtype=torch.float32, device=dev)
+    dk = torch.empty_like(k)
+    dv = torch.empty_like(v)
+    d = NV.KdAttnBwdDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                         delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, HKV, S, hd, hdp,
+                         int(causal))
+    NV.call("kd_attn_bwd", C.byref(d), _stream())
+    return dq, dk, dv
+
+
+# -------------------------------------------------------------------- norms ----
+def norm_fwd(x, weight, bias=None, eps: float = 1e-6, rms: bool = False, out=None, save_stats: bool = True):
+    """LayerNorm (rms=False) / RMSNorm (rms=True) over the last dim of a 2-D bf16 tensor."""
+    R, D = x.shape
+    y = out if out is not None else torch.empty((R, D), dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty(R, dtype=torch.float32, device=x.device) if (save_stats and not rms) else None
+    rstd = torch.empty(R, dtype=torch.float32, device=x.device) if save_stats else None
+    NV.call("kd_norm_fwd", int(rms), x.data_ptr(), x.stride(0), weight.data_ptr(), _ptr(bias), y.data_ptr(),
+            y.stride(0), _ptr(mean), _ptr(rstd), R, D, float(eps), _stream())
+    return y, mean, rstd
+
+
+def norm_bwd(x, weight, dy, mean, rstd, dx=None, dx_accum: bool = False, dweight=None, dbias=None,
+             accum_w: bool = True, rms: bool = False):
+    R, D = x.shape
+    if dx is None:
+        dx = torch.empty((R, D), dtype=torch.bfloat16, device=x.device)
+    nb = NV.lib().kd_norm_bwd_workspace_size(R, D)
+    ws = _workspace("norm_bwd", nb, x.device)
+    NV.call("kd_norm_bwd", int(rms), x.data_ptr(), x.stride(0), weight.data_ptr(), dy.data_ptr(), dy.stride(0),
+            _ptr(mean), rstd.data_ptr(), dx.data_ptr(), dx.stride(0), int(dx_accum), _ptr(dweight), _ptr(dbias),
+            int(accum_w), ws.data_ptr(), ws.numel(), R, D, _stream())
+    return dx
+
+
+# -------------------------------------------------------------- q/k/v, mlp ----
+def qkv_split(qkv, B, S, nq, nkv, hd, hdp, cos=None, sin=None):
+    dev = qkv.device
+    q = torch.empty((B, nq, S, hdp), dtype=torch.bfloat16, device=dev)
+    k = torch.empty((B, nkv, S, hdp), dtype=torch.bfloat16, device=dev)
+    v = torch.empty((B, nkv, S, hdp), dtype=torch.bfloat16, device=dev)
+    NV.call("kd_qkv_split", qkv.data_ptr(), qkv.stride(0), q.data_ptr(), k.data_ptr(), v.data_ptr(), _ptr(cos),
+            _ptr(sin), B, S, nq, nkv, hd, hdp, _stream())
+    return q, k, v
+
+
+def qkv_merge(dq, dk, dv, B, S, nq, nkv, hd, hdp, cos=None, sin=None, out=None):
+    if out is None:
+        out = torch.empty((B * S, (nq + 2 * nkv) * hd), dtype=torch.bfloat16, device=dq.device)
+    NV.call("kd_qkv_merge", dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), out.data_ptr(), out.stride(0), _ptr(cos),
+            _ptr(sin), B, S, nq, nkv, hd, hdp, _stream())
+    return out
+
+
+def swiglu_fwd(gu, I: int, out=None):
+    M = gu.shape[0]
+    h = out if out is not None else torch.empty((M, I), dtype=torch.bfloat16, device=gu.device)
+    NV.call("kd_swiglu_fwd", gu.data_ptr(), gu.stride(0), h.data_ptr(), h.stride(0), M, I, _stream())
+    return h
+
+
+def swiglu_bwd(gu, dh, I: int, out=None):
+    M = gu.shape[0]
+    dgu = out if out is not None else torch.empty((M, 2 * I), dtype=torch.bfloat16, device=gu.device)
+    NV.call("kd_swiglu_bwd", gu.data_ptr(), gu.stride(0), dh.data_ptr(), dh.stride(0), dgu.data_ptr(), dgu.stride(0),
+            M, I, _stream())
+    return dgu
+
+
+def act_bwd(pre, dy, act: str, out=None):
+    dx = out if out is not None else torch.empty_like(dy)
+    NV.call("kd_act_bwd", pre.data_ptr(), dy.data_ptr(), dx.data_ptr(), dy.numel(), ACTS[act], _stream())
+    return dx
+
+
+def patchify(pixels, ps: int, kp: int):
+    """pixels [NI, 3, img, img] (fp32/bf16) -> [NI*(img/ps)^2, kp] bf16."""
+    NI, _, img, _ = pixels.shape
+    pixels = pixels.contiguous()
+    out = torch.empty((NI * (img // ps) ** 2, kp), dtype=torch.bfloat16, device=pixels.device)
+    NV.call("kd_patchify", pixels.data_ptr(), _DT[pixels.dtype], out.data_ptr(), NI, img, ps, kp, _stream())
+    return out
+
+
+def embed_assemble(ids, src, table, feats, newline, err):
+    M = ids.numel()
+    H = table.shape[1]
+    out = torch.empty((M, H), dtype=torch.bfloat16, device=ids.device)
+    NV.call("kd_embed_assemble", ids.data_ptr(), src.data_ptr(), table.data_ptr(), _ptr(feats), _ptr(newline),
+            out.data_ptr(), M, H, table.shape[0], err.data_ptr(), _stream())
+    return out
+
+
+def embed_bwd(ids, src, dout, dtable=None, dfeats=None, dnewline=None):
+    M, H = dout.shape
+    NV.call("kd_embed_bwd", ids.data_ptr(), src.data_ptr(), dout.data_ptr(), _ptr(dtable), _ptr(dfeats),
+            _ptr(dnewline), M, H, _stream())
+
+
+def colsum(dy, out, accumulate: bool = True):
+    M, Nn = dy.shape
+    NV.call("kd_colsum", dy.data_ptr(), dy.stride(0), M, Nn, out.data_ptr(), int(accumulate), _stream())
+    return out
+
+
+def row_group_mean(x, G: int, P: int):
+    D = x.shape[1]
+    out = torch.empty((G, D), dtype=torch.float32, device=x.device)
+    NV.call("kd_row_group_mean", x.data_ptr(), x.stride(0), G, P, D, out.data_ptr(), _stream())
+    return out
+
+
+def row_group_mean_bwd(dpool, P: int, out=None):
+    G, D = dpool.shape
+    if out is None:
+        out = torch.empty((G * P, D), dtype=torch.bfloat16, device=dpool.device)
+    NV.call("kd_row_group_mean_bwd", dpool.data_ptr(), G, P, D, out.data_ptr(), out.stride(0), _stream())
+    return out
+
+
+def ntxent(fs, ft, tau: float = 0.07, weight: float = 1.0, want_grad: bool = True, grad_scale: float = 1.0):
+    """fs/ft: pooled features [n, D] fp32.  Returns (loss2 [weighted, raw], dfs | None)."""
+    n, D = fs.shape
+    loss = torch.empty(2, dtype=torch.float32, device=fs.device)
+    dfs = torch.empty_like(fs) if want_grad else None
+    NV.call("kd_ntxent", fs.contiguous().data_ptr(), ft.contiguous().data_ptr(), n, D, float(tau), float(weight),
+            loss.data_ptr(), _ptr(dfs), float(grad_scale), _stream())
+    return loss, dfs
+
+
+def adamw(p, pb, g, m, v, lr, b1, b2, eps, wd, step, gscale=None):
+    NV.call("kd_adamw", p.data_ptr(), pb.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr),
+            float(b1), float(b2), float(eps), float(wd), int(step), _ptr(gscale), _stream())
+
+
+def sumsq(x, out):
+    NV.call("kd_sumsq", x.data_ptr(), x.numel(), out.data_ptr(), _stream())
+    return out
+
+
+def cast_f32_bf16(x, y):
+    NV.call("kd_cast_f32_bf16", x.data_ptr(), y.data_ptr(), x.numel(), _stream())
+    return y

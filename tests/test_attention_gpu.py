@@ -1,0 +1,84 @@
+"""Flash attention fwd/bwd (kd_attn_fwd / kd_attn_bwd) against a torch fp32 reference.
+
+Inputs are bf16; the reference runs in fp32 on the same bf16 values.  Tolerances:
+o (bf16 out, P rounded to bf16 in the kernel): |err| <= 2e-2 * rms(ref) + 1e-2 |ref|;
+lse 1e-4 relative; grads 3e-2 * rms(ref) + 3e-2 |ref| (bf16 dS / P operands).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
+    return ops
+
+
+def _ref(q, k, v, causal, hd):
+    # q [B,H,S,hd], k/v [B,HKV,S,hd] fp32
+    B, H, S, _ = q.shape
+    rep = H // k.shape[1]
+    kk = k.repeat_interleave(rep, 1)
+    vv = v.repeat_interleave(rep, 1)
+    s = q @ kk.transpose(-1, -2) / math.sqrt(hd)
+    if causal:
+        s = s.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool, device=q.device), 1), float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    o = torch.softmax(s, -1) @ vv
+    return o, lse
+
+
+def _close(got, ref, tol):
+    ref = ref.float()
+    err = (got.float() - ref).abs()
+    bound = tol * ref.pow(2).mean().sqrt() + tol * ref.abs()
+    assert bool((err <= bound).all()), f"max err {err.max().item():.3e}, rms ref {ref.pow(2).mean().sqrt().item():.3e}"
+
+
+CASES = [  # B, H, HKV, S, hd, hdp, causal
+    (2, 4, 2, 200, 64, 64, True),
+    (1, 14, 2, 256, 64, 64, True),        # student GQA 7:1
+    (1, 4, 1, 130, 128, 128, True),       # teacher head dim
+    (2, 2, 2, 729, 72, 96, False),        # SigLIP: seq 729, hd 72 padded to 96
+    (1, 3, 3, 100, 64, 64, False),
+]
+
+
+def _inputs(B, H, HKV, S, hd, hdp, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn(B, H, S, hd, generator=g)
+    k = torch.randn(B, HKV, S, hd, generator=g)
+    v = torch.randn(B, HKV, S, hd, generator=g)
+    pad = lambda t: torch.nn.functional.pad(t, (0, hdp - hd)).to(dev, torch.bfloat16).contiguous()
+    return pad(q), pad(k), pad(v)
+
+
+@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
+def test_attn_fwd(B, H, HKV, S, hd, hdp, causal, dev):
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev)
+    o, lse = ops.attn_fwd(q, k, v, hd, causal)
+    ro, rlse = _ref(q[..., :hd].float(), k[..., :hd].float(), v[..., :hd].float(), causal, hd)
+    _close(o, ro.permute(0, 2, 1, 3), 2e-2)
+    assert (lse - rlse).abs().max().item() < 1e-3 * rlse.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
+def test_attn_bwd(B, H, HKV, S, hd, hdp, causal, dev):
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=1)
+    o, lse = ops.attn_fwd(q, k, v, hd, causal)
+    g = torch.Generator().manual_seed(2)
+    do = torch.randn(B, S, H, hd, generator=g).to(dev, torch.bfloat16)
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, hd, causal)
+    qf = q[..., :hd].float().requires_grad_(True)
+    kf = k[..., :hd].float().requires_grad_(True)
+    vf = v[..., :hd].float().requires_grad_(True)
+    ro, _ = _ref(qf, kf, vf, causal, hd)
+    ro.permute(0, 2, 1, 3).backward(do.float())
+    _close(dq[..., :hd], qf.grad, 3e-2)
+    _close(dk[..., :hd], kf.grad, 3e-2)
+    _close(dv[..., :hd], vf.grad, 3e-2)

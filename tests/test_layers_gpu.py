@@ -1,0 +1,217 @@
+"""Layer kernels (include/kdstep.h layer ops) against torch fp32 references of the same ops."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
+    return ops
+
+
+def _r(*shape, seed=0, scale=1.0, dev="cuda"):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev, torch.bfloat16)
+
+
+def _close(got, ref, tol=1e-2):
+    ref = ref.float()
+    err = (got.float() - ref).abs()
+    bound = tol * ref.pow(2).mean().sqrt() + tol * ref.abs() + 1e-6
+    assert bool((err <= bound).all()), f"max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("rms,R,D", [(False, 300, 1152), (True, 257, 896), (True, 64, 3584), (False, 10, 64)])
+def test_norm_fwd_bwd(rms, R, D, dev):
+    ops = _ops()
+    x = _r(R, D, seed=1, dev=dev)
+    w = _r(D, seed=2, dev=dev)
+    b = None if rms else _r(D, seed=3, dev=dev)
+    y, mean, rstd = ops.norm_fwd(x, w, b, eps=1e-6, rms=rms)
+    xf = x.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    bf = None if rms else b.float().requires_grad_(True)
+    if rms:
+        ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * wf
+    else:
+        ref = F.layer_norm(xf, (D,), wf, bf, eps=1e-6)
+    _close(y, ref)
+    if D > 2048:
+        return
+    dy = _r(R, D, seed=4, dev=dev)
+    ref.backward(dy.float())
+    dw = torch.zeros(D, device=dev)
+    db = None if rms else torch.zeros(D, device=dev)
+    dx = ops.norm_bwd(x, w, dy, mean, rstd, dweight=dw, dbias=db, rms=rms)
+    _close(dx, xf.grad, 2e-2)
+    _close(dw, wf.grad, 1e-3)
+    if not rms:
+        _close(db, bf.grad, 1e-3)
+
+
+def _rope_tables(S, hd, theta=1e6):
+    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, dtype=torch.float32) / hd))
+    f = torch.arange(S, dtype=torch.float32)[:, None] * inv[None]
+    return f.cos(), f.sin()
+
+
+def test_qkv_split_rope_and_merge(dev):
+    ops = _ops()
+    B, S, nq, nkv, hd, hdp = 2, 33, 4, 2, 64, 64
+    qkv = _r(B * S, (nq + 2 * nkv) * hd, seed=5, dev=dev)
+    cos, sin = _rope_tables(S, hd)
+    cos_d, sin_d = cos.to(dev), sin.to(dev)
+    q, k, v = ops.qkv_split(qkv, B, S, nq, nkv, hd, hdp, cos_d, sin_d)
+    x = qkv.float().view(B, S, nq + 2 * nkv, hd).permute(0, 2, 1, 3)
+    cc = torch.cat([cos, cos], -1).to(dev)
+    ss = torch.cat([sin, sin], -1).to(dev)
+    rot = lambda t: torch.cat([-t[..., hd // 2:], t[..., :hd // 2]], -1)
+    xr = x * cc + rot(x) * ss
+    _close(q, xr[:, :nq])
+    _close(k, xr[:, nq:nq + nkv])
+    _close(v, x[:, nq + nkv:])
+    # merge is the transpose of split (incl. rotation): check <merge(g), x> == <g, split(x)>
+    dq = torch.randn(B, nq, S, hdp, device=dev)
+    dk = _r(B, nkv, S, hdp, seed=6, dev=dev)
+    dv = _r(B, nkv, S, hdp, seed=7, dev=dev)
+    dqkv = ops.qkv_merge(dq, dk, dv, B, S, nq, nkv, hd, hdp, cos_d, sin_d)
+    lhs = (dqkv.float() * qkv.float()).sum()
+    rhs = (dq * q.float()).sum() + (dk.float() * k.float()).sum() + (dv.float() * v.float()).sum()
+    assert abs(lhs.item() - rhs.item()) < 2e-2 * (abs(rhs.item()) + 10)
+
+
+def test_qkv_split_vit_padding(dev):
+    ops = _ops()
+    B, S, nh, hd, hdp = 2, 729, 16, 72, 96
+    qkv = _r(B * S, 3 * nh * hd, seed=8, dev=dev)
+    q, k, v = ops.qkv_split(qkv, B, S, nh, nh, hd, hdp)
+    x = qkv.float().view(B, S, 3 * nh, hd).permute(0, 2, 1, 3)
+    _close(q[..., :hd], x[:, :nh])
+    assert q[..., hd:].abs().max().item() == 0 and v[..., hd:].abs().max().item() == 0
+
+
+def test_swiglu_fwd_bwd(dev):
+    ops = _ops()
+    M, I = 130, 4864 // 4
+    gu = _r(M, 2 * I, seed=9, dev=dev)
+    h = ops.swiglu_fwd(gu, I)
+    g = gu.float()[:, :I].requires_grad_(True)
+    u = gu.float()[:, I:].requires_grad_(True)
+    ref = F.silu(g) * u
+    _close(h, ref)
+    dh = _r(M, I, seed=10, dev=dev)
+    ref.backward(dh.float())
+    dgu = ops.swiglu_bwd(gu, dh, I)
+    _close(dgu[:, :I], g.grad, 2e-2)
+    _close(dgu[:, I:], u.grad, 2e-2)
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "gelu_erf", "silu"])
+def test_act_bwd(act, dev):
+    ops = _ops()
+    pre = _r(64, 4304, seed=11, dev=dev)
+    dy = _r(64, 4304, seed=12, dev=dev)
+    x = pre.float().requires_grad_(True)
+    f = {"gelu_tanh": lambda t: F.gelu(t, approximate="tanh"), "gelu_erf": F.gelu, "silu": F.silu}[act]
+    f(x).backward(dy.float())
+    _close(ops.act_bwd(pre, dy, act), x.grad, 2e-2)
+
+
+def test_patchify_matches_conv(dev):
+    ops = _ops()
+    g = torch.Generator().manual_seed(13)
+    px = torch.rand(3, 3, 384, 384, generator=g).mul(2).sub(1).to(dev)
+    w = _r(64, 3, 14, 14, seed=14, scale=0.05, dev=dev)
+    rows = ops.patchify(px, 14, 592)
+    assert rows.shape == (3 * 729, 592)
+    wp = torch.zeros(64, 592, dtype=torch.bfloat16, device=dev)
+    wp[:, :588] = w.reshape(64, 588)
+    out = ops.gemm(rows, wp)
+    ref = F.conv2d(px.bfloat16().float(), w.float(), stride=14).flatten(2).transpose(1, 2).reshape(-1, 64)
+    _close(out, ref)
+
+
+def test_embed_assemble_and_bwd(dev):
+    ops = _ops()
+    V, H, M, NF = 500, 64, 40, 10
+    table = _r(V, H, seed=15, dev=dev)
+    feats = _r(NF, H, seed=16, dev=dev)
+    nl = _r(H, seed=17, dev=dev)
+    ids = torch.randint(0, V, (M,), generator=torch.Generator().manual_seed(18)).to(dev)
+    src = torch.full((M,), -2, dtype=torch.int32)
+    src[5:15] = torch.arange(10, dtype=torch.int32)
+    src[15] = -1
+    src[30] = -1
+    src = src.to(dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = ops.embed_assemble(ids, src, table, feats, nl, err)
+    ref = table[ids].clone()
+    ref[5:15] = feats
+    ref[15] = nl
+    ref[30] = nl
+    assert torch.equal(out, ref) and err.item() == 0
+    dout = _r(M, H, seed=19, dev=dev)
+    dtab = torch.zeros(V, H, device=dev)
+    dfe = torch.empty(NF, H, dtype=torch.bfloat16, device=dev)
+    dnl = torch.zeros(H, device=dev)
+    ops.embed_bwd(ids, src, dout, dtab, dfe, dnl)
+    rt = torch.zeros(V, H, device=dev)
+    text = (src == -2)
+    rt.index_add_(0, ids[text], dout.float()[text])
+    assert torch.allclose(dtab, rt, atol=1e-5)
+    assert torch.equal(dfe, dout[5:15])
+    assert torch.allclose(dnl, dout.float()[15] + dout.float()[30], atol=1e-5)
+
+
+def test_colsum_and_group_mean(dev):
+    ops = _ops()
+    dy = _r(1000, 1152, seed=20, dev=dev)
+    out = torch.ones(1152, device=dev)
+    ops.colsum(dy, out, accumulate=True)
+    assert torch.allclose(out, 1 + dy.float().sum(0), rtol=1e-4, atol=1e-3)
+    x = _r(4 * 729, 1152, seed=21, dev=dev)
+    pm = ops.row_group_mean(x, 4, 729)
+    assert torch.allclose(pm, x.float().view(4, 729, 1152).mean(1), atol=1e-5)
+    dx = ops.row_group_mean_bwd(pm, 729)
+    assert torch.allclose(dx.float().view(4, 729, 1152), pm[:, None].expand(4, 729, 1152) / 729, rtol=1e-2, atol=1e-8)
+
+
+def test_ntxent_matches_oracle(dev):
+    from oracle import kd_losses as O
+    ops = _ops()
+    g = torch.Generator().manual_seed(22)
+    fs = torch.randn(8, 1152, generator=g)
+    ft = torch.randn(8, 1152, generator=g) + 0.3 * fs
+    loss, dfs = ops.ntxent(fs.to(dev), ft.to(dev), weight=0.5)
+    x = fs.clone().requires_grad_(True)
+    ref = O.nt_xent(O.l2_normalize(x), O.l2_normalize(ft))
+    (0.5 * ref).backward()
+    assert abs(loss[1].item() - ref.item()) < 1e-5 * abs(ref.item()) + 1e-5
+    assert torch.allclose(dfs.cpu(), x.grad, rtol=1e-3, atol=1e-7)
+
+
+def test_adamw_matches_torch(dev):
+    ops = _ops()
+    n = 10000
+    g = torch.Generator().manual_seed(23)
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) for _ in range(3)]
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=0.01)
+    p = p0.clone().to(dev)
+    pb = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    for step, gr in enumerate(grads, 1):
+        ref.grad = gr.clone()
+        opt.step()
+        ops.adamw(p, pb, gr.to(dev), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+    assert torch.allclose(p.cpu(), ref.detach(), rtol=1e-6, atol=1e-7)
+    assert torch.equal(pb.cpu(), ref.detach().bfloat16())
+    out = torch.zeros(1, device=dev)
+    ops.sumsq(grads[0].to(dev), out)
+    assert abs(out.item() - grads[0].pow(2).sum().item()) < 1e-3 * grads[0].pow(2).sum().item()
