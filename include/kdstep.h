@@ -131,6 +131,7 @@ typedef struct {
     int64_t ldr;
     void* aux;                /* optional bf16 [M][N] pre-activation output */
     int64_t ld_aux;
+    int32_t residual_row_mod; /* >0: residual row index = m % residual_row_mod (SigLIP pos-emb) */
 } kd_gemm_desc;
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream);
@@ -190,13 +191,19 @@ int kd_patchify(const void* pixels, int pixel_dtype, void* out, int NI, int img,
  * -2: token embedding.  err (device int) is OR-ed with 1 on an id outside [0, vocab). */
 int kd_embed_assemble(const int64_t* ids, const int32_t* src, const void* table, const void* feats,
                       const void* newline, void* out, int M, int H, int vocab, int32_t* err, void* stream);
+/* Device-side index map for kd_embed_assemble: the j-th image token (id == image_token)
+ * of sample b reads map[b*map_ld + j] (feature row or -1 = newline), text tokens -2.
+ * err |= 2 when a sample's image-token count differs from map_len[b]. */
+int kd_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, const int32_t* map, int map_ld,
+                     const int32_t* map_len, int32_t* src, int32_t* err, void* stream);
 int kd_embed_bwd(const int64_t* ids, const int32_t* src, const void* dout, float* dtable, void* dfeats,
                  float* dnewline, int M, int H, void* stream);
 /* bias gradient: out[n] (+)= sum_m dy[m][n] (fp32). */
 int kd_colsum(const void* dy, int64_t ld, int M, int N, float* out, int accumulate, void* stream);
 /* hook feature pooling (DT:243-244): out[g][d] = mean_p x[g*P+p][d] (fp32), and its backward. */
 int kd_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float* out, void* stream);
-int kd_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, void* stream);
+int kd_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, const float* scale_dev,
+                          void* stream);
 /* NT-Xent (DT:246-248 + contrastive_loss DT:393-416): loss_out[0] = weight * loss,
  * loss_out[1] = loss; dfs = d(weight*loss)/d(fs) * grad_scale (may be NULL). n <= 64. */
 int kd_ntxent(const float* fs, const float* ft, int n, int D, float tau, float weight, float* loss_out,

@@ -57,6 +57,7 @@ class KdGemmDesc(C.Structure):
         ("bias", C.c_void_p), ("bias_dtype", C.c_int32), ("act", C.c_int32),
         ("residual", C.c_void_p), ("ldr", C.c_int64),
         ("aux", C.c_void_p), ("ld_aux", C.c_int64),
+        ("residual_row_mod", C.c_int32),
     ]
 
 
@@ -105,10 +106,11 @@ SIGNATURES = {
     "kd_act_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "kd_patchify": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp]),
     "kd_embed_assemble": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    "kd_image_src_map": (_i32, [_vp, _i32, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _vp]),
     "kd_embed_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
     "kd_colsum": (_i32, [_vp, _i64, _i32, _i32, _vp, _i32, _vp]),
     "kd_row_group_mean": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp]),
-    "kd_row_group_mean_bwd": (_i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp]),
+    "kd_row_group_mean_bwd": (_i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _vp]),
     "kd_ntxent": (_i32, [_vp, _vp, _i32, _i32, _f32, _f32, _vp, _vp, _f32, _vp]),
     "kd_adamw": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
     "kd_sumsq": (_i32, [_vp, _i64, _vp, _vp]),

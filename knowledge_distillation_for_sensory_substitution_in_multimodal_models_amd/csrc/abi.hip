@@ -43,12 +43,14 @@ int launch_embed_bwd(const int64_t* ids, const int* src, const void* dout, float
                      int M, int H, void* stream);
 int launch_colsum(const void* dy, int64_t ld, int M, int N, float* out, int accumulate, void* stream);
 int launch_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float* out, void* stream);
-int launch_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, void* stream);
+int launch_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, const float* sc, void* stream);
 int launch_ntxent(const float* fs, const float* ft, int n, int D, float tau, float weight, float* loss_out, float* dfs,
                   float grad_scale, void* stream);
 int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                  float eps, float wd, int step, const float* gscale, void* stream);
 int launch_sumsq(const float* x, int64_t n, float* out, void* stream);
+int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, const int* map, int map_ld,
+                         const int* map_len, int* src, int* err, void* stream);
 int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 
 }  // namespace kd
@@ -124,8 +126,8 @@ int kd_colsum(const void* dy, int64_t ld, int M, int N, float* out, int acc, voi
 int kd_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float* out, void* s) {
     return kd::launch_row_group_mean(x, ld, G, P, D, out, s);
 }
-int kd_row_group_mean_bwd(const float* dp, int G, int P, int D, void* dx, int64_t ld, void* s) {
-    return kd::launch_row_group_mean_bwd(dp, G, P, D, dx, ld, s);
+int kd_row_group_mean_bwd(const float* dp, int G, int P, int D, void* dx, int64_t ld, const float* sc, void* s) {
+    return kd::launch_row_group_mean_bwd(dp, G, P, D, dx, ld, sc, s);
 }
 int kd_ntxent(const float* fs, const float* ft, int n, int D, float tau, float w, float* lo, float* dfs, float gs, void* s) {
     return kd::launch_ntxent(fs, ft, n, D, tau, w, lo, dfs, gs, s);
@@ -135,6 +137,10 @@ int kd_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, 
     return kd::launch_adamw(p, pb, g, m, v, n, lr, b1, b2, eps, wd, step, gscale, s);
 }
 int kd_sumsq(const float* x, int64_t n, float* out, void* s) { return kd::launch_sumsq(x, n, out, s); }
+int kd_image_src_map(const int64_t* ids, int B, int L, int64_t tok, const int32_t* map, int ld, const int32_t* len,
+                     int32_t* src, int32_t* err, void* s) {
+    return kd::launch_image_src_map(ids, B, L, tok, map, ld, len, src, err, s);
+}
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* s) { return kd::launch_cast_f32_bf16(x, y, n, s); }
 
 }  // extern "C"

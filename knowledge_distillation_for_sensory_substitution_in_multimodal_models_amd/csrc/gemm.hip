@@ -37,7 +37,7 @@ struct GemmP {
     int64_t lda, ldb, ldc, ldr, ld_aux;
     int M, N, K;
     float alpha;
-    int c_f32, accumulate, bias_f32, act;
+    int c_f32, accumulate, bias_f32, act, res_mod;
 };
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
                 float v = acc[i][j][r] * alpha + bcol;
                 if (p.aux) p.aux[(int64_t)row * p.ld_aux + col] = (bf16)v;
                 v = apply_act(v, p.act);
-                if (p.resid) v += (float)p.resid[(int64_t)row * p.ldr + col];
+                if (p.resid) v += (float)p.resid[(int64_t)(p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col];
                 const int64_t o = (int64_t)row * p.ldc + col;
                 if (p.c_f32) {
                     float* c = (float*)p.C;
@@ -244,6 +244,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.M = d->M; p.N = d->N; p.K = d->K; p.alpha = d->alpha;
     p.c_f32 = d->c_dtype == KD_DTYPE_F32; p.accumulate = d->accumulate; p.bias_f32 = d->bias_dtype == KD_DTYPE_F32;
     p.act = d->act;
+    p.res_mod = d->residual_row_mod;
     const int tiles = ceil_div(d->M, BM) * ceil_div(d->N, BN);
     const size_t smem = 4 * TILE_BYTES;
     hipStream_t st = as_stream(stream_);

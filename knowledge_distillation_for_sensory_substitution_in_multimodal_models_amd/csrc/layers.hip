@@ -435,13 +435,15 @@ __global__ void k_row_group_mean(const bf16* __restrict__ x, int64_t ld, int G, 
 }
 
 // dx[g*P+p][d] = dpool[g][d] / P (broadcast)
-__global__ void k_row_group_mean_bwd(const float* __restrict__ dpool, int G, int P, int D, bf16* __restrict__ dx, int64_t ld) {
+__global__ void k_row_group_mean_bwd(const float* __restrict__ dpool, int G, int P, int D, bf16* __restrict__ dx, int64_t ld,
+                                     const float* __restrict__ scale_dev) {
+    const float sc = scale_dev ? *scale_dev : 1.f;
     const int64_t total = (int64_t)G * P * D;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
         const int d = (int)(idx % D);
         const int64_t r = idx / D;
         const int g = (int)(r / P);
-        dx[r * ld + d] = (bf16)(dpool[(int64_t)g * D + d] / P);
+        dx[r * ld + d] = (bf16)(dpool[(int64_t)g * D + d] * sc / P);
     }
 }
 
@@ -566,6 +568,43 @@ __global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16* __restrict__ 
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = (bf16)x[i];
 }
 
+// src[b*L + l] for inputs_embeds assembly: the j-th image token of sample b takes
+// map[b*map_ld + j] (a packed feature row, or -1 for image_newline); text tokens -2.
+// Counts that differ from map_len[b] flag err (HF raises "Image features and image tokens
+// do not match", HF5 llava_onevision :460-470).  One workgroup per sample.
+__global__ void __launch_bounds__(256) k_image_src_map(const int64_t* __restrict__ ids, int L, int64_t image_token,
+                                                       const int* __restrict__ map, int map_ld,
+                                                       const int* __restrict__ map_len, int* __restrict__ src,
+                                                       int* __restrict__ err) {
+    __shared__ int counts[256];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int per = (L + 255) / 256;
+    const int l0 = t * per, l1 = min(L, l0 + per);
+    int c = 0;
+    for (int l = l0; l < l1; ++l) c += (ids[(int64_t)b * L + l] == image_token);
+    counts[t] = c;
+    __syncthreads();
+    // inclusive scan (Hillis-Steele)
+    for (int o = 1; o < 256; o <<= 1) {
+        const int v = t >= o ? counts[t - o] : 0;
+        __syncthreads();
+        counts[t] += v;
+        __syncthreads();
+    }
+    int j = counts[t] - c;  // exclusive prefix
+    const int n = map_len[b];
+    for (int l = l0; l < l1; ++l) {
+        const int64_t id = ids[(int64_t)b * L + l];
+        int sv = -2;
+        if (id == image_token) {
+            sv = j < n ? map[(int64_t)b * map_ld + j] : -2;
+            ++j;
+        }
+        src[(int64_t)b * L + l] = sv;
+    }
+    if (t == 255 && counts[255] != n) atomicOr(err, 2);
+}
+
 inline int grid_for(int64_t work, int per_block = 256, int cap = 8192) {
     int64_t g = (work + per_block - 1) / per_block;
     return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -669,7 +708,7 @@ int launch_act_bwd(const void* pre, const void* dy, void* dx, int64_t n, int act
 
 int launch_patchify(const void* px, int px_dtype, void* out, int NI, int img, int ps, int Kp, void* stream) {
     KD_CHECK_ARG(px && out, "patchify: null pointer");
-    KD_CHECK_SHAPE(img % ps == 0 && Kp >= 3 * ps * ps, "patchify: shape");
+    KD_CHECK_SHAPE(img >= ps && Kp >= 3 * ps * ps, "patchify: shape");  // conv floors: 384/14 -> 27
     const int64_t work = (int64_t)NI * (img / ps) * (img / ps) * Kp;
     if (px_dtype == KD_DTYPE_F32)
         hipLaunchKernelGGL(k_patchify<float>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), (const float*)px,
@@ -720,10 +759,11 @@ int launch_row_group_mean(const void* x, int64_t ld, int G, int P, int D, float*
     return KD_OK;
 }
 
-int launch_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, void* stream) {
+int launch_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int64_t ld, const float* scale_dev,
+                              void* stream) {
     KD_CHECK_ARG(dpool && dx, "row_group_mean_bwd: null pointer");
     hipLaunchKernelGGL(k_row_group_mean_bwd, dim3(grid_for((int64_t)G * P * D)), dim3(256), 0, as_stream(stream), dpool, G,
-                       P, D, (bf16*)dx, ld);
+                       P, D, (bf16*)dx, ld, scale_dev);
     KD_LAUNCH_CHECK("k_row_group_mean_bwd");
     return KD_OK;
 }
@@ -747,6 +787,15 @@ int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t
     hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 256, 16384)), dim3(256), 0, as_stream(stream), p, (bf16*)pb, g, m, v, n,
                        lr, b1, b2, eps, wd, bc1, bc2, gscale);
     KD_LAUNCH_CHECK("k_adamw");
+    return KD_OK;
+}
+
+int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, const int* map, int map_ld,
+                         const int* map_len, int* src, int* err, void* stream) {
+    KD_CHECK_ARG(ids && map && map_len && src && err, "image_src_map: null pointer");
+    hipLaunchKernelGGL(k_image_src_map, dim3(B), dim3(256), 0, as_stream(stream), ids, L, image_token, map, map_ld,
+                       map_len, src, err);
+    KD_LAUNCH_CHECK("k_image_src_map");
     return KD_OK;
 }
 

@@ -1,0 +1,394 @@
+"""Drop-in KD LightningModules (the reference's L3 contract).
+
+  OnlineKnowledgeDistillationLLavaOneVision   double-trouble module, phases 1/2/3 (DT)
+  LogitBasedKD                                logit-based module, LoCa at T=1 (LB)
+  FeatureBasedKD                              feature-based module (FB)
+  LlavaOnevisionModule                        depth-student SFT baseline (BD)
+
+Same constructor arguments, attributes (`student_model`, `teacher_model`, `phase`, `T`,
+`gamma`, `soft_target_loss_weight`, `ce_loss_weight`, `learning_rate`), methods
+(`training_step`, `validation_step`, `configure_optimizers`, `forward`, the freeze
+helpers) and `self.log("train_loss" | "val_loss")` as the reference, and checkpoints
+with `student_model.*` / `teacher_model.*` keys in the transformers-4.45 layout.
+
+`training_step` returns a 0-d loss that requires grad; `loss.backward()` runs the
+student backward (hand-written kernels, explicit order) into flat fp32 gradient
+buffers, and the optimizer from `configure_optimizers()` is a fused AdamW over those
+buffers.  Data-parallel ranks all-reduce the trainable gradient range in buckets as the
+backward produces them (RCCL over xGMI), and the optimizer step of step t runs on a
+side stream so the teacher forward of step t+1 overlaps it.
+"""
+from __future__ import annotations
+
+import math
+import os
+import re
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .modeling import (STUDENT_05B, TEACHER_7B, LlavaOnevisionModel, tiny_config)
+
+try:  # the reference's base class when installed; otherwise a minimal stand-in
+    import pytorch_lightning as _pl  # noqa: F401
+    _Base = _pl.LightningModule
+except Exception:  # pragma: no cover - pytorch_lightning is not in this image
+    class _Base(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.logged = {}
+
+        def log(self, name, value, **kw):
+            self.logged[name] = value
+
+
+MODEL_CONFIGS = {
+    "llava-hf/llava-onevision-qwen2-0.5b-ov-hf": STUDENT_05B,
+    "llava-hf/llava-onevision-qwen2-7b-ov-hf": TEACHER_7B,
+    "tiny-student": tiny_config(teacher=False),
+    "tiny-teacher": tiny_config(teacher=True),
+}
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("the KD step runs on the MI355X HIP kernels only (no CPU path)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class _KDStepFn(torch.autograd.Function):
+    """Bridges Lightning's `loss.backward()` to the explicit student backward."""
+
+    @staticmethod
+    def forward(ctx, anchor, total, runner):
+        ctx.runner = runner
+        return total.clone()
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        ctx.runner._backward(grad_out.reshape(1).float().contiguous())
+        ctx.runner = None
+        return None, None, None
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW semantics (DT:198-201) as one kernel over the trainable range."""
+
+    def __init__(self, module, lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__([module._anchor], dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.module = module
+        self.step_count = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        m = self.module
+        g = self.param_groups[0]
+        self.step_count += 1
+        m._finish_grad_sync()
+        P = m.student_model.P
+        lo, hi = m._trainable_range()
+        if hi > lo:
+            side = m._opt_stream
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                ops.adamw(P.master[lo:hi], P.flat[lo:hi], P.grad[lo:hi], P.exp_avg[lo:hi], P.exp_avg_sq[lo:hi],
+                          g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count)
+                m._opt_done.record(side)
+            m._opt_pending = True
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        m = self.module
+        if m._opt_pending:   # the AdamW read the grads on the side stream
+            torch.cuda.current_stream().wait_event(m._opt_done)
+        lo, hi = m._trainable_range()
+        m.student_model.P.grad[lo:hi].zero_()
+
+
+class _KDBase(_Base):
+    # subclass hooks
+    uses_teacher = True
+
+    def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1,
+                 seed_teacher: int = 1, seed_student: int = 2, state_dict=None, world=None):
+        super().__init__()
+        self.phase = phase
+        self.learning_rate = learning_rate
+        self.processor = processor
+        self.model_name_student, self.model_name_teacher = model_name_student, model_name_teacher
+        dev = _device()
+        small = model_name_student.startswith("tiny")
+        self.student_model = LlavaOnevisionModel(MODEL_CONFIGS[model_name_student], dev, trainable=True,
+                                                 seed=seed_student, cpu_rng=small)
+        self.teacher_model = None
+        if self.uses_teacher:
+            self.teacher_model = LlavaOnevisionModel(MODEL_CONFIGS[model_name_teacher], dev, trainable=False,
+                                                     seed=seed_teacher, cpu_rng=small)
+        if state_dict is not None:
+            self.load_kd_state_dict(state_dict)
+        self.config = self.student_model.cfg
+        self._anchor = nn.Parameter(torch.zeros((), device=dev))
+        self._opt_stream = torch.cuda.Stream(device=dev)
+        self._opt_done = torch.cuda.Event()
+        self._opt_pending = False
+        self._ctx = None
+        self.last_terms = None
+        # data parallel
+        import torch.distributed as dist
+        self._dist = dist if (dist.is_available() and dist.is_initialized()) else None
+        self._works = []
+        self._sync_hi = None
+        self._bucket_bytes = 256 << 20
+        if self._dist is not None and self.uses_teacher:
+            # teacher weights broadcast once from rank 0, then read-only in every GPU's HBM
+            self._dist.broadcast(self.teacher_model.P.flat, src=0)
+        if self._dist is not None:
+            self._dist.broadcast(self.student_model.P.flat, src=0)
+            self.student_model.P.master.copy_(self.student_model.P.flat.float())
+
+    # ------------------------------------------------------------- freezing ----
+    def _trainable_range(self):
+        s = self.student_model
+        R = s.P.regions
+        parts = []
+        if s.train_vision:
+            parts.append(R["vision"])
+        if s.train_projector:
+            parts.append(R["projector"])
+        if s.train_language:
+            parts.append(R["language"])
+        if not parts:
+            return 0, 0
+        lo, hi = min(p[0] for p in parts), max(p[1] for p in parts)
+        if sum(p[1] - p[0] for p in parts) != hi - lo:
+            raise RuntimeError("trainable regions must be contiguous (vision|projector|language)")
+        return lo, hi
+
+    def freeze_student_language_layers(self):            # DT:468-483
+        self.student_model.train_language = False
+
+    def unfreeze_student_language_layers(self):          # DT:486-499
+        self.student_model.train_language = True
+
+    def freeze_student_vision_layers(self):              # DT:501-508
+        self.student_model.train_vision = False
+
+    def unfreeze_student_vision_layers(self):            # DT:516-523
+        self.student_model.train_vision = True
+
+    def setup(self, stage=None):                         # DT:88-91
+        pass
+
+    # --------------------------------------------------------------- losses ----
+    def _loss_spec(self):
+        """(kd variant, T, kd_weight, ce_weight, ntxent weight or None)."""
+        raise NotImplementedError
+
+    def configure_optimizers(self):                      # DT:198-201
+        opt = FusedAdamW(self, lr=self.learning_rate)
+        sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
+        return [opt], [sched]
+
+    # ------------------------------------------------------------- the step ----
+    def forward(self, batch, train: bool = False):
+        """The reference's forward(batch) (DT:206-271): total loss as a 0-d fp32 tensor."""
+        variant, T, kd_w, ce_w, ctr_w = self._loss_spec()
+        labels = batch["labels"]
+        image_sizes = batch["image_sizes"]
+        B, L = batch["depth_input_ids"].shape
+        need_feats = ctr_w is not None
+        t_logits = None
+        tfwd = None
+        if self.uses_teacher:
+            tfwd = self.teacher_model.forward(batch["rgb_input_ids"], batch["rgb_pixel_values"], image_sizes,
+                                              save=False, want_post_ln=need_feats)
+            t_logits = self.teacher_model.logits(tfwd["hn"])
+            del tfwd["hn"]
+        if self._opt_pending:  # the student weights of step t+1 need the AdamW of step t
+            torch.cuda.current_stream().wait_event(self._opt_done)
+            self._opt_pending = False
+        s = self.student_model
+        sfwd = s.forward(batch["depth_input_ids"], batch["depth_pixel_values"], image_sizes, save=train,
+                         want_post_ln=need_feats)
+        s_logits = s.logits(sfwd["hn"])
+        Vs = s_logits.shape[1]
+        loss4, dlogits = ops.kd_loss_fwd_bwd(
+            s_logits.view(B, L, Vs), None if t_logits is None else t_logits.view(B, L, -1), labels, variant,
+            temperature=T, alpha=0.8, kd_weight=kd_w, ce_weight=ce_w, want_grad=train)
+        del s_logits, t_logits
+        total = loss4[3]
+        dps = None
+        if need_feats:
+            NI = sfwd["post_ln"].shape[0] // s.cfg.vision.n_patches
+            ps = ops.row_group_mean(sfwd["post_ln"], NI, s.cfg.vision.n_patches)        # DT:243-244
+            pt = ops.row_group_mean(tfwd["post_ln"], NI, s.cfg.vision.n_patches)
+            ntx, dps = ops.ntxent(ps, pt, tau=0.07, weight=ctr_w, want_grad=train)      # DT:393-416
+            total = total + ntx[0]
+            self.last_ntxent = ntx
+        self.last_terms = loss4
+        if train:
+            self._ctx = dict(sfwd=sfwd, dlogits=dlogits, dps=dps)
+        return total
+
+    def _backward(self, gscale):
+        ctx, self._ctx = self._ctx, None
+        s = self.student_model
+        sf = ctx["sfwd"]
+        hn = sf["hn"]
+        W = s.lm_head_weight()
+        dl = ctx["dlogits"].view(hn.shape[0], -1)
+        dhn = ops.gemm(dl, W.t(), alpha_dev=gscale)                          # lm_head dgrad
+        if s.train_language:                                                  # lm_head / tied embed wgrad
+            ops.gemm(dl.t(), hn.t(), out=s.lm_head_grad(), accumulate=True, alpha_dev=gscale)
+        del dl, ctx["dlogits"]
+        dpost = None
+        if ctx["dps"] is not None and s.train_vision:
+            dpost = ops.row_group_mean_bwd(ctx["dps"], s.cfg.vision.n_patches, scale_dev=gscale)
+        s.backward(sf, dhn, dpost, on_layer_done=self._on_layer_done if self._dist else None)
+        self._launch_grad_sync(final=True)
+
+    # ------------------------------------------------------- data parallel ----
+    def _on_layer_done(self, i):
+        """Bucketed all-reduce of LM grads as soon as the backward has made them final.
+
+        Flat layout [vision | projector | embed, layers 0..N-1, norm(, lm_head)]; the backward
+        finishes the tail first (lm_head, norm), then layers N-1..0, then embed / projector /
+        vision.  Everything from layer i's first parameter to the current high-water mark is
+        final once layer i is done."""
+        s = self.student_model
+        if not s.train_language:
+            return
+        P = s.P
+        if self._sync_hi is None:
+            self._sync_hi = P.numel
+        first = P.offsets[f"language_model.model.layers.{i}.self_attn.q_proj.weight"][0]
+        if (self._sync_hi - first) * 4 >= self._bucket_bytes:
+            self._allreduce(first, self._sync_hi)
+            self._sync_hi = first
+
+    def _launch_grad_sync(self, final: bool):
+        if self._dist is None:
+            return
+        lo, hi = self._trainable_range()
+        top = hi if self._sync_hi is None else min(hi, self._sync_hi)
+        if top > lo:
+            self._allreduce(lo, top)
+        self._sync_hi = None
+
+    def _allreduce(self, lo, hi):
+        g = self.student_model.P.grad[lo:hi]
+        self._works.append(self._dist.all_reduce(g, op=self._dist.ReduceOp.AVG, async_op=True))
+
+    def _finish_grad_sync(self):
+        for w in self._works:
+            w.wait()
+        self._works = []
+
+    # ---------------------------------------------------------- Lightning API ----
+    def training_step(self, batch, batch_idx):           # DT:123-131
+        total = self.forward(batch, train=True)
+        loss = _KDStepFn.apply(self._anchor, total, self)
+        self.log("train_loss", loss, on_step=True, on_epoch=True, prog_bar=True, logger=True)
+        return loss
+
+    def validation_step(self, batch, batch_idx):         # DT:133-138
+        with torch.no_grad():
+            loss = self.forward(batch, train=False)
+        self.log("val_loss", loss, on_step=False, on_epoch=True, prog_bar=True, logger=True)
+        return loss
+
+    # ------------------------------------------------------------ checkpoints ----
+    def kd_state_dict(self):
+        sd = {f"student_model.{k}": v for k, v in self.student_model.P.state_dict().items()}
+        if self.teacher_model is not None:
+            sd.update({f"teacher_model.{k}": v for k, v in self.teacher_model.P.state_dict().items()})
+        return sd
+
+    def load_kd_state_dict(self, sd):
+        self.student_model.P.load_state_dict(sd, prefix="student_model.")
+        if self.teacher_model is not None and any(k.startswith("teacher_model.") for k in sd):
+            self.teacher_model.P.load_state_dict(sd, prefix="teacher_model.")
+
+    def save_checkpoint(self, path, epoch: int = 0, global_step: int = 0):
+        """Lightning-style .ckpt: {'state_dict': {student_model.*, teacher_model.*}, ...}."""
+        sd = {k: v.detach().cpu() for k, v in self.kd_state_dict().items()}
+        torch.save({"state_dict": sd, "epoch": epoch, "global_step": global_step,
+                    "pytorch-lightning_version": "2.4.0",
+                    "hyper_parameters": {"model_name_student": self.model_name_student,
+                                         "model_name_teacher": self.model_name_teacher,
+                                         "learning_rate": self.learning_rate, "phase": self.phase}}, path)
+
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, model_name_student=None, model_name_teacher=None, processor=None,
+                             map_location=None, **kw):
+        ck = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+        hp = ck.get("hyper_parameters", {})
+        return cls(model_name_student or hp["model_name_student"], model_name_teacher or hp["model_name_teacher"],
+                   processor, learning_rate=kw.pop("learning_rate", hp.get("learning_rate", 1e-5)),
+                   state_dict=ck["state_dict"], **{k: v for k, v in kw.items() if k in ("phase",)})
+
+
+class OnlineKnowledgeDistillationLLavaOneVision(_KDBase):
+    """Double-trouble KD module (DT): phase 1 vision loss, 2 LoCa, 3 combined."""
+
+    def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1, **kw):
+        super().__init__(model_name_student, model_name_teacher, processor, learning_rate, phase, **kw)
+        self.soft_target_loss_weight = 0.1   # DT:67-71
+        self.ce_loss_weight = 0.5
+        self.gamma = 0.8
+        self.T = 0.8
+
+    def _loss_spec(self):
+        if self.phase == 1:   # compute_vision_loss: 0.1 KL T^2 + 0.5 NT-Xent, no CE (DT:316-354)
+            return "kl", self.T, self.soft_target_loss_weight, 0.0, self.ce_loss_weight
+        if self.phase == 2:   # compute_loca_loss + CE (DT:253-254)
+            return "loca", self.T, 1.0, 1.0, None
+        if self.phase == 3:   # gamma (loca + CE) + (1-gamma) CE (DT:257-260)
+            return "loca", self.T, self.gamma, 1.0, None
+        raise ValueError(f"phase {self.phase}")
+
+
+class LogitBasedKD(_KDBase):
+    """Logit-based module (LB): compute_loca_loss at T=1 (LB:164-165, :208-261)."""
+
+    def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, **kw):
+        super().__init__(model_name_student, model_name_teacher, processor, learning_rate, phase=0, **kw)
+        self.soft_target_loss_weight = 0.5   # LB:73-75
+        self.ce_loss_weight = 0.5
+        self.T = 1.0
+
+    def _loss_spec(self):
+        return "loca", self.T, 1.0, 1.0, None
+
+
+class FeatureBasedKD(_KDBase):
+    """Feature-based module (FB): 0.1 KL(log_target quirk) T^2 + 0.8 CE + NT-Xent (FB:161-227)."""
+
+    def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=2e-5, **kw):
+        super().__init__(model_name_student, model_name_teacher, processor, learning_rate, phase=0, **kw)
+        self.soft_target_loss_weight = 0.1   # FB:72-74
+        self.ce_loss_weight = 0.8
+        self.T = 0.8
+
+    def _loss_spec(self):
+        return "kl_logtarget", self.T, self.soft_target_loss_weight, self.ce_loss_weight, 1.0
+
+    def configure_optimizers(self):        # FB:233-234 (no scheduler)
+        return FusedAdamW(self, lr=self.learning_rate)
+
+
+class LlavaOnevisionModule(_KDBase):
+    """Depth-student SFT baseline (BD:6-138): loss = the student's CE only."""
+    uses_teacher = False
+
+    def __init__(self, model_name, processor=None, learning_rate=2e-5, **kw):
+        super().__init__(model_name, None, processor, learning_rate, phase=0, **kw)
+        self.model = self.student_model
+
+    def _loss_spec(self):
+        return "none", 1.0, 0.0, 1.0, None
+
+    def configure_optimizers(self):        # BD:137-138
+        return FusedAdamW(self, lr=self.learning_rate)

@@ -105,7 +105,7 @@ def _operand(x: torch.Tensor, name: str):
 
 def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
          residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
-         out_dtype=torch.bfloat16) -> torch.Tensor:
+         out_dtype=torch.bfloat16, residual_row_mod: int = 0) -> torch.Tensor:
     """out[M, N] = epilogue(alpha * a[M, K] @ b[N, K]^T).
 
     `a`/`b` may be K-contiguous tensors or transposed views (x.t() of a contiguous tensor):
@@ -132,6 +132,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     if residual is not None:
         _require(residual, torch.bfloat16, "gemm.residual")
         d.residual, d.ldr = residual.data_ptr(), residual.stride(0)
+        d.residual_row_mod = int(residual_row_mod)
     if aux is not None:
         _require(aux, torch.bfloat16, "gemm.aux")
         d.aux, d.ld_aux = aux.data_ptr(), aux.stride(0)
@@ -275,11 +276,12 @@ def row_group_mean(x, G: int, P: int):
     return out
 
 
-def row_group_mean_bwd(dpool, P: int, out=None):
+def row_group_mean_bwd(dpool, P: int, out=None, scale_dev=None):
     G, D = dpool.shape
     if out is None:
         out = torch.empty((G * P, D), dtype=torch.bfloat16, device=dpool.device)
-    NV.call("kd_row_group_mean_bwd", dpool.data_ptr(), G, P, D, out.data_ptr(), out.stride(0), _stream())
+    NV.call("kd_row_group_mean_bwd", dpool.data_ptr(), G, P, D, out.data_ptr(), out.stride(0), _ptr(scale_dev),
+            _stream())
     return out
 
 
@@ -306,3 +308,12 @@ def sumsq(x, out):
 def cast_f32_bf16(x, y):
     NV.call("kd_cast_f32_bf16", x.data_ptr(), y.data_ptr(), x.numel(), _stream())
     return y
+
+
+def image_src_map(ids, image_token: int, maps, map_len, err):
+    """ids [B, L] int64 -> src int32 [B*L] (see include/kdstep.h kd_image_src_map)."""
+    B, L = ids.shape
+    src = torch.empty(B * L, dtype=torch.int32, device=ids.device)
+    NV.call("kd_image_src_map", ids.contiguous().data_ptr(), B, L, int(image_token), maps.data_ptr(), maps.shape[1],
+            map_len.data_ptr(), src.data_ptr(), err.data_ptr(), _stream())
+    return src

@@ -52,6 +52,17 @@ def _load(name, path):
     return m.OnlineKnowledgeDistillationLLavaOneVision
 
 
+BD_PATH = REF / "distillation/baseline_depth/LLavaOneVisionModule.py"
+
+
+def _load_bd():
+    spec = importlib.util.spec_from_file_location("ref_bd", BD_PATH)
+    m = importlib.util.module_from_spec(spec)
+    sys.modules["ref_bd"] = m
+    spec.loader.exec_module(m)
+    return m.LlavaOnevisionModule
+
+
 def _bare(cls, **attrs):
     obj = cls.__new__(cls)
     torch.nn.Module.__init__(obj)

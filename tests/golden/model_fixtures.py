@@ -1,0 +1,66 @@
+"""Shared helpers for the tiny end-to-end fixtures (tests/golden/model_*.npz)."""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+import torch
+
+HERE = Path(__file__).resolve().parent
+KINDS = {"lb": ("lb", 0), "dt1": ("dt", 1), "dt2": ("dt", 2), "dt3": ("dt", 3), "fb": ("fb", 0), "bd": ("bd", 0)}
+
+
+def load(name):
+    z = np.load(HERE / f"model_{name}.npz", allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    return meta, {k: z[k] for k in z.files if k != "meta"}
+
+
+def tiny_weights(teacher: bool, seed: int):
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import ParamStore, tiny_config
+    P = ParamStore(tiny_config(teacher), "cpu")
+    P.init_(seed, cpu_rng=True)
+    sd = {k: v.float().clone() for k, v in P.state_dict().items()}
+    if P.cfg.text.tie:   # one tensor for embed_tokens and the tied lm_head (as in transformers)
+        del sd["language_model.lm_head.weight"]
+    return sd
+
+
+def batch(meta, device="cpu"):
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    return synthetic_batch(meta["B"], device, L=meta["L"], seed=meta["seed_data"], pixel_dtype=torch.bfloat16,
+                           cpu_rng=True)
+
+
+def frozen(kind, phase):
+    """(vision, projector, language) trainable flags as the reference's train scripts set them."""
+    if kind == "dt" and phase == 1:
+        return True, True, False      # DT1T:105/111 freeze_student_language_layers
+    if kind == "dt" and phase == 2:
+        return False, True, True      # DT2T:106/112 freeze_student_vision_layers
+    return True, True, True
+
+
+def oracle_grads(name):
+    """Run the CPU oracle step for fixture `name`; returns (total, {param: grad})."""
+    from oracle.model import OracleLlava, kd_step_losses
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import tiny_config
+    meta, _ = load(name)
+    kind, phase = KINDS[name]
+    ssd = tiny_weights(False, meta["seed_s"])
+    tsd = tiny_weights(True, meta["seed_t"]) if kind != "bd" else None
+    tv, tp, tl = frozen(kind, phase)
+    for k, v in ssd.items():
+        train = (tl if k.startswith("language_model") else tp if (k.startswith("multi_modal") or k == "image_newline")
+                 else tv)
+        v.requires_grad_(train)
+    b = batch(meta)
+    for k in ("rgb_pixel_values", "depth_pixel_values"):
+        b[k] = b[k].float()
+    student = OracleLlava(ssd, tiny_config(False))
+    teacher = OracleLlava(tsd, tiny_config(True)) if tsd else None
+    total, _ = kd_step_losses(kind, teacher, student, b, phase=phase)
+    total.backward()
+    grads = {k: v.grad for k, v in ssd.items() if v.grad is not None and k != "language_model.lm_head.weight"}
+    return total.item(), grads
