@@ -14,6 +14,32 @@ from . import _native as NV
 _WS: dict = {}
 
 
+class KernelTimer:
+    """Optional HIP-event brackets around GEMM launches (bench.py roofline measurement).
+
+    Events are recorded on the stream the kernel is launched on (the current stream)."""
+
+    def __init__(self):
+        self.enabled = False
+        self.records = []   # (kind, flops, start_event, end_event)
+
+    def reset(self):
+        self.records = []
+
+    def summary(self, kind):
+        recs = [r for r in self.records if r[0] == kind]
+        if not recs:
+            return None
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for _, _, a, b in recs]
+        flops = sum(r[1] for r in recs)
+        return dict(launches=len(recs), total_ms=sum(ms), avg_ms=sum(ms) / len(ms), flops=flops,
+                    flops_per_launch=flops / len(recs))
+
+
+TIMER = KernelTimer()
+
+
 def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
@@ -136,7 +162,14 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     if aux is not None:
         _require(aux, torch.bfloat16, "gemm.aux")
         d.aux, d.ld_aux = aux.data_ptr(), aux.stride(0)
-    NV.call("kd_gemm", C.byref(d), _stream())
+    if TIMER.enabled:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        NV.call("kd_gemm", C.byref(d), _stream())
+        e1.record()
+        TIMER.records.append((f"gemm_{'kn'[la]}{'kn'[lb]}", 2.0 * M * N * K, e0, e1))
+    else:
+        NV.call("kd_gemm", C.byref(d), _stream())
     return out
 
 
