@@ -279,11 +279,17 @@ class _KDBase(_Base):
 
     def _allreduce(self, lo, hi):
         g = self.student_model.P.grad[lo:hi]
-        self._works.append(self._dist.all_reduce(g, op=self._dist.ReduceOp.AVG, async_op=True))
+        if self._dist.get_backend() == "nccl":   # RCCL: AVG in the collective
+            self._works.append((self._dist.all_reduce(g, op=self._dist.ReduceOp.AVG, async_op=True), None))
+        else:                                      # gloo (CPU tests): SUM, divided after the wait
+            self._works.append((self._dist.all_reduce(g, op=self._dist.ReduceOp.SUM, async_op=True), g))
 
     def _finish_grad_sync(self):
-        for w in self._works:
+        ws = self._dist.get_world_size() if self._dist is not None else 1
+        for w, g in self._works:
             w.wait()
+            if g is not None:
+                g.div_(ws)
         self._works = []
 
     # ---------------------------------------------------------- Lightning API ----
