@@ -141,6 +141,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timer", action="store_true", help="skip the per-GEMM HIP-event brackets")
+    ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
     a = ap.parse_args()
 
     import torch
@@ -198,6 +199,9 @@ def main():
             br[kind] = dict(launches=s["launches"], avg_us=round(s["avg_ms"] * 1e3, 2),
                             tflops=round(s["flops"] / (s["total_ms"] * 1e-3) / 1e12, 1),
                             share_of_step=round(s["total_ms"] * 1e-3 / dt, 3))
+    if a.shapes and rank == 0 and ops.TIMER.records:
+        with open(a.shapes, "w") as f:
+            json.dump(ops.TIMER.by_shape(top=200), f, indent=1)
     fwd = ops.TIMER.summary("gemm_kk")
     if fwd:
         ach = fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12

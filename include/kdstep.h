@@ -132,7 +132,16 @@ typedef struct {
     void* aux;                /* optional bf16 [M][N] pre-activation output */
     int64_t ld_aux;
     int32_t residual_row_mod; /* >0: residual row index = m % residual_row_mod (SigLIP pos-emb) */
+    int32_t variant;          /* 0 auto; 1 128x128 4-wave; 2/3/4 256x256 / 256x128 / 128x256 8-wave (tests) */
+    int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
+    void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
+    uint64_t workspace_bytes;
 } kd_gemm_desc;
+
+/* Bytes of workspace the auto (or forced) split-K plan for `desc` wants; 0 = no split.
+ * With split-K the K range is cut into S chunks, each an independent tile grid writing
+ * fp32 partials, and one reduce pass applies the epilogue above (deterministic). */
+size_t kd_gemm_workspace_size(const kd_gemm_desc* desc);
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream);
 
@@ -150,12 +159,16 @@ typedef struct {
 int kd_attn_fwd(const kd_attn_desc* desc, void* stream);
 
 /* Backward: dO [B,S,H,hd]; delta workspace [B,H,S] fp32; dq fp32 [B,H,S,hdp] (scaled,
- * overwritten); dk/dv bf16 [B,HKV,S,hdp]. */
+ * overwritten); dk/dv bf16 [B,HKV,S,hdp]. Two kernels (dK/dV per key block and query
+ * head; dQ per query block), no atomics. GQA (H > HKV) needs `workspace` of
+ * kd_attn_bwd_workspace_size() bytes for the per-query-head dK/dV partials. */
 typedef struct {
     const void* q; const void* k; const void* v; const void* o; const void* dO;
     const float* lse; float* delta; float* dq; void* dk; void* dv;
     int32_t B, H, HKV, S, hd, hdp, causal;
+    void* workspace; uint64_t workspace_bytes;
 } kd_attn_bwd_desc;
+size_t kd_attn_bwd_workspace_size(const kd_attn_bwd_desc* desc);
 int kd_attn_bwd(const kd_attn_bwd_desc* desc, void* stream);
 
 /* ------------------------------------------------------------ layer ops ---- */

@@ -58,6 +58,8 @@ class KdGemmDesc(C.Structure):
         ("residual", C.c_void_p), ("ldr", C.c_int64),
         ("aux", C.c_void_p), ("ld_aux", C.c_int64),
         ("residual_row_mod", C.c_int32),
+        ("variant", C.c_int32),
+        ("split_k", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64),
     ]
 
 
@@ -72,7 +74,7 @@ class KdAttnBwdDesc(C.Structure):
                 ("lse", C.c_void_p), ("delta", C.c_void_p), ("dq", C.c_void_p), ("dk", C.c_void_p),
                 ("dv", C.c_void_p),
                 ("B", C.c_int32), ("H", C.c_int32), ("HKV", C.c_int32), ("S", C.c_int32), ("hd", C.c_int32),
-                ("hdp", C.c_int32), ("causal", C.c_int32)]
+                ("hdp", C.c_int32), ("causal", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64)]
 
 
 class KdError(RuntimeError):
@@ -95,6 +97,8 @@ SIGNATURES = {
     "kd_gemm": (_i32, [C.POINTER(KdGemmDesc), _vp]),
     "kd_attn_fwd": (_i32, [C.POINTER(KdAttnDesc), _vp]),
     "kd_attn_bwd": (_i32, [C.POINTER(KdAttnBwdDesc), _vp]),
+    "kd_attn_bwd_workspace_size": (C.c_size_t, [C.POINTER(KdAttnBwdDesc)]),
+    "kd_gemm_workspace_size": (C.c_size_t, [C.POINTER(KdGemmDesc)]),
     "kd_norm_fwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _f32, _vp]),
     "kd_norm_bwd_workspace_size": (_sz, [_i32, _i32]),
     "kd_norm_bwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _sz,

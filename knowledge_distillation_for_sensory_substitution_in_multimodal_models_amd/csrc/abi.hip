@@ -20,8 +20,10 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
 size_t kd_loss_ws(int B, int L, int V);
 int kd_loss_check_impl(const void* ws, void* stream);
 int launch_gemm(const kd_gemm_desc* d, void* stream);
+size_t gemm_workspace_size(const kd_gemm_desc* d);
 int launch_attn_fwd(const kd_attn_desc* d, void* stream);
 int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream);
+size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d);
 int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy,
                     float* mean, float* rstd, int R, int D, float eps, void* stream);
 size_t norm_bwd_ws(int R, int D);
@@ -80,8 +82,10 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t, const voi
 int kd_loss_check(const void* workspace, void* stream) { return kd::kd_loss_check_impl(workspace, stream); }
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream) { return kd::launch_gemm(desc, stream); }
+size_t kd_gemm_workspace_size(const kd_gemm_desc* desc) { return kd::gemm_workspace_size(desc); }
 int kd_attn_fwd(const kd_attn_desc* d, void* s) { return kd::launch_attn_fwd(d, s); }
 int kd_attn_bwd(const kd_attn_bwd_desc* d, void* s) { return kd::launch_attn_bwd(d, s); }
+size_t kd_attn_bwd_workspace_size(const kd_attn_bwd_desc* d) { return kd::attn_bwd_workspace_size(d); }
 int kd_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy, float* mean,
                 float* rstd, int R, int D, float eps, void* s) {
     return kd::launch_norm_fwd(rms, x, ldx, w, b, y, ldy, mean, rstd, R, D, eps, s);

@@ -207,24 +207,40 @@ struct AttnBwdP {
     const bf16* q; const bf16* k; const bf16* v;   // [B, heads, S, HDP]
     const bf16* dO;                                  // [B, S, H, hd]
     const float* lse; const float* delta;           // [B, H, S]
-    float* dq;                                      // [B, H, S, HDP] fp32, pre-zeroed
+    float* dq;                                      // [B, H, S, HDP] fp32 (scaled)
     bf16* dk; bf16* dv;                             // [B, HKV, S, HDP]
+    float* dkp; float* dvp;                         // GQA partials [B, H, S, HDP] fp32 (grp > 1)
     int B, H, HKV, S, hd;
     float scale, scale_log2;
 };
 
-// stage 32 rows x HDP of a [S][row_stride] matrix (hd real columns) into an LDS image
-// [32][RB] swizzled with swK (register staging: 16-B loads, ds_write_b128)
+// 64 rows x ncols of a row-strided matrix (token-major dO) -> swK LDS image [64][RB];
+// columns >= ncols and rows >= S land as zeros (out-of-range buffer offsets)
 template <int HDP>
-__device__ __forceinline__ void stage_rows32(char* lds, const bf16* base, int64_t row_stride, int row0, int S,
-                                             int ncols, int tid) {
-    constexpr int RB = Geo<HDP>::RB, CH = RB / 16;
-    for (int i = tid; i < 32 * CH; i += 256) {
-        const int r = i / CH, c = i % CH;
-        bf16x8 val = (bf16x8){};
-        if (c * 8 < ncols && row0 + r < S) val = *(const bf16x8*)(base + (int64_t)(row0 + r) * row_stride + c * 8);
-        *(bf16x8*)(lds + r * RB + ((c ^ swK<RB>(r)) << 4)) = val;
+__device__ __forceinline__ void stage_rows_dma(char* lds, const bf16* base, int64_t row_stride, int ncols, int row0,
+                                               int S, int wid, int lane) {
+    constexpr int RB = Geo<HDP>::RB;
+    constexpr int ROWS_PER = 1024 / RB, CH = RB / 16, NINSTR = 64 / ROWS_PER;
+    const int rows_valid = min(64, S - row0);
+    const uint32_t bytes = rows_valid <= 0 ? 0u : (uint32_t)(((int64_t)(rows_valid - 1) * row_stride + ncols) * 2);
+    auto rs = rsrc(base + (int64_t)row0 * row_stride, bytes);
+#pragma unroll
+    for (int s = 0; s < NINSTR / 4; ++s) {
+        const int i = wid * (NINSTR / 4) + s;
+        const int r = i * ROWS_PER + lane / CH;
+        const int c = lane % CH;
+        const int gc = c ^ swK<RB>(r);
+        const uint32_t voff = (gc * 8 < ncols && r < rows_valid) ? (uint32_t)((r * row_stride + gc * 8) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(lds + i * 1024), 16, voff, 0, 0, 0);
     }
+}
+
+// 64 consecutive fp32 of a [S] row (lse / delta) -> LDS, one dword per lane (wave 0 only)
+__device__ __forceinline__ void stage_vec64(float* lds, const float* base, int row0, int S, int lane) {
+    const int rows_valid = min(64, S - row0);
+    auto rs = rsrc(base + row0, rows_valid <= 0 ? 0u : (uint32_t)(rows_valid * 4));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 4, lane < rows_valid ? (uint32_t)(lane * 4) : OOB,
+                                             0, 0, 0);
 }
 
 // transposed read from a swK-swizzled image (rows r, 4 consecutive cols starting at d)
@@ -235,28 +251,38 @@ __device__ __forceinline__ bf16x4 tr_read_k(const char* lds, int r, int d) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a);
 }
 
+__device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
+    bf16x8 r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+    return r;
+}
+
+// dK / dV for 64 keys of ONE query head (4 waves x 16 keys, key on the lane), looping
+// over 64-row query tiles double-buffered through LDS-DMA (Q, dO images + lse, delta):
+//   S = Q K^T, dP = dO V^T  (A = Q / dO rows from LDS, B = K / V fragments in registers)
+//   dV^T += dO^T P, dK^T += Q^T dS  (A = transposed LDS reads, B = P / dS registers)
+// MHA writes bf16 dK (scaled) / dV; GQA writes fp32 per-query-head partials that
+// k_attn_group_sum folds over the group (deterministic, no atomics).
 template <int HDP, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) k_attn_bwd(AttnBwdP p) {
+__global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
     constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* lK = smem;                    // [64 keys][RB]  (swK image)
-    char* lQ = lK + 64 * RB;            // [32 q][RB]
-    char* lO = lQ + 32 * RB;            // [32 q][RB]    dO
-    char* lS = lO + 32 * RB;            // [32 q][64 keys] bf16 dS, 128-B rows (swizzled)
-    float* lL = (float*)(lS + 32 * 128);  // lse*log2e [32], delta [32]
-    float* lD = lL + 32;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int TILE = 64 * RB, BUF = 2 * TILE + 512;
+    extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][Q TILE | dO TILE | lse2 64 | delta 64]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = lane >> 4, li = lane & 15;
     const int kb0 = blockIdx.x * 64;
-    const int kvh = blockIdx.y, b = blockIdx.z;
-    const int grp = p.H / p.HKV;
+    const int h = blockIdx.y, b = blockIdx.z;
+    const int grp = p.H / p.HKV, kvh = h / grp;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
+    const bf16* dO = p.dO + ((int64_t)b * p.S * p.H + h) * p.hd;   // row q at + q*H*hd
+    const float* LSE = p.lse + ((int64_t)b * p.H + h) * p.S;
+    const float* DEL = p.delta + ((int64_t)b * p.H + h) * p.S;
+    const int64_t ldo = (int64_t)p.H * p.hd;
     const int mykey = kb0 + wid * 16 + li;
 
-    // K image for the dQ product; K / V fragments (B operands) in registers
-    stage_rows32<HDP>(lK, K, HDP, kb0, p.S, HDP, tid);
-    stage_rows32<HDP>(lK + 32 * RB, K, HDP, kb0 + 32, p.S, HDP, tid);
     bf16x8 kf[KS], vf[KS];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
@@ -271,111 +297,212 @@ __global__ void __launch_bounds__(256, 1) k_attn_bwd(AttnBwdP p) {
 #pragma unroll
     for (int d = 0; d < DT; ++d) { dk[d] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
 
-    const int qt_first = CAUSAL ? (kb0 / 32) : 0;
-    const int nqt = (p.S + 31) / 32;
-    for (int hh = 0; hh < grp; ++hh) {
-        const int h = kvh * grp + hh;
-        const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
-        const bf16* dO = p.dO + ((int64_t)b * p.S * p.H + h) * p.hd;  // row q at + q*H*hd
-        const float* LSE = p.lse + ((int64_t)b * p.H + h) * p.S;
-        const float* DEL = p.delta + ((int64_t)b * p.H + h) * p.S;
-        float* dQ = p.dq + ((int64_t)(b * p.H + h) * p.S) * HDP;
-        for (int qt = qt_first; qt < nqt; ++qt) {
-            const int q0 = qt * 32;
-            __syncthreads();  // previous iteration done with lQ/lO/lS
-            stage_rows32<HDP>(lQ, Q, HDP, q0, p.S, HDP, tid);
-            stage_rows32<HDP>(lO, dO, (int64_t)p.H * p.hd, q0, p.S, p.hd, tid);
-            if (tid < 32) {
-                const int q = q0 + tid;
-                lL[tid] = q < p.S ? LSE[q] * 1.4426950408889634f : 0.f;
-                lD[tid] = q < p.S ? DEL[q] : 0.f;
-            }
-            __syncthreads();
-            // S = Q K^T, dP = dO V^T : rows q = 16qs + 4g + r, col = my key
-            f32x4 s[2], dp[2];
+    const int nqt = (p.S + 63) / 64;
+    const int qt0 = CAUSAL ? (int)blockIdx.x : 0;
+    auto stage = [&](char* buf, int qt) {
+        stage_kv<HDP, false>(buf, Q, qt * 64, p.S, wid, lane);
+        stage_rows_dma<HDP>(buf + TILE, dO, ldo, p.hd, qt * 64, p.S, wid, lane);
+        if (wid == 0) {
+            stage_vec64((float*)(buf + 2 * TILE), LSE, qt * 64, p.S, lane);
+            stage_vec64((float*)(buf + 2 * TILE + 256), DEL, qt * 64, p.S, lane);
+        }
+    };
+    stage(smem, qt0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int qt = qt0; qt < nqt; ++qt) {
+        const int cur = (qt - qt0) & 1;
+        if (qt + 1 < nqt) stage(smem + (cur ^ 1) * BUF, qt + 1);
+        const char* lQ = smem + cur * BUF;
+        const char* lO = lQ + TILE;
+        const float* lL = (const float*)(lQ + 2 * TILE);
+        const float* lD = lL + 64;
+        const int q0 = qt * 64;
+        // S, dP: rows q = q0 + 16qs + 4g + r, col = my key
+        f32x4 s[4], dp[4];
 #pragma unroll
-            for (int qs = 0; qs < 2; ++qs) {
-                s[qs] = (f32x4){0.f, 0.f, 0.f, 0.f};
-                dp[qs] = s[qs];
+        for (int qs = 0; qs < 4; ++qs) {
+            s[qs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            dp[qs] = s[qs];
 #pragma unroll
-                for (int kk = 0; kk < KS; ++kk) {
-                    s[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lQ, 16 * qs + li, kk * 4 + g), kf[kk], s[qs], 0, 0, 0);
-                    dp[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lO, 16 * qs + li, kk * 4 + g), vf[kk], dp[qs], 0, 0, 0);
-                }
+            for (int kk = 0; kk < KS; ++kk) {
+                s[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lQ, 16 * qs + li, kk * 4 + g), kf[kk], s[qs], 0, 0, 0);
+                dp[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lO, 16 * qs + li, kk * 4 + g), vf[kk], dp[qs], 0, 0, 0);
             }
+        }
+#pragma unroll
+        for (int qs = 0; qs < 4; ++qs)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ql = 16 * qs + 4 * g + r, q = q0 + ql;
+                float pv = exp2f(s[qs][r] * p.scale_log2 - lL[ql] * 1.4426950408889634f);
+                if (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q)) pv = 0.f;
+                s[qs][r] = pv;
+                dp[qs][r] = pv * (dp[qs][r] - lD[ql]);
+            }
+        // dV^T += dO^T P ; dK^T += Q^T dS over two 32-query steps
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
             bf16x8 pfr, dsf;
 #pragma unroll
-            for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int ql = 16 * qs + 4 * g + r, q = q0 + ql;
-                    float pv = exp2f(s[qs][r] * p.scale_log2 - lL[ql]);
-                    if (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q)) pv = 0.f;
-                    const float ds = pv * (dp[qs][r] - lD[ql]);
-                    pfr[qs * 4 + r] = (bf16)pv;
-                    dsf[qs * 4 + r] = (bf16)ds;
-                    // dS -> LDS [q][key] (128-B rows, chunk swizzle on q)
-                    const int key = wid * 16 + li;
-                    const int ch = key >> 3;
-                    *(bf16*)(lS + ql * 128 + (((ch ^ ((ql >> 1) & 7))) << 4) + (key & 7) * 2) = (bf16)ds;
-                }
-            // dV^T += dO^T P ; dK^T += Q^T dS   (A: transposed reads of the dO / Q images)
+            for (int r = 0; r < 4; ++r) {
+                pfr[r] = (bf16)s[2 * ks][r]; pfr[4 + r] = (bf16)s[2 * ks + 1][r];
+                dsf[r] = (bf16)dp[2 * ks][r]; dsf[4 + r] = (bf16)dp[2 * ks + 1][r];
+            }
+            const int qr = 32 * ks + 4 * g + (li >> 2);
 #pragma unroll
             for (int d = 0; d < DT; ++d) {
                 const int dc = d * 16 + 4 * (li & 3);
-                const int qr = 4 * g + (li >> 2);
-                bf16x4 a0 = tr_read_k<RB>(lO, qr, dc), a1 = tr_read_k<RB>(lO, qr + 16, dc);
-                bf16x8 af;
-                af[0] = a0[0]; af[1] = a0[1]; af[2] = a0[2]; af[3] = a0[3];
-                af[4] = a1[0]; af[5] = a1[1]; af[6] = a1[2]; af[7] = a1[3];
-                dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, pfr, dv[d], 0, 0, 0);
-                bf16x4 c0 = tr_read_k<RB>(lQ, qr, dc), c1 = tr_read_k<RB>(lQ, qr + 16, dc);
-                bf16x8 cf;
-                cf[0] = c0[0]; cf[1] = c0[1]; cf[2] = c0[2]; cf[3] = c0[3];
-                cf[4] = c1[0]; cf[5] = c1[1]; cf[6] = c1[2]; cf[7] = c1[3];
-                dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf, dsf, dk[d], 0, 0, 0);
+                dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(tr_read_k<RB>(lO, qr, dc), tr_read_k<RB>(lO, qr + 16, dc)),
+                                                               pfr, dv[d], 0, 0, 0);
+                dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(tr_read_k<RB>(lQ, qr, dc), tr_read_k<RB>(lQ, qr + 16, dc)),
+                                                               dsf, dk[d], 0, 0, 0);
             }
-            __syncthreads();
-            // dQ[32 q][hd] += dS[32][64] K[64][hd]: 2 x DT output tiles over 4 waves
-            for (int tix = wid; tix < 2 * DT; tix += 4) {
-                const int qs = tix / DT, d = tix % DT;
-                f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // lane owns key = mykey, d = 16d + 4g + r
+    if (mykey < p.S) {
+        if (grp == 1) {
+            bf16* dKr = p.dk + ((int64_t)(b * p.HKV + kvh) * p.S + mykey) * HDP;
+            bf16* dVr = p.dv + ((int64_t)(b * p.HKV + kvh) * p.S + mykey) * HDP;
 #pragma unroll
-                for (int ks = 0; ks < 2; ++ks) {
-                    const int qrow = 16 * qs + li;
-                    const int ch = ks * 4 + g;
-                    const bf16x8 af = *(const bf16x8*)(lS + qrow * 128 + ((ch ^ ((qrow >> 1) & 7)) << 4));
-                    const int kr = 32 * ks + 8 * g + (li >> 2);   // B[k = key][col = d]
-                    const int dc = d * 16 + 4 * (li & 3);
-                    bf16x4 b0 = tr_read_k<RB>(lK, kr, dc), b1 = tr_read_k<RB>(lK, kr + 4, dc);
-                    bf16x8 bf;
-                    bf[0] = b0[0]; bf[1] = b0[1]; bf[2] = b0[2]; bf[3] = b0[3];
-                    bf[4] = b1[0]; bf[5] = b1[1]; bf[6] = b1[2]; bf[7] = b1[3];
-                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
-                }
-                const int dcol = d * 16 + li;
-                if (dcol < p.hd) {
+            for (int d = 0; d < DT; ++d) {
+                const int dd = d * 16 + 4 * g;
+                bf16x4 wk, wv;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int q = q0 + 16 * qs + 4 * g + r;
-                        if (q < p.S) atomicAdd(dQ + (int64_t)q * HDP + dcol, acc[r] * p.scale);
-                    }
-                }
+                for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(dk[d][r] * p.scale); wv[r] = (bf16)dv[d][r]; }
+                *(bf16x4*)(dKr + dd) = wk;
+                *(bf16x4*)(dVr + dd) = wv;
+            }
+        } else {
+            float* dKr = p.dkp + ((int64_t)(b * p.H + h) * p.S + mykey) * HDP;
+            float* dVr = p.dvp + ((int64_t)(b * p.H + h) * p.S + mykey) * HDP;
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
+                const int dd = d * 16 + 4 * g;
+                *(f32x4*)(dKr + dd) = dk[d];
+                *(f32x4*)(dVr + dd) = dv[d];
             }
         }
     }
-    // write dK (scaled), dV: lane owns key = mykey, d = 16d + 4g + r
-    if (mykey < p.S) {
-        bf16* dKr = p.dk + ((int64_t)(b * p.HKV + kvh) * p.S + mykey) * HDP;
-        bf16* dVr = p.dv + ((int64_t)(b * p.HKV + kvh) * p.S + mykey) * HDP;
-#pragma unroll
-        for (int d = 0; d < DT; ++d) {
-            const int dd = d * 16 + 4 * g;
-            bf16x4 wk, wv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(dk[d][r] * p.scale); wv[r] = (bf16)dv[d][r]; }
-            if (dd < HDP) { *(bf16x4*)(dKr + dd) = wk; *(bf16x4*)(dVr + dd) = wv; }
+}
+
+// dK[b,kvh] = scale * sum_{h in group} dKp[b,h], dV likewise (d < 16*DT columns)
+__global__ void k_attn_group_sum(const float* __restrict__ dkp, const float* __restrict__ dvp, bf16* __restrict__ dk,
+                                 bf16* __restrict__ dv, int B, int H, int HKV, int S, int hdp, int dcols, float scale) {
+    const int grp = H / HKV, c4 = dcols / 4;
+    const int64_t total = (int64_t)B * HKV * S * c4;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(idx % c4) * 4;
+        const int64_t rs = idx / c4;               // (b, kvh, s)
+        const int s = (int)(rs % S);
+        const int64_t bk = rs / S;
+        const int kvh = (int)(bk % HKV), b = (int)(bk / HKV);
+        f32x4 ak = (f32x4){0.f, 0.f, 0.f, 0.f}, av = ak;
+        for (int j = 0; j < grp; ++j) {
+            const int64_t off = (((int64_t)b * H + kvh * grp + j) * S + s) * hdp + c;
+            ak += *(const f32x4*)(dkp + off);
+            av += *(const f32x4*)(dvp + off);
         }
+        bf16x4 wk, wv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(ak[r] * scale); wv[r] = (bf16)av[r]; }
+        *(bf16x4*)(dk + rs * hdp + c) = wk;
+        *(bf16x4*)(dv + rs * hdp + c) = wv;
+    }
+}
+
+// dQ for 64 query rows of one head (4 waves x 16 rows, query on the lane), the forward's
+// structure: K / V tiles double-buffered through LDS-DMA, S^T = K Q^T and dP^T = V dO^T
+// recomputed, dS^T in registers feeds dQ^T += K^T dS^T (A = transposed K reads).
+// No atomics: each workgroup owns its rows of dQ.
+template <int HDP, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
+    constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
+    constexpr int TILE = 64 * RB;
+    extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][K TILE | V TILE]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int g = lane >> 4, li = lane & 15;
+    const int nqb = (p.S + 63) / 64;
+    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+    const int h = blockIdx.y, b = blockIdx.z, kvh = h / (p.H / p.HKV);
+    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
+    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const int myq = qb * 64 + wid * 16 + li;
+    const bool qok = myq < p.S;
+
+    bf16x8 qf[KS], df[KS];
+    const bf16* dOr = p.dO + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+        const int d0 = kk * 32 + 8 * g;
+        qf[kk] = qok ? *(const bf16x8*)(Q + (int64_t)myq * HDP + d0) : (bf16x8){};
+        df[kk] = (qok && d0 < p.hd) ? *(const bf16x8*)(dOr + d0) : (bf16x8){};
+    }
+    const float lse2 = qok ? p.lse[((int64_t)b * p.H + h) * p.S + myq] * 1.4426950408889634f : 0.f;
+    const float dl = qok ? p.delta[((int64_t)b * p.H + h) * p.S + myq] : 0.f;
+    f32x4 acc[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) acc[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nkv = CAUSAL ? min(qb + 1, nqb) : nqb;
+    stage_kv<HDP, false>(smem, K, 0, p.S, wid, lane);
+    stage_kv<HDP, false>(smem + TILE, V, 0, p.S, wid, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nkv; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < nkv) {
+            char* nb = smem + (cur ^ 1) * 2 * TILE;
+            stage_kv<HDP, false>(nb, K, (t + 1) * 64, p.S, wid, lane);
+            stage_kv<HDP, false>(nb + TILE, V, (t + 1) * 64, p.S, wid, lane);
+        }
+        const char* lK = smem + cur * 2 * TILE;
+        const char* lV = lK + TILE;
+        // S^T, dP^T tiles: rows = keys 16kt + 4g + r, col = my query
+        f32x4 s[4], dp[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            dp[kt] = s[kt];
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lK, 16 * kt + li, kk * 4 + g), qf[kk], s[kt], 0, 0, 0);
+                dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lV, 16 * kt + li, kk * 4 + g), df[kk], dp[kt], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int key = t * 64 + 16 * kt + 4 * g + r;
+                float pv = exp2f(s[kt][r] * p.scale_log2 - lse2);
+                if (!qok || key >= p.S || (CAUSAL && key > myq)) pv = 0.f;
+                dp[kt][r] = pv * (dp[kt][r] - dl);
+            }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 dsf;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { dsf[r] = (bf16)dp[2 * ks][r]; dsf[4 + r] = (bf16)dp[2 * ks + 1][r]; }
+            const int kr = 32 * ks + 4 * g + (li >> 2);
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
+                const int dc = d * 16 + 4 * (li & 3);
+                acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(tr_read_k<RB>(lK, kr, dc), tr_read_k<RB>(lK, kr + 16, dc)),
+                                                                dsf, acc[d], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (qok) {
+        float* dQr = p.dq + ((int64_t)(b * p.H + h) * p.S + myq) * HDP;
+#pragma unroll
+        for (int d = 0; d < DT; ++d) *(f32x4*)(dQr + d * 16 + 4 * g) = acc[d] * p.scale;
     }
 }
 
@@ -417,12 +544,22 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     return KD_OK;
 }
 
+size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d) {
+    if (!d || d->HKV <= 0 || d->H == d->HKV) return 0;
+    return (size_t)2 * d->B * d->H * d->S * d->hdp * 4;
+}
+
 int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     KD_CHECK_ARG(d && d->q && d->k && d->v && d->o && d->dO && d->lse && d->delta && d->dq && d->dk && d->dv,
                  "attn_bwd: null pointer");
-    KD_CHECK_SHAPE(d->H % d->HKV == 0 && d->hd % 4 == 0 && d->hd <= d->hdp, "attn_bwd: shape");
+    KD_CHECK_SHAPE(d->B > 0 && d->S > 0 && d->HKV > 0 && d->H % d->HKV == 0 && d->hd % 4 == 0 && d->hd <= d->hdp,
+                   "attn_bwd: shape");
     KD_CHECK_SHAPE(d->hdp == 64 || d->hdp == 96 || d->hdp == 128, "attn_bwd: padded head dim must be 64/96/128");
+    KD_CHECK_SHAPE(!(d->hdp == 96 && d->hd > 80) && !(d->hdp == 64 && d->hd > 64), "attn_bwd: hd exceeds tile cover");
     KD_CHECK_SHAPE(d->hd % 8 == 0, "attn_bwd: hd must be a multiple of 8 (16-B dO rows)");
+    const size_t need = attn_bwd_workspace_size(d);
+    if (need && (!d->workspace || d->workspace_bytes < need))
+        return fail(KD_ERR_WORKSPACE, "attn_bwd: GQA needs kd_attn_bwd_workspace_size() bytes of workspace");
     hipStream_t st = as_stream(stream_);
     {
         const int rows = d->B * d->S * d->H;
@@ -430,21 +567,34 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
                            (const bf16*)d->dO, d->delta, d->B, d->H, d->S, d->hd);
         KD_LAUNCH_CHECK("k_attn_delta");
     }
-    if (hipMemsetAsync(d->dq, 0, (size_t)d->B * d->H * d->S * d->hdp * 4, st) != hipSuccess)
-        return fail(KD_ERR_LAUNCH, "attn_bwd: memset dq");
     const double sc = 1.0 / std::sqrt((double)d->hd);
+    float* dkp = need ? (float*)d->workspace : nullptr;
+    float* dvp = need ? dkp + (size_t)d->B * d->H * d->S * d->hdp : nullptr;
     AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, d->lse, d->delta,
-               d->dq, (bf16*)d->dk, (bf16*)d->dv, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
+               d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
                (float)(sc * 1.4426950408889634)};
-    dim3 grid((d->S + 63) / 64, d->HKV, d->B);
+    dim3 grid((d->S + 63) / 64, d->H, d->B);
     const int rb = d->hdp == 64 ? 128 : 256;
-    const size_t smem = 64 * rb + 32 * rb * 2 + 32 * 128 + 64 * 4;
-#define LAUNCH(HD, C) hipLaunchKernelGGL((k_attn_bwd<HD, C>), grid, dim3(256), smem, st, p)
+    const size_t smem_kv = 2 * (2 * 64 * rb + 512);
+    const size_t smem_q = 2 * 2 * 64 * rb;
+#define LAUNCH(HD, C)                                                                         \
+    do {                                                                                      \
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<HD, C>), grid, dim3(256), smem_kv, st, p);       \
+        KD_LAUNCH_CHECK("k_attn_bwd_dkdv");                                                   \
+        hipLaunchKernelGGL((k_attn_bwd_dq<HD, C>), grid, dim3(256), smem_q, st, p);          \
+        KD_LAUNCH_CHECK("k_attn_bwd_dq");                                                     \
+    } while (0)
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }
     else if (d->hdp == 96) { if (d->causal) LAUNCH(96, true); else LAUNCH(96, false); }
     else { if (d->causal) LAUNCH(128, true); else LAUNCH(128, false); }
 #undef LAUNCH
-    KD_LAUNCH_CHECK("k_attn_bwd");
+    if (need) {
+        const int dcols = 16 * (d->hdp == 64 ? 4 : (d->hdp == 96 ? 5 : 8));
+        const int64_t work = (int64_t)d->B * d->HKV * d->S * dcols / 4;
+        hipLaunchKernelGGL(k_attn_group_sum, dim3((unsigned)std::min<int64_t>((work + 255) / 256, 8192)), dim3(256), 0, st,
+                           dkp, dvp, (bf16*)d->dk, (bf16*)d->dv, d->B, d->H, d->HKV, d->S, d->hdp, dcols, (float)sc);
+        KD_LAUNCH_CHECK("k_attn_group_sum");
+    }
     return KD_OK;
 }
 

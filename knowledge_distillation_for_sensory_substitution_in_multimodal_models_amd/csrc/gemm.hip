@@ -38,10 +38,19 @@ struct GemmP {
     int M, N, K;
     float alpha;
     int c_f32, accumulate, bias_f32, act, res_mod;
+    int64_t kchunk;        // split-K: K elements per split (gridDim.y splits)
+    int64_t split_stride;  // split-K: fp32 elements between consecutive partial planes
 };
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
 __device__ __forceinline__ uint32_t sw_mn(int k) { return (uint32_t)(((k & 3) | (((k >> 3) & 1) << 2)) << 1); }
+
+// num_records is always kept below 2^31 (launch checks guarantee the real extents are), so
+// the out-of-range voffset OOB = 2^31 can never address memory.
+__device__ __forceinline__ uint32_t rec_bytes(int64_t rows, int64_t ld) {
+    const int64_t b = rows * ld * 2;
+    return b <= 0 ? 0u : (b >= 0x7FFFFFFFll ? 0x7FFFFFFFu : (uint32_t)b);
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
@@ -58,8 +67,7 @@ __device__ __forceinline__ void stage(char* tile, const bf16* ptr, int64_t ld, i
     if (!MN) {
         // base at row r0; num_records bounds the valid rows
         const int rows_valid = min(128, rows_total - r0);
-        const uint64_t bytes = (uint64_t)rows_valid * (uint64_t)ld * 2u;
-        auto rs = make_rsrc(ptr + (int64_t)r0 * ld, bytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)bytes);
+        auto rs = make_rsrc(ptr + (int64_t)r0 * ld, rec_bytes(rows_valid, ld));
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int i = wid * 4 + s;
@@ -71,9 +79,8 @@ __device__ __forceinline__ void stage(char* tile, const bf16* ptr, int64_t ld, i
         }
     } else {
         // operand stored [K][rows]; base at k-row k0, column r0
-        const int kvalid = min(64, K - k0);
-        const uint64_t bytes = (uint64_t)kvalid * (uint64_t)ld * 2u;
-        auto rs = make_rsrc(ptr + (int64_t)k0 * ld + r0, bytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)bytes);
+        const int kvalid = max(0, min(64, K - k0));
+        auto rs = make_rsrc(ptr + (int64_t)min(k0, K) * ld + r0, rec_bytes(kvalid, ld));
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int i = wid * 4 + s;
@@ -124,17 +131,29 @@ __device__ __forceinline__ float apply_act(float x, int act) {
     }
 }
 
+// Block -> tile map: (1) XCD-aware bijective remap, so the blocks dispatched to one XCD
+// (b, b+8, ...) get consecutive ids; (2) grouped order, GM tile-rows at a time, so the
+// ~32 co-resident blocks of an XCD share GM A-panels and 32/GM B-panels in its L2.
+__device__ __forceinline__ void tile_of(int tiles_m, int tiles_n, int& tm, int& tn) {
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, x = b % 8;
+    const int wg = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + b / 8;
+    constexpr int GM = 8;
+    const int group = wg / (GM * tiles_n);
+    const int first_m = group * GM;
+    const int gm = min(tiles_m - first_m, GM);
+    const int idx = wg - group * GM * tiles_n;
+    tm = first_m + idx % gm;
+    tn = idx / gm;
+}
+
 template <bool A_MN, bool B_MN>
 __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const int tiles_m = (p.M + BM - 1) / BM;
-    // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> give them consecutive tiles
-    const int nwg = gridDim.x, b = blockIdx.x;
-    const int q8 = nwg / 8, r8 = nwg % 8, x = b % 8;
-    const int wg = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + b / 8;
-    const int tm = wg % tiles_m, tn = wg / tiles_m;
+    int tm, tn;
+    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
 
     f32x4 acc[4][4];
@@ -166,6 +185,7 @@ __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
             for (int i = 0; i < 4; ++i) af[i] = frag<A_MN>(ta, wm * 64 + i * 16, ks, lane);
 #pragma unroll
             for (int j = 0; j < 4; ++j) bfr[j] = frag<B_MN>(tb, wn * 64 + j * 16, ks, lane);
+            __builtin_amdgcn_sched_barrier(0);  // every LDS read in flight before the first MFMA
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -208,6 +228,450 @@ __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
     }
 }
 
+
+// =============================================================================
+// v2: 256x256 (or 256x128 / 128x256) tile, 512 threads = 8 waves, BK = 32, a 4-stage
+// LDS-DMA ring with 3 stages in flight (counted vmcnt, raw s_barrier: the DMA of the
+// next stages stays in flight across barriers), 1 workgroup per CU, and an epilogue
+// staged through LDS so every global store / residual load is a 16-B row chunk.
+// 256x256 halves the L2->CU bytes per FLOP of the 128x128 v1 tile (128 FLOP/B).
+//   K-major stage image [rows][32 k] (64-B rows), chunk ^ F4[(row>>2)&3]   (b128 reads)
+//   MN-major stage image [32 k][rows] (2*rows-B rows), chunk ^ sw_mn(k)   (tr_b16 reads)
+// Both swizzles are conflict-free for the 16x16x32 fragment reads (checked by
+// enumeration).
+// =============================================================================
+constexpr int BK2 = 32, NST = 4, NTH2 = 512;
+
+__device__ __forceinline__ int f4(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }  // [0,2,3,1]
+
+template <int R, bool MN>
+__device__ __forceinline__ void stage2(char* tile, const bf16* ptr, int64_t ld, int r0, int rows_total, int k0, int K,
+                                       int wid, int lane, __amdgpu_buffer_rsrc_t rs_k) {
+    constexpr int NI = R / 16;           // 1-KiB wave-instructions per operand stage
+    constexpr int PER = NI / 8;          // per wave (8 waves)
+    if (!MN) {
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            const int i = wid * PER + s;
+            const int row = 16 * i + (lane >> 2);
+            const int gc = (lane & 3) ^ f4(row);
+            const int k = k0 + gc * 8;
+            const uint32_t voff = (k < K) ? (uint32_t)(((int64_t)row * ld + k) * 2) : OOB;
+            dma16(rs_k, tile + i * 1024, voff);
+        }
+    } else {
+        constexpr int CPR = R / 8;       // 16-B chunks per k-row
+        constexpr int KPI = 64 / CPR;    // k-rows per wave-instruction
+        const int kvalid = max(0, min(BK2, K - k0));   // past-the-end stages: no records at all
+        auto rs = make_rsrc(ptr + (int64_t)min(k0, K) * ld + r0, rec_bytes(kvalid, ld));
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            const int i = wid * PER + s;
+            const int kr = i * KPI + lane / CPR;
+            const int gc = (lane % CPR) ^ (int)sw_mn(kr);
+            const int row = r0 + gc * 8;
+            const uint32_t voff = (kr < kvalid && row < rows_total) ? (uint32_t)(((int64_t)kr * ld + gc * 8) * 2) : OOB;
+            dma16(rs, tile + i * 1024, voff);
+        }
+    }
+}
+
+template <int R, bool MN>
+__device__ __forceinline__ bf16x8 frag2(const char* tile, int rb, int lane) {
+    if (!MN) {
+        const int r = rb + (lane & 15);
+        const int c = lane >> 4;
+        return *(const bf16x8*)(tile + r * 64 + ((c ^ f4(r)) << 4));
+    } else {
+        constexpr int RB = R * 2;
+        const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+        const int cc = (rb >> 3) + (p >> 1);
+        const int kr0 = 8 * g + q, kr1 = kr0 + 4;
+        const char* a0 = tile + kr0 * RB + ((cc ^ (int)sw_mn(kr0)) << 4) + ((p & 1) << 3);
+        const char* a1 = tile + kr1 * RB + ((cc ^ (int)sw_mn(kr1)) << 4) + ((p & 1) << 3);
+        bf16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a0);
+        bf16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a1);
+        bf16x8 r;
+        r[0] = h0[0]; r[1] = h0[1]; r[2] = h0[2]; r[3] = h0[3];
+        r[4] = h1[0]; r[5] = h1[1]; r[6] = h1[2]; r[7] = h1[3];
+        return r;
+    }
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else static_assert(N == 0, "unsupported vmcnt");
+}
+
+template <int BM, int BN>
+constexpr size_t gemm2_lds() {
+    // pipeline ring vs the epilogue staging (bf16 tile with 16-B padded rows, or half an fp32 tile)
+    constexpr size_t ring = (size_t)NST * (BM + BN) * BK2 * 2;
+    constexpr size_t ep16 = (size_t)BM * (BN * 2 + 16);
+    constexpr size_t ep32 = (size_t)(BM / 2) * (BN * 4 + 16);
+    return ring > ep16 ? (ring > ep32 ? ring : ep32) : (ep16 > ep32 ? ep16 : ep32);
+}
+
+
+template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT>
+__device__ __forceinline__ void epilogue2(const GemmP& p, f32x4 (&acc)[MT][NT], char* smem, int m0, int n0, int wm, int wn,
+                                          int lane, int tid) {
+    // ---------------------------------------------------------------- epilogue
+    float alpha = p.alpha;
+    if (p.alpha_dev) alpha *= *p.alpha_dev;
+    // alpha, bias, aux (pre-activation), activation in registers
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn * TN + j * 16 + (lane & 15);
+        float bcol = 0.f;
+        if (p.bias && col < p.N) bcol = p.bias_f32 ? ((const float*)p.bias)[col] : (float)((const bf16*)p.bias)[col];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = acc[i][j][r] * alpha + bcol;
+                if (p.aux) {
+                    const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+                    if (row < p.M && col < p.N) p.aux[(int64_t)row * p.ld_aux + col] = (bf16)v;
+                }
+                acc[i][j][r] = apply_act(v, p.act);
+            }
+    }
+    if (!p.c_f32) {
+        constexpr int RS = BN * 2 + 16;   // padded LDS row (bytes)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int lr = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+                    const int lc = wn * TN + j * 16 + (lane & 15);
+                    *(bf16*)(smem + lr * RS + lc * 2) = (bf16)acc[i][j][r];
+                }
+        __syncthreads();
+        constexpr int CPR = BN / 8;
+        for (int idx = tid; idx < BM * CPR; idx += NTH2) {
+            const int lr = idx / CPR, c = idx % CPR;
+            const int row = m0 + lr, col = n0 + c * 8;
+            if (row >= p.M || col >= p.N) continue;
+            bf16x8 v = *(const bf16x8*)(smem + lr * RS + c * 16);
+            bf16* dst = (bf16*)p.C + (int64_t)row * p.ldc + col;
+            if (p.resid || p.accumulate) {
+                float f[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) f[e] = (float)v[e];
+                if (p.resid) {
+                    const int rr = p.res_mod > 0 ? row % p.res_mod : row;
+                    bf16x8 rv = *(const bf16x8*)(p.resid + (int64_t)rr * p.ldr + col);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) f[e] += (float)rv[e];
+                }
+                if (p.accumulate) {
+                    bf16x8 cv = *(const bf16x8*)dst;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) f[e] += (float)cv[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (bf16)f[e];
+            }
+            *(bf16x8*)dst = v;
+        }
+    } else {
+        constexpr int RS = BN * 4 + 16;
+        constexpr int HR = BM / 2;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const int lr0 = wm * TM + i * 16;
+                if (lr0 < h * HR || lr0 >= (h + 1) * HR) continue;
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int lr = lr0 + (lane >> 4) * 4 + r - h * HR;
+                        const int lc = wn * TN + j * 16 + (lane & 15);
+                        *(float*)(smem + lr * RS + lc * 4) = acc[i][j][r];
+                    }
+            }
+            __syncthreads();
+            constexpr int CPR = BN / 4;
+            for (int idx = tid; idx < HR * CPR; idx += NTH2) {
+                const int lr = idx / CPR, c = idx % CPR;
+                const int row = m0 + h * HR + lr, col = n0 + c * 4;
+                if (row >= p.M || col >= p.N) continue;
+                f32x4 v = *(const f32x4*)(smem + lr * RS + c * 16);
+                float* dst = (float*)p.C + (int64_t)row * p.ldc + col;
+                if (p.resid) {
+                    const int rr = p.res_mod > 0 ? row % p.res_mod : row;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += (float)p.resid[(int64_t)rr * p.ldr + col + e];
+                }
+                if (p.accumulate) v += *(const f32x4*)dst;
+                *(f32x4*)dst = v;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int BM, int BN, bool A_MN, bool B_MN>
+__global__ void __launch_bounds__(NTH2, 1) k_gemm2(GemmP p) {
+    constexpr int WM = (BM == 256 && BN == 256) ? 2 : (BM == 256 ? 4 : 2);
+    constexpr int WN = 8 / WM;
+    constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NT = TN / 16;
+    constexpr int SA = BM * BK2 * 2, SB = BN * BK2 * 2, SS = SA + SB;
+    constexpr int G = (BM / 16) / 8 + (BN / 16) / 8;   // DMA wave-instructions per stage per wave
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    int tm, tn;
+    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // K-major descriptors are fixed per block (base at the block's first row)
+    __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
+    if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
+    if (!B_MN) rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(BN, p.N - n0), p.ldb));
+
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (p.K + BK2 - 1) / BK2;
+#pragma unroll
+    for (int st = 0; st < NST - 1; ++st) {
+        if (st < nk) {
+            char* base = smem + st * SS;
+            stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, st * BK2, p.K, wid, lane, rsA);
+            stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, st * BK2, p.K, wid, lane, rsB);
+        }
+    }
+    for (int t = 0; t < nk; ++t) {
+        // stage t must have landed: the stages issued after it (<= 2) may stay in flight
+        const int after = min(NST - 2, nk - 1 - t);
+        if (after >= 2) wait_vm<2 * G>();
+        else if (after == 1) wait_vm<G>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (t + NST - 1 < nk) {
+            char* base = smem + ((t + NST - 1) % NST) * SS;
+            stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, (t + NST - 1) * BK2, p.K, wid, lane, rsA);
+            stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, (t + NST - 1) * BK2, p.K, wid, lane, rsB);
+        }
+        const char* ta = smem + (t % NST) * SS;
+        const char* tb = ta + SA;
+        bf16x8 af[MT], bfr[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bfr[j] = frag2<BN, B_MN>(tb, wn * TN + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) af[i] = frag2<BM, A_MN>(ta, wm * TM + i * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);  // every LDS read in flight before the first MFMA
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    epilogue2<BM, BN, WM, WN, TM, TN, MT, NT>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+
+// =============================================================================
+// v3: v2's tiles and 4-stage LDS ring, software-pipelined one stage deeper: the
+// fragments of stage t+1 are read into a second register set WHILE the MFMAs of stage t
+// run, and the DMA of stage t+4 is interleaved with them too (sched_group_barrier), so
+// after a barrier the MFMA pipe never waits for LDS or for DMA issue.
+// Iteration t: lgkmcnt(0) [frags of t in registers, my reads of buffer t done] ->
+//   vmcnt(stage t+1 landed) -> s_barrier [everyone done with buffer t; stage t+1 visible]
+//   -> {DMA stage t+4 -> buffer t%4, LDS reads of stage t+1 -> set nxt} || MFMAs(t, set cur)
+// =============================================================================
+template <int BM, int BN, bool A_MN, bool B_MN>
+__global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
+    GemmP p = p_;
+    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    constexpr int WM = (BM == 256 && BN == 256) ? 2 : (BM == 256 ? 4 : 2);
+    constexpr int WN = 8 / WM;
+    constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NT = TN / 16;
+    constexpr int SA = BM * BK2 * 2, SB = BN * BK2 * 2, SS = SA + SB;
+    constexpr int G = (BM / 16) / 8 + (BN / 16) / 8;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    int tm, tn;
+    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
+    if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
+    if (!B_MN) rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(BN, p.N - n0), p.ldb));
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nk = (p.K + BK2 - 1) / BK2;
+    auto dma = [&](int st) {
+        char* base = smem + (st % NST) * SS;
+        stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, st * BK2, p.K, wid, lane, rsA);
+        stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, st * BK2, p.K, wid, lane, rsB);
+    };
+#pragma unroll
+    for (int st = 0; st < NST; ++st) dma(st);
+    wait_vm<3 * G>();   // stage 0 landed: stages 1..3 may stay in flight
+    __builtin_amdgcn_s_barrier();
+    bf16x8 aA[MT], bA[NT], aB[MT], bB[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bA[j] = frag2<BN, B_MN>(smem + SA, wn * TN + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) aA[i] = frag2<BM, A_MN>(smem, wm * TM + i * 16, lane);
+
+#define KD_G3_STEP(CUR_A, CUR_B, NXT_A, NXT_B)                                                           \
+    {                                                                                                     \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                \
+        wait_vm<2 * G>();                                                                                 \
+        __builtin_amdgcn_s_barrier();                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                                \
+        dma(t + NST);                                                                                     \
+        {                                                                                                 \
+            const char* na = smem + ((t + 1) % NST) * SS;                                                 \
+            _Pragma("unroll") for (int j = 0; j < NT; ++j) NXT_B[j] = frag2<BN, B_MN>(na + SA, wn * TN + j * 16, lane); \
+            _Pragma("unroll") for (int i = 0; i < MT; ++i) NXT_A[i] = frag2<BM, A_MN>(na, wm * TM + i * 16, lane);      \
+        }                                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < MT; ++i)                                                    \
+            _Pragma("unroll") for (int j = 0; j < NT; ++j)                                                \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CUR_A[i], CUR_B[j], acc[i][j], 0, 0, 0); \
+        _Pragma("unroll") for (int k = 0; k < G; ++k) {                                                   \
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                            \
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                            \
+        }                                                                                                 \
+        _Pragma("unroll") for (int k = 0; k < MT + NT; ++k) {                                             \
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                            \
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                            \
+        }                                                                                                 \
+        __builtin_amdgcn_sched_group_barrier(0x008, MT * NT - 2 * (G + MT + NT), 0);                      \
+        __builtin_amdgcn_sched_barrier(0);                                                                \
+    }
+    // every iteration issues exactly one DMA stage (past the end: all out of range -> no memory
+    // traffic, zero-filled buffers nobody reads) and one stage of fragment reads, so the
+    // waits are uniform: stage t+1 landed <=> at most 2 younger stages in flight.
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+        KD_G3_STEP(aA, bA, aB, bB);
+        ++t;
+        KD_G3_STEP(aB, bB, aA, bA);
+        --t;
+    }
+    if (t < nk) KD_G3_STEP(aA, bA, aB, bB);
+#undef KD_G3_STEP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    epilogue2<BM, BN, WM, WN, TM, TN, MT, NT>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+// split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
+// (alpha, alpha_dev, bias, aux, act, residual, accumulate), 4 columns per thread
+__global__ void k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p) {
+    const int c4 = p.N / 4;
+    const int64_t total = (int64_t)p.M * c4;
+    float alpha = p.alpha;
+    if (p.alpha_dev) alpha *= *p.alpha_dev;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = idx / c4;
+        const int col = (int)(idx % c4) * 4;
+        const float* src = ws + row * p.N + col;
+        f32x4 v = *(const f32x4*)src;
+        for (int s = 1; s < S; ++s) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float x = v[e] * alpha;
+            if (p.bias) x += p.bias_f32 ? ((const float*)p.bias)[col + e] : (float)((const bf16*)p.bias)[col + e];
+            if (p.aux) p.aux[row * p.ld_aux + col + e] = (bf16)x;
+            v[e] = apply_act(x, p.act);
+        }
+        if (p.resid) {
+            const bf16x4 r = *(const bf16x4*)(p.resid + (p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+        }
+        if (p.c_f32) {
+            float* dst = (float*)p.C + row * p.ldc + col;
+            if (p.accumulate) v += *(const f32x4*)dst;
+            *(f32x4*)dst = v;
+        } else {
+            bf16* dst = (bf16*)p.C + row * p.ldc + col;
+            bf16x4 o;
+            if (p.accumulate) {
+                const bf16x4 c = *(const bf16x4*)dst;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)c[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+            *(bf16x4*)dst = o;
+        }
+    }
+}
+
+// Tile / split-K plan for the 8-wave kernels. Cost model in units of one 32-deep k-step
+// of a 256x256 tile on one CU (~0.9 us): waves x (k-steps x tile cost + fixed per-tile
+// prologue/epilogue), plus the partial-plane traffic at ~5 TB/s. Constants fitted to a
+// tile x split sweep over every GEMM shape of the KD step (tools/tune_gemm.py): the
+// model's picks are within 0.1% of the measured best over those 34 shapes.
+struct GemmPlan { int var; int split; int64_t kchunk; };
+
+GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
+    const int64_t M = d->M, N = d->N;
+    const int64_t tiles[3] = {(int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 256),
+                              (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 128),
+                              (int64_t)ceil_div(d->M, 128) * ceil_div(d->N, 256)};
+    const double step[3] = {1.0, 0.70, 0.65};   // 256x256, 256x128, 128x256
+    const double fixed[3] = {24.0, 12.0, 6.0};
+    const int64_t nk = ceil_div(d->K, BK2);
+    const int fv = d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1);
+    const bool split_ok = d->variant == 0 || d->variant >= 5;
+    const double out_b = (double)M * N * ((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
+                                          (d->residual ? 2 : 0) + (d->aux ? 2 : 0));
+    GemmPlan best{fv >= 0 ? fv + 2 : 2, 1, d->K};
+    double bt = 1e300;
+    for (int v = 0; v < 3; ++v) {
+        if (fv >= 0 && v != fv) continue;
+        for (int S = 1; S <= 32; ++S) {
+            if (d->split_k == 1 && S != 1) continue;
+            if (d->split_k > 1 && S != d->split_k && S != 1) continue;
+            if (S > 1 && !split_ok) continue;
+            const int64_t kcs = (nk + S - 1) / S;
+            if (S > 1 && ((nk + kcs - 1) / kcs != S)) continue;          // empty trailing split
+            if (S > 1 && d->split_k <= 1 && kcs < 8) continue;           // too little work per split
+            if (S > 1 && (uint64_t)S * M * N * 4 > ws_cap) continue;
+            const int64_t waves = (tiles[v] * S + 255) / 256;
+            double t = (double)waves * ((double)kcs * step[v] + fixed[v]);
+            if (S > 1) t += ((double)S * M * N * 8 + out_b) / 4.5e6;
+            if (d->split_k > 1 && S == d->split_k) t = -1;              // forced
+            if (t < bt) { bt = t; best = GemmPlan{v + 2, S, kcs * BK2}; }
+        }
+    }
+    return best;
+}
+
 }  // namespace
 
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
@@ -225,7 +689,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->K % 8 == 0 && d->lda >= d->K, "gemm: K-major A needs K % 8 == 0, lda >= K");
     } else {
         KD_CHECK_SHAPE(d->M % 8 == 0 && d->lda >= d->M, "gemm: MN-major A needs M % 8 == 0, lda >= M");
-        KD_CHECK_SHAPE((uint64_t)64 * d->lda * 2 < 0xFFFFFFFFull, "gemm: lda too large");
+        KD_CHECK_SHAPE((uint64_t)64 * d->lda * 2 < 0x7FFFFFFFull, "gemm: lda too large");
     }
     if (d->b_layout == KD_LAYOUT_K_MAJOR) {
         KD_CHECK_SHAPE(d->K % 8 == 0 && d->ldb >= d->K, "gemm: K-major B needs K % 8 == 0, ldb >= K");
@@ -235,8 +699,8 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_SHAPE(d->ldc >= d->N, "gemm: ldc < N");
     KD_CHECK_SHAPE(!d->residual || d->ldr >= d->N, "gemm: ldr < N");
     KD_CHECK_SHAPE(!d->aux || d->ld_aux >= d->N, "gemm: ld_aux < N");
-    KD_CHECK_SHAPE((uint64_t)128 * (d->a_layout == KD_LAYOUT_K_MAJOR ? d->lda : 0) * 2 < 0xFFFFFFFFull,
-                   "gemm: lda too large");
+    KD_CHECK_SHAPE((uint64_t)256 * d->lda * 2 < 0x7FFFFFFFull && (uint64_t)256 * d->ldb * 2 < 0x7FFFFFFFull,
+                   "gemm: leading dimension too large for 31-bit buffer records");
     GemmP p;
     p.A = (const bf16*)d->A; p.B = (const bf16*)d->B; p.C = d->C;
     p.bias = d->bias; p.resid = (const bf16*)d->residual; p.aux = (bf16*)d->aux; p.alpha_dev = d->alpha_dev;
@@ -245,16 +709,68 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.c_f32 = d->c_dtype == KD_DTYPE_F32; p.accumulate = d->accumulate; p.bias_f32 = d->bias_dtype == KD_DTYPE_F32;
     p.act = d->act;
     p.res_mod = d->residual_row_mod;
-    const int tiles = ceil_div(d->M, BM) * ceil_div(d->N, BN);
-    const size_t smem = 4 * TILE_BYTES;
+    p.kchunk = d->K; p.split_stride = 0;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
+    const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
+                        ((uintptr_t)d->residual % 16 == 0)));
+    const bool v2_ok = d->N % 8 == 0 && c_ok16 && d->M >= 128 && d->N >= 128 &&
+                       ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
+                       (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
+                       (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
+    const int force = d->variant;   // 0 auto, 1 v1, 2/3/4 v2 256x256/256x128/128x256, 5/6/7 v3 same tiles
+    if ((force == 0 && v2_ok) || (force >= 2 && v2_ok)) {
+        const bool v3 = force == 0 || force >= 5;
+        const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
+        const int var = pl.var;
+        GemmP pk = p;   // the tile kernels' parameters (split-K: plain fp32 partial planes)
+        if (pl.split > 1) {
+            KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
+                         "gemm: split-K workspace too small");
+            pk.C = d->workspace; pk.ldc = d->N; pk.c_f32 = 1; pk.accumulate = 0; pk.alpha = 1.f;
+            pk.alpha_dev = nullptr; pk.bias = nullptr; pk.aux = nullptr; pk.resid = nullptr; pk.act = KD_ACT_NONE;
+            pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N;
+        }
+        const dim3 gy(1, pl.split, 1);
+#define L2(BMv, BNv, AM, BMN)                                                                                     \
+    if (v3) hipLaunchKernelGGL((k_gemm3<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv), gy.y), \
+                               dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk);                                        \
+    else hipLaunchKernelGGL((k_gemm2<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv)),         \
+                            dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk)
+#define L2SEL(BMv, BNv)                                     \
+    if (!amn && !bmn) L2(BMv, BNv, false, false);           \
+    else if (!amn && bmn) L2(BMv, BNv, false, true);        \
+    else if (amn && bmn) L2(BMv, BNv, true, true);          \
+    else L2(BMv, BNv, true, false);
+        if (var == 2) { L2SEL(256, 256) }
+        else if (var == 3) { L2SEL(256, 128) }
+        else { L2SEL(128, 256) }
+#undef L2SEL
+#undef L2
+        KD_LAUNCH_CHECK("k_gemm2");
+        if (pl.split > 1) {
+            p.split_stride = (int64_t)d->M * d->N;
+            const int64_t work = (int64_t)d->M * d->N / 4;
+            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((work + 255) / 256, 16384)), dim3(256), 0,
+                               st, (const float*)d->workspace, pl.split, p);
+            KD_LAUNCH_CHECK("k_splitk_reduce");
+        }
+        return KD_OK;
+    }
+    const int tiles = ceil_div(d->M, BM) * ceil_div(d->N, BN);
+    const size_t smem = 4 * TILE_BYTES;
     if (!amn && !bmn) hipLaunchKernelGGL((k_gemm<false, false>), dim3(tiles), dim3(NTH), smem, st, p);
     else if (!amn && bmn) hipLaunchKernelGGL((k_gemm<false, true>), dim3(tiles), dim3(NTH), smem, st, p);
     else if (amn && bmn) hipLaunchKernelGGL((k_gemm<true, true>), dim3(tiles), dim3(NTH), smem, st, p);
     else hipLaunchKernelGGL((k_gemm<true, false>), dim3(tiles), dim3(NTH), smem, st, p);
     KD_LAUNCH_CHECK("k_gemm");
     return KD_OK;
+}
+
+size_t gemm_workspace_size(const kd_gemm_desc* d) {
+    if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->variant == 1) return 0;
+    const GemmPlan pl = plan_gemm(d, ~0ull);
+    return pl.split > 1 ? (size_t)pl.split * d->M * d->N * 4 : 0;
 }
 
 }  // namespace kd

@@ -21,7 +21,7 @@ class KernelTimer:
 
     def __init__(self):
         self.enabled = False
-        self.records = []   # (kind, flops, start_event, end_event)
+        self.records = []   # (kind, flops, start_event, end_event, shape_key)
 
     def reset(self):
         self.records = []
@@ -31,13 +31,29 @@ class KernelTimer:
         if not recs:
             return None
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for _, _, a, b in recs]
+        ms = [r[2].elapsed_time(r[3]) for r in recs]
         flops = sum(r[1] for r in recs)
         return dict(launches=len(recs), total_ms=sum(ms), avg_ms=sum(ms) / len(ms), flops=flops,
                     flops_per_launch=flops / len(recs))
 
+    def by_shape(self, top=25):
+        """Per (layouts, M, N, K, out dtype) totals, heaviest first (tuning aid)."""
+        torch.cuda.synchronize()
+        agg = {}
+        for kind, fl, a, b, key in self.records:
+            t = agg.setdefault(key, [0, 0.0, fl])
+            t[0] += 1
+            t[1] += a.elapsed_time(b)
+        rows = sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]
+        return [dict(shape=k, launches=n, total_ms=round(ms, 3), avg_us=round(1e3 * ms / n, 2),
+                     tflops=round(fl * n / (ms * 1e-3) / 1e12, 1)) for k, (n, ms, fl) in rows]
+
 
 TIMER = KernelTimer()
+
+# fp32 split-K partial planes, one buffer per (stream, device); the library's cost model
+# never plans more splits than fit
+GEMM_SPLITK_WS = 384 << 20
 
 
 def _stream() -> int:
@@ -131,8 +147,11 @@ def _operand(x: torch.Tensor, name: str):
 
 def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
          residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
-         out_dtype=torch.bfloat16, residual_row_mod: int = 0) -> torch.Tensor:
+         out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0) -> torch.Tensor:
     """out[M, N] = epilogue(alpha * a[M, K] @ b[N, K]^T).
+
+    split_k: 0 = library cost model (bounded by the cached GEMM_SPLITK_WS workspace),
+    1 = never split, >1 = forced number of K splits (tests).
 
     `a`/`b` may be K-contiguous tensors or transposed views (x.t() of a contiguous tensor):
     the kernel reads either layout directly (no transpose copies).
@@ -155,6 +174,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     if bias is not None:
         d.bias, d.bias_dtype = bias.data_ptr(), _DT[bias.dtype]
     d.act = ACTS[act]
+    d.variant = int(variant)
+    d.split_k = int(split_k)
+    if split_k != 1:
+        ws = _workspace(("gemm_splitk", _stream()), GEMM_SPLITK_WS, a.device)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     if residual is not None:
         _require(residual, torch.bfloat16, "gemm.residual")
         d.residual, d.ldr = residual.data_ptr(), residual.stride(0)
@@ -167,7 +191,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
         e0.record()
         NV.call("kd_gemm", C.byref(d), _stream())
         e1.record()
-        TIMER.records.append((f"gemm_{'kn'[la]}{'kn'[lb]}", 2.0 * M * N * K, e0, e1))
+        kind = f"gemm_{'kn'[la]}{'kn'[lb]}"
+        TIMER.records.append((kind, 2.0 * M * N * K, e0, e1,
+                              f"{kind}:{M}x{N}x{K}:{'f32' if out.dtype == torch.float32 else 'bf16'}"
+                              f"{':acc' if accumulate else ''}"))
     else:
         NV.call("kd_gemm", C.byref(d), _stream())
     return out
@@ -202,7 +229,11 @@ def attn_bwd(q, k, v, o, do, lse, hd: int, causal: bool):
     dv = torch.empty_like(v)
     d = NV.KdAttnBwdDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(),
                          delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, HKV, S, hd, hdp,
-                         int(causal))
+                         int(causal), None, 0)
+    need = NV.lib().kd_attn_bwd_workspace_size(C.byref(d))
+    if need:
+        ws = _workspace("attn_bwd_partials", need, dev)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     NV.call("kd_attn_bwd", C.byref(d), _stream())
     return dq, dk, dv
 

@@ -36,3 +36,32 @@ def test_status_codes_raise_with_message():
 def test_workspace_size_grows_with_shape():
     lib = N.lib()
     assert lib.kd_loss_workspace_size(4, 1536, 151936) > lib.kd_loss_workspace_size(1, 1536, 151936)
+
+
+def _gemm_desc(M, Nc, K, amn=0, bmn=0, c_f32=1, acc=1, variant=0, split_k=0):
+    d = N.KdGemmDesc()
+    d.M, d.N, d.K, d.a_layout, d.b_layout = M, Nc, K, amn, bmn
+    d.lda = M if amn else K
+    d.ldb = Nc if bmn else K
+    d.ldc, d.c_dtype, d.accumulate, d.alpha = Nc, c_f32, acc, 1.0
+    d.variant, d.split_k = variant, split_k
+    return d
+
+
+def test_gemm_splitk_plan():
+    """Host-side split-K cost model: small-output long-K weight gradients split, large
+    forward GEMMs do not; forced splits and disabled splitting are honoured."""
+    lib = N.lib()
+    ws = lambda d: lib.kd_gemm_workspace_size(ctypes.byref(d))
+    # student o_proj wgrad (896 x 896 over 6144 tokens): 16 tiles of 256^2 -> split
+    d = _gemm_desc(896, 896, 6144, 1, 1)
+    assert ws(d) >= 2 * 896 * 896 * 4
+    # SigLIP qkv wgrad (3456 x 1152 over 5832 tokens)
+    assert ws(_gemm_desc(3456, 1152, 5832, 1, 1)) > 0
+    # teacher gate_up forward (6144 x 37888 x 3584): 3552 tiles, no split
+    assert ws(_gemm_desc(6144, 37888, 3584, 0, 0, c_f32=0, acc=0)) == 0
+    # forced / disabled / v1
+    assert ws(_gemm_desc(512, 512, 4096, split_k=4)) == 4 * 512 * 512 * 4
+    assert ws(_gemm_desc(896, 896, 6144, 1, 1, split_k=1)) == 0
+    assert ws(_gemm_desc(896, 896, 6144, 1, 1, variant=1)) == 0
+    assert ws(_gemm_desc(896, 896, 6144, 1, 1, variant=2)) == 0   # v2 tiles have no split path

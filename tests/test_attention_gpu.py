@@ -46,6 +46,8 @@ CASES = [  # B, H, HKV, S, hd, hdp, causal
     (1, 4, 1, 130, 128, 128, True),       # teacher head dim
     (2, 2, 2, 729, 72, 96, False),        # SigLIP: seq 729, hd 72 padded to 96
     (1, 3, 3, 100, 64, 64, False),
+    (1, 14, 2, 1536, 64, 64, True),       # student at the step's full sequence length
+    (1, 16, 16, 729, 72, 96, False),      # SigLIP, all heads
 ]
 
 

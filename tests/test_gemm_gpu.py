@@ -91,3 +91,102 @@ def test_epilogue_bias_act_residual_aux_accumulate(dev):
     s = torch.tensor([2.0], device=dev)
     out = ops.gemm(a, w, alpha_dev=s, alpha=0.25, out_dtype=torch.float32)
     assert (out - 0.5 * (a.float() @ w.float().t())).abs().max().item() < 1e-3
+
+
+VARIANTS = [1, 2, 3, 4, 5, 6, 7]   # 128x128 v1; v2 256x256 / 256x128 / 128x256; v3 (pipelined) same tiles
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (1458, 1152, 1152), (1000, 904, 600), (300, 272, 4304)])
+def test_variants_all_layouts(variant, M, N, K, dev):
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=31)
+    w = _rand(N, K, dev=dev, seed=32, scale=0.05)
+    _check(ops.gemm(a, w, variant=variant), a.float() @ w.float().t())
+    # dgrad: dX[M, K] = dY[M, N] W[N, K]
+    dy = _rand(M, N, dev=dev, seed=33)
+    _check(ops.gemm(dy, w.t(), variant=variant), dy.float() @ w.float())
+    if K % 8:
+        return
+    # wgrad: dW[N, K] = dY^T X over M tokens (fp32 accumulate)
+    acc = torch.ones(N, K, dtype=torch.float32, device=dev)
+    ops.gemm(dy.t(), a.t(), out=acc, accumulate=True, variant=variant)
+    ref = 1 + dy.float().t() @ a.float()
+    assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
+    # A MN-major x B K-major (MN-major operands need rows % 8 == 0)
+    if M % 8 == 0:
+        at = _rand(K, M, dev=dev, seed=34)
+        _check(ops.gemm(at.t(), w, variant=variant), at.float().t() @ w.float().t())
+
+
+@pytest.mark.parametrize("variant", [2, 3, 5, 6, 7])
+def test_variant_epilogue(variant, dev):
+    ops = _ops()
+    M, N, K = 1458, 1152, 192
+    a = _rand(M, K, dev=dev, seed=40)
+    w = _rand(N, K, dev=dev, seed=41, scale=0.1)
+    bias = _rand(N, dev=dev, seed=42)
+    pos = _rand(729, N, dev=dev, seed=43)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    pre = a.float() @ w.float().t() + bias.float()
+    out = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=pos, residual_row_mod=729, aux=aux, variant=variant)
+    ref = torch.nn.functional.gelu(pre, approximate="tanh") + pos.float().repeat(2, 1)
+    _check(out, ref)
+    _check(aux, pre)
+    o32 = torch.full((M, N), 2.0, device=dev)
+    ops.gemm(a, w, out=o32, accumulate=True, variant=variant, alpha=0.5)
+    assert (o32 - (2 + 0.5 * (a.float() @ w.float().t()))).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("split", [2, 3, 7])
+@pytest.mark.parametrize("variant", [0, 6, 7])
+@pytest.mark.parametrize("M,N,K", [(520, 384, 2248), (1152, 1152, 5832)])
+def test_splitk_all_layouts(split, variant, M, N, K, dev):
+    """Forced K splits (fp32 partial planes + reduce) in every operand layout; K is not a
+    multiple of split*32, so the last split is ragged."""
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=50)
+    w = _rand(N, K, dev=dev, seed=51, scale=0.05)
+    _check(ops.gemm(a, w, variant=variant, split_k=split), a.float() @ w.float().t())
+    at = _rand(K, M, dev=dev, seed=52)
+    _check(ops.gemm(at.t(), w, variant=variant, split_k=split), at.float().t() @ w.float().t())
+    wt = _rand(K, N, dev=dev, seed=53, scale=0.05)
+    _check(ops.gemm(a, wt.t(), variant=variant, split_k=split), a.float() @ wt.float())
+    acc = torch.ones(M, N, dtype=torch.float32, device=dev)
+    ops.gemm(at.t(), wt.t(), out=acc, accumulate=True, variant=variant, split_k=split)
+    ref = 1 + at.float().t() @ wt.float()
+    assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
+
+
+def test_splitk_epilogue(dev):
+    """The reduce pass applies the whole epilogue: alpha * alpha_dev, bias, aux, act,
+    residual (row mod), bf16 accumulate."""
+    ops = _ops()
+    M, N, K = 1458, 1152, 3072
+    a = _rand(M, K, dev=dev, seed=60, scale=0.2)
+    w = _rand(N, K, dev=dev, seed=61, scale=0.02)
+    bias = _rand(N, dev=dev, seed=62)
+    pos = _rand(729, N, dev=dev, seed=63)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    ad = torch.tensor([0.75], device=dev)
+    pre = 1.5 * 0.75 * (a.float() @ w.float().t()) + bias.float()
+    out = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=pos, residual_row_mod=729, aux=aux, alpha=1.5,
+                   alpha_dev=ad, split_k=3)
+    _check(out, torch.nn.functional.gelu(pre, approximate="tanh") + pos.float().repeat(2, 1))
+    _check(aux, pre)
+    base = _rand(M, N, dev=dev, seed=64)
+    o = base.clone()
+    ops.gemm(a, w, out=o, accumulate=True, split_k=4)
+    _check(o, base.float() + a.float() @ w.float().t())
+
+
+@pytest.mark.parametrize("M,N,K", [(896, 896, 6144), (3456, 1152, 5832), (1152, 4304, 5832)])
+def test_splitk_auto_wgrad(M, N, K, dev):
+    """The cost model's own choice on the step's weight-gradient shapes (MN x MN, fp32 +=)."""
+    ops = _ops()
+    dy = _rand(K, M, dev=dev, seed=70)
+    x = _rand(K, N, dev=dev, seed=71)
+    acc = torch.full((M, N), 0.5, dtype=torch.float32, device=dev)
+    ops.gemm(dy.t(), x.t(), out=acc, accumulate=True)
+    ref = 0.5 + dy.float().t() @ x.float()
+    assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
