@@ -307,13 +307,15 @@ template <int N> __device__ __forceinline__ void wait_vm() {
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
     else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else static_assert(N == 0, "unsupported vmcnt");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NS = NST>
 constexpr size_t gemm2_lds() {
     // pipeline ring vs the epilogue staging (bf16 tile with 16-B padded rows, or half an fp32 tile)
-    constexpr size_t ring = (size_t)NST * (BM + BN) * BK2 * 2;
+    constexpr size_t ring = (size_t)NS * (BM + BN) * BK2 * 2;
     constexpr size_t ep16 = (size_t)BM * (BN * 2 + 16);
     constexpr size_t ep32 = (size_t)(BM / 2) * (BN * 4 + 16);
     return ring > ep16 ? (ring > ep32 ? ring : ep32) : (ep16 > ep32 ? ep16 : ep32);
@@ -499,7 +501,7 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm2(GemmP p) {
 //   vmcnt(stage t+1 landed) -> s_barrier [everyone done with buffer t; stage t+1 visible]
 //   -> {DMA stage t+4 -> buffer t%4, LDS reads of stage t+1 -> set nxt} || MFMAs(t, set cur)
 // =============================================================================
-template <int BM, int BN, bool A_MN, bool B_MN>
+template <int BM, int BN, bool A_MN, bool B_MN, int NS = NST, int ABL = 0>
 __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     GemmP p = p_;
     if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
@@ -530,13 +532,13 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
         for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int nk = (p.K + BK2 - 1) / BK2;
     auto dma = [&](int st) {
-        char* base = smem + (st % NST) * SS;
+        char* base = smem + (st % NS) * SS;
         stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, st * BK2, p.K, wid, lane, rsA);
         stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, st * BK2, p.K, wid, lane, rsB);
     };
 #pragma unroll
-    for (int st = 0; st < NST; ++st) dma(st);
-    wait_vm<3 * G>();   // stage 0 landed: stages 1..3 may stay in flight
+    for (int st = 0; st < NS; ++st) dma(st);
+    wait_vm<(NS - 1) * G>();   // stage 0 landed: stages 1..NS-1 may stay in flight
     __builtin_amdgcn_s_barrier();
     bf16x8 aA[MT], bA[NT], aB[MT], bB[NT];
 #pragma unroll
@@ -547,15 +549,18 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
 #define KD_G3_STEP(CUR_A, CUR_B, NXT_A, NXT_B)                                                           \
     {                                                                                                     \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                \
-        wait_vm<2 * G>();                                                                                 \
-        __builtin_amdgcn_s_barrier();                                                                     \
+        if (ABL != 1) wait_vm<(NS - 2) * G>();   \
+        if (ABL != 2) __builtin_amdgcn_s_barrier();   \
         __builtin_amdgcn_sched_barrier(0);                                                                \
-        dma(t + NST);                                                                                     \
-        {                                                                                                 \
-            const char* na = smem + ((t + 1) % NST) * SS;                                                 \
+        if (ABL != 1) dma(t + NS);   \
+        if (ABL != 3) {   \
+            const char* na = smem + ((t + 1) % NS) * SS;                                                  \
             _Pragma("unroll") for (int j = 0; j < NT; ++j) NXT_B[j] = frag2<BN, B_MN>(na + SA, wn * TN + j * 16, lane); \
             _Pragma("unroll") for (int i = 0; i < MT; ++i) NXT_A[i] = frag2<BM, A_MN>(na, wm * TM + i * 16, lane);      \
-        }                                                                                                 \
+        } else {   \
+            _Pragma("unroll") for (int j = 0; j < NT; ++j) NXT_B[j] = CUR_B[j];   \
+            _Pragma("unroll") for (int i = 0; i < MT; ++i) NXT_A[i] = CUR_A[i];   \
+        }   \
         _Pragma("unroll") for (int i = 0; i < MT; ++i)                                                    \
             _Pragma("unroll") for (int j = 0; j < NT; ++j)                                                \
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CUR_A[i], CUR_B[j], acc[i][j], 0, 0, 0); \
@@ -585,6 +590,249 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     epilogue2<BM, BN, WM, WN, TM, TN, MT, NT>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+// =============================================================================
+// v4: 256x256 tile, BK = 64, two K-tile buffers (A | B, 64 KiB each), 8 waves as 2 (M)
+// x 4 (N) groups, each wave 128x64 of C. A K-tile runs as 4 phases, one C quadrant
+// (64x32, 16 MFMAs over K = 64) per phase:
+//   load section: ds_read this phase's fragments (+ DMA of half of K-tile k+1 in phases
+//                 0 and 1; counted vmcnt(0) for K-tile k+1 in phase 3)
+//   s_barrier -> lgkmcnt(0) -> setprio(1) MFMA x16 setprio(0) -> s_barrier
+// The wm = 1 group runs one barrier behind the wm = 0 group, so on every SIMD (one wave
+// of each group) one wave's MFMA cluster overlaps the other's load section.
+// Hazards (barrier counts): K-tile k+1's DMA lands (vmcnt 0) in phase 3 before the
+// barrier that both groups pass before reading it; buffer k&1 is last read in phase 2
+// of K-tile k and rewritten from phase 0 of K-tile k+2, >= 4 barriers later.
+// K-major LDS image: 128-B rows, 16-B chunk c of row r stored at slot c ^ ((r >> 1) & 7)
+// (conflict-free for the ds_read_b128 lane groups); MN-major: two stacked 32-deep
+// images of v2/v3's layout.
+// =============================================================================
+constexpr int BK4 = 64;
+
+template <bool MN>
+__device__ __forceinline__ void stage4(char* tile, const bf16* ptr, int64_t ld, int r0, int rows_total, int k0, int K,
+                                       int wid, int lane, int h, __amdgpu_buffer_rsrc_t rs_k) {
+    if (!MN) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int i = 16 * h + wid * 2 + s;
+            const int row = i * 8 + (lane >> 3);
+            const int gc = (lane & 7) ^ ((row >> 1) & 7);
+            const int k = k0 + gc * 8;
+            const uint32_t voff = (k < K) ? (uint32_t)(((int64_t)row * ld + k) * 2) : OOB;
+            dma16(rs_k, tile + i * 1024, voff);
+        }
+    } else {
+        const int kvalid = max(0, min(BK4, K - k0));
+        auto rs = make_rsrc(ptr + (int64_t)min(k0, K) * ld + r0, rec_bytes(kvalid, ld));
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int i = 16 * h + wid * 2 + s;
+            const int kr = i * 2 + (lane >> 5);
+            const int gc = (lane & 31) ^ (int)sw_mn(kr);
+            const int row = r0 + gc * 8;
+            const uint32_t voff = (kr < kvalid && row < rows_total) ? (uint32_t)(((int64_t)kr * ld + gc * 8) * 2) : OOB;
+            dma16(rs, tile + i * 1024, voff);
+        }
+    }
+}
+
+template <bool MN>
+__device__ __forceinline__ bf16x8 frag4(const char* tile, int rb, int kk, int lane) {
+    if (!MN) {
+        const int r = rb + (lane & 15);
+        const int c = kk * 4 + (lane >> 4);
+        return *(const bf16x8*)(tile + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+    } else {
+        return frag2<256, true>(tile + kk * 32 * 512, rb, lane);
+    }
+}
+
+template <bool A_MN, bool B_MN>
+__global__ void __launch_bounds__(NTH2, 1) k_gemm4(GemmP p_) {
+    GemmP p = p_;
+    if (gridDim.y > 1) {   // split-K (as v3)
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    constexpr int OPB = 256 * BK4 * 2;   // one operand of one K-tile
+    constexpr int KTB = 2 * OPB;         // one K-tile buffer
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 2, wn = wid & 3;
+    int tm, tn;
+    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
+    if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
+    if (!B_MN) rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nk = (p.K + BK4 - 1) / BK4;
+    auto dma_half = [&](int kt, int h) {
+        char* base = smem + (kt & 1) * KTB;
+        stage4<A_MN>(base, p.A, p.lda, m0, p.M, kt * BK4, p.K, wid, lane, h, rsA);
+        stage4<B_MN>(base + OPB, p.B, p.ldb, n0, p.N, kt * BK4, p.K, wid, lane, h, rsB);
+    };
+    dma_half(0, 0);
+    dma_half(0, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();   // stagger the two wave groups by one barrier
+    __builtin_amdgcn_sched_barrier(0);
+
+    bf16x8 af[4][2], b0[2][2], b1[2][2];
+    const int ra0 = wm * 128, cb0 = wn * 64;
+#define KD_G4_MMA(QM, QN, BF)                                                                              \
+    {                                                                                                      \
+        __builtin_amdgcn_s_barrier();                                                                      \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        __builtin_amdgcn_s_setprio(1);                                                                     \
+        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                   \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
+                    acc[(QM) * 4 + i][(QN) * 2 + j] =                                                      \
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], BF[j][kk], acc[(QM) * 4 + i][(QN) * 2 + j], 0, 0, 0); \
+        __builtin_amdgcn_s_setprio(0);                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        __builtin_amdgcn_s_barrier();                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* ta = smem + (kt & 1) * KTB;
+        const char* tb = ta + OPB;
+        const bool pf = kt + 1 < nk;
+        // phase 0: B(qn 0), A(qm 0); DMA half 0 of K-tile kt+1
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b0[j][kk] = frag4<B_MN>(tb, cb0 + j * 16, kk, lane);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i][kk] = frag4<A_MN>(ta, ra0 + i * 16, kk, lane);
+        if (pf) dma_half(kt + 1, 0);
+        KD_G4_MMA(0, 0, b0)
+        // phase 1: B(qn 1); DMA half 1
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b1[j][kk] = frag4<B_MN>(tb, cb0 + 32 + j * 16, kk, lane);
+        if (pf) dma_half(kt + 1, 1);
+        KD_G4_MMA(0, 1, b1)
+        // phase 2: A(qm 1)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i][kk] = frag4<A_MN>(ta, ra0 + 64 + i * 16, kk, lane);
+        KD_G4_MMA(1, 0, b0)
+        // phase 3: K-tile kt+1 landed (my DMAs); the barrier publishes everyone's
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        KD_G4_MMA(1, 1, b1)
+    }
+#undef KD_G4_MMA
+    if (wm == 0) __builtin_amdgcn_s_barrier();   // rebalance the barrier count
+    __syncthreads();
+    epilogue2<256, 256, 2, 4, 128, 64, 8, 4>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+// =============================================================================
+// v6: v3's tile (256x256, 8 waves 2x4, wave 128x64) and 4-slot BK=32 LDS ring, run as
+// two phases per stage with the wave groups ping-ponging: the wm = 1 group trails the
+// wm = 0 group by one barrier, so on every SIMD one wave's 16-MFMA cluster overlaps the
+// other wave's load section.
+//   phase a (stage t): ds_read B(t) + A(t) rows 0..63 ; s_barrier ; lgkmcnt(0) ;
+//                      setprio(1) 16 MFMA setprio(0) ; s_barrier
+//   phase b (stage t): ds_read A(t) rows 64..127 ; DMA stage t+3 -> slot (t+3)%4 ;
+//                      vmcnt(2G) [stage t+1 landed] ; s_barrier ; lgkmcnt(0) ; MFMA ; s_barrier
+// WAR: slot (t+3)%4 held stage t-1, whose last reads (phase b of t-1) every wave retired
+// (lgkmcnt 0) before the barrier that precedes either group's phase b of stage t.
+// RAW: stage t+1 is read in phase a of t+1, after the barrier that follows both groups'
+// vmcnt waits. DMA past the last stage is issued anyway (out-of-range, zero-fill) so the
+// counts stay uniform.
+// =============================================================================
+template <bool A_MN, bool B_MN>
+__global__ void __launch_bounds__(NTH2, 1) k_gemm6(GemmP p_) {
+    GemmP p = p_;
+    if (gridDim.y > 1) {
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    constexpr int BM = 256, BN = 256, NS = 4;
+    constexpr int SA = BM * BK2 * 2, SS = SA + BN * BK2 * 2;
+    constexpr int G = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 2, wn = wid & 3;
+    int tm, tn;
+    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
+    if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
+    if (!B_MN) rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(BN, p.N - n0), p.ldb));
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nk = (p.K + BK2 - 1) / BK2;
+    auto dma = [&](int st) {
+        char* base = smem + (st % NS) * SS;
+        stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, st * BK2, p.K, wid, lane, rsA);
+        stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, st * BK2, p.K, wid, lane, rsB);
+    };
+    dma(0); dma(1); dma(2);
+    wait_vm<2 * G>();
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 af[4], bfr[4];
+    const int ra = wm * 128, cb = wn * 64;
+#define KD_G6_MMA(I0)                                                                                       \
+    {                                                                                                       \
+        __builtin_amdgcn_s_barrier();                                                                       \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                                  \
+        __builtin_amdgcn_s_setprio(1);                                                                      \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                   \
+                acc[(I0) + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[(I0) + i][j], 0, 0, 0); \
+        __builtin_amdgcn_s_setprio(0);                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                                  \
+        __builtin_amdgcn_s_barrier();                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                                  \
+    }
+    for (int t = 0; t < nk; ++t) {
+        const char* ta = smem + (t % NS) * SS;
+        // phase a
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag2<BN, B_MN>(ta + SA, cb + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = frag2<BM, A_MN>(ta, ra + i * 16, lane);
+        KD_G6_MMA(0)
+        // phase b
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = frag2<BM, A_MN>(ta, ra + 64 + i * 16, lane);
+        dma(t + 3);
+        wait_vm<2 * G>();
+        KD_G6_MMA(4)
+    }
+#undef KD_G6_MMA
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    epilogue2<256, 256, 2, 4, 128, 64, 8, 4>(p, acc, smem, m0, n0, wm, wn, lane, tid);
 }
 
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
@@ -646,7 +894,7 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const double step[3] = {1.0, 0.70, 0.65};   // 256x256, 256x128, 128x256
     const double fixed[3] = {24.0, 12.0, 6.0};
     const int64_t nk = ceil_div(d->K, BK2);
-    const int fv = d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1);
+    const int fv = (d->variant >= 8 && d->variant <= 13) ? 0 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
     const bool split_ok = d->variant == 0 || d->variant >= 5;
     const double out_b = (double)M * N * ((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
                                           (d->residual ? 2 : 0) + (d->aux ? 2 : 0));
@@ -718,7 +966,10 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                        ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
                        (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
                        (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
-    const int force = d->variant;   // 0 auto, 1 v1, 2/3/4 v2 256x256/256x128/128x256, 5/6/7 v3 same tiles
+    const int force = d->variant;   // 0 auto, 1 v1, 2/3/4 v2 256x256/256x128/128x256, 5/6/7 v3 same tiles,
+                                    // 8 v4 256x256, 9 v3 256x256 with a 5-stage ring, 10 v6 256x256 ping-pong,
+                                    // 11/12/13 timing ablations of v3 (no DMA / no barrier / no fragment
+                                    // reads in the loop: WRONG results, tools/ablate_gemm.py only)
     if ((force == 0 && v2_ok) || (force >= 2 && v2_ok)) {
         const bool v3 = force == 0 || force >= 5;
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
@@ -732,8 +983,25 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N;
         }
         const dim3 gy(1, pl.split, 1);
+        const bool v4 = force == 8, v5 = force == 9, v6 = force == 10;
 #define L2(BMv, BNv, AM, BMN)                                                                                     \
-    if (v3) hipLaunchKernelGGL((k_gemm3<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv), gy.y), \
+    if (v4 && BMv == 256 && BNv == 256)                                                                           \
+        hipLaunchKernelGGL((k_gemm4<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH2),   \
+                           (gemm2_lds<256, 256>()), st, pk);                                                      \
+    else if (force >= 11 && force <= 13 && BMv == 256 && BNv == 256) {                                              \
+        if (force == 11) hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 4, 1>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), \
+                                            dim3(NTH2), (gemm2_lds<256, 256>()), st, pk);                         \
+        else if (force == 12) hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 4, 2>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), \
+                                                 dim3(NTH2), (gemm2_lds<256, 256>()), st, pk);                    \
+        else hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 4, 3>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), \
+                                dim3(NTH2), (gemm2_lds<256, 256>()), st, pk);                                     \
+    } else if (v6 && BMv == 256 && BNv == 256)                                                                      \
+        hipLaunchKernelGGL((k_gemm6<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH2),   \
+                           (gemm2_lds<256, 256>()), st, pk);                                                      \
+    else if (v5 && BMv == 256 && BNv == 256)                                                                      \
+        hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 5>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y),  \
+                           dim3(NTH2), (gemm2_lds<256, 256, 5>()), st, pk);                                       \
+    else if (v3) hipLaunchKernelGGL((k_gemm3<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv), gy.y), \
                                dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk);                                        \
     else hipLaunchKernelGGL((k_gemm2<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv)),         \
                             dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk)

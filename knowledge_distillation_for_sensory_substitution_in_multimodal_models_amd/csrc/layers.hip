@@ -117,35 +117,39 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
     const int nch = D / 8;
     for (int i = threadIdx.x; i < 2 * D; i += NT) sacc[i] = 0.f;
     __syncthreads();
-    float pw[BWD_IT][8], pb[BWD_IT][8];
+    float pw[BWD_IT][8], pb[BWD_IT][8], wr[BWD_IT][8];
 #pragma unroll
-    for (int it = 0; it < BWD_IT; ++it)
+    for (int it = 0; it < BWD_IT; ++it) {
+        const int c = lane + it * 64;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { pw[it][j] = 0.f; pb[it][j] = 0.f; }
+        for (int j = 0; j < 8; ++j) { pw[it][j] = 0.f; pb[it][j] = 0.f; wr[it][j] = 0.f; }
+        if (c < nch) load8(w + c * 8, wr[it]);
+    }
     const int r_begin = blockIdx.x * rows_per_block;
     const int r_end = min(R, r_begin + rows_per_block);
     for (int row = r_begin + wv; row < r_end; row += 4) {
         const bf16* xr = x + (int64_t)row * ldx;
         const bf16* gr = dy + (int64_t)row * lddy;
         const float mean = RMS ? 0.f : mean_in[row], rstd = rstd_in[row];
-        float a1 = 0.f, a2 = 0.f;
+        bf16x8 xs[BWD_IT], gs[BWD_IT];   // the row stays in registers for the second pass
 #pragma unroll
         for (int it = 0; it < BWD_IT; ++it) {
             const int c = lane + it * 64;
-            if (c < nch) {
-                float xv[8], dv[8], wv8[8];
-                load8(xr + c * 8, xv);
-                load8(gr + c * 8, dv);
-                load8(w + c * 8, wv8);
+            if (c < nch) { xs[it] = *(const bf16x8*)(xr + c * 8); gs[it] = *(const bf16x8*)(gr + c * 8); }
+            else { xs[it] = (bf16x8){}; gs[it] = (bf16x8){}; }
+        }
+        float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float xh = (xv[j] - mean) * rstd;
-                    const float g = dv[j] * wv8[j];
-                    a1 += g;
-                    a2 += g * xh;
-                    pw[it][j] += dv[j] * xh;
-                    pb[it][j] += dv[j];
-                }
+        for (int it = 0; it < BWD_IT; ++it) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float xv = (float)xs[it][j], dv = (float)gs[it][j];
+                const float xh = (xv - mean) * rstd;
+                const float g = dv * wr[it][j];
+                a1 += g;
+                a2 += g * xh;
+                pw[it][j] += dv * xh;
+                pb[it][j] += dv;
             }
         }
         a1 = wave_sum(a1) / D;
@@ -155,14 +159,11 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
         for (int it = 0; it < BWD_IT; ++it) {
             const int c = lane + it * 64;
             if (c < nch) {
-                float xv[8], dv[8], wv8[8], o[8];
-                load8(xr + c * 8, xv);
-                load8(gr + c * 8, dv);
-                load8(w + c * 8, wv8);
+                float o[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float xh = (xv[j] - mean) * rstd;
-                    o[j] = rstd * (dv[j] * wv8[j] - (RMS ? 0.f : a1) - xh * a2);
+                    const float xh = ((float)xs[it][j] - mean) * rstd;
+                    o[j] = rstd * ((float)gs[it][j] * wr[it][j] - (RMS ? 0.f : a1) - xh * a2);
                 }
                 if (dx_accum) {
                     float prev[8];
@@ -191,88 +192,117 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
     }
 }
 
-// out[d] (+)= sum_p part[p][d]
-__global__ void k_reduce_parts(const float* __restrict__ part, int P, int D, float* __restrict__ out, int accum) {
-    const int d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= D) return;
+// out[d] (+)= sum_p part[p][d]: 64 columns x 16 row lanes per 1024-thread block, LDS tree
+__global__ void __launch_bounds__(1024) k_reduce_parts(const float* __restrict__ part, int P, int D,
+                                                       float* __restrict__ out, int accum) {
+    __shared__ float red[16][65];
+    const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+    const int d = blockIdx.x * 64 + cx;
     float s = 0.f;
-    for (int p = 0; p < P; ++p) s += part[(int64_t)p * D + d];
-    out[d] = accum ? out[d] + s : s;
+    if (d < D)
+        for (int p = ry; p < P; p += 16) s += part[(int64_t)p * D + d];
+    red[ry][cx] = s;
+    __syncthreads();
+    for (int h = 8; h > 0; h >>= 1) {
+        if (ry < h) red[ry][cx] += red[ry + h][cx];
+        __syncthreads();
+    }
+    if (ry == 0 && d < D) out[d] = accum ? out[d] + red[0][cx] : red[0][cx];
 }
 
 // ------------------------------------------------------------------ q/k/v ----
 // qkv [M = B*S, (nq + 2 nkv) * hd] -> q [B,nq,S,HDP], k/v [B,nkv,S,HDP] (zero pad),
 // with RoPE (rotate_half convention) on q and k when cos/sin tables are given.
+// One thread per (token, head, VEC-wide chunk of the first half): the chunk and its
+// rotate_half partner (i + hd/2) are read, rotated and written as VEC-wide vectors;
+// chunks past hd/2 zero the padding [hd, hdp).
+template <int VEC>
 __global__ void k_qkv_split(const bf16* __restrict__ qkv, int64_t ld, bf16* __restrict__ q, bf16* __restrict__ k,
                             bf16* __restrict__ v, const float* __restrict__ cos_t, const float* __restrict__ sin_t,
                             int B, int S, int nq, int nkv, int hd, int hdp) {
-    // one thread per (token, head, pair i < hdp/2)
+    typedef bf16 vec_t __attribute__((ext_vector_type(VEC)));
     const int heads = nq + 2 * nkv;
-    const int half = hdp / 2, hh = hd / 2;
-    const int64_t total = (int64_t)B * S * heads * half;
+    const int hh = hd / 2;
+    const int nch = hh / VEC, npad = (hdp - hd) / VEC, per = nch + npad;
+    const int64_t total = (int64_t)B * S * heads * per;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
-        const int i = (int)(idx % half);
-        const int64_t th = idx / half;
+        const int ci = (int)(idx % per);
+        const int64_t th = idx / per;
         const int head = (int)(th % heads);
         const int64_t tok = th / heads;
         const int s = (int)(tok % S), b = (int)(tok / S);
         bf16* dst;
-        int hidx;
-        if (head < nq) { dst = q; hidx = head; }
-        else if (head < nq + nkv) { dst = k; hidx = head - nq; }
-        else { dst = v; hidx = head - nq - nkv; }
-        const int nh = head < nq ? nq : nkv;
+        int hidx, nh;
+        if (head < nq) { dst = q; hidx = head; nh = nq; }
+        else if (head < nq + nkv) { dst = k; hidx = head - nq; nh = nkv; }
+        else { dst = v; hidx = head - nq - nkv; nh = nkv; }
         bf16* drow = dst + (((int64_t)b * nh + hidx) * S + s) * hdp;
-        // element pair (i, i + hd/2) for i < hd/2; padding columns hd.. zeroed
-        if (i < hh) {
+        if (ci < nch) {
+            const int i = ci * VEC;
             const bf16* srow = qkv + tok * ld + (int64_t)head * hd;
-            float x1 = (float)srow[i], x2 = (float)srow[i + hh];
+            vec_t a = *(const vec_t*)(srow + i), c2 = *(const vec_t*)(srow + i + hh);
             if (cos_t && head < nq + nkv) {
-                const float c = cos_t[(int64_t)s * hh + i], sn = sin_t[(int64_t)s * hh + i];
-                const float y1 = x1 * c - x2 * sn, y2 = x2 * c + x1 * sn;
-                x1 = y1; x2 = y2;
+                const float* cr = cos_t + (int64_t)s * hh + i;
+                const float* sr = sin_t + (int64_t)s * hh + i;
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) {
+                    const float x1 = (float)a[e], x2 = (float)c2[e], cs = cr[e], sn = sr[e];
+                    a[e] = (bf16)(x1 * cs - x2 * sn);
+                    c2[e] = (bf16)(x2 * cs + x1 * sn);
+                }
             }
-            drow[i] = (bf16)x1;
-            drow[i + hh] = (bf16)x2;
+            *(vec_t*)(drow + i) = a;
+            *(vec_t*)(drow + i + hh) = c2;
         } else {
-            // zero the padding [hd, hdp): thread i in [hh, half) covers 2 columns
-            const int c0 = hd + 2 * (i - hh);
-            if (c0 < hdp) drow[c0] = (bf16)0.f;
-            if (c0 + 1 < hdp) drow[c0 + 1] = (bf16)0.f;
+            *(vec_t*)(drow + hd + (ci - nch) * VEC) = (vec_t){};
         }
     }
 }
 
-// inverse: dq (fp32, [B,nq,S,HDP]), dk/dv (bf16 [B,nkv,S,HDP]) -> dqkv [M, (nq+2nkv)*hd]
+// inverse: dq (fp32, [B,nq,S,HDP]), dk/dv (bf16 [B,nkv,S,HDP]) -> dqkv [M, (nq+2nkv)*hd],
+// VEC-wide chunks of the first half and their partners, transposed rotation
+template <int VEC>
 __global__ void k_qkv_merge(const float* __restrict__ dq, const bf16* __restrict__ dk, const bf16* __restrict__ dv,
                             bf16* __restrict__ dqkv, int64_t ld, const float* __restrict__ cos_t,
                             const float* __restrict__ sin_t, int B, int S, int nq, int nkv, int hd, int hdp) {
-    const int heads = nq + 2 * nkv, hh = hd / 2;
-    const int64_t total = (int64_t)B * S * heads * hh;
+    typedef bf16 vec_t __attribute__((ext_vector_type(VEC)));
+    const int heads = nq + 2 * nkv, hh = hd / 2, nch = hh / VEC;
+    const int64_t total = (int64_t)B * S * heads * nch;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
-        const int i = (int)(idx % hh);
-        const int64_t th = idx / hh;
+        const int i = (int)(idx % nch) * VEC;
+        const int64_t th = idx / nch;
         const int head = (int)(th % heads);
         const int64_t tok = th / heads;
         const int s = (int)(tok % S), b = (int)(tok / S);
-        float g1, g2;
+        float g1[VEC], g2[VEC];
         if (head < nq) {
             const float* r = dq + (((int64_t)b * nq + head) * S + s) * hdp;
-            g1 = r[i]; g2 = r[i + hh];
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) { g1[e] = r[i + e]; g2[e] = r[i + hh + e]; }
         } else {
             const bool isk = head < nq + nkv;
             const int hidx = isk ? head - nq : head - nq - nkv;
             const bf16* r = (isk ? dk : dv) + (((int64_t)b * nkv + hidx) * S + s) * hdp;
-            g1 = (float)r[i]; g2 = (float)r[i + hh];
+            const vec_t a = *(const vec_t*)(r + i), c2 = *(const vec_t*)(r + i + hh);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) { g1[e] = (float)a[e]; g2[e] = (float)c2[e]; }
         }
         if (cos_t && head < nq + nkv) {  // transpose of the rotation
-            const float c = cos_t[(int64_t)s * hh + i], sn = sin_t[(int64_t)s * hh + i];
-            const float y1 = g1 * c + g2 * sn, y2 = g2 * c - g1 * sn;
-            g1 = y1; g2 = y2;
+            const float* cr = cos_t + (int64_t)s * hh + i;
+            const float* sr = sin_t + (int64_t)s * hh + i;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                const float c = cr[e], sn = sr[e];
+                const float y1 = g1[e] * c + g2[e] * sn, y2 = g2[e] * c - g1[e] * sn;
+                g1[e] = y1; g2[e] = y2;
+            }
         }
+        vec_t o1, o2;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) { o1[e] = (bf16)g1[e]; o2[e] = (bf16)g2[e]; }
         bf16* d = dqkv + tok * ld + (int64_t)head * hd;
-        d[i] = (bf16)g1;
-        d[i + hh] = (bf16)g2;
+        *(vec_t*)(d + i) = o1;
+        *(vec_t*)(d + i + hh) = o2;
     }
 }
 
@@ -408,19 +438,32 @@ __global__ void k_embed_bwd(const int64_t* __restrict__ ids, const int* __restri
 
 // ---------------------------------------------------------------- colsum ----
 // out[n] (+)= sum_m dy[m][n] ; grid.x over 256-column groups of 8 (2048 cols), grid.y row chunks
-__global__ void k_colsum(const bf16* __restrict__ dy, int64_t ld, int M, int N, float* __restrict__ out, int rows_per) {
-    const int c = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
-    if (c >= N) return;
+__global__ void __launch_bounds__(256) k_colsum(const bf16* __restrict__ dy, int64_t ld, int M, int N,
+                                                float* __restrict__ out, int rows_per) {
+    // 32 eight-column chunks x 8 row lanes; a wave reads 2 rows x 512 contiguous bytes
+    __shared__ float red[8][32 * 8 + 4];
+    const int cx = threadIdx.x & 31, ry = threadIdx.x >> 5;
+    const int c = (blockIdx.x * 32 + cx) * 8;
     const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int r = r0; r < r1; ++r) {
-        float f[8];
-        load8(dy + (int64_t)r * ld + c, f);
+    if (c < N) {
+#pragma unroll 4
+        for (int r = r0 + ry; r < r1; r += 8) {
+            float f[8];
+            load8(dy + (int64_t)r * ld + c, f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] += f[j];
+            for (int j = 0; j < 8; ++j) s[j] += f[j];
+        }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(out + c + j, s[j]);
+    for (int j = 0; j < 8; ++j) red[ry][cx * 8 + j] = s[j];
+    __syncthreads();
+    const int col = threadIdx.x;   // 256 columns of the block
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 8; ++y) t += red[y][col];
+    const int gc = blockIdx.x * 256 + col;
+    if (gc < N) atomicAdd(out + gc, t);
 }
 
 // ------------------------------------------------------- row-group mean ----
@@ -626,9 +669,11 @@ int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const vo
     return KD_OK;
 }
 
+// workgroups of k_norm_bwd: ~8 rows each (2 per wave), at most 512 (2 per CU)
+static int norm_bwd_blocks(int R) { return std::max(1, std::min(512, (R + 7) / 8)); }
+
 size_t norm_bwd_ws(int R, int D) {
-    const int nb = R < 512 ? (R + 3) / 4 : 128;
-    return (size_t)nb * D * 4 * 2;
+    return (size_t)norm_bwd_blocks(R) * D * 4 * 2;
 }
 
 int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
@@ -636,7 +681,7 @@ int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const vo
                     void* ws, size_t ws_bytes, int R, int D, void* stream) {
     KD_CHECK_ARG(x && w && dy && rstd && dx && (rms || mean), "norm_bwd: null pointer");
     KD_CHECK_SHAPE(D % 8 == 0 && D <= 2048, "norm_bwd: D must be a multiple of 8, <= 2048");
-    const int nb = R < 512 ? (R + 3) / 4 : 128;
+    const int nb = norm_bwd_blocks(R);
     const int rows_per = (R + nb - 1) / nb;
     if (ws_bytes < (size_t)nb * D * 8) return fail(KD_ERR_WORKSPACE, "norm_bwd: workspace");
     float* dwp = (float*)ws;
@@ -650,8 +695,8 @@ int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const vo
                             (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,
                             db ? dbp : nullptr, R, D, rows_per);
     KD_LAUNCH_CHECK("k_norm_bwd");
-    if (dw) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 255) / 256), dim3(256), 0, st, dwp, nb, D, dw, accum_w);
-    if (db) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 255) / 256), dim3(256), 0, st, dbp, nb, D, db, accum_w);
+    if (dw) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 63) / 64), dim3(1024), 0, st, dwp, nb, D, dw, accum_w);
+    if (db) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 63) / 64), dim3(1024), 0, st, dbp, nb, D, db, accum_w);
     KD_LAUNCH_CHECK("k_reduce_parts");
     return KD_OK;
 }
@@ -660,9 +705,19 @@ int launch_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, con
                      int B, int S, int nq, int nkv, int hd, int hdp, void* stream) {
     KD_CHECK_ARG(qkv && q && k && v, "qkv_split: null pointer");
     KD_CHECK_SHAPE(hd % 2 == 0 && hdp >= hd && hdp % 2 == 0, "qkv_split: head dims");
-    const int64_t work = (int64_t)B * S * (nq + 2 * nkv) * (hdp / 2);
-    hipLaunchKernelGGL(k_qkv_split, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), (const bf16*)qkv, ld, (bf16*)q,
-                       (bf16*)k, (bf16*)v, cos_t, sin_t, B, S, nq, nkv, hd, hdp);
+    const int hh = hd / 2;
+    auto ok = [&](int vec) {
+        const uintptr_t al = (uintptr_t)vec * 2 - 1;
+        return hh % vec == 0 && (hdp - hd) % vec == 0 && ld % vec == 0 && hdp % vec == 0 &&
+               !((uintptr_t)qkv & al) && !((uintptr_t)q & al) && !((uintptr_t)k & al) && !((uintptr_t)v & al);
+    };
+    const int vec = ok(8) ? 8 : ok(4) ? 4 : ok(2) ? 2 : 1;
+    const int64_t work = (int64_t)B * S * (nq + 2 * nkv) * (hh / vec + (hdp - hd) / vec);
+#define LQS(VEC)                                                                                                 \
+    hipLaunchKernelGGL(k_qkv_split<VEC>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), (const bf16*)qkv, ld, \
+                       (bf16*)q, (bf16*)k, (bf16*)v, cos_t, sin_t, B, S, nq, nkv, hd, hdp)
+    if (vec == 8) LQS(8); else if (vec == 4) LQS(4); else if (vec == 2) LQS(2); else LQS(1);
+#undef LQS
     KD_LAUNCH_CHECK("k_qkv_split");
     return KD_OK;
 }
@@ -670,9 +725,20 @@ int launch_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, con
 int launch_qkv_merge(const float* dq, const void* dk, const void* dv, void* dqkv, int64_t ld, const float* cos_t,
                      const float* sin_t, int B, int S, int nq, int nkv, int hd, int hdp, void* stream) {
     KD_CHECK_ARG(dq && dk && dv && dqkv, "qkv_merge: null pointer");
-    const int64_t work = (int64_t)B * S * (nq + 2 * nkv) * (hd / 2);
-    hipLaunchKernelGGL(k_qkv_merge, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), dq, (const bf16*)dk,
-                       (const bf16*)dv, (bf16*)dqkv, ld, cos_t, sin_t, B, S, nq, nkv, hd, hdp);
+    KD_CHECK_SHAPE(hd % 2 == 0 && hdp >= hd, "qkv_merge: head dims");
+    const int hh = hd / 2;
+    auto ok = [&](int vec) {
+        const uintptr_t al = (uintptr_t)vec * 2 - 1;
+        return hh % vec == 0 && ld % vec == 0 && hdp % vec == 0 && !((uintptr_t)dqkv & al) && !((uintptr_t)dk & al) &&
+               !((uintptr_t)dv & al);
+    };
+    const int vec = ok(8) ? 8 : ok(4) ? 4 : ok(2) ? 2 : 1;
+    const int64_t work = (int64_t)B * S * (nq + 2 * nkv) * (hh / vec);
+#define LQM(VEC)                                                                                                   \
+    hipLaunchKernelGGL(k_qkv_merge<VEC>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), dq, (const bf16*)dk, \
+                       (const bf16*)dv, (bf16*)dqkv, ld, cos_t, sin_t, B, S, nq, nkv, hd, hdp)
+    if (vec == 8) LQM(8); else if (vec == 4) LQM(4); else if (vec == 2) LQM(2); else LQM(1);
+#undef LQM
     KD_LAUNCH_CHECK("k_qkv_merge");
     return KD_OK;
 }
@@ -745,7 +811,7 @@ int launch_colsum(const void* dy, int64_t ld, int M, int N, float* out, int accu
     hipStream_t st = as_stream(stream);
     if (!accumulate && hipMemsetAsync(out, 0, (size_t)N * 4, st) != hipSuccess) return fail(KD_ERR_LAUNCH, "colsum memset");
     const int rows_per = 64;
-    dim3 grid((N / 8 + 255) / 256, (M + rows_per - 1) / rows_per);
+    dim3 grid((N + 255) / 256, (M + rows_per - 1) / rows_per);
     hipLaunchKernelGGL(k_colsum, grid, dim3(256), 0, st, (const bf16*)dy, ld, M, N, out, rows_per);
     KD_LAUNCH_CHECK("k_colsum");
     return KD_OK;

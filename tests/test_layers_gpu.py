@@ -25,7 +25,8 @@ def _close(got, ref, tol=1e-2):
     assert bool((err <= bound).all()), f"max err {err.max().item():.3e}"
 
 
-@pytest.mark.parametrize("rms,R,D", [(False, 300, 1152), (True, 257, 896), (True, 64, 3584), (False, 10, 64)])
+@pytest.mark.parametrize("rms,R,D", [(False, 300, 1152), (True, 257, 896), (True, 64, 3584), (False, 10, 64),
+                                     (True, 6144, 896), (False, 5832, 1152)])
 def test_norm_fwd_bwd(rms, R, D, dev):
     ops = _ops()
     x = _r(R, D, seed=1, dev=dev)
@@ -59,10 +60,14 @@ def _rope_tables(S, hd, theta=1e6):
     return f.cos(), f.sin()
 
 
-def test_qkv_split_rope_and_merge(dev):
+@pytest.mark.parametrize("hd,off", [(64, 0), (128, 0), (64, 2), (64, 1)])
+def test_qkv_split_rope_and_merge(hd, off, dev):
+    """off > 0 views qkv at an element offset inside a wider buffer (ld not a multiple of
+    8, rows not 16-B aligned): the launcher must fall back to narrower vectors."""
     ops = _ops()
-    B, S, nq, nkv, hd, hdp = 2, 33, 4, 2, 64, 64
-    qkv = _r(B * S, (nq + 2 * nkv) * hd, seed=5, dev=dev)
+    B, S, nq, nkv, hdp = 2, 33, 4, 2, hd
+    W = (nq + 2 * nkv) * hd
+    qkv = _r(B * S, W + off, seed=5, dev=dev)[:, off:] if off else _r(B * S, W, seed=5, dev=dev)
     cos, sin = _rope_tables(S, hd)
     cos_d, sin_d = cos.to(dev), sin.to(dev)
     q, k, v = ops.qkv_split(qkv, B, S, nq, nkv, hd, hdp, cos_d, sin_d)
@@ -74,14 +79,17 @@ def test_qkv_split_rope_and_merge(dev):
     _close(q, xr[:, :nq])
     _close(k, xr[:, nq:nq + nkv])
     _close(v, x[:, nq + nkv:])
-    # merge is the transpose of split (incl. rotation): check <merge(g), x> == <g, split(x)>
-    dq = torch.randn(B, nq, S, hdp, device=dev)
+    # merge is the transpose of split: dx = g*cos + rot^T(g*sin), rot^T([y1, y2]) = [y2, -y1]
+    g = torch.Generator().manual_seed(11)
+    dq = torch.randn(B, nq, S, hdp, generator=g).to(dev)
     dk = _r(B, nkv, S, hdp, seed=6, dev=dev)
     dv = _r(B, nkv, S, hdp, seed=7, dev=dev)
     dqkv = ops.qkv_merge(dq, dk, dv, B, S, nq, nkv, hd, hdp, cos_d, sin_d)
-    lhs = (dqkv.float() * qkv.float()).sum()
-    rhs = (dq * q.float()).sum() + (dk.float() * k.float()).sum() + (dv.float() * v.float()).sum()
-    assert abs(lhs.item() - rhs.item()) < 2e-2 * (abs(rhs.item()) + 10)
+    assert dqkv.shape == qkv.shape
+    rot_t = lambda t: torch.cat([t[..., hd // 2:], -t[..., :hd // 2]], -1)
+    adj = lambda t: t * cc + rot_t(t * ss)
+    ref = torch.cat([adj(dq[..., :hd].float()), adj(dk[..., :hd].float()), dv[..., :hd].float()], 1)
+    _close(dqkv.view(B, S, nq + 2 * nkv, hd).permute(0, 2, 1, 3), ref)
 
 
 def test_qkv_split_vit_padding(dev):
@@ -173,6 +181,10 @@ def test_colsum_and_group_mean(dev):
     out = torch.ones(1152, device=dev)
     ops.colsum(dy, out, accumulate=True)
     assert torch.allclose(out, 1 + dy.float().sum(0), rtol=1e-4, atol=1e-3)
+    dy = _r(6141, 896, seed=22, dev=dev)
+    out = torch.empty(896, device=dev)
+    ops.colsum(dy, out, accumulate=False)
+    assert torch.allclose(out, dy.float().sum(0), rtol=1e-4, atol=1e-2)
     x = _r(4 * 729, 1152, seed=21, dev=dev)
     pm = ops.row_group_mean(x, 4, 729)
     assert torch.allclose(pm, x.float().view(4, 729, 1152).mean(1), atol=1e-5)

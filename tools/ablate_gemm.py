@@ -1,0 +1,36 @@
+"""Timing ablations of the v3 GEMM main loop (variants 11/12/13 compute WRONG results on
+purpose: no in-loop DMA / no barrier / no fragment reads) against the real kernel.
+    python tools/ablate_gemm.py [M N K]"""
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops  # noqa: E402
+
+M, N, K = (int(x) for x in sys.argv[1:4]) if len(sys.argv) > 3 else (6144, 37888, 3584)
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+a = torch.randn(M, K, device=dev, generator=g).bfloat16()
+b = torch.randn(N, K, device=dev, generator=g).bfloat16()
+out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+names = {5: "v3", 11: "v3 no-DMA", 12: "v3 no-barrier", 13: "v3 no-frag-reads", 9: "v3 5-stage", 10: "v6 ping-pong",
+         8: "v4 BK64"}
+res = {v: [] for v in names}
+for rnd in range(3):
+    for v in names:
+        f = lambda: ops.gemm(a, b, out=out, variant=v, split_k=1)
+        f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        res[v].append(e0.elapsed_time(e1) / 10)
+fl = 2.0 * M * N * K
+for v, n in names.items():
+    t = min(res[v])
+    print(f"{n:18s} {t:8.4f} ms {fl / t / 1e9:7.1f} TF/s  (rounds {[round(x, 4) for x in res[v]]})", flush=True)

@@ -47,7 +47,7 @@ for sh in shapes:
     fl = 2.0 * M * N * K
     auto = timeit(lambda: ops.gemm(a, b, out=out, accumulate=acc))
     res = {}
-    for var in (5, 6, 7):
+    for var in (5, 6, 7, 8, 9, 10):
         for sk in (1, 2, 3, 4, 6, 8, 12, 16):
             if sk > 1 and (K // 32) // sk < 4:
                 continue
@@ -57,6 +57,6 @@ for sh in shapes:
     best = min(res, key=res.get)
     row = dict(shape=sh, auto_ms=round(auto, 4), auto_tf=round(fl / auto / 1e9, 1), best=list(best),
                best_ms=round(res[best], 4), best_tf=round(fl / res[best] / 1e9, 1),
-               s1={v: round(res[(v, 1)], 4) for v in (5, 6, 7)},
+               s1={v: round(res[(v, 1)], 4) for v in (5, 6, 7, 8, 9, 10)},
                all={f"{v}/{s}": round(t, 4) for (v, s), t in sorted(res.items())})
     print(json.dumps(row), flush=True)
