@@ -309,6 +309,7 @@ template <int N> __device__ __forceinline__ void wait_vm() {
     else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
     else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
     else static_assert(N == 0, "unsupported vmcnt");
 }
 
@@ -322,7 +323,7 @@ constexpr size_t gemm2_lds() {
 }
 
 
-template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT>
+template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2>
 __device__ __forceinline__ void epilogue2(const GemmP& p, f32x4 (&acc)[MT][NT], char* smem, int m0, int n0, int wm, int wn,
                                           int lane, int tid) {
     // ---------------------------------------------------------------- epilogue
@@ -360,7 +361,7 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, f32x4 (&acc)[MT][NT], 
                 }
         __syncthreads();
         constexpr int CPR = BN / 8;
-        for (int idx = tid; idx < BM * CPR; idx += NTH2) {
+        for (int idx = tid; idx < BM * CPR; idx += NTHR) {
             const int lr = idx / CPR, c = idx % CPR;
             const int row = m0 + lr, col = n0 + c * 8;
             if (row >= p.M || col >= p.N) continue;
@@ -406,7 +407,7 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, f32x4 (&acc)[MT][NT], 
             }
             __syncthreads();
             constexpr int CPR = BN / 4;
-            for (int idx = tid; idx < HR * CPR; idx += NTH2) {
+            for (int idx = tid; idx < HR * CPR; idx += NTHR) {
                 const int lr = idx / CPR, c = idx % CPR;
                 const int row = m0 + h * HR + lr, col = n0 + c * 4;
                 if (row >= p.M || col >= p.N) continue;
@@ -835,6 +836,270 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm6(GemmP p_) {
     epilogue2<256, 256, 2, 4, 128, 64, 8, 4>(p, acc, smem, m0, n0, wm, wn, lane, tid);
 }
 
+// =============================================================================
+// v5: 256x256 tile, BK = 64, FOUR waves (one per SIMD) of 128x128 each, two 64 KiB LDS
+// stages (v4's image layouts). One wave per SIMD, so each wave pipelines its own work:
+//   step t (F0 = kk 0 fragments of stage t, already read):
+//     lgkmcnt(0) ; 64 MFMA(F0), the first 32 interleaved with the 16 DMA instructions
+//     of stage t+1 (-> the other buffer) and the 16 reads of F1 (kk 1 of stage t)
+//     lgkmcnt(0) ; 32 MFMA(F1, rows 0..63)
+//     vmcnt(0) ; s_barrier      [stage t+1 landed for everyone; stage t-1's buffer free]
+//     32 MFMA(F1, rows 64..127) interleaved with the 16 reads of F0 of stage t+1
+// WAR: the buffer refilled in step t held stage t-1, whose last reads (F1 of t-1) every
+// wave retired before the barrier of step t-1. RAW: stage t+1 is read only after the
+// barrier of step t, behind every wave's vmcnt(0).
+// =============================================================================
+constexpr int NTH5 = 256;
+
+// one 1-KiB wave-instruction (index i of 32) of a BK=64 operand stage (v4 layout)
+template <bool MN>
+__device__ __forceinline__ void dma5(char* tile, __amdgpu_buffer_rsrc_t rs, int64_t ld, int rows_total, int r0,
+                                     int k0, int K, int kvalid, int i, int lane) {
+    if (!MN) {
+        const int row = i * 8 + (lane >> 3);
+        const int gc = (lane & 7) ^ ((row >> 1) & 7);
+        const int k = k0 + gc * 8;
+        const uint32_t voff = (k < K) ? (uint32_t)(((int64_t)row * ld + k) * 2) : OOB;
+        dma16(rs, tile + i * 1024, voff);
+    } else {
+        const int kr = i * 2 + (lane >> 5);
+        const int gc = (lane & 31) ^ (int)sw_mn(kr);
+        const int row = r0 + gc * 8;
+        const uint32_t voff = (kr < kvalid && row < rows_total) ? (uint32_t)(((int64_t)kr * ld + gc * 8) * 2) : OOB;
+        dma16(rs, tile + i * 1024, voff);
+    }
+}
+
+template <bool A_MN, bool B_MN>
+__global__ void __launch_bounds__(NTH5, 1) k_gemm5(GemmP p_) {
+    GemmP p = p_;
+    if (gridDim.y > 1) {
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    constexpr int OPB = 256 * BK4 * 2, KTB = 2 * OPB;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    int tm, tn;
+    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A, 0), rsBk = make_rsrc(p.B, 0);
+    if (!A_MN) rsAk = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
+    if (!B_MN) rsBk = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
+    const int nk = (p.K + BK4 - 1) / BK4;
+    // descriptors of stage st: K-major fixed; MN-major per stage (k rows of the stage)
+    auto rs_of = [&](bool mn, const bf16* ptr, int64_t ld, int r0, __amdgpu_buffer_rsrc_t rk, int st, int& kvalid) {
+        if (!mn) { kvalid = BK4; return rk; }
+        const int k0 = st * BK4;
+        kvalid = max(0, min(BK4, p.K - k0));
+        return make_rsrc(ptr + (int64_t)min(k0, p.K) * ld + r0, rec_bytes(kvalid, ld));
+    };
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 f0a[8], f0b[8], f1a[8], f1b[8];
+    const int ra = wm * 128, cb = wn * 128;
+    {   // prologue: stage 0 -> buffer 0, F0(0)
+        int kva, kvb;
+        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, 0, kva);
+        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, 0, kvb);
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) {
+            dma5<A_MN>(smem, ra_, p.lda, p.M, m0, 0, p.K, kva, wid * 8 + s8, lane);
+            dma5<B_MN>(smem + OPB, rb_, p.ldb, p.N, n0, 0, p.K, kvb, wid * 8 + s8, lane);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f0a[i] = frag4<A_MN>(smem, ra + i * 16, 0, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f0b[j] = frag4<B_MN>(smem + OPB, cb + j * 16, 0, lane);
+    }
+    for (int t = 0; t < nk; ++t) {
+        const char* ta = smem + (t & 1) * KTB;
+        const char* tb = ta + OPB;
+        char* na = smem + ((t + 1) & 1) * KTB;
+        int kva, kvb;
+        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, t + 1, kva);
+        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, t + 1, kvb);
+        const int k1 = (t + 1) * BK4;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        // 64 MFMA(F0); the first 32 in pairs, each pair behind one DMA of stage t+1 and one
+        // F1 fragment read (order pinned with sched_barrier: the scheduler would bunch the DMA)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if (q < 8) dma5<A_MN>(na, ra_, p.lda, p.M, m0, k1, p.K, kva, wid * 8 + q, lane);
+            else dma5<B_MN>(na + OPB, rb_, p.ldb, p.N, n0, k1, p.K, kvb, wid * 8 + q - 8, lane);
+            if (q < 8) f1a[q] = frag4<A_MN>(ta, ra + q * 16, 1, lane);
+            else f1b[q - 8] = frag4<B_MN>(tb, cb + (q - 8) * 16, 1, lane);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int m = 2 * q + e, i = m >> 3, j = m & 7;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0a[i], f0b[j], acc[i][j], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int m = 32; m < 64; ++m)
+            acc[m >> 3][m & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0a[m >> 3], f0b[m & 7], acc[m >> 3][m & 7], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1a[i], f1b[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // 32 MFMA(F1, rows 64..127) in pairs, each behind one read of F0 of stage t+1
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if (q < 8) f0a[q] = frag4<A_MN>(na, ra + q * 16, 0, lane);
+            else f0b[q - 8] = frag4<B_MN>(na + OPB, cb + (q - 8) * 16, 0, lane);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int m = 2 * q + e, i = 4 + (m >> 3), j = m & 7;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1a[i], f1b[j], acc[i][j], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH5>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+// =============================================================================
+// v7: v3's 4-slot BK=32 LDS ring (three stages in flight) with v5's four waves of
+// 128x128 (half the fragment reads per MFMA of the 8-wave 128x64 layout).
+//   iteration t: lgkmcnt(0) [fragments of t in registers] ; vmcnt(2 stages x 8) [stage
+//   t+1 landed] ; s_barrier ; 64 MFMA(t) in 8 units of {1 DMA of stage t+4 -> slot t%4,
+//   2 fragment reads of stage t+1, 8 MFMA}, order pinned by sched_barrier.
+// WAR: slot t%4 was last read (fragments of t, during iteration t-1) before every wave's
+// lgkmcnt(0) + barrier of iteration t. RAW: stage t+1 is read after the barrier that
+// follows every wave's vmcnt for it. DMA past the last stage is issued anyway
+// (out-of-range, zero-fill) so the counts stay uniform.
+// =============================================================================
+template <bool MN>
+__device__ __forceinline__ void dma7(char* tile, __amdgpu_buffer_rsrc_t rs, int64_t ld, int rows_total, int r0, int k0,
+                                     int K, int kvalid, int i, int lane) {
+    if (!MN) {   // 256 rows x 64 B, 16 rows per 1-KiB instruction
+        const int row = 16 * i + (lane >> 2);
+        const int gc = (lane & 3) ^ f4(row);
+        const int k = k0 + gc * 8;
+        const uint32_t voff = (k < K) ? (uint32_t)(((int64_t)row * ld + k) * 2) : OOB;
+        dma16(rs, tile + i * 1024, voff);
+    } else {     // 32 k-rows x 512 B, 2 k-rows per instruction
+        const int kr = i * 2 + (lane >> 5);
+        const int gc = (lane & 31) ^ (int)sw_mn(kr);
+        const int row = r0 + gc * 8;
+        const uint32_t voff = (kr < kvalid && row < rows_total) ? (uint32_t)(((int64_t)kr * ld + gc * 8) * 2) : OOB;
+        dma16(rs, tile + i * 1024, voff);
+    }
+}
+
+template <bool A_MN, bool B_MN>
+__global__ void __launch_bounds__(NTH5, 1) k_gemm7(GemmP p_) {
+    GemmP p = p_;
+    if (gridDim.y > 1) {
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    constexpr int NS = 4, SA = 256 * BK2 * 2, SS = 2 * SA;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    int tm, tn;
+    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A, 0), rsBk = make_rsrc(p.B, 0);
+    if (!A_MN) rsAk = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
+    if (!B_MN) rsBk = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
+    const int nk = (p.K + BK2 - 1) / BK2;
+    auto rs_of = [&](bool mn, const bf16* ptr, int64_t ld, int r0, __amdgpu_buffer_rsrc_t rk, int st, int& kvalid) {
+        if (!mn) { kvalid = BK2; return rk; }
+        const int k0 = st * BK2;
+        kvalid = max(0, min(BK2, p.K - k0));
+        return make_rsrc(ptr + (int64_t)min(k0, p.K) * ld + r0, rec_bytes(kvalid, ld));
+    };
+    // DMA instruction u (0..7) of this wave for stage st: A instructions wid*4 + u (u < 4),
+    // B instructions wid*4 + u - 4
+    auto dma_u = [&](int st, int u, __amdgpu_buffer_rsrc_t ra_, __amdgpu_buffer_rsrc_t rb_, int kva, int kvb) {
+        char* base = smem + (st % NS) * SS;
+        if (u < 4) dma7<A_MN>(base, ra_, p.lda, p.M, m0, st * BK2, p.K, kva, wid * 4 + u, lane);
+        else dma7<B_MN>(base + SA, rb_, p.ldb, p.N, n0, st * BK2, p.K, kvb, wid * 4 + u - 4, lane);
+    };
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int ra = wm * 128, cb = wn * 128;
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+        int kva, kvb;
+        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, st, kva);
+        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, st, kvb);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dma_u(st, u, ra_, rb_, kva, kvb);
+    }
+    wait_vm<24>();   // stage 0 landed
+    __builtin_amdgcn_s_barrier();
+    bf16x8 xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xa[i] = frag2<256, A_MN>(smem, ra + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xb[j] = frag2<256, B_MN>(smem + SA, cb + j * 16, lane);
+
+#define KD_G7_STEP(CA, CB, NA, NB)                                                                           \
+    {                                                                                                         \
+        int kva, kvb;                                                                                         \
+        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, t + NS, kva);                                      \
+        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, t + NS, kvb);                                      \
+        const char* na = smem + ((t + 1) % NS) * SS;                                                          \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                    \
+        wait_vm<16>();                                                                                        \
+        __builtin_amdgcn_s_barrier();                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                                    \
+        _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
+            dma_u(t + NS, u, ra_, rb_, kva, kvb);                                                             \
+            NA[u] = frag2<256, A_MN>(na, ra + u * 16, lane);                                                  \
+            NB[u] = frag2<256, B_MN>(na + SA, cb + u * 16, lane);                                             \
+            __builtin_amdgcn_sched_barrier(0);                                                                \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                     \
+                acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CA[u], CB[j], acc[u][j], 0, 0, 0);        \
+            __builtin_amdgcn_sched_barrier(0);                                                                \
+        }                                                                                                     \
+    }
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+        KD_G7_STEP(xa, xb, ya, yb);
+        ++t;
+        KD_G7_STEP(ya, yb, xa, xb);
+        --t;
+    }
+    if (t < nk) KD_G7_STEP(xa, xb, ya, yb);
+#undef KD_G7_STEP
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH5>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
 // (alpha, alpha_dev, bias, aux, act, residual, accumulate), 4 columns per thread
 __global__ void k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p) {
@@ -894,7 +1159,7 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const double step[3] = {1.0, 0.70, 0.65};   // 256x256, 256x128, 128x256
     const double fixed[3] = {24.0, 12.0, 6.0};
     const int64_t nk = ceil_div(d->K, BK2);
-    const int fv = (d->variant >= 8 && d->variant <= 13) ? 0 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
+    const int fv = (d->variant >= 8 && d->variant <= 15) ? 0 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
     const bool split_ok = d->variant == 0 || d->variant >= 5;
     const double out_b = (double)M * N * ((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
                                           (d->residual ? 2 : 0) + (d->aux ? 2 : 0));
@@ -969,7 +1234,8 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     const int force = d->variant;   // 0 auto, 1 v1, 2/3/4 v2 256x256/256x128/128x256, 5/6/7 v3 same tiles,
                                     // 8 v4 256x256, 9 v3 256x256 with a 5-stage ring, 10 v6 256x256 ping-pong,
                                     // 11/12/13 timing ablations of v3 (no DMA / no barrier / no fragment
-                                    // reads in the loop: WRONG results, tools/ablate_gemm.py only)
+                                    // reads in the loop: WRONG results, tools/ablate_gemm.py only),
+                                    // 14 v5 256x256 four waves of 128x128, 15 v7 (v3 ring, 4 waves)
     if ((force == 0 && v2_ok) || (force >= 2 && v2_ok)) {
         const bool v3 = force == 0 || force >= 5;
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
@@ -983,10 +1249,16 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N;
         }
         const dim3 gy(1, pl.split, 1);
-        const bool v4 = force == 8, v5 = force == 9, v6 = force == 10;
+        const bool v4 = force == 8, v5 = force == 9, v6 = force == 10, v7 = force == 14, v8 = force == 15;
 #define L2(BMv, BNv, AM, BMN)                                                                                     \
     if (v4 && BMv == 256 && BNv == 256)                                                                           \
         hipLaunchKernelGGL((k_gemm4<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH2),   \
+                           (gemm2_lds<256, 256>()), st, pk);                                                      \
+    else if (v8 && BMv == 256 && BNv == 256)                                                                      \
+        hipLaunchKernelGGL((k_gemm7<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH5),   \
+                           (gemm2_lds<256, 256>()), st, pk);                                                      \
+    else if (v7 && BMv == 256 && BNv == 256)                                                                      \
+        hipLaunchKernelGGL((k_gemm5<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH5),   \
                            (gemm2_lds<256, 256>()), st, pk);                                                      \
     else if (force >= 11 && force <= 13 && BMv == 256 && BNv == 256) {                                              \
         if (force == 11) hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 4, 1>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), \

@@ -16,7 +16,7 @@ a = torch.randn(M, K, device=dev, generator=g).bfloat16()
 b = torch.randn(N, K, device=dev, generator=g).bfloat16()
 out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
 names = {5: "v3", 11: "v3 no-DMA", 12: "v3 no-barrier", 13: "v3 no-frag-reads", 9: "v3 5-stage", 10: "v6 ping-pong",
-         8: "v4 BK64"}
+         8: "v4 BK64", 14: "v5 4-wave", 15: "v7 ring 4-wave"}
 res = {v: [] for v in names}
 for rnd in range(3):
     for v in names:
