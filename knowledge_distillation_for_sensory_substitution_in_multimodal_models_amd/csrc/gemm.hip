@@ -230,8 +230,8 @@ __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
 
 
 // =============================================================================
-// v2: 256x256 (or 256x128 / 128x256) tile, 512 threads = 8 waves, BK = 32, a 4-stage
-// LDS-DMA ring with 3 stages in flight (counted vmcnt, raw s_barrier: the DMA of the
+// Stage layouts of the 256-row kernels (v3, v8). v3: 256x256 (or 256x128 / 128x256) tile,
+// 512 threads = 8 waves, BK = 32, a 4-stage LDS-DMA ring with 3 stages in flight (counted vmcnt, raw s_barrier: the DMA of the
 // next stages stays in flight across barriers), 1 workgroup per CU, and an epilogue
 // staged through LDS so every global store / residual load is a 16-B row chunk.
 // 256x256 halves the L2->CU bytes per FLOP of the 128x128 v1 tile (128 FLOP/B).
@@ -323,178 +323,144 @@ constexpr size_t gemm2_lds() {
 }
 
 
-template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2>
-__device__ __forceinline__ void epilogue2(const GemmP& p, f32x4 (&acc)[MT][NT], char* smem, int m0, int n0, int wm, int wn,
-                                          int lane, int tid) {
-    // ---------------------------------------------------------------- epilogue
-    float alpha = p.alpha;
-    if (p.alpha_dev) alpha *= *p.alpha_dev;
-    // alpha, bias, aux (pre-activation), activation in registers
+// Epilogue of the 256-row kernels. Every condition is wave-uniform and hoisted out of the
+// per-element loops (a per-element switch on the activation compiled to ~2,800 branches
+// and dominated the v8 tile time); the accumulators are only read (so v8's stay in the
+// AGPR file), one 16x16 tile at a time, into an LDS image that is then written out in
+// 16-B row chunks: pre = alpha*acc + bias -> [aux <- pre] -> C <- act(pre) (+ resid, + C).
+template <int ACT, int TM, int TN, int MT, int NT, bool F32>
+__device__ __forceinline__ void epi_to_lds(const f32x4 (&acc)[MT][NT], char* smem, int rs, float alpha, const float (&bcol)[NT],
+                                           int wm, int wn, int lane, int r_lo, int r_hi) {
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int col = n0 + wn * TN + j * 16 + (lane & 15);
-        float bcol = 0.f;
-        if (p.bias && col < p.N) bcol = p.bias_f32 ? ((const float*)p.bias)[col] : (float)((const bf16*)p.bias)[col];
+    for (int i = 0; i < MT; ++i) {
+        const int lr0 = wm * TM + i * 16;
+        if (lr0 < r_lo || lr0 >= r_hi) continue;
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int j = 0; j < NT; ++j) {
+            const f32x4 a = acc[i][j];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float v = acc[i][j][r] * alpha + bcol;
-                if (p.aux) {
-                    const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-                    if (row < p.M && col < p.N) p.aux[(int64_t)row * p.ld_aux + col] = (bf16)v;
-                }
-                acc[i][j][r] = apply_act(v, p.act);
+                const float v = apply_act(a[r] * alpha + bcol[j], ACT);
+                const int lr = lr0 - r_lo + (lane >> 4) * 4 + r;
+                const int lc = wn * TN + j * 16 + (lane & 15);
+                if (F32) *(float*)(smem + lr * rs + lc * 4) = v;
+                else *(bf16*)(smem + lr * rs + lc * 2) = (bf16)v;
             }
+        }
     }
-    if (!p.c_f32) {
-        constexpr int RS = BN * 2 + 16;   // padded LDS row (bytes)
+}
+
+template <int TM, int TN, int MT, int NT, bool F32>
+__device__ __forceinline__ void epi_to_lds_act(int act, const f32x4 (&acc)[MT][NT], char* smem, int rs, float alpha,
+                                               const float (&bcol)[NT], int wm, int wn, int lane, int r_lo, int r_hi) {
+    switch (act) {
+        case KD_ACT_GELU_TANH: epi_to_lds<KD_ACT_GELU_TANH, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+        case KD_ACT_GELU_ERF: epi_to_lds<KD_ACT_GELU_ERF, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+        case KD_ACT_SILU: epi_to_lds<KD_ACT_SILU, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+        default: epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+    }
+}
+
+// LDS image rows [0, ROWS) -> global rows m0 + row_off + lr, 16-B chunks (+ resid, + dst)
+template <int ROWS, int BN, int NTHR, bool F32, bool RES, bool ACC>
+__device__ __forceinline__ void epi_flush(const GemmP& p, const char* smem, int rs, void* dst_, int64_t ld, int m0, int n0,
+                                          int tid, bool full) {
+    constexpr int EPC = F32 ? 4 : 8;   // elements per 16-B chunk
+    constexpr int CPR = BN / EPC;
+#pragma unroll 4
+    for (int idx = tid; idx < ROWS * CPR; idx += NTHR) {
+        const int lr = idx / CPR, c = idx % CPR;
+        const int row = m0 + lr, col = n0 + c * EPC;
+        if (!full && (row >= p.M || col >= p.N)) continue;
+        const int rr = RES ? (p.res_mod > 0 ? row % p.res_mod : row) : 0;
+        if (F32) {
+            f32x4 v = *(const f32x4*)(smem + lr * rs + c * 16);
+            float* o = (float*)dst_ + (int64_t)row * ld + col;
+            if (RES) {
+                const bf16x4 rv = *(const bf16x4*)(p.resid + (int64_t)rr * p.ldr + col);
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int lr = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-                    const int lc = wn * TN + j * 16 + (lane & 15);
-                    *(bf16*)(smem + lr * RS + lc * 2) = (bf16)acc[i][j][r];
-                }
-        __syncthreads();
-        constexpr int CPR = BN / 8;
-        for (int idx = tid; idx < BM * CPR; idx += NTHR) {
-            const int lr = idx / CPR, c = idx % CPR;
-            const int row = m0 + lr, col = n0 + c * 8;
-            if (row >= p.M || col >= p.N) continue;
-            bf16x8 v = *(const bf16x8*)(smem + lr * RS + c * 16);
-            bf16* dst = (bf16*)p.C + (int64_t)row * p.ldc + col;
-            if (p.resid || p.accumulate) {
+                for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+            }
+            if (ACC) v += *(const f32x4*)o;
+            *(f32x4*)o = v;
+        } else {
+            bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
+            bf16* o = (bf16*)dst_ + (int64_t)row * ld + col;
+            if (RES || ACC) {
                 float f[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) f[e] = (float)v[e];
-                if (p.resid) {
-                    const int rr = p.res_mod > 0 ? row % p.res_mod : row;
-                    bf16x8 rv = *(const bf16x8*)(p.resid + (int64_t)rr * p.ldr + col);
+                if (RES) {
+                    const bf16x8 rv = *(const bf16x8*)(p.resid + (int64_t)rr * p.ldr + col);
 #pragma unroll
                     for (int e = 0; e < 8; ++e) f[e] += (float)rv[e];
                 }
-                if (p.accumulate) {
-                    bf16x8 cv = *(const bf16x8*)dst;
+                if (ACC) {
+                    const bf16x8 cv = *(const bf16x8*)o;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) f[e] += (float)cv[e];
                 }
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] = (bf16)f[e];
             }
-            *(bf16x8*)dst = v;
+            *(bf16x8*)o = v;
         }
+    }
+}
+
+template <int ROWS, int BN, int NTHR, bool F32>
+__device__ __forceinline__ void epi_flush_sel(const GemmP& p, const char* smem, int rs, void* dst, int64_t ld, int m0, int n0,
+                                              int tid, bool full, bool res, bool accum) {
+    if (!res && !accum) epi_flush<ROWS, BN, NTHR, F32, false, false>(p, smem, rs, dst, ld, m0, n0, tid, full);
+    else if (res && !accum) epi_flush<ROWS, BN, NTHR, F32, true, false>(p, smem, rs, dst, ld, m0, n0, tid, full);
+    else if (!res && accum) epi_flush<ROWS, BN, NTHR, F32, false, true>(p, smem, rs, dst, ld, m0, n0, tid, full);
+    else epi_flush<ROWS, BN, NTHR, F32, true, true>(p, smem, rs, dst, ld, m0, n0, tid, full);
+}
+
+// HAS_ACT: the activation epilogue is instantiated for the forward (K-major x K-major) kernels
+// only; the launcher rejects an activation with MN-major operands or an fp32 output.
+template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2, bool HAS_ACT = true>
+__device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int n0, int wm,
+                                          int wn, int lane, int tid) {
+    const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
+    float alpha = p.alpha;
+    if (p.alpha_dev) alpha *= *p.alpha_dev;
+    float bcol[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bcol[j] = 0.f;
+    if (p.bias) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int col = min(n0 + wn * TN + j * 16 + (lane & 15), p.N - 1);
+            bcol[j] = p.bias_f32 ? ((const float*)p.bias)[col] : (float)((const bf16*)p.bias)[col];
+        }
+    }
+    constexpr int RS16 = BN * 2 + 16, RS32 = BN * 4 + 16;
+    if (p.aux) {   // pre-activation (bf16) for the backward
+        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        __syncthreads();
+        epi_flush<BM, BN, NTHR, false, false, false>(p, smem, RS16, p.aux, p.ld_aux, m0, n0, tid, full);
+        __syncthreads();
+    }
+    const bool res = p.resid != nullptr, accum = p.accumulate != 0;
+    if (!p.c_f32) {
+        if (HAS_ACT) epi_to_lds_act<TM, TN, MT, NT, false>(p.act, acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        else epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        __syncthreads();
+        epi_flush_sel<BM, BN, NTHR, false>(p, smem, RS16, p.C, p.ldc, m0, n0, tid, full, res, accum);
     } else {
-        constexpr int RS = BN * 4 + 16;
-        constexpr int HR = BM / 2;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                const int lr0 = wm * TM + i * 16;
-                if (lr0 < h * HR || lr0 >= (h + 1) * HR) continue;
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int lr = lr0 + (lane >> 4) * 4 + r - h * HR;
-                        const int lc = wn * TN + j * 16 + (lane & 15);
-                        *(float*)(smem + lr * RS + lc * 4) = acc[i][j][r];
-                    }
-            }
+        for (int h = 0; h < 2; ++h) {   // fp32: two half tiles of BM/2 rows
+            epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, true>(acc, smem, RS32, alpha, bcol, wm, wn, lane, h * BM / 2, (h + 1) * BM / 2);
             __syncthreads();
-            constexpr int CPR = BN / 4;
-            for (int idx = tid; idx < HR * CPR; idx += NTHR) {
-                const int lr = idx / CPR, c = idx % CPR;
-                const int row = m0 + h * HR + lr, col = n0 + c * 4;
-                if (row >= p.M || col >= p.N) continue;
-                f32x4 v = *(const f32x4*)(smem + lr * RS + c * 16);
-                float* dst = (float*)p.C + (int64_t)row * p.ldc + col;
-                if (p.resid) {
-                    const int rr = p.res_mod > 0 ? row % p.res_mod : row;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] += (float)p.resid[(int64_t)rr * p.ldr + col + e];
-                }
-                if (p.accumulate) v += *(const f32x4*)dst;
-                *(f32x4*)dst = v;
-            }
+            epi_flush_sel<BM / 2, BN, NTHR, true>(p, smem, RS32, p.C, p.ldc, m0 + h * BM / 2, n0, tid, full, res, accum);
             __syncthreads();
         }
     }
 }
-
-template <int BM, int BN, bool A_MN, bool B_MN>
-__global__ void __launch_bounds__(NTH2, 1) k_gemm2(GemmP p) {
-    constexpr int WM = (BM == 256 && BN == 256) ? 2 : (BM == 256 ? 4 : 2);
-    constexpr int WN = 8 / WM;
-    constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NT = TN / 16;
-    constexpr int SA = BM * BK2 * 2, SB = BN * BK2 * 2, SS = SA + SB;
-    constexpr int G = (BM / 16) / 8 + (BN / 16) / 8;   // DMA wave-instructions per stage per wave
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid / WN, wn = wid % WN;
-    int tm, tn;
-    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    // K-major descriptors are fixed per block (base at the block's first row)
-    __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
-    if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
-    if (!B_MN) rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(BN, p.N - n0), p.ldb));
-
-    f32x4 acc[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    const int nk = (p.K + BK2 - 1) / BK2;
-#pragma unroll
-    for (int st = 0; st < NST - 1; ++st) {
-        if (st < nk) {
-            char* base = smem + st * SS;
-            stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, st * BK2, p.K, wid, lane, rsA);
-            stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, st * BK2, p.K, wid, lane, rsB);
-        }
-    }
-    for (int t = 0; t < nk; ++t) {
-        // stage t must have landed: the stages issued after it (<= 2) may stay in flight
-        const int after = min(NST - 2, nk - 1 - t);
-        if (after >= 2) wait_vm<2 * G>();
-        else if (after == 1) wait_vm<G>();
-        else wait_vm<0>();
-        __builtin_amdgcn_s_barrier();
-        if (t + NST - 1 < nk) {
-            char* base = smem + ((t + NST - 1) % NST) * SS;
-            stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, (t + NST - 1) * BK2, p.K, wid, lane, rsA);
-            stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, (t + NST - 1) * BK2, p.K, wid, lane, rsB);
-        }
-        const char* ta = smem + (t % NST) * SS;
-        const char* tb = ta + SA;
-        bf16x8 af[MT], bfr[NT];
-#pragma unroll
-        for (int j = 0; j < NT; ++j) bfr[j] = frag2<BN, B_MN>(tb, wn * TN + j * 16, lane);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) af[i] = frag2<BM, A_MN>(ta, wm * TM + i * 16, lane);
-        __builtin_amdgcn_sched_barrier(0);  // every LDS read in flight before the first MFMA
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    epilogue2<BM, BN, WM, WN, TM, TN, MT, NT>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-}
-
 
 // =============================================================================
-// v3: v2's tiles and 4-stage LDS ring, software-pipelined one stage deeper: the
+// v3: the tiles above and their 4-stage LDS ring, software-pipelined one stage deeper: the
 // fragments of stage t+1 are read into a second register set WHILE the MFMAs of stage t
 // run, and the DMA of stage t+4 is interleaved with them too (sched_group_barrier), so
 // after a barrier the MFMA pipe never waits for LDS or for DMA issue.
@@ -502,7 +468,7 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm2(GemmP p) {
 //   vmcnt(stage t+1 landed) -> s_barrier [everyone done with buffer t; stage t+1 visible]
 //   -> {DMA stage t+4 -> buffer t%4, LDS reads of stage t+1 -> set nxt} || MFMAs(t, set cur)
 // =============================================================================
-template <int BM, int BN, bool A_MN, bool B_MN, int NS = NST, int ABL = 0>
+template <int BM, int BN, bool A_MN, bool B_MN, int NS = NST>
 __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     GemmP p = p_;
     if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
@@ -550,18 +516,15 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
 #define KD_G3_STEP(CUR_A, CUR_B, NXT_A, NXT_B)                                                           \
     {                                                                                                     \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                \
-        if (ABL != 1) wait_vm<(NS - 2) * G>();   \
-        if (ABL != 2) __builtin_amdgcn_s_barrier();   \
+        wait_vm<(NS - 2) * G>();                                                                          \
+        __builtin_amdgcn_s_barrier();                                                                     \
         __builtin_amdgcn_sched_barrier(0);                                                                \
-        if (ABL != 1) dma(t + NS);   \
-        if (ABL != 3) {   \
+        dma(t + NS);                                                                                      \
+        {                                                                                                 \
             const char* na = smem + ((t + 1) % NS) * SS;                                                  \
             _Pragma("unroll") for (int j = 0; j < NT; ++j) NXT_B[j] = frag2<BN, B_MN>(na + SA, wn * TN + j * 16, lane); \
             _Pragma("unroll") for (int i = 0; i < MT; ++i) NXT_A[i] = frag2<BM, A_MN>(na, wm * TM + i * 16, lane);      \
-        } else {   \
-            _Pragma("unroll") for (int j = 0; j < NT; ++j) NXT_B[j] = CUR_B[j];   \
-            _Pragma("unroll") for (int i = 0; i < MT; ++i) NXT_A[i] = CUR_A[i];   \
-        }   \
+        }                                                                                                 \
         _Pragma("unroll") for (int i = 0; i < MT; ++i)                                                    \
             _Pragma("unroll") for (int j = 0; j < NT; ++j)                                                \
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CUR_A[i], CUR_B[j], acc[i][j], 0, 0, 0); \
@@ -590,459 +553,102 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
 #undef KD_G3_STEP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    epilogue2<BM, BN, WM, WN, TM, TN, MT, NT>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+    epilogue2<BM, BN, WM, WN, TM, TN, MT, NT, NTH2, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
 }
 
 // =============================================================================
-// v4: 256x256 tile, BK = 64, two K-tile buffers (A | B, 64 KiB each), 8 waves as 2 (M)
-// x 4 (N) groups, each wave 128x64 of C. A K-tile runs as 4 phases, one C quadrant
-// (64x32, 16 MFMAs over K = 64) per phase:
-//   load section: ds_read this phase's fragments (+ DMA of half of K-tile k+1 in phases
-//                 0 and 1; counted vmcnt(0) for K-tile k+1 in phase 3)
-//   s_barrier -> lgkmcnt(0) -> setprio(1) MFMA x16 setprio(0) -> s_barrier
-// The wm = 1 group runs one barrier behind the wm = 0 group, so on every SIMD (one wave
-// of each group) one wave's MFMA cluster overlaps the other's load section.
-// Hazards (barrier counts): K-tile k+1's DMA lands (vmcnt 0) in phase 3 before the
-// barrier that both groups pass before reading it; buffer k&1 is last read in phase 2
-// of K-tile k and rewritten from phase 0 of K-tile k+2, >= 4 barriers later.
-// K-major LDS image: 128-B rows, 16-B chunk c of row r stored at slot c ^ ((r >> 1) & 7)
-// (conflict-free for the ds_read_b128 lane groups); MN-major: two stacked 32-deep
-// images of v2/v3's layout.
+// v8: 256x256 tile, FOUR waves (one per SIMD), each 128x128 of C = 8x8 MFMA 16x16x32
+// tiles, v3's 4-slot BK=32 LDS-DMA ring (three stages in flight). The 256 accumulator
+// registers live in the AGPR file for the whole kernel (MFMA through asm with an "a"
+// operand): with the builtin, hipcc splits them over both files and moves ~330
+// registers per iteration between them. VGPRs hold two fragment sets (stage t in use,
+// stage t+1 being read) and the loop-invariant per-lane DMA offsets.
+//   step t (slot t%4, unrolled x4 so every slot index is a constant):
+//     lgkmcnt(0) [fragments of t in registers] ; vmcnt(16) [stage t+1 landed] ; s_barrier
+//     8 units of { 1 DMA of stage t+4 -> slot t%4, 2 fragment reads of stage t+1, 8 MFMA }
+// WAR: slot t%4 was last read (fragments of t, during step t-1) before every wave's
+// lgkmcnt(0) + barrier of step t. RAW: stage t+1 is read after the barrier that follows
+// every wave's vmcnt for it. DMA past the last stage is issued anyway (all lanes out of
+// range: no memory traffic, the slot is never read) so the counts stay uniform.
+// K-major operands: one descriptor per block, per-lane voffset fixed, the stage's k
+// offset in soffset. MN-major: one descriptor per stage (its k rows), voffset fixed.
 // =============================================================================
-constexpr int BK4 = 64;
+constexpr int NTH8 = 256, NS8 = 4;
 
+__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// per-lane byte offset of this wave's DMA instruction i (0..15 of an operand stage)
 template <bool MN>
-__device__ __forceinline__ void stage4(char* tile, const bf16* ptr, int64_t ld, int r0, int rows_total, int k0, int K,
-                                       int wid, int lane, int h, __amdgpu_buffer_rsrc_t rs_k) {
-    if (!MN) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int i = 16 * h + wid * 2 + s;
-            const int row = i * 8 + (lane >> 3);
-            const int gc = (lane & 7) ^ ((row >> 1) & 7);
-            const int k = k0 + gc * 8;
-            const uint32_t voff = (k < K) ? (uint32_t)(((int64_t)row * ld + k) * 2) : OOB;
-            dma16(rs_k, tile + i * 1024, voff);
-        }
-    } else {
-        const int kvalid = max(0, min(BK4, K - k0));
-        auto rs = make_rsrc(ptr + (int64_t)min(k0, K) * ld + r0, rec_bytes(kvalid, ld));
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int i = 16 * h + wid * 2 + s;
-            const int kr = i * 2 + (lane >> 5);
-            const int gc = (lane & 31) ^ (int)sw_mn(kr);
-            const int row = r0 + gc * 8;
-            const uint32_t voff = (kr < kvalid && row < rows_total) ? (uint32_t)(((int64_t)kr * ld + gc * 8) * 2) : OOB;
-            dma16(rs, tile + i * 1024, voff);
-        }
-    }
-}
-
-template <bool MN>
-__device__ __forceinline__ bf16x8 frag4(const char* tile, int rb, int kk, int lane) {
-    if (!MN) {
-        const int r = rb + (lane & 15);
-        const int c = kk * 4 + (lane >> 4);
-        return *(const bf16x8*)(tile + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-    } else {
-        return frag2<256, true>(tile + kk * 32 * 512, rb, lane);
-    }
-}
-
-template <bool A_MN, bool B_MN>
-__global__ void __launch_bounds__(NTH2, 1) k_gemm4(GemmP p_) {
-    GemmP p = p_;
-    if (gridDim.y > 1) {   // split-K (as v3)
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += A_MN ? k0 * p.lda : k0;
-        p.B += B_MN ? k0 * p.ldb : k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
-    constexpr int OPB = 256 * BK4 * 2;   // one operand of one K-tile
-    constexpr int KTB = 2 * OPB;         // one K-tile buffer
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 2, wn = wid & 3;
-    int tm, tn;
-    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
-    const int m0 = tm * 256, n0 = tn * 256;
-    __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
-    if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
-    if (!B_MN) rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int nk = (p.K + BK4 - 1) / BK4;
-    auto dma_half = [&](int kt, int h) {
-        char* base = smem + (kt & 1) * KTB;
-        stage4<A_MN>(base, p.A, p.lda, m0, p.M, kt * BK4, p.K, wid, lane, h, rsA);
-        stage4<B_MN>(base + OPB, p.B, p.ldb, n0, p.N, kt * BK4, p.K, wid, lane, h, rsB);
-    };
-    dma_half(0, 0);
-    dma_half(0, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (wm == 1) __builtin_amdgcn_s_barrier();   // stagger the two wave groups by one barrier
-    __builtin_amdgcn_sched_barrier(0);
-
-    bf16x8 af[4][2], b0[2][2], b1[2][2];
-    const int ra0 = wm * 128, cb0 = wn * 64;
-#define KD_G4_MMA(QM, QN, BF)                                                                              \
-    {                                                                                                      \
-        __builtin_amdgcn_s_barrier();                                                                      \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                 \
-        __builtin_amdgcn_sched_barrier(0);                                                                 \
-        __builtin_amdgcn_s_setprio(1);                                                                     \
-        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                   \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
-                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
-                    acc[(QM) * 4 + i][(QN) * 2 + j] =                                                      \
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], BF[j][kk], acc[(QM) * 4 + i][(QN) * 2 + j], 0, 0, 0); \
-        __builtin_amdgcn_s_setprio(0);                                                                     \
-        __builtin_amdgcn_sched_barrier(0);                                                                 \
-        __builtin_amdgcn_s_barrier();                                                                      \
-        __builtin_amdgcn_sched_barrier(0);                                                                 \
-    }
-    for (int kt = 0; kt < nk; ++kt) {
-        const char* ta = smem + (kt & 1) * KTB;
-        const char* tb = ta + OPB;
-        const bool pf = kt + 1 < nk;
-        // phase 0: B(qn 0), A(qm 0); DMA half 0 of K-tile kt+1
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) b0[j][kk] = frag4<B_MN>(tb, cb0 + j * 16, kk, lane);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) af[i][kk] = frag4<A_MN>(ta, ra0 + i * 16, kk, lane);
-        if (pf) dma_half(kt + 1, 0);
-        KD_G4_MMA(0, 0, b0)
-        // phase 1: B(qn 1); DMA half 1
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) b1[j][kk] = frag4<B_MN>(tb, cb0 + 32 + j * 16, kk, lane);
-        if (pf) dma_half(kt + 1, 1);
-        KD_G4_MMA(0, 1, b1)
-        // phase 2: A(qm 1)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) af[i][kk] = frag4<A_MN>(ta, ra0 + 64 + i * 16, kk, lane);
-        KD_G4_MMA(1, 0, b0)
-        // phase 3: K-tile kt+1 landed (my DMAs); the barrier publishes everyone's
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        KD_G4_MMA(1, 1, b1)
-    }
-#undef KD_G4_MMA
-    if (wm == 0) __builtin_amdgcn_s_barrier();   // rebalance the barrier count
-    __syncthreads();
-    epilogue2<256, 256, 2, 4, 128, 64, 8, 4>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-}
-
-// =============================================================================
-// v6: v3's tile (256x256, 8 waves 2x4, wave 128x64) and 4-slot BK=32 LDS ring, run as
-// two phases per stage with the wave groups ping-ponging: the wm = 1 group trails the
-// wm = 0 group by one barrier, so on every SIMD one wave's 16-MFMA cluster overlaps the
-// other wave's load section.
-//   phase a (stage t): ds_read B(t) + A(t) rows 0..63 ; s_barrier ; lgkmcnt(0) ;
-//                      setprio(1) 16 MFMA setprio(0) ; s_barrier
-//   phase b (stage t): ds_read A(t) rows 64..127 ; DMA stage t+3 -> slot (t+3)%4 ;
-//                      vmcnt(2G) [stage t+1 landed] ; s_barrier ; lgkmcnt(0) ; MFMA ; s_barrier
-// WAR: slot (t+3)%4 held stage t-1, whose last reads (phase b of t-1) every wave retired
-// (lgkmcnt 0) before the barrier that precedes either group's phase b of stage t.
-// RAW: stage t+1 is read in phase a of t+1, after the barrier that follows both groups'
-// vmcnt waits. DMA past the last stage is issued anyway (out-of-range, zero-fill) so the
-// counts stay uniform.
-// =============================================================================
-template <bool A_MN, bool B_MN>
-__global__ void __launch_bounds__(NTH2, 1) k_gemm6(GemmP p_) {
-    GemmP p = p_;
-    if (gridDim.y > 1) {
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += A_MN ? k0 * p.lda : k0;
-        p.B += B_MN ? k0 * p.ldb : k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
-    constexpr int BM = 256, BN = 256, NS = 4;
-    constexpr int SA = BM * BK2 * 2, SS = SA + BN * BK2 * 2;
-    constexpr int G = 4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 2, wn = wid & 3;
-    int tm, tn;
-    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-    __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
-    if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
-    if (!B_MN) rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(BN, p.N - n0), p.ldb));
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int nk = (p.K + BK2 - 1) / BK2;
-    auto dma = [&](int st) {
-        char* base = smem + (st % NS) * SS;
-        stage2<BM, A_MN>(base, p.A, p.lda, m0, p.M, st * BK2, p.K, wid, lane, rsA);
-        stage2<BN, B_MN>(base + SA, p.B, p.ldb, n0, p.N, st * BK2, p.K, wid, lane, rsB);
-    };
-    dma(0); dma(1); dma(2);
-    wait_vm<2 * G>();
-    __builtin_amdgcn_s_barrier();
-    if (wm == 1) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 af[4], bfr[4];
-    const int ra = wm * 128, cb = wn * 64;
-#define KD_G6_MMA(I0)                                                                                       \
-    {                                                                                                       \
-        __builtin_amdgcn_s_barrier();                                                                       \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                  \
-        __builtin_amdgcn_sched_barrier(0);                                                                  \
-        __builtin_amdgcn_s_setprio(1);                                                                      \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
-            _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                   \
-                acc[(I0) + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[(I0) + i][j], 0, 0, 0); \
-        __builtin_amdgcn_s_setprio(0);                                                                      \
-        __builtin_amdgcn_sched_barrier(0);                                                                  \
-        __builtin_amdgcn_s_barrier();                                                                       \
-        __builtin_amdgcn_sched_barrier(0);                                                                  \
-    }
-    for (int t = 0; t < nk; ++t) {
-        const char* ta = smem + (t % NS) * SS;
-        // phase a
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = frag2<BN, B_MN>(ta + SA, cb + j * 16, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = frag2<BM, A_MN>(ta, ra + i * 16, lane);
-        KD_G6_MMA(0)
-        // phase b
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = frag2<BM, A_MN>(ta, ra + 64 + i * 16, lane);
-        dma(t + 3);
-        wait_vm<2 * G>();
-        KD_G6_MMA(4)
-    }
-#undef KD_G6_MMA
-    if (wm == 0) __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    epilogue2<256, 256, 2, 4, 128, 64, 8, 4>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-}
-
-// =============================================================================
-// v5: 256x256 tile, BK = 64, FOUR waves (one per SIMD) of 128x128 each, two 64 KiB LDS
-// stages (v4's image layouts). One wave per SIMD, so each wave pipelines its own work:
-//   step t (F0 = kk 0 fragments of stage t, already read):
-//     lgkmcnt(0) ; 64 MFMA(F0), the first 32 interleaved with the 16 DMA instructions
-//     of stage t+1 (-> the other buffer) and the 16 reads of F1 (kk 1 of stage t)
-//     lgkmcnt(0) ; 32 MFMA(F1, rows 0..63)
-//     vmcnt(0) ; s_barrier      [stage t+1 landed for everyone; stage t-1's buffer free]
-//     32 MFMA(F1, rows 64..127) interleaved with the 16 reads of F0 of stage t+1
-// WAR: the buffer refilled in step t held stage t-1, whose last reads (F1 of t-1) every
-// wave retired before the barrier of step t-1. RAW: stage t+1 is read only after the
-// barrier of step t, behind every wave's vmcnt(0).
-// =============================================================================
-constexpr int NTH5 = 256;
-
-// one 1-KiB wave-instruction (index i of 32) of a BK=64 operand stage (v4 layout)
-template <bool MN>
-__device__ __forceinline__ void dma5(char* tile, __amdgpu_buffer_rsrc_t rs, int64_t ld, int rows_total, int r0,
-                                     int k0, int K, int kvalid, int i, int lane) {
-    if (!MN) {
-        const int row = i * 8 + (lane >> 3);
-        const int gc = (lane & 7) ^ ((row >> 1) & 7);
-        const int k = k0 + gc * 8;
-        const uint32_t voff = (k < K) ? (uint32_t)(((int64_t)row * ld + k) * 2) : OOB;
-        dma16(rs, tile + i * 1024, voff);
-    } else {
-        const int kr = i * 2 + (lane >> 5);
-        const int gc = (lane & 31) ^ (int)sw_mn(kr);
-        const int row = r0 + gc * 8;
-        const uint32_t voff = (kr < kvalid && row < rows_total) ? (uint32_t)(((int64_t)kr * ld + gc * 8) * 2) : OOB;
-        dma16(rs, tile + i * 1024, voff);
-    }
-}
-
-template <bool A_MN, bool B_MN>
-__global__ void __launch_bounds__(NTH5, 1) k_gemm5(GemmP p_) {
-    GemmP p = p_;
-    if (gridDim.y > 1) {
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += A_MN ? k0 * p.lda : k0;
-        p.B += B_MN ? k0 * p.ldb : k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
-    constexpr int OPB = 256 * BK4 * 2, KTB = 2 * OPB;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-    int tm, tn;
-    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
-    const int m0 = tm * 256, n0 = tn * 256;
-    __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A, 0), rsBk = make_rsrc(p.B, 0);
-    if (!A_MN) rsAk = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
-    if (!B_MN) rsBk = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
-    const int nk = (p.K + BK4 - 1) / BK4;
-    // descriptors of stage st: K-major fixed; MN-major per stage (k rows of the stage)
-    auto rs_of = [&](bool mn, const bf16* ptr, int64_t ld, int r0, __amdgpu_buffer_rsrc_t rk, int st, int& kvalid) {
-        if (!mn) { kvalid = BK4; return rk; }
-        const int k0 = st * BK4;
-        kvalid = max(0, min(BK4, p.K - k0));
-        return make_rsrc(ptr + (int64_t)min(k0, p.K) * ld + r0, rec_bytes(kvalid, ld));
-    };
-    f32x4 acc[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 f0a[8], f0b[8], f1a[8], f1b[8];
-    const int ra = wm * 128, cb = wn * 128;
-    {   // prologue: stage 0 -> buffer 0, F0(0)
-        int kva, kvb;
-        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, 0, kva);
-        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, 0, kvb);
-#pragma unroll
-        for (int s8 = 0; s8 < 8; ++s8) {
-            dma5<A_MN>(smem, ra_, p.lda, p.M, m0, 0, p.K, kva, wid * 8 + s8, lane);
-            dma5<B_MN>(smem + OPB, rb_, p.ldb, p.N, n0, 0, p.K, kvb, wid * 8 + s8, lane);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 8; ++i) f0a[i] = frag4<A_MN>(smem, ra + i * 16, 0, lane);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f0b[j] = frag4<B_MN>(smem + OPB, cb + j * 16, 0, lane);
-    }
-    for (int t = 0; t < nk; ++t) {
-        const char* ta = smem + (t & 1) * KTB;
-        const char* tb = ta + OPB;
-        char* na = smem + ((t + 1) & 1) * KTB;
-        int kva, kvb;
-        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, t + 1, kva);
-        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, t + 1, kvb);
-        const int k1 = (t + 1) * BK4;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        // 64 MFMA(F0); the first 32 in pairs, each pair behind one DMA of stage t+1 and one
-        // F1 fragment read (order pinned with sched_barrier: the scheduler would bunch the DMA)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            if (q < 8) dma5<A_MN>(na, ra_, p.lda, p.M, m0, k1, p.K, kva, wid * 8 + q, lane);
-            else dma5<B_MN>(na + OPB, rb_, p.ldb, p.N, n0, k1, p.K, kvb, wid * 8 + q - 8, lane);
-            if (q < 8) f1a[q] = frag4<A_MN>(ta, ra + q * 16, 1, lane);
-            else f1b[q - 8] = frag4<B_MN>(tb, cb + (q - 8) * 16, 1, lane);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int m = 2 * q + e, i = m >> 3, j = m & 7;
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0a[i], f0b[j], acc[i][j], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int m = 32; m < 64; ++m)
-            acc[m >> 3][m & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0a[m >> 3], f0b[m & 7], acc[m >> 3][m & 7], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1a[i], f1b[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        // 32 MFMA(F1, rows 64..127) in pairs, each behind one read of F0 of stage t+1
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            if (q < 8) f0a[q] = frag4<A_MN>(na, ra + q * 16, 0, lane);
-            else f0b[q - 8] = frag4<B_MN>(na + OPB, cb + (q - 8) * 16, 0, lane);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int m = 2 * q + e, i = 4 + (m >> 3), j = m & 7;
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1a[i], f1b[j], acc[i][j], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH5>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-}
-
-// =============================================================================
-// v7: v3's 4-slot BK=32 LDS ring (three stages in flight) with v5's four waves of
-// 128x128 (half the fragment reads per MFMA of the 8-wave 128x64 layout).
-//   iteration t: lgkmcnt(0) [fragments of t in registers] ; vmcnt(2 stages x 8) [stage
-//   t+1 landed] ; s_barrier ; 64 MFMA(t) in 8 units of {1 DMA of stage t+4 -> slot t%4,
-//   2 fragment reads of stage t+1, 8 MFMA}, order pinned by sched_barrier.
-// WAR: slot t%4 was last read (fragments of t, during iteration t-1) before every wave's
-// lgkmcnt(0) + barrier of iteration t. RAW: stage t+1 is read after the barrier that
-// follows every wave's vmcnt for it. DMA past the last stage is issued anyway
-// (out-of-range, zero-fill) so the counts stay uniform.
-// =============================================================================
-template <bool MN>
-__device__ __forceinline__ void dma7(char* tile, __amdgpu_buffer_rsrc_t rs, int64_t ld, int rows_total, int r0, int k0,
-                                     int K, int kvalid, int i, int lane) {
-    if (!MN) {   // 256 rows x 64 B, 16 rows per 1-KiB instruction
+__device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, int rows_total) {
+    if (!MN) {   // [256 rows][32 k]: 16 rows x 64 B per instruction
         const int row = 16 * i + (lane >> 2);
         const int gc = (lane & 3) ^ f4(row);
-        const int k = k0 + gc * 8;
-        const uint32_t voff = (k < K) ? (uint32_t)(((int64_t)row * ld + k) * 2) : OOB;
-        dma16(rs, tile + i * 1024, voff);
-    } else {     // 32 k-rows x 512 B, 2 k-rows per instruction
-        const int kr = i * 2 + (lane >> 5);
+        return (uint32_t)((int64_t)row * ld * 2 + gc * 16);
+    } else {     // [32 k][256 rows]: 2 k-rows x 512 B per instruction
+        const int kr = 2 * i + (lane >> 5);
         const int gc = (lane & 31) ^ (int)sw_mn(kr);
-        const int row = r0 + gc * 8;
-        const uint32_t voff = (kr < kvalid && row < rows_total) ? (uint32_t)(((int64_t)kr * ld + gc * 8) * 2) : OOB;
-        dma16(rs, tile + i * 1024, voff);
+        return (r0 + gc * 8 < rows_total) ? (uint32_t)((int64_t)kr * ld * 2 + gc * 16) : OOB;
     }
 }
 
-template <bool A_MN, bool B_MN>
-__global__ void __launch_bounds__(NTH5, 1) k_gemm7(GemmP p_) {
+// STAMP (variant 17, diagnostic only): per-wave s_memtime cycle totals of the top-of-step
+// waits, the MFMA units, the prologue and the epilogue, written as uint32 to p.aux
+// (which then carries no pre-activation output).
+template <bool A_MN, bool B_MN, bool STAMP = false>
+__global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     GemmP p = p_;
-    if (gridDim.y > 1) {
+    uint32_t* stamps = nullptr;
+    if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
+    uint64_t s_pro = 0, s_lgkm = 0, s_vm = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
+    if (STAMP) ts0 = __builtin_amdgcn_s_memtime();
+    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
         const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
         p.K = (int)min((int64_t)p.K - k0, p.kchunk);
         p.A += A_MN ? k0 * p.lda : k0;
         p.B += B_MN ? k0 * p.ldb : k0;
         p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
     }
-    constexpr int NS = 4, SA = 256 * BK2 * 2, SS = 2 * SA;
+    constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
     int tm, tn;
     tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
     const int m0 = tm * 256, n0 = tn * 256;
-    __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A, 0), rsBk = make_rsrc(p.B, 0);
-    if (!A_MN) rsAk = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
-    if (!B_MN) rsBk = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
-    const int nk = (p.K + BK2 - 1) / BK2;
-    auto rs_of = [&](bool mn, const bf16* ptr, int64_t ld, int r0, __amdgpu_buffer_rsrc_t rk, int st, int& kvalid) {
-        if (!mn) { kvalid = BK2; return rk; }
-        const int k0 = st * BK2;
-        kvalid = max(0, min(BK2, p.K - k0));
-        return make_rsrc(ptr + (int64_t)min(k0, p.K) * ld + r0, rec_bytes(kvalid, ld));
-    };
-    // DMA instruction u (0..7) of this wave for stage st: A instructions wid*4 + u (u < 4),
-    // B instructions wid*4 + u - 4
-    auto dma_u = [&](int st, int u, __amdgpu_buffer_rsrc_t ra_, __amdgpu_buffer_rsrc_t rb_, int kva, int kvb) {
-        char* base = smem + (st % NS) * SS;
-        if (u < 4) dma7<A_MN>(base, ra_, p.lda, p.M, m0, st * BK2, p.K, kva, wid * 4 + u, lane);
-        else dma7<B_MN>(base + SA, rb_, p.ldb, p.N, n0, st * BK2, p.K, kvb, wid * 4 + u - 4, lane);
+    const int K = p.K;
+    const int nk = (K + BK2 - 1) / BK2;
+    const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (A_MN ? 0 : (int64_t)m0 * p.lda), A_MN ? 0u : rec_bytes(min(256, p.M - m0), p.lda));
+    const __amdgpu_buffer_rsrc_t rsBk = make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
+    uint32_t va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        va[u] = voff8<A_MN>(wid * 4 + u, lane, p.lda, m0, p.M);
+        vb[u] = voff8<B_MN>(wid * 4 + u, lane, p.ldb, n0, p.N);
+    }
+    // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl
+    auto dma = [&](int st, int sl, int u) {
+        const bool isA = u < 4;
+        const bool mn = isA ? A_MN : B_MN;
+        const int i = wid * 4 + (u & 3);
+        char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
+        const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
+        uint32_t v = isA ? va[u & 3] : vb[u & 3];
+        if (!mn) {
+            if (kleft < BK2) {   // K tail / past the end: zero the chunks at k >= K
+                const int row = 16 * i + (lane >> 2);
+                const int gc = (lane & 3) ^ f4(row);
+                if (gc * 8 >= kleft) v = OOB;
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, v, kleft > 0 ? st * BK2 * 2 : 0, 0, 0);
+        } else {
+            const bf16* base = isA ? p.A + m0 : p.B + n0;
+            const int64_t ld = isA ? p.lda : p.ldb;
+            const int kv = max(0, min(BK2, kleft));
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)min(st * BK2, K) * ld, rec_bytes(kv, ld));
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)dst, 16, v, 0, 0, 0);
+        }
     };
     f32x4 acc[8][8];
 #pragma unroll
@@ -1051,54 +657,77 @@ __global__ void __launch_bounds__(NTH5, 1) k_gemm7(GemmP p_) {
         for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int ra = wm * 128, cb = wn * 128;
 #pragma unroll
-    for (int st = 0; st < NS; ++st) {
-        int kva, kvb;
-        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, st, kva);
-        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, st, kvb);
+    for (int st = 0; st < NS8; ++st)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dma_u(st, u, ra_, rb_, kva, kvb);
-    }
-    wait_vm<24>();   // stage 0 landed
+        for (int u = 0; u < 8; ++u) dma(st, st, u);
+    wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
     __builtin_amdgcn_s_barrier();
+    uint64_t tprev = 0;
+    if (STAMP) { tprev = __builtin_amdgcn_s_memtime(); s_pro = tprev - ts0; }
     bf16x8 xa[8], xb[8], ya[8], yb[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xa[i] = frag2<256, A_MN>(smem, ra + i * 16, lane);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xb[j] = frag2<256, B_MN>(smem + SA, cb + j * 16, lane);
+    for (int u = 0; u < 8; ++u) {
+        xa[u] = frag2<256, A_MN>(smem, ra + u * 16, lane);
+        xb[u] = frag2<256, B_MN>(smem + SA, cb + u * 16, lane);
+    }
 
-#define KD_G7_STEP(CA, CB, NA, NB)                                                                           \
+#define KD_G8_STEP(SL, CA, CB, NA, NB)                                                                       \
     {                                                                                                         \
-        int kva, kvb;                                                                                         \
-        const auto ra_ = rs_of(A_MN, p.A, p.lda, m0, rsAk, t + NS, kva);                                      \
-        const auto rb_ = rs_of(B_MN, p.B, p.ldb, n0, rsBk, t + NS, kvb);                                      \
-        const char* na = smem + ((t + 1) % NS) * SS;                                                          \
+        const int t_ = t + (SL);                                                                              \
+        uint64_t ta_ = 0, tb_ = 0, tc_ = 0, td_ = 0;                                                          \
+        if (STAMP) ta_ = __builtin_amdgcn_s_memtime();                                                        \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                    \
+        if (STAMP) tb_ = __builtin_amdgcn_s_memtime();                                                        \
         wait_vm<16>();                                                                                        \
+        if (STAMP) tc_ = __builtin_amdgcn_s_memtime();                                                        \
         __builtin_amdgcn_s_barrier();                                                                         \
+        if (STAMP) {                                                                                          \
+            td_ = __builtin_amdgcn_s_memtime();                                                               \
+            if (tprev) s_units += ta_ - tprev;                                                                \
+            s_lgkm += tb_ - ta_; s_vm += tc_ - tb_; s_bar += td_ - tc_; tprev = td_;                          \
+        }                                                                                                     \
         __builtin_amdgcn_sched_barrier(0);                                                                    \
+        const char* na_ = smem + (((SL) + 1) % NS8) * SS;                                                     \
         _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
-            dma_u(t + NS, u, ra_, rb_, kva, kvb);                                                             \
-            NA[u] = frag2<256, A_MN>(na, ra + u * 16, lane);                                                  \
-            NB[u] = frag2<256, B_MN>(na + SA, cb + u * 16, lane);                                             \
+            dma(t_ + NS8, (SL), u);                                                                           \
+            NA[u] = frag2<256, A_MN>(na_, ra + u * 16, lane);                                                 \
+            NB[u] = frag2<256, B_MN>(na_ + SA, cb + u * 16, lane);                                            \
             __builtin_amdgcn_sched_barrier(0);                                                                \
-            _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                     \
-                acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CA[u], CB[j], acc[u][j], 0, 0, 0);        \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) mfma_agpr(acc[u][j], CA[u], CB[j]);                 \
             __builtin_amdgcn_sched_barrier(0);                                                                \
         }                                                                                                     \
     }
     int t = 0;
-    for (; t + 1 < nk; t += 2) {
-        KD_G7_STEP(xa, xb, ya, yb);
-        ++t;
-        KD_G7_STEP(ya, yb, xa, xb);
-        --t;
+    for (; t + NS8 <= nk; t += NS8) {
+        KD_G8_STEP(0, xa, xb, ya, yb)
+        KD_G8_STEP(1, ya, yb, xa, xb)
+        KD_G8_STEP(2, xa, xb, ya, yb)
+        KD_G8_STEP(3, ya, yb, xa, xb)
     }
-    if (t < nk) KD_G7_STEP(xa, xb, ya, yb);
-#undef KD_G7_STEP
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const int rem = nk - t;
+    if (rem > 0) KD_G8_STEP(0, xa, xb, ya, yb)
+    if (rem > 1) KD_G8_STEP(1, ya, yb, xa, xb)
+    if (rem > 2) KD_G8_STEP(2, xa, xb, ya, yb)
+#undef KD_G8_STEP
+    // drain the ring (out-of-range DMAs still write LDS) and the MFMA pipe before the
+    // accumulators are read back (asm MFMAs are invisible to the hazard recognizer)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    uint64_t te0 = 0;
+    if (STAMP) { te0 = __builtin_amdgcn_s_memtime(); s_units += te0 - tprev; }
     __syncthreads();
-    epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH5>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+    epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+    if (STAMP) {
+        const uint64_t te1 = __builtin_amdgcn_s_memtime();
+        s_epi = te1 - te0;
+        if (lane == 0) {
+            uint32_t* o = stamps + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wid) * 8;
+            o[0] = (uint32_t)s_pro; o[1] = (uint32_t)s_lgkm; o[2] = (uint32_t)s_vm; o[3] = (uint32_t)s_bar;
+            o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
+        }
+    }
 }
+
 
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
 // (alpha, alpha_dev, bias, aux, act, residual, accumulate), 4 columns per thread
@@ -1159,8 +788,9 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const double step[3] = {1.0, 0.70, 0.65};   // 256x256, 256x128, 128x256
     const double fixed[3] = {24.0, 12.0, 6.0};
     const int64_t nk = ceil_div(d->K, BK2);
-    const int fv = (d->variant >= 8 && d->variant <= 15) ? 0 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
-    const bool split_ok = d->variant == 0 || d->variant >= 5;
+    // forced tile: variants 2/5 (and v8 = 16) 256x256, 3/6 256x128, 4/7 128x256; 0 = model's choice
+    const int fv = d->variant >= 16 ? 0 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
+    const bool split_ok = true;
     const double out_b = (double)M * N * ((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
                                           (d->residual ? 2 : 0) + (d->aux ? 2 : 0));
     GemmPlan best{fv >= 0 ? fv + 2 : 2, 1, d->K};
@@ -1187,6 +817,7 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
 
 }  // namespace
 
+
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d != nullptr, "gemm: null descriptor");
     KD_CHECK_ARG(d->A && d->B && d->C, "gemm: null operand");
@@ -1195,6 +826,10 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->b_layout == KD_LAYOUT_K_MAJOR || d->b_layout == KD_LAYOUT_MN_MAJOR, "gemm: b_layout");
     KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16 || d->c_dtype == KD_DTYPE_F32, "gemm: c_dtype");
     KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_SILU, "gemm: act");
+    KD_CHECK_ARG(d->act == KD_ACT_NONE || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
+                                          d->c_dtype == KD_DTYPE_BF16),
+                 "gemm: an activation epilogue needs K-major operands and a bf16 output");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || d->variant == 16 || d->variant == 17, "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     KD_CHECK_SHAPE(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
@@ -1227,19 +862,14 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
                         ((uintptr_t)d->residual % 16 == 0)));
-    const bool v2_ok = d->N % 8 == 0 && c_ok16 && d->M >= 128 && d->N >= 128 &&
-                       ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
-                       (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
-                       (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
-    const int force = d->variant;   // 0 auto, 1 v1, 2/3/4 v2 256x256/256x128/128x256, 5/6/7 v3 same tiles,
-                                    // 8 v4 256x256, 9 v3 256x256 with a 5-stage ring, 10 v6 256x256 ping-pong,
-                                    // 11/12/13 timing ablations of v3 (no DMA / no barrier / no fragment
-                                    // reads in the loop: WRONG results, tools/ablate_gemm.py only),
-                                    // 14 v5 256x256 four waves of 128x128, 15 v7 (v3 ring, 4 waves)
-    if ((force == 0 && v2_ok) || (force >= 2 && v2_ok)) {
-        const bool v3 = force == 0 || force >= 5;
+    const bool big_ok = d->N % 8 == 0 && c_ok16 && d->M >= 128 && d->N >= 128 &&
+                        ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
+                        (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
+                        (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
+    const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,
+                                    // 16 v8 256x256 (4 waves, AGPR accumulators)
+    if (force != 1 && big_ok) {
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
-        const int var = pl.var;
         GemmP pk = p;   // the tile kernels' parameters (split-K: plain fp32 partial planes)
         if (pl.split > 1) {
             KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
@@ -1248,46 +878,39 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             pk.alpha_dev = nullptr; pk.bias = nullptr; pk.aux = nullptr; pk.resid = nullptr; pk.act = KD_ACT_NONE;
             pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N;
         }
-        const dim3 gy(1, pl.split, 1);
-        const bool v4 = force == 8, v5 = force == 9, v6 = force == 10, v7 = force == 14, v8 = force == 15;
-#define L2(BMv, BNv, AM, BMN)                                                                                     \
-    if (v4 && BMv == 256 && BNv == 256)                                                                           \
-        hipLaunchKernelGGL((k_gemm4<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH2),   \
-                           (gemm2_lds<256, 256>()), st, pk);                                                      \
-    else if (v8 && BMv == 256 && BNv == 256)                                                                      \
-        hipLaunchKernelGGL((k_gemm7<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH5),   \
-                           (gemm2_lds<256, 256>()), st, pk);                                                      \
-    else if (v7 && BMv == 256 && BNv == 256)                                                                      \
-        hipLaunchKernelGGL((k_gemm5<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH5),   \
-                           (gemm2_lds<256, 256>()), st, pk);                                                      \
-    else if (force >= 11 && force <= 13 && BMv == 256 && BNv == 256) {                                              \
-        if (force == 11) hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 4, 1>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), \
-                                            dim3(NTH2), (gemm2_lds<256, 256>()), st, pk);                         \
-        else if (force == 12) hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 4, 2>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), \
-                                                 dim3(NTH2), (gemm2_lds<256, 256>()), st, pk);                    \
-        else hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 4, 3>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), \
-                                dim3(NTH2), (gemm2_lds<256, 256>()), st, pk);                                     \
-    } else if (v6 && BMv == 256 && BNv == 256)                                                                      \
-        hipLaunchKernelGGL((k_gemm6<AM, BMN>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y), dim3(NTH2),   \
-                           (gemm2_lds<256, 256>()), st, pk);                                                      \
-    else if (v5 && BMv == 256 && BNv == 256)                                                                      \
-        hipLaunchKernelGGL((k_gemm3<256, 256, AM, BMN, 5>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy.y),  \
-                           dim3(NTH2), (gemm2_lds<256, 256, 5>()), st, pk);                                       \
-    else if (v3) hipLaunchKernelGGL((k_gemm3<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv), gy.y), \
-                               dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk);                                        \
-    else hipLaunchKernelGGL((k_gemm2<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv)),         \
-                            dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk)
-#define L2SEL(BMv, BNv)                                     \
-    if (!amn && !bmn) L2(BMv, BNv, false, false);           \
-    else if (!amn && bmn) L2(BMv, BNv, false, true);        \
-    else if (amn && bmn) L2(BMv, BNv, true, true);          \
-    else L2(BMv, BNv, true, false);
-        if (var == 2) { L2SEL(256, 256) }
-        else if (var == 3) { L2SEL(256, 128) }
-        else { L2SEL(128, 256) }
-#undef L2SEL
-#undef L2
-        KD_LAUNCH_CHECK("k_gemm2");
+        const unsigned gy = (unsigned)pl.split;
+        if (force == 17) {   // v8 with in-kernel stamps (diagnostic: aux receives the stamps)
+            const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy);
+            const size_t lds = gemm2_lds<256, 256>();
+            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, true>), grid, dim3(NTH8), lds, st, pk);
+            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, true>), grid, dim3(NTH8), lds, st, pk);
+            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, true>), grid, dim3(NTH8), lds, st, pk);
+            else hipLaunchKernelGGL((k_gemm8<true, false, true>), grid, dim3(NTH8), lds, st, pk);
+            KD_LAUNCH_CHECK("k_gemm8<stamp>");
+        } else if (force == 16) {
+            const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy);
+            const size_t lds = gemm2_lds<256, 256>();
+            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false>), grid, dim3(NTH8), lds, st, pk);
+            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true>), grid, dim3(NTH8), lds, st, pk);
+            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true>), grid, dim3(NTH8), lds, st, pk);
+            else hipLaunchKernelGGL((k_gemm8<true, false>), grid, dim3(NTH8), lds, st, pk);
+            KD_LAUNCH_CHECK("k_gemm8");
+        } else {
+#define L3(BMv, BNv, AM, BMN)                                                                                     \
+    hipLaunchKernelGGL((k_gemm3<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv), gy),        \
+                       dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk)
+#define L3SEL(BMv, BNv)                                     \
+    if (!amn && !bmn) L3(BMv, BNv, false, false);           \
+    else if (!amn && bmn) L3(BMv, BNv, false, true);        \
+    else if (amn && bmn) L3(BMv, BNv, true, true);          \
+    else L3(BMv, BNv, true, false);
+            if (pl.var == 2) { L3SEL(256, 256) }
+            else if (pl.var == 3) { L3SEL(256, 128) }
+            else { L3SEL(128, 256) }
+#undef L3SEL
+#undef L3
+            KD_LAUNCH_CHECK("k_gemm3");
+        }
         if (pl.split > 1) {
             p.split_stride = (int64_t)d->M * d->N;
             const int64_t work = (int64_t)d->M * d->N / 4;

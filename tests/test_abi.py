@@ -64,4 +64,4 @@ def test_gemm_splitk_plan():
     assert ws(_gemm_desc(512, 512, 4096, split_k=4)) == 4 * 512 * 512 * 4
     assert ws(_gemm_desc(896, 896, 6144, 1, 1, split_k=1)) == 0
     assert ws(_gemm_desc(896, 896, 6144, 1, 1, variant=1)) == 0
-    assert ws(_gemm_desc(896, 896, 6144, 1, 1, variant=2)) == 0   # v2 tiles have no split path
+    assert ws(_gemm_desc(896, 896, 6144, 1, 1, variant=16)) > 0   # forced 256x256 tile still splits

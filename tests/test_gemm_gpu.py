@@ -93,7 +93,7 @@ def test_epilogue_bias_act_residual_aux_accumulate(dev):
     assert (out - 0.5 * (a.float() @ w.float().t())).abs().max().item() < 1e-3
 
 
-VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 14, 15]   # 128x128 v1; v2 256x256 / 256x128 / 128x256; v3 (pipelined) same tiles; v4 256x256 BK64
+VARIANTS = [1, 5, 6, 7, 16]   # 128x128 v1; v3 256x256 / 256x128 / 128x256 (8 waves); v8 256x256 (4 waves, AGPR acc)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -119,7 +119,7 @@ def test_variants_all_layouts(variant, M, N, K, dev):
         _check(ops.gemm(at.t(), w, variant=variant), at.float().t() @ w.float().t())
 
 
-@pytest.mark.parametrize("variant", [2, 3, 5, 6, 7, 8, 9, 10, 14])
+@pytest.mark.parametrize("variant", [5, 6, 7, 16])
 def test_variant_epilogue(variant, dev):
     ops = _ops()
     M, N, K = 1458, 1152, 192
@@ -139,7 +139,7 @@ def test_variant_epilogue(variant, dev):
 
 
 @pytest.mark.parametrize("split", [2, 3, 7])
-@pytest.mark.parametrize("variant", [0, 6, 7, 8, 9, 10, 14])
+@pytest.mark.parametrize("variant", [0, 6, 7, 16])
 @pytest.mark.parametrize("M,N,K", [(520, 384, 2248), (1152, 1152, 5832)])
 def test_splitk_all_layouts(split, variant, M, N, K, dev):
     """Forced K splits (fp32 partial planes + reduce) in every operand layout; K is not a

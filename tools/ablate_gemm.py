@@ -1,5 +1,4 @@
-"""Timing ablations of the v3 GEMM main loop (variants 11/12/13 compute WRONG results on
-purpose: no in-loop DMA / no barrier / no fragment reads) against the real kernel.
+"""A/B timing of the GEMM main-loop variants on one shape, interleaved rounds in one process.
     python tools/ablate_gemm.py [M N K]"""
 import sys
 from pathlib import Path
@@ -15,8 +14,7 @@ g = torch.Generator(device=dev).manual_seed(0)
 a = torch.randn(M, K, device=dev, generator=g).bfloat16()
 b = torch.randn(N, K, device=dev, generator=g).bfloat16()
 out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-names = {5: "v3", 11: "v3 no-DMA", 12: "v3 no-barrier", 13: "v3 no-frag-reads", 9: "v3 5-stage", 10: "v6 ping-pong",
-         8: "v4 BK64", 14: "v5 4-wave", 15: "v7 ring 4-wave"}
+names = {5: "v3 (8 waves)", 16: "v8 (4 waves, AGPR acc)"}
 res = {v: [] for v in names}
 for rnd in range(3):
     for v in names:

@@ -1,0 +1,14 @@
+# PMC passes (one rocprofv3 run per counter set) on one GEMM shape: kd_gemm (variant V) vs torch.mm (hipBLASLt)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+M=${M:-6144}; N=${N:-37888}; K=${K:-3584}; V=${V:-5}
+i=0
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES" \
+           "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_MFMA" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_kd/p$i -o p -- python3 tools/gemm_one.py $M $N $K $V nt 5 > gpurun_out/pmc_kd_p$i.log 2>&1 || { echo "kd pmc p$i failed"; tail -5 gpurun_out/pmc_kd_p$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_bl/p$i -o p -- python3 tools/torch_mm_one.py $M $N $K 5 > gpurun_out/pmc_bl_p$i.log 2>&1 || { echo "bl pmc p$i failed"; tail -5 gpurun_out/pmc_bl_p$i.log; exit 1; }
+done
+timeout -s KILL 90 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc_bl/kt -o k -- python3 tools/torch_mm_one.py $M $N $K 5 > gpurun_out/pmc_bl_kt.log 2>&1 || { echo kt failed; exit 1; }
+echo pmc done
