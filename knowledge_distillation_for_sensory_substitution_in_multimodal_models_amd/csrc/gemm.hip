@@ -21,6 +21,8 @@
 // 16x16x32 operand access pattern (derivation in DESIGN.md §GEMM).
 #include "common.h"
 
+#include <type_traits>
+
 namespace kd {
 namespace {
 
@@ -563,13 +565,19 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
 // operand): with the builtin, hipcc splits them over both files and moves ~330
 // registers per iteration between them. VGPRs hold two fragment sets (stage t in use,
 // stage t+1 being read) and the loop-invariant per-lane DMA offsets.
-//   step t (slot t%4, unrolled x4 so every slot index is a constant):
-//     lgkmcnt(0) [fragments of t in registers] ; vmcnt(16) [stage t+1 landed] ; s_barrier
-//     8 units of { 1 DMA of stage t+4 -> slot t%4, 2 fragment reads of stage t+1, 8 MFMA }
-// WAR: slot t%4 was last read (fragments of t, during step t-1) before every wave's
-// lgkmcnt(0) + barrier of step t. RAW: stage t+1 is read after the barrier that follows
-// every wave's vmcnt for it. DMA past the last stage is issued anyway (all lanes out of
-// range: no memory traffic, the slot is never read) so the counts stay uniform.
+// One wave per SIMD issues everything itself, so every non-MFMA instruction goes into its
+// own MFMA gap (a DMA issue costs ~60 cycles of MFMA pipe if it shares a 16-cycle gap with
+// other work; MI355X_MICROARCH.md constants table):
+//   step t (slot t%4, unrolled x4 so every slot index is a constant), unit u = 0..7:
+//     8 MFMA acc[u][*] += CA[u] * CB[*]; between them: 1 DMA of stage t+4 -> slot t%4,
+//     and in units 0-3 four fragment reads of stage t+1 -> NXT
+//     before the last MFMA of the step: lgkmcnt(0) [NXT complete] ; vmcnt(16) [stage t+2
+//     landed] ; s_barrier
+// WAR: slot (t+1)%4 (refilled in step t+1) held stage t+1, whose reads every wave retired
+// (lgkmcnt 0) before the barrier at the end of step t. RAW: stage t+2 is read in step t+1,
+// after the barrier that follows every wave's vmcnt for it. DMA past the last stage is
+// issued anyway (all lanes out of range: no memory traffic, the slot is never read) so
+// the counts stay uniform.
 // K-major operands: one descriptor per block, per-lane voffset fixed, the stage's k
 // offset in soffset. MN-major: one descriptor per stage (its k rows), voffset fixed.
 // =============================================================================
@@ -593,15 +601,18 @@ __device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, i
     }
 }
 
-// STAMP (variant 17, diagnostic only): per-wave s_memtime cycle totals of the top-of-step
-// waits, the MFMA units, the prologue and the epilogue, written as uint32 to p.aux
-// (which then carries no pre-activation output).
-template <bool A_MN, bool B_MN, bool STAMP = false>
+// EXP (diagnostic variants 17-19 only; production = 0): bit 0 writes per-wave s_memtime
+// cycle totals (step-end sync, MFMA units, prologue, epilogue) as uint32 to p.aux (which
+// then carries no pre-activation output); bit 1 drops the in-loop DMA (timing ablation:
+// WRONG results); bit 6 re-reads stage 0 for every stage (same addresses, L2-hot:
+// separates issue cost from memory-system cost; WRONG results).
+template <bool A_MN, bool B_MN, int EXP = 0>
 __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
+    constexpr bool STAMP = EXP & 1, NODMA = EXP & 2, HOT = EXP & 64;
     GemmP p = p_;
     uint32_t* stamps = nullptr;
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
-    uint64_t s_pro = 0, s_lgkm = 0, s_vm = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
+    uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
     if (STAMP) ts0 = __builtin_amdgcn_s_memtime();
     if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
         const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
@@ -612,13 +623,14 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     }
     constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: LDS-DMA bases in SGPRs
     const int wm = wid >> 1, wn = wid & 1;
     int tm, tn;
     tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
     const int m0 = tm * 256, n0 = tn * 256;
     const int K = p.K;
-    const int nk = (K + BK2 - 1) / BK2;
+    const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
     const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (A_MN ? 0 : (int64_t)m0 * p.lda), A_MN ? 0u : rec_bytes(min(256, p.M - m0), p.lda));
     const __amdgpu_buffer_rsrc_t rsBk = make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
     uint32_t va[4], vb[4];
@@ -627,29 +639,38 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
         va[u] = voff8<A_MN>(wid * 4 + u, lane, p.lda, m0, p.M);
         vb[u] = voff8<B_MN>(wid * 4 + u, lane, p.ldb, n0, p.N);
     }
-    // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl
-    auto dma = [&](int st, int sl, int u) {
+    // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl;
+    // FULL: the stage lies wholly inside K (no per-lane tail masking)
+    auto dma = [&](int st, int sl, int u, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        if (NODMA) return;
         const bool isA = u < 4;
         const bool mn = isA ? A_MN : B_MN;
         const int i = wid * 4 + (u & 3);
         char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
-        const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
         uint32_t v = isA ? va[u & 3] : vb[u & 3];
         if (!mn) {
-            if (kleft < BK2) {   // K tail / past the end: zero the chunks at k >= K
-                const int row = 16 * i + (lane >> 2);
-                const int gc = (lane & 3) ^ f4(row);
-                if (gc * 8 >= kleft) v = OOB;
+            int soff = HOT ? 0 : st * BK2 * 2;
+            if (!FULL) {
+                const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
+                if (kleft < BK2) {                // zero the chunks at k >= K
+                    const int row = 16 * i + (lane >> 2);
+                    const int gc = (lane & 3) ^ f4(row);
+                    if (gc * 8 >= kleft) v = OOB;
+                    if (kleft <= 0) soff = 0;
+                }
             }
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, v, kleft > 0 ? st * BK2 * 2 : 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, v, soff, 0, 0);
         } else {
             const bf16* base = isA ? p.A + m0 : p.B + n0;
             const int64_t ld = isA ? p.lda : p.ldb;
-            const int kv = max(0, min(BK2, kleft));
-            const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)min(st * BK2, K) * ld, rec_bytes(kv, ld));
+            const int kv = FULL ? BK2 : max(0, min(BK2, K - st * BK2));
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)(FULL ? st * BK2 : min(st * BK2, K)) * ld, rec_bytes(kv, ld));
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)dst, 16, v, 0, 0, 0);
         }
     };
+    using FullT = std::integral_constant<bool, true>;
+    using PartT = std::integral_constant<bool, false>;
     f32x4 acc[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -659,8 +680,9 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
 #pragma unroll
     for (int st = 0; st < NS8; ++st)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dma(st, st, u);
-    wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
+        for (int u = 0; u < 8; ++u) dma(st, st, u, PartT{});
+    if (NODMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
     __builtin_amdgcn_s_barrier();
     uint64_t tprev = 0;
     if (STAMP) { tprev = __builtin_amdgcn_s_memtime(); s_pro = tprev - ts0; }
@@ -670,45 +692,66 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
         xa[u] = frag2<256, A_MN>(smem, ra + u * 16, lane);
         xb[u] = frag2<256, B_MN>(smem + SA, cb + u * 16, lane);
     }
-
-#define KD_G8_STEP(SL, CA, CB, NA, NB)                                                                       \
+    // step-end sync (also closes the prologue): my reads of the current slot are done,
+    // the stage the next step reads has landed for every wave
+#define KD_G8_SYNC()                                                                                         \
     {                                                                                                         \
-        const int t_ = t + (SL);                                                                              \
-        uint64_t ta_ = 0, tb_ = 0, tc_ = 0, td_ = 0;                                                          \
+        uint64_t ta_ = 0, tb_ = 0;                                                                            \
         if (STAMP) ta_ = __builtin_amdgcn_s_memtime();                                                        \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                    \
-        if (STAMP) tb_ = __builtin_amdgcn_s_memtime();                                                        \
-        wait_vm<16>();                                                                                        \
-        if (STAMP) tc_ = __builtin_amdgcn_s_memtime();                                                        \
+        if (!NODMA) wait_vm<16>();                                                                            \
         __builtin_amdgcn_s_barrier();                                                                         \
         if (STAMP) {                                                                                          \
-            td_ = __builtin_amdgcn_s_memtime();                                                               \
-            if (tprev) s_units += ta_ - tprev;                                                                \
-            s_lgkm += tb_ - ta_; s_vm += tc_ - tb_; s_bar += td_ - tc_; tprev = td_;                          \
+            tb_ = __builtin_amdgcn_s_memtime();                                                               \
+            s_units += ta_ - tprev; s_bar += tb_ - ta_; tprev = tb_;                                          \
         }                                                                                                     \
-        __builtin_amdgcn_sched_barrier(0);                                                                    \
+    }
+    KD_G8_SYNC()
+    __builtin_amdgcn_sched_barrier(0);
+#define KD_SB __builtin_amdgcn_sched_barrier(0);
+#define KD_G8_STEP(SL, CA, CB, NA, NB, FT)                                                                   \
+    {                                                                                                         \
+        const int t_ = t + (SL);                                                                              \
         const char* na_ = smem + (((SL) + 1) % NS8) * SS;                                                     \
         _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
-            dma(t_ + NS8, (SL), u);                                                                           \
-            NA[u] = frag2<256, A_MN>(na_, ra + u * 16, lane);                                                 \
-            NB[u] = frag2<256, B_MN>(na_ + SA, cb + u * 16, lane);                                            \
-            __builtin_amdgcn_sched_barrier(0);                                                                \
-            _Pragma("unroll") for (int j = 0; j < 8; ++j) mfma_agpr(acc[u][j], CA[u], CB[j]);                 \
-            __builtin_amdgcn_sched_barrier(0);                                                                \
+            mfma_agpr(acc[u][0], CA[u], CB[0]); KD_SB                                                         \
+            dma(t_ + NS8, (SL), u, FT{}); KD_SB                                                               \
+            mfma_agpr(acc[u][1], CA[u], CB[1]); KD_SB                                                         \
+            if (u < 4) NA[2 * u] = frag2<256, A_MN>(na_, ra + 2 * u * 16, lane);                              \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][2], CA[u], CB[2]); mfma_agpr(acc[u][3], CA[u], CB[3]); KD_SB                     \
+            if (u < 4) NB[2 * u] = frag2<256, B_MN>(na_ + SA, cb + 2 * u * 16, lane);                         \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][4], CA[u], CB[4]); mfma_agpr(acc[u][5], CA[u], CB[5]); KD_SB                     \
+            if (u < 4) NA[2 * u + 1] = frag2<256, A_MN>(na_, ra + (2 * u + 1) * 16, lane);                    \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][6], CA[u], CB[6]); KD_SB                                                         \
+            if (u < 4) NB[2 * u + 1] = frag2<256, B_MN>(na_ + SA, cb + (2 * u + 1) * 16, lane);               \
+            if (u == 7) KD_G8_SYNC()                                                                          \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][7], CA[u], CB[7]); KD_SB                                                         \
         }                                                                                                     \
     }
     int t = 0;
+    for (; t + 2 * NS8 <= nk_full; t += NS8) {   // every DMA of these steps lies inside K
+        KD_G8_STEP(0, xa, xb, ya, yb, FullT)
+        KD_G8_STEP(1, ya, yb, xa, xb, FullT)
+        KD_G8_STEP(2, xa, xb, ya, yb, FullT)
+        KD_G8_STEP(3, ya, yb, xa, xb, FullT)
+    }
     for (; t + NS8 <= nk; t += NS8) {
-        KD_G8_STEP(0, xa, xb, ya, yb)
-        KD_G8_STEP(1, ya, yb, xa, xb)
-        KD_G8_STEP(2, xa, xb, ya, yb)
-        KD_G8_STEP(3, ya, yb, xa, xb)
+        KD_G8_STEP(0, xa, xb, ya, yb, PartT)
+        KD_G8_STEP(1, ya, yb, xa, xb, PartT)
+        KD_G8_STEP(2, xa, xb, ya, yb, PartT)
+        KD_G8_STEP(3, ya, yb, xa, xb, PartT)
     }
     const int rem = nk - t;
-    if (rem > 0) KD_G8_STEP(0, xa, xb, ya, yb)
-    if (rem > 1) KD_G8_STEP(1, ya, yb, xa, xb)
-    if (rem > 2) KD_G8_STEP(2, xa, xb, ya, yb)
+    if (rem > 0) KD_G8_STEP(0, xa, xb, ya, yb, PartT)
+    if (rem > 1) KD_G8_STEP(1, ya, yb, xa, xb, PartT)
+    if (rem > 2) KD_G8_STEP(2, xa, xb, ya, yb, PartT)
 #undef KD_G8_STEP
+#undef KD_G8_SYNC
+#undef KD_SB
     // drain the ring (out-of-range DMAs still write LDS) and the MFMA pipe before the
     // accumulators are read back (asm MFMAs are invisible to the hazard recognizer)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -722,12 +765,11 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
         s_epi = te1 - te0;
         if (lane == 0) {
             uint32_t* o = stamps + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wid) * 8;
-            o[0] = (uint32_t)s_pro; o[1] = (uint32_t)s_lgkm; o[2] = (uint32_t)s_vm; o[3] = (uint32_t)s_bar;
+            o[0] = (uint32_t)s_pro; o[1] = 0; o[2] = 0; o[3] = (uint32_t)s_bar;
             o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
         }
     }
 }
-
 
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
 // (alpha, alpha_dev, bias, aux, act, residual, accumulate), 4 columns per thread
@@ -773,43 +815,46 @@ __global__ void k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p) {
     }
 }
 
-// Tile / split-K plan for the 8-wave kernels. Cost model in units of one 32-deep k-step
-// of a 256x256 tile on one CU (~0.9 us): waves x (k-steps x tile cost + fixed per-tile
-// prologue/epilogue), plus the partial-plane traffic at ~5 TB/s. Constants fitted to a
-// tile x split sweep over every GEMM shape of the KD step (tools/tune_gemm.py): the
-// model's picks are within 0.1% of the measured best over those 34 shapes.
-struct GemmPlan { int var; int split; int64_t kchunk; };
+// Kernel / tile / split-K plan. Cost model in microseconds: waves x (32-deep k-steps per
+// split x per-step tile cost + fixed per-tile prologue/epilogue), plus the fp32
+// partial-plane traffic of a split at ~6.2 TB/s. Candidates: v3 256x256 / 256x128 /
+// 128x256 (8 waves) and v8 256x256 (4 waves, K-major x K-major only). Constants fitted
+// (least squares on log time) to a kernel x tile x split sweep over all 42 GEMM shapes of
+// the c1 KD step (tools/tune_gemm.py, profiles/r01/gemm_tune.jsonl): the model's picks
+// are within 0.4% of the measured best per step (129.7 vs 129.3 ms of GEMM).
+struct GemmPlan { int var; int split; int64_t kchunk; };   // var: 2/3/4 v3 tiles, 16 v8
 
 GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t M = d->M, N = d->N;
-    const int64_t tiles[3] = {(int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 256),
-                              (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 128),
-                              (int64_t)ceil_div(d->M, 128) * ceil_div(d->N, 256)};
-    const double step[3] = {1.0, 0.70, 0.65};   // 256x256, 256x128, 128x256
-    const double fixed[3] = {24.0, 12.0, 6.0};
+    const int64_t t256 = (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 256);
+    const int64_t tiles[4] = {t256, (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 128),
+                              (int64_t)ceil_div(d->M, 128) * ceil_div(d->N, 256), t256};
+    const double step[4] = {0.9848, 0.7656, 0.7569, 0.6844};   // v3 256x256, 256x128, 128x256; v8
+    const double fixed[4] = {3.968, 1.711, 1.166, 7.695};
+    const int vcode[4] = {2, 3, 4, 16};
+    const bool kk = d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR;
     const int64_t nk = ceil_div(d->K, BK2);
-    // forced tile: variants 2/5 (and v8 = 16) 256x256, 3/6 256x128, 4/7 128x256; 0 = model's choice
-    const int fv = d->variant >= 16 ? 0 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
-    const bool split_ok = true;
+    // forced: variants 2/5 v3 256x256, 3/6 256x128, 4/7 128x256, 16+ v8; 0 = model's choice
+    const int fv = d->variant >= 16 ? 3 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
     const double out_b = (double)M * N * ((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
                                           (d->residual ? 2 : 0) + (d->aux ? 2 : 0));
-    GemmPlan best{fv >= 0 ? fv + 2 : 2, 1, d->K};
+    GemmPlan best{fv >= 0 ? vcode[fv] : 2, 1, d->K};
     double bt = 1e300;
-    for (int v = 0; v < 3; ++v) {
+    for (int v = 0; v < 4; ++v) {
         if (fv >= 0 && v != fv) continue;
+        if (v == 3 && !kk && fv != 3) continue;   // v8's MN-major paths are not competitive
         for (int S = 1; S <= 32; ++S) {
             if (d->split_k == 1 && S != 1) continue;
             if (d->split_k > 1 && S != d->split_k && S != 1) continue;
-            if (S > 1 && !split_ok) continue;
             const int64_t kcs = (nk + S - 1) / S;
             if (S > 1 && ((nk + kcs - 1) / kcs != S)) continue;          // empty trailing split
             if (S > 1 && d->split_k <= 1 && kcs < 8) continue;           // too little work per split
             if (S > 1 && (uint64_t)S * M * N * 4 > ws_cap) continue;
             const int64_t waves = (tiles[v] * S + 255) / 256;
             double t = (double)waves * ((double)kcs * step[v] + fixed[v]);
-            if (S > 1) t += ((double)S * M * N * 8 + out_b) / 4.5e6;
+            if (S > 1) t += ((double)S * M * N * 8 + out_b) / 6.222e6;
             if (d->split_k > 1 && S == d->split_k) t = -1;              // forced
-            if (t < bt) { bt = t; best = GemmPlan{v + 2, S, kcs * BK2}; }
+            if (t < bt) { bt = t; best = GemmPlan{vcode[v], S, kcs * BK2}; }
         }
     }
     return best;
@@ -829,7 +874,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->act == KD_ACT_NONE || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
                                           d->c_dtype == KD_DTYPE_BF16),
                  "gemm: an activation epilogue needs K-major operands and a bf16 output");
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || d->variant == 16 || d->variant == 17, "gemm: unknown variant");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 19), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     KD_CHECK_SHAPE(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
@@ -867,7 +912,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                         (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
                         (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
     const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,
-                                    // 16 v8 256x256 (4 waves, AGPR accumulators)
+                                    // 16 v8 256x256 (4 waves, AGPR accumulators), 17-19 v8 diagnostics
     if (force != 1 && big_ok) {
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
         GemmP pk = p;   // the tile kernels' parameters (split-K: plain fp32 partial planes)
@@ -879,21 +924,29 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N;
         }
         const unsigned gy = (unsigned)pl.split;
-        if (force == 17) {   // v8 with in-kernel stamps (diagnostic: aux receives the stamps)
+        if (pl.var == 16) {   // v8; forced variants 17-19 are its diagnostic builds (EXP bits above)
             const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy);
             const size_t lds = gemm2_lds<256, 256>();
-            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, true>), grid, dim3(NTH8), lds, st, pk);
-            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, true>), grid, dim3(NTH8), lds, st, pk);
-            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, true>), grid, dim3(NTH8), lds, st, pk);
-            else hipLaunchKernelGGL((k_gemm8<true, false, true>), grid, dim3(NTH8), lds, st, pk);
-            KD_LAUNCH_CHECK("k_gemm8<stamp>");
-        } else if (force == 16) {
-            const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy);
-            const size_t lds = gemm2_lds<256, 256>();
-            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false>), grid, dim3(NTH8), lds, st, pk);
-            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true>), grid, dim3(NTH8), lds, st, pk);
-            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true>), grid, dim3(NTH8), lds, st, pk);
-            else hipLaunchKernelGGL((k_gemm8<true, false>), grid, dim3(NTH8), lds, st, pk);
+#define L8(E)                                                                                                   \
+    {                                                                                                           \
+        if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, pk);        \
+        else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, E>), grid, dim3(NTH8), lds, st, pk);     \
+        else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, E>), grid, dim3(NTH8), lds, st, pk);       \
+        else hipLaunchKernelGGL((k_gemm8<true, false, E>), grid, dim3(NTH8), lds, st, pk);                      \
+    }
+#define L8K(E)                                                                                                  \
+    {                                                                                                           \
+        if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, pk);        \
+        else L8(0)                                                                                              \
+    }
+            switch (force) {   // the diagnostic builds exist for the forward (K-major x K-major) layout only
+                case 17: L8K(1) break;
+                case 18: L8K(2) break;
+                case 19: L8K(64) break;
+                default: L8(0) break;
+            }
+#undef L8K
+#undef L8
             KD_LAUNCH_CHECK("k_gemm8");
         } else {
 #define L3(BMv, BNv, AM, BMN)                                                                                     \

@@ -14,7 +14,9 @@ g = torch.Generator(device=dev).manual_seed(0)
 a = torch.randn(M, K, device=dev, generator=g).bfloat16()
 b = torch.randn(N, K, device=dev, generator=g).bfloat16()
 out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-names = {5: "v3 (8 waves)", 16: "v8 (4 waves, AGPR acc)"}
+names = {k: v for k, v in {5: "v3 (8 waves)", 16: "v8 (4 waves, AGPR acc)", 18: "v8 no DMA (ablation)",
+                            19: "v8 L2-hot DMA (ablation)"}.items()
+         if not __import__("os").environ.get("VARS") or str(k) in __import__("os").environ["VARS"].split(",")}
 res = {v: [] for v in names}
 for rnd in range(3):
     for v in names:

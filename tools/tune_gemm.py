@@ -1,4 +1,4 @@
-"""Sweep tile (v3 256x256 / 256x128 / 128x256) x split-K for the KD step's GEMM shapes and
+"""Sweep kernel/tile (v3 256x256 / 256x128 / 128x256, v8 256x256 for K-major x K-major) x split-K for the KD step's GEMM shapes and
 print the measured best next to the library's own plan (calibrates gemm.hip:plan_gemm).
     python tools/tune_gemm.py [shapes.json] [top]"""
 import json
@@ -12,7 +12,7 @@ from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd im
 
 dev = torch.device("cuda:0")
 src = sys.argv[1] if len(sys.argv) > 1 else None
-top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+top = int(sys.argv[2]) if len(sys.argv) > 2 else 60
 if src:
     rows = json.load(open(src))[:top]
     shapes = [r["shape"] for r in rows]
@@ -47,7 +47,8 @@ for sh in shapes:
     fl = 2.0 * M * N * K
     auto = timeit(lambda: ops.gemm(a, b, out=out, accumulate=acc))
     res = {}
-    for var in (5, 6, 7, 8, 9, 10):
+    VARS = (5, 6, 7, 16) if kind == "gemm_kk" else (5, 6, 7)
+    for var in VARS:
         for sk in (1, 2, 3, 4, 6, 8, 12, 16):
             if sk > 1 and (K // 32) // sk < 4:
                 continue
@@ -57,6 +58,6 @@ for sh in shapes:
     best = min(res, key=res.get)
     row = dict(shape=sh, auto_ms=round(auto, 4), auto_tf=round(fl / auto / 1e9, 1), best=list(best),
                best_ms=round(res[best], 4), best_tf=round(fl / res[best] / 1e9, 1),
-               s1={v: round(res[(v, 1)], 4) for v in (5, 6, 7, 8, 9, 10)},
+               s1={v: round(res[(v, 1)], 4) for v in VARS},
                all={f"{v}/{s}": round(t, 4) for (v, s), t in sorted(res.items())})
     print(json.dumps(row), flush=True)
