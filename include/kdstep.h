@@ -112,7 +112,13 @@ int kd_loss_check(const void* workspace, void* stream);
  * rows % 8 == 0 for MN-major ones.  Any M/N/K otherwise (tails read as zeros). */
 typedef enum { KD_LAYOUT_K_MAJOR = 0, KD_LAYOUT_MN_MAJOR = 1 } kd_layout;
 typedef enum { KD_DTYPE_BF16 = 0, KD_DTYPE_F32 = 1 } kd_dtype;
-typedef enum { KD_ACT_NONE = 0, KD_ACT_GELU_TANH = 1, KD_ACT_GELU_ERF = 2, KD_ACT_SILU = 3 } kd_act;
+/* KD_ACT_SWIGLU: Qwen2MLP's act_fn(gate_proj(x)) * up_proj(x) (HF5 qwen2 :35-50) fused into
+ * the gate|up GEMM: B = [gate; up] is [N = 2I][K] (I % 128 == 0), C is [M][I] =
+ * silu(v[:, :I]) * v[:, I:] with v = alpha * acc rounded to bf16 first (as the unfused
+ * GEMM output), aux (optional) receives v [M][2I] for the backward.  K-major operands,
+ * bf16 C, no bias / residual / accumulate / split-K. */
+typedef enum { KD_ACT_NONE = 0, KD_ACT_GELU_TANH = 1, KD_ACT_GELU_ERF = 2, KD_ACT_SILU = 3,
+               KD_ACT_SWIGLU = 4 } kd_act;
 
 typedef struct {
     int32_t M, N, K;
@@ -132,7 +138,9 @@ typedef struct {
     void* aux;                /* optional bf16 [M][N] pre-activation output */
     int64_t ld_aux;
     int32_t residual_row_mod; /* >0: residual row index = m % residual_row_mod (SigLIP pos-emb) */
-    int32_t variant;          /* 0 auto; 1 128x128 4-wave; 2/3/4 256x256 / 256x128 / 128x256 8-wave (tests) */
+    int32_t variant;          /* 0 auto (cost model); forced (tests/tools): 1 128x128 4-wave; 2|5 / 3|6 / 4|7
+                                 256x256 / 256x128 / 128x256 8-wave; 16 256x256 4-wave (AGPR accumulators);
+                                 17-19 diagnostic builds of 16 (tools/stamp_gemm.py, tools/ablate_gemm.py) */
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;

@@ -42,7 +42,7 @@ class KdLossParams(C.Structure):
 # kd_layout / kd_dtype / kd_act
 KD_LAYOUT_K_MAJOR, KD_LAYOUT_MN_MAJOR = 0, 1
 KD_DTYPE_BF16, KD_DTYPE_F32 = 0, 1
-KD_ACT_NONE, KD_ACT_GELU_TANH, KD_ACT_GELU_ERF, KD_ACT_SILU = 0, 1, 2, 3
+KD_ACT_NONE, KD_ACT_GELU_TANH, KD_ACT_GELU_ERF, KD_ACT_SILU, KD_ACT_SWIGLU = 0, 1, 2, 3, 4
 
 
 class KdGemmDesc(C.Structure):

@@ -42,6 +42,7 @@ struct GemmP {
     int c_f32, accumulate, bias_f32, act, res_mod;
     int64_t kchunk;        // split-K: K elements per split (gridDim.y splits)
     int64_t split_stride;  // split-K: fp32 elements between consecutive partial planes
+    int glu;               // SwiGLU epilogue (v8, K-major): I = N/2; B rows [0,I) gate, [I,2I) up; 0 = off
 };
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
@@ -461,6 +462,50 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
     }
 }
 
+// SwiGLU epilogue (KD_ACT_SWIGLU, v8 only): the 256-column tile holds gate features
+// [nb, nb+128) in columns 0-127 and the matching up features in columns 128-255 (the B
+// rows are gathered that way by the DMA), so C[:, nb + c] = silu(gate) * up needs no
+// second pass over HBM: pre-activations are staged once as bf16 in LDS (the rounding the
+// unfused GEMM output had), optionally written to aux ([M, 2I] gate | up, for the
+// backward), then combined in fp32 exactly as k_swiglu_fwd does.
+template <int TM, int TN, int MT, int NT, int NTHR>
+__device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int nb, int wm,
+                                             int wn, int lane, int tid) {
+    float alpha = p.alpha;
+    if (p.alpha_dev) alpha *= *p.alpha_dev;
+    float bcol[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bcol[j] = 0.f;
+    constexpr int RS = 256 * 2 + 16;
+    epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS, alpha, bcol, wm, wn, lane, 0, 256);
+    __syncthreads();
+    const int I = p.glu;
+    const bool full = m0 + 256 <= p.M;
+    if (p.aux) {
+#pragma unroll 4
+        for (int idx = tid; idx < 256 * 32; idx += NTHR) {
+            const int lr = idx >> 5, c = idx & 31, row = m0 + lr;
+            if (!full && row >= p.M) continue;
+            const int col = c < 16 ? nb + c * 8 : I + nb + (c - 16) * 8;
+            *(bf16x8*)(p.aux + (int64_t)row * p.ld_aux + col) = *(const bf16x8*)(smem + lr * RS + c * 16);
+        }
+    }
+#pragma unroll 4
+    for (int idx = tid; idx < 256 * 16; idx += NTHR) {
+        const int lr = idx >> 4, c = idx & 15, row = m0 + lr;
+        if (!full && row >= p.M) continue;
+        const bf16x8 g = *(const bf16x8*)(smem + lr * RS + c * 16);
+        const bf16x8 u = *(const bf16x8*)(smem + lr * RS + 256 + c * 16);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float gf = (float)g[e];
+            o[e] = (bf16)(gf / (1.f + __expf(-gf)) * (float)u[e]);
+        }
+        *(bf16x8*)((bf16*)p.C + (int64_t)row * p.ldc + nb + c * 8) = o;
+    }
+}
+
 // =============================================================================
 // v3: the tiles above and their 4-stage LDS ring, software-pipelined one stage deeper: the
 // fragments of stage t+1 are read into a second register set WHILE the MFMAs of stage t
@@ -632,12 +677,22 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
     const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (A_MN ? 0 : (int64_t)m0 * p.lda), A_MN ? 0u : rec_bytes(min(256, p.M - m0), p.lda));
-    const __amdgpu_buffer_rsrc_t rsBk = make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
+    const bool glu = !B_MN && p.glu != 0;   // gate rows [nb, nb+128) and up rows [I+nb, I+nb+128)
+    const int nb = tn * 128;
+    const __amdgpu_buffer_rsrc_t rsBk =
+        glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
+            : make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
     uint32_t va[4], vb[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         va[u] = voff8<A_MN>(wid * 4 + u, lane, p.lda, m0, p.M);
         vb[u] = voff8<B_MN>(wid * 4 + u, lane, p.ldb, n0, p.N);
+        if (glu) {   // tile row r -> weight row (r < 128 ? nb + r : I + nb + r - 128); same LDS swizzle
+            const int row = 16 * (wid * 4 + u) + (lane >> 2);
+            const int gc = (lane & 3) ^ f4(row);
+            const int wrow = row < 128 ? nb + row : p.glu + nb + row - 128;
+            vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
+        }
     }
     // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl;
     // FULL: the stage lies wholly inside K (no per-lane tail masking)
@@ -759,7 +814,8 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     uint64_t te0 = 0;
     if (STAMP) { te0 = __builtin_amdgcn_s_memtime(); s_units += te0 - tprev; }
     __syncthreads();
-    epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+    if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
+    else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
     if (STAMP) {
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         s_epi = te1 - te0;
@@ -870,7 +926,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->a_layout == KD_LAYOUT_K_MAJOR || d->a_layout == KD_LAYOUT_MN_MAJOR, "gemm: a_layout");
     KD_CHECK_ARG(d->b_layout == KD_LAYOUT_K_MAJOR || d->b_layout == KD_LAYOUT_MN_MAJOR, "gemm: b_layout");
     KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16 || d->c_dtype == KD_DTYPE_F32, "gemm: c_dtype");
-    KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_SILU, "gemm: act");
+    KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_SWIGLU, "gemm: act");
     KD_CHECK_ARG(d->act == KD_ACT_NONE || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
                                           d->c_dtype == KD_DTYPE_BF16),
                  "gemm: an activation epilogue needs K-major operands and a bf16 output");
@@ -889,7 +945,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     } else {
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldb >= d->N, "gemm: MN-major B needs N % 8 == 0, ldb >= N");
     }
-    KD_CHECK_SHAPE(d->ldc >= d->N, "gemm: ldc < N");
+    KD_CHECK_SHAPE(d->ldc >= (d->act == KD_ACT_SWIGLU ? d->N / 2 : d->N), "gemm: ldc < N (N/2 for swiglu)");
     KD_CHECK_SHAPE(!d->residual || d->ldr >= d->N, "gemm: ldr < N");
     KD_CHECK_SHAPE(!d->aux || d->ld_aux >= d->N, "gemm: ld_aux < N");
     KD_CHECK_SHAPE((uint64_t)256 * d->lda * 2 < 0x7FFFFFFFull && (uint64_t)256 * d->ldb * 2 < 0x7FFFFFFFull,
@@ -902,7 +958,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.c_f32 = d->c_dtype == KD_DTYPE_F32; p.accumulate = d->accumulate; p.bias_f32 = d->bias_dtype == KD_DTYPE_F32;
     p.act = d->act;
     p.res_mod = d->residual_row_mod;
-    p.kchunk = d->K; p.split_stride = 0;
+    p.kchunk = d->K; p.split_stride = 0; p.glu = 0;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
@@ -911,6 +967,20 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                         ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
                         (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
                         (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
+    if (d->act == KD_ACT_SWIGLU) {   // fused gate|up GEMM + silu(gate) * up, on v8
+        KD_CHECK_SHAPE(d->N % 256 == 0 && d->M >= 1, "gemm swiglu: N = 2I needs I % 128 == 0");
+        KD_CHECK_ARG(!d->bias && !d->residual && !d->accumulate && d->split_k <= 1,
+                     "gemm swiglu: no bias / residual / accumulate / split-K");
+        KD_CHECK_ARG(!amn && !bmn && d->c_dtype == KD_DTYPE_BF16 && c_ok16 && d->ldc >= d->N / 2,
+                     "gemm swiglu: K-major operands, 16-B aligned bf16 output [M, N/2]");
+        KD_CHECK_ARG(!d->aux || (d->ld_aux % 8 == 0 && (uintptr_t)d->aux % 16 == 0), "gemm swiglu: aux alignment");
+        GemmP pk = p;
+        pk.glu = d->N / 2; pk.act = KD_ACT_NONE;
+        const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
+        hipLaunchKernelGGL((k_gemm8<false, false, 0>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        KD_LAUNCH_CHECK("k_gemm8<swiglu>");
+        return KD_OK;
+    }
     const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,
                                     // 16 v8 256x256 (4 waves, AGPR accumulators), 17-19 v8 diagnostics
     if (force != 1 && big_ok) {
@@ -984,7 +1054,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
 }
 
 size_t gemm_workspace_size(const kd_gemm_desc* d) {
-    if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->variant == 1) return 0;
+    if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->variant == 1 || d->act == KD_ACT_SWIGLU) return 0;
     const GemmPlan pl = plan_gemm(d, ~0ull);
     return pl.split > 1 ? (size_t)pl.split * d->M * d->N * 4 : 0;
 }

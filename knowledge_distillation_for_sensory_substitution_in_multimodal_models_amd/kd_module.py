@@ -15,8 +15,11 @@ with `student_model.*` / `teacher_model.*` keys in the transformers-4.45 layout.
 student backward (hand-written kernels, explicit order) into flat fp32 gradient
 buffers, and the optimizer from `configure_optimizers()` is a fused AdamW over those
 buffers.  Data-parallel ranks all-reduce the trainable gradient range in buckets as the
-backward produces them (RCCL over xGMI), and the optimizer step of step t runs on a
-side stream so the teacher forward of step t+1 overlaps it.
+backward produces them (RCCL over xGMI).  Three streams per step: the teacher forward on
+the main stream; the student forward, which does not read any teacher output, on a second
+stream beside it (they fill each other's small-kernel gaps and GEMM wave-quantisation
+tails); the AdamW and gradient zeroing of step t on a third, overlapping the teacher
+forward of step t+1 (the student forward of step t+1 waits for them).
 """
 from __future__ import annotations
 
@@ -101,10 +104,13 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def zero_grad(self, set_to_none: bool = False):
         m = self.module
-        if m._opt_pending:   # the AdamW read the grads on the side stream
-            torch.cuda.current_stream().wait_event(m._opt_done)
         lo, hi = m._trainable_range()
-        m.student_model.P.grad[lo:hi].zero_()
+        if m._opt_pending:   # zero behind the AdamW on its stream; the next backward is ordered after it
+            with torch.cuda.stream(m._opt_stream):
+                m.student_model.P.grad[lo:hi].zero_()
+                m._opt_done.record(m._opt_stream)
+        else:
+            m.student_model.P.grad[lo:hi].zero_()
 
 
 class _KDBase(_Base):
@@ -131,6 +137,8 @@ class _KDBase(_Base):
         self.config = self.student_model.cfg
         self._anchor = nn.Parameter(torch.zeros((), device=dev))
         self._opt_stream = torch.cuda.Stream(device=dev)
+        self._stu_stream = torch.cuda.Stream(device=dev)
+        self.concurrent_student = True   # False: student forward on the main stream (bench.py --serial)
         self._opt_done = torch.cuda.Event()
         self._opt_pending = False
         self._ctx = None
@@ -199,6 +207,21 @@ class _KDBase(_Base):
         image_sizes = batch["image_sizes"]
         B, L = batch["depth_input_ids"].shape
         need_feats = ctr_w is not None
+        main = torch.cuda.current_stream()
+        s = self.student_model
+        # student forward on its own stream beside the teacher forward. It first waits for
+        # everything already queued on the main stream (so caching-allocator blocks the
+        # previous step freed there are reusable) and for the previous optimizer step (the
+        # student weights); the main stream joins it before the loss.
+        side = self._stu_stream if self.concurrent_student else main
+        side.wait_stream(main)
+        if self._opt_pending:
+            side.wait_event(self._opt_done)
+            self._opt_pending = False
+        with torch.cuda.stream(side):
+            sfwd = s.forward(batch["depth_input_ids"], batch["depth_pixel_values"], image_sizes, save=train,
+                             want_post_ln=need_feats)
+            s_logits = s.logits(sfwd["hn"])
         t_logits = None
         tfwd = None
         if self.uses_teacher:
@@ -206,13 +229,7 @@ class _KDBase(_Base):
                                               save=False, want_post_ln=need_feats)
             t_logits = self.teacher_model.logits(tfwd["hn"])
             del tfwd["hn"]
-        if self._opt_pending:  # the student weights of step t+1 need the AdamW of step t
-            torch.cuda.current_stream().wait_event(self._opt_done)
-            self._opt_pending = False
-        s = self.student_model
-        sfwd = s.forward(batch["depth_input_ids"], batch["depth_pixel_values"], image_sizes, save=train,
-                         want_post_ln=need_feats)
-        s_logits = s.logits(sfwd["hn"])
+        main.wait_stream(side)
         Vs = s_logits.shape[1]
         loss4, dlogits = ops.kd_loss_fwd_bwd(
             s_logits.view(B, L, Vs), None if t_logits is None else t_logits.view(B, L, -1), labels, variant,
@@ -307,6 +324,8 @@ class _KDBase(_Base):
 
     # ------------------------------------------------------------ checkpoints ----
     def kd_state_dict(self):
+        if self._opt_pending:   # weights of a queued optimizer step
+            torch.cuda.current_stream().wait_event(self._opt_done)
         sd = {f"student_model.{k}": v for k, v in self.student_model.P.state_dict().items()}
         if self.teacher_model is not None:
             sd.update({f"teacher_model.{k}": v for k, v in self.teacher_model.P.state_dict().items()})

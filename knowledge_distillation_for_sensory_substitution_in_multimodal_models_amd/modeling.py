@@ -472,8 +472,12 @@ class LlavaOnevisionModel:
             h2, _, r2 = ops.norm_fwd(x_mid, P[p + "post_attention_layernorm.weight"], None, T.eps, rms=True,
                                      save_stats=save)
             Wgu = P.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight", 2 * T.inter, T.hidden)
-            gu = ops.gemm(h2, Wgu)
-            a = ops.swiglu_fwd(gu, T.inter)
+            if T.inter % 128 == 0:   # SwiGLU fused into the gate|up GEMM; gate|up kept only for the backward
+                gu = torch.empty((M, 2 * T.inter), dtype=torch.bfloat16, device=self.device) if save else None
+                a = ops.gemm(h2, Wgu, act="swiglu", aux=gu)
+            else:
+                gu = ops.gemm(h2, Wgu)
+                a = ops.swiglu_fwd(gu, T.inter)
             x_out = ops.gemm(a, P[p + "mlp.down_proj.weight"], residual=x_mid)
             if save:
                 layers.append(Saved(x=x, h=h, r1=r1, q=q, k=k, v=v, o=o2, lse=lse, x_mid=x_mid, h2=h2, r2=r2, gu=gu, a=a))

@@ -128,7 +128,7 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
 
 # --------------------------------------------------------------------- GEMM ----
 ACTS = {None: NV.KD_ACT_NONE, "none": NV.KD_ACT_NONE, "gelu_tanh": NV.KD_ACT_GELU_TANH,
-        "gelu_erf": NV.KD_ACT_GELU_ERF, "silu": NV.KD_ACT_SILU}
+        "gelu_erf": NV.KD_ACT_GELU_ERF, "silu": NV.KD_ACT_SILU, "swiglu": NV.KD_ACT_SWIGLU}
 _DT = {torch.bfloat16: NV.KD_DTYPE_BF16, torch.float32: NV.KD_DTYPE_F32}
 
 
@@ -155,6 +155,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
 
     `a`/`b` may be K-contiguous tensors or transposed views (x.t() of a contiguous tensor):
     the kernel reads either layout directly (no transpose copies).
+
+    act="swiglu": b = [gate; up] ([2I, K]), out [M, I] = silu(gate) * up, aux (optional)
+    the [M, 2I] pre-activation (include/kdstep.h KD_ACT_SWIGLU).
     """
     M, K = a.shape
     N, K2 = b.shape
@@ -163,7 +166,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     pa, lda, la = _operand(a, "gemm.a")
     pb, ldb, lb = _operand(b, "gemm.b")
     if out is None:
-        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+        out = torch.empty((M, N // 2 if act == "swiglu" else N), dtype=out_dtype, device=a.device)
     if out.stride(1) != 1:
         raise RuntimeError("gemm: out must have a contiguous last dim")
     d = NV.KdGemmDesc()

@@ -190,3 +190,23 @@ def test_splitk_auto_wgrad(M, N, K, dev):
     ops.gemm(dy.t(), x.t(), out=acc, accumulate=True)
     ref = 0.5 + dy.float().t() @ x.float()
     assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("M,I,K", [(300, 256, 96), (1536, 384, 896), (257, 128, 600), (512, 1280, 3584)])
+def test_swiglu_epilogue_bitexact(M, I, K, dev):
+    """act='swiglu' (gate|up GEMM + silu(gate)*up fused, v8) == the unfused GEMM + k_swiglu_fwd,
+    bit for bit (same accumulation order, same bf16 rounding of gate/up, same fp32 formula);
+    aux carries the [M, 2I] pre-activation the backward reads."""
+    ops = _ops()
+    h = _rand(M, K, dev=dev, seed=21)
+    w = _rand(2 * I, K, dev=dev, seed=22, scale=0.05)
+    gu_ref = ops.gemm(h, w, variant=16, split_k=1)
+    a_ref = ops.swiglu_fwd(gu_ref, I)
+    aux = torch.empty(M, 2 * I, dtype=torch.bfloat16, device=dev)
+    a = ops.gemm(h, w, act="swiglu", aux=aux)
+    assert a.shape == (M, I)
+    assert torch.equal(aux, gu_ref)
+    assert torch.equal(a, a_ref)
+    assert torch.equal(ops.gemm(h, w, act="swiglu"), a_ref)
+    g = gu_ref.float()
+    _check(a, torch.nn.functional.silu(g[:, :I]) * g[:, I:])
