@@ -7,24 +7,30 @@
 //   the in-model student CE (HF ForCausalLMLoss: shift by one, ignore -100, mean)
 // and the autograd backward of all of them w.r.t. the student logits.
 //
-// Kernels (one row = one (b, l) position; one 256-thread workgroup per row,
-// grid-strided over rows):
-//   k_row_stats : one pass over teacher+student rows -> max / sum-exp at T and 1,
+// Kernels (one row = one (b, l) position, grid-strided over rows; every lane keeps 4 / 2
+// 16-B chunks of a row in flight so one workgroup's loads cover the HBM latency):
+//   k_row_stats : one pass over teacher+student rows (256 threads per row) -> max /
+//                 sum-exp at T and 1 (one exp per element when T = 1),
 //                 teacher top-2 (LoCa "klogits", DT:170-171), gathers at the label;
 //                 LoCa: records the LAST row-major position per label id and per
 //                 klogit id (atomicMax) — the global last-write-wins semantics of
 //                 `loca[:, :, labels] = X` (DT:184-185; SURVEY §4 KAT 1).
-//   k_ovr_mask  : bitmask of overridden vocab columns (LoCa only).
+//   k_ovr_mask  : bitmask of overridden vocab columns and their override values q
+//                 (LoCa only; one [V] table, so the per-row passes gather nothing).
 //   k_loss_grad : pass A sums the KD term and the row scalar S, pass B writes
-//                 dlogits (re-read of the row is served by L2 / Infinity Cache).
+//                 dlogits; one 1024-thread workgroup per CU (256 rows in flight), so
+//                 pass B's re-read of the row is served by the Infinity Cache.
 //   k_finalize  : deterministic fp64 reduction of the per-row partials.
 #include "common.h"
 
 namespace kd {
 namespace {
 
-constexpr int NT = 256;  // threads per workgroup
+constexpr int NT = 256;  // threads per workgroup (row statistics, finalize)
 constexpr int NW = NT / 64;
+constexpr int RS_U = 4;  // 16-B chunks in flight per lane in k_row_stats
+constexpr int LG_NT = 1024, LG_NW = LG_NT / 64;   // k_loss_grad: one 16-wave workgroup per CU
+constexpr int LG_U = 2;  // chunk pairs in flight per lane in k_loss_grad
 
 struct RowStats {
     float mt, zt;     // teacher max over [0,V_s) and sum exp((t-mt)/T)
@@ -42,7 +48,7 @@ struct RowStats {
 static_assert(sizeof(RowStats) == 64, "RowStats layout");
 
 struct Layout {
-    size_t stats, lab_last, klo_last, mask, part_kl, err, total;
+    size_t stats, lab_last, klo_last, mask, ovr, part_kl, err, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
@@ -56,6 +62,7 @@ inline Layout make_layout(int B, int L, int V) {
     lo.lab_last = off; off = align16(off + (size_t)V * 4);
     lo.klo_last = off; off = align16(off + (size_t)V * 4);
     lo.mask = off;     off = align16(off + (size_t)((V + 63) / 64) * 8);
+    lo.ovr = off;      off = align16(off + (size_t)V * 4);
     lo.part_kl = off;  off = align16(off + rows * 4);
     lo.total = off;
     return lo;
@@ -95,47 +102,91 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
     for (int r = blockIdx.x; r < rows; r += gridDim.x) {
         const bf16* srow = S_ + (int64_t)r * ld_s;
         const bf16* trow = has_t ? T_ + (int64_t)r * ld_t : nullptr;
-        // ---- student: max / sum-exp at T and at 1 (same max)
+        // ---- student: max / sum-exp at T and at 1 (same max); RS_U chunks in flight per lane
         float ms = -INFINITY, zs = 0.f, zs1 = 0.f;
-        for (int v = tid * 8; v < V_s; v += NT * 8) {
-            bf16x8 x = *(const bf16x8*)(srow + v);
-            float f[8], cm = -INFINITY;
+        const bool t1 = invT == 1.f;   // T = 1 (LB): the two sums coincide, one exp per element
+        for (int v0 = tid * 8; v0 < V_s; v0 += NT * 8 * RS_U) {
+            bf16x8 xs[RS_U];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { f[j] = (float)x[j]; cm = fmaxf(cm, f[j]); }
-            if (cm > ms) {
-                if (ms != -INFINITY) { zs *= __expf((ms - cm) * invT); zs1 *= __expf(ms - cm); }
-                ms = cm;
+            for (int u = 0; u < RS_U; ++u) {
+                const int v = v0 + u * NT * 8;
+                if (v < V_s) xs[u] = *(const bf16x8*)(srow + v);
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { zs += __expf((f[j] - ms) * invT); zs1 += __expf(f[j] - ms); }
+            for (int u = 0; u < RS_U; ++u) {
+                if (v0 + u * NT * 8 >= V_s) break;
+                float f[8], cm = -INFINITY;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { f[j] = (float)xs[u][j]; cm = fmaxf(cm, f[j]); }
+                if (cm > ms) {
+                    if (ms != -INFINITY) { zs *= __expf((ms - cm) * invT); if (!t1) zs1 *= __expf(ms - cm); }
+                    ms = cm;
+                }
+                if (t1) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) zs += __expf(f[j] - ms);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { zs += __expf((f[j] - ms) * invT); zs1 += __expf(f[j] - ms); }
+                }
+            }
         }
+        if (t1) zs1 = zs;
         // ---- teacher: max/sum over V_s at T, top-2 over V_s; max/sum over V_t at 1
         float mt = -INFINITY, zt = 0.f, mtf = -INFINITY, ztf = 0.f;
         float v1 = -INFINITY, v2 = -INFINITY;
         int i1 = 0x7fffffff, i2 = 0x7fffffff;
         if (has_t) {
-            for (int v = tid * 8; v < V_t; v += NT * 8) {
-                bf16x8 x = *(const bf16x8*)(trow + v);
-                float f[8], cm = -INFINITY, cmf = -INFINITY;
-                const bool in_s = v < V_s;  // V_s % 8 == 0: chunks never straddle
+            for (int v0 = tid * 8; v0 < V_t; v0 += NT * 8 * RS_U) {
+                bf16x8 xt[RS_U];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) { f[j] = (float)x[j]; cmf = fmaxf(cmf, f[j]); }
-                if (in_s) cm = cmf;
-                if (want_tce) {
-                    if (cmf > mtf) { if (mtf != -INFINITY) ztf *= __expf(mtf - cmf); mtf = cmf; }
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) ztf += __expf(f[j] - mtf);
+                for (int u = 0; u < RS_U; ++u) {
+                    const int v = v0 + u * NT * 8;
+                    if (v < V_t) xt[u] = *(const bf16x8*)(trow + v);
                 }
-                if (in_s) {
-                    if (cm > mt) { if (mt != -INFINITY) zt *= __expf((mt - cm) * invT); mt = cm; }
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        zt += __expf((f[j] - mt) * invT);
-                        top2_push(f[j], v + j, v1, i1, v2, i2);
+                for (int u = 0; u < RS_U; ++u) {
+                    const int v = v0 + u * NT * 8;
+                    if (v >= V_t) break;
+                    float f[8], cm = -INFINITY, cmf = -INFINITY;
+                    const bool in_s = v < V_s;  // V_s % 8 == 0: chunks never straddle
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { f[j] = (float)xt[u][j]; cmf = fmaxf(cmf, f[j]); }
+                    if (in_s) cm = cmf;
+                    if (want_tce && t1) {
+                        // T = 1: one exp per element feeds both sums, all relative to the V_t max;
+                        // zt is rebased on the V_s max after the loop
+                        if (cmf > mtf) {
+                            if (mtf != -INFINITY) { const float sc = __expf(mtf - cmf); ztf *= sc; zt *= sc; }
+                            mtf = cmf;
+                        }
+                        float e8 = 0.f;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) e8 += __expf(f[j] - mtf);
+                        ztf += e8;
+                        if (in_s) { zt += e8; mt = fmaxf(mt, cm); }
+                    } else {
+                        if (want_tce) {
+                            if (cmf > mtf) { if (mtf != -INFINITY) ztf *= __expf(mtf - cmf); mtf = cmf; }
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) ztf += __expf(f[j] - mtf);
+                        }
+                        if (in_s) {
+                            if (cm > mt) { if (mt != -INFINITY) zt *= __expf((mt - cm) * invT); mt = cm; }
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) zt += __expf((f[j] - mt) * invT);
+                        }
+                    }
+                    if (in_s) {
+                        if (cm > v2 || (cm == v2 && v < i2)) {   // a chunk that can change the top-2
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) top2_push(f[j], v + j, v1, i1, v2, i2);
+                        }
                     }
                 }
             }
         }
+        if (has_t && want_tce && t1 && mt != -INFINITY) zt *= __expf(mtf - mt);   // sum exp(t - mt) over V_s
         // ---- wave reductions
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -220,11 +271,15 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
 }
 
 __global__ void k_ovr_mask(const int* __restrict__ lab_last, const int* __restrict__ klo_last,
-                           int V, unsigned long long* __restrict__ mask) {
+                           const RowStats* __restrict__ stats, int V, unsigned long long* __restrict__ mask,
+                           float* __restrict__ ovr) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool on = (v < V) && (lab_last[v] >= 0 || klo_last[v] >= 0);
+    const int kl = v < V ? klo_last[v] : -1, ll = v < V ? lab_last[v] : -1;
+    const bool on = kl >= 0 || ll >= 0;
     const unsigned long long bits = __ballot(on);
     if ((threadIdx.x & 63) == 0 && v < V + 63) mask[v >> 6] = bits;
+    // klogits are written second (DT:185) and win over the label columns (DT:184)
+    if (v < V) ovr[v] = kl >= 0 ? stats[kl].ovy : (ll >= 0 ? stats[ll].ovx : 0.f);
 }
 
 template <int VARIANT>
@@ -233,7 +288,7 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
             const bf16* __restrict__ S_, int64_t ld_s, int V,
             int rows, float invT, float clamp_min,
             const RowStats* __restrict__ stats,
-            const int* __restrict__ lab_last, const int* __restrict__ klo_last,
+            const float* __restrict__ ovr,
             const unsigned long long* __restrict__ mask_g,
             float kd_coef,   // kd_weight * T / N * grad_scale
             float ce_coef,   // ce_weight / n_valid * grad_scale   (host-computed count)
@@ -242,7 +297,7 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
     const int tid = threadIdx.x;
     const int nwords = (V + 63) / 64;
     if (VARIANT == KD_LOSS_LOCA) {
-        for (int i = tid; i < nwords; i += NT) smask[i] = mask_g[i];
+        for (int i = tid; i < nwords; i += LG_NT) smask[i] = mask_g[i];
         __syncthreads();
     }
     const float log_clamp = logf(clamp_min);
@@ -257,9 +312,18 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
         if (VARIANT != KD_LOSS_NONE) {
             // ---- pass A: KD term and S
             float term = 0.f, sacc = 0.f;
-            for (int v = tid * 8; v < V; v += NT * 8) {
-                bf16x8 xt = *(const bf16x8*)(trow + v);
-                bf16x8 xs = *(const bf16x8*)(srow + v);
+            for (int v0 = tid * 8; v0 < V; v0 += LG_NT * 8 * LG_U) {
+              bf16x8 xtu[LG_U], xsu[LG_U];
+#pragma unroll
+              for (int u = 0; u < LG_U; ++u) {
+                  const int v = v0 + u * LG_NT * 8;
+                  if (v < V) { xtu[u] = *(const bf16x8*)(trow + v); xsu[u] = *(const bf16x8*)(srow + v); }
+              }
+#pragma unroll
+              for (int u = 0; u < LG_U; ++u) {
+                const int v = v0 + u * LG_NT * 8;
+                if (v >= V) break;
+                const bf16x8 xt = xtu[u], xs = xsu[u];
                 unsigned int mbits = 0;
                 if (VARIANT == KD_LOSS_LOCA) mbits = (unsigned)(smask[v >> 6] >> (v & 63)) & 0xffu;
 #pragma unroll
@@ -270,8 +334,7 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
                     if (VARIANT == KD_LOSS_LOCA) {
                         float q = pT, logq = lt - log_zt;
                         if (mbits & (1u << j)) {
-                            const int kl = klo_last[v + j];
-                            q = (kl >= 0) ? stats[kl].ovy : stats[lab_last[v + j]].ovx;
+                            q = ovr[v + j];
                             logq = logf(q);
                         }
                         const float ps = __expf(lps);
@@ -288,9 +351,10 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
                         sacc += e;
                     }
                 }
+              }
             }
-            term = block_sum<NW>(term, red);
-            Ssum = block_sum<NW>(sacc, red);
+            term = block_sum<LG_NW>(term, red);
+            Ssum = block_sum<LG_NW>(sacc, red);
             if (tid == 0) part_kl[r] = term;
         } else {
             if (tid == 0) part_kl[r] = 0.f;
@@ -298,30 +362,42 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
         if (D_ != nullptr) {
             // ---- pass B: dlogits
             const float log_zs1 = logf(st.zs1);
+            const bool t1 = invT == 1.f && st.zs1 == st.zs;   // the CE softmax == the KD softmax at T = 1
             const float cec = st.valid ? ce_coef : 0.f;
             bf16* drow = D_ + (int64_t)r * ld_d;
-            for (int v = tid * 8; v < V; v += NT * 8) {
-                bf16x8 xs = *(const bf16x8*)(srow + v);
+            for (int v0 = tid * 8; v0 < V; v0 += LG_NT * 8 * LG_U) {
+              bf16x8 xsu[LG_U], xtu[LG_U];
+#pragma unroll
+              for (int u = 0; u < LG_U; ++u) {
+                  const int v = v0 + u * LG_NT * 8;
+                  if (v < V) {
+                      xsu[u] = *(const bf16x8*)(srow + v);
+                      if (VARIANT != KD_LOSS_NONE) xtu[u] = *(const bf16x8*)(trow + v);
+                  }
+              }
+#pragma unroll
+              for (int u = 0; u < LG_U; ++u) {
+                const int v = v0 + u * LG_NT * 8;
+                if (v >= V) break;
+                const bf16x8 xs = xsu[u];
                 bf16x8 xt;
-                if (VARIANT != KD_LOSS_NONE) xt = *(const bf16x8*)(trow + v);
+                if (VARIANT != KD_LOSS_NONE) xt = xtu[u];
                 unsigned int mbits = 0;
                 if (VARIANT == KD_LOSS_LOCA) mbits = (unsigned)(smask[v >> 6] >> (v & 63)) & 0xffu;
                 bf16x8 out;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float sv = (float)xs[j];
-                    float g = 0.f;
+                    float g = 0.f, ps_keep = 0.f;
                     if (VARIANT != KD_LOSS_NONE) {
                         const float lt = ((float)xt[j] - st.mt) * invT;
                         const float pT = __expf(lt) * inv_zt;
                         const float ps = __expf((sv - st.ms) * invT - log_zs);
+                        ps_keep = ps;
                         float gq;
                         if (VARIANT == KD_LOSS_LOCA) {
                             float q = pT;
-                            if (mbits & (1u << j)) {
-                                const int kl = klo_last[v + j];
-                                q = (kl >= 0) ? stats[kl].ovy : stats[lab_last[v + j]].ovx;
-                            }
+                            if (mbits & (1u << j)) q = ovr[v + j];
                             gq = (ps >= clamp_min) ? q : 0.f;
                         } else if (VARIANT == KD_LOSS_KL) {
                             gq = pT;
@@ -331,12 +407,13 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
                         g = kd_coef * (ps * Ssum - gq);
                     }
                     if (cec != 0.f) {
-                        const float p1 = __expf(sv - st.ms - log_zs1);
+                        const float p1 = (VARIANT != KD_LOSS_NONE && t1) ? ps_keep : __expf(sv - st.ms - log_zs1);
                         g += cec * (p1 - ((v + j) == st.lab_next ? 1.f : 0.f));
                     }
                     out[j] = (bf16)g;
                 }
                 *(bf16x8*)(drow + v) = out;
+              }
             }
         }
     }
@@ -385,19 +462,19 @@ __global__ void k_count_valid(const int64_t* __restrict__ labels, int B, int L, 
 }
 
 template <int VARIANT>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(LG_NT)
 k_loss_grad(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
             int V, int rows, float invT, float clamp_min, const RowStats* __restrict__ stats,
-            const int* __restrict__ lab_last, const int* __restrict__ klo_last,
+            const float* __restrict__ ovr,
             const unsigned long long* __restrict__ mask_g, float kd_coef, float ce_coef_num,
             const float* __restrict__ n_valid, bf16* __restrict__ D_, int64_t ld_d,
             float* __restrict__ part_kl) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smask[];
-    __shared__ float red[NW];
+    __shared__ float red[LG_NW];
     // the CE mean's denominator lives on the device (no host sync)
     const float nv = *n_valid;
     const float ce_coef = nv > 0.f ? ce_coef_num / nv : 0.f;
-    loss_grad_body<VARIANT>(T_, ld_t, S_, ld_s, V, rows, invT, clamp_min, stats, lab_last, klo_last,
+    loss_grad_body<VARIANT>(T_, ld_t, S_, ld_s, V, rows, invT, clamp_min, stats, ovr,
                             mask_g, kd_coef, ce_coef, D_, ld_d, part_kl, smask, red);
 }
 
@@ -431,6 +508,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     int* lab_last = (int*)(w + lo.lab_last);
     int* klo_last = (int*)(w + lo.klo_last);
     unsigned long long* mask = (unsigned long long*)(w + lo.mask);
+    float* ovr = (float*)(w + lo.ovr);
     float* part_kl = (float*)(w + lo.part_kl);
     int* err = (int*)(w + lo.err);
     float* nvalid = (float*)(w + lo.err + 4);
@@ -452,7 +530,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     KD_LAUNCH_CHECK("k_row_stats");
     if (variant == KD_LOSS_LOCA) {
         const int nb = (V_s + 255) / 256;
-        hipLaunchKernelGGL(k_ovr_mask, dim3(nb), dim3(256), 0, stream, lab_last, klo_last, V_s, mask);
+        hipLaunchKernelGGL(k_ovr_mask, dim3(nb), dim3(256), 0, stream, lab_last, klo_last, stats, V_s, mask, ovr);
         KD_LAUNCH_CHECK("k_ovr_mask");
     }
     hipLaunchKernelGGL(k_count_valid, dim3(1), dim3(NT), 0, stream, labels, B, L, V_s, nvalid);
@@ -464,9 +542,12 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     const size_t smem = variant == KD_LOSS_LOCA ? (size_t)((V_s + 63) / 64) * 8 : 0;
     if (smem > 150 * 1024) return fail(KD_ERR_SHAPE, "kd_loss: vocab too large for LDS mask");
     bf16* D_ = (bf16*)dlogits;
+    // one 16-wave workgroup per CU: ~256 rows in flight, so pass B's re-read of a row (both
+    // logits, 2 x 304 KB at V = 152K) is served by the 256 MB Infinity Cache, not HBM
+    const int lg_grid = rows < 256 ? rows : 256;
 #define KD_LAUNCH_LG(VAR)                                                                          \
-    hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(grid), dim3(NT), smem, stream, T_, ld_t, S_, ld_s, \
-                       V_s, rows, invT, p.clamp_min, stats, lab_last, klo_last, mask, kd_coef,     \
+    hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, \
+                       V_s, rows, invT, p.clamp_min, stats, ovr, mask, kd_coef,                    \
                        ce_num, nvalid, D_, ld_d, part_kl)
     switch (variant) {
         case KD_LOSS_NONE: KD_LAUNCH_LG(KD_LOSS_NONE); break;
