@@ -258,7 +258,10 @@ class _KDBase(_Base):
         dl = ctx["dlogits"].view(hn.shape[0], -1)
         dhn = ops.gemm(dl, W.t(), alpha_dev=gscale)                          # lm_head dgrad
         if s.train_language:                                                  # lm_head / tied embed wgrad
-            ops.gemm(dl.t(), hn.t(), out=s.lm_head_grad(), accumulate=True, alpha_dev=gscale)
+            ev = s.wlane.run(lambda: ops.gemm(dl.t(), hn.t(), out=s.lm_head_grad(), accumulate=True, alpha_dev=gscale),
+                             dl, hn, gscale)
+            if s.cfg.text.tie:
+                s.tied_grad_event = ev
         del dl, ctx["dlogits"]
         dpost = None
         if ctx["dps"] is not None and s.train_vision:
@@ -282,6 +285,9 @@ class _KDBase(_Base):
             self._sync_hi = P.numel
         first = P.offsets[f"language_model.model.layers.{i}.self_attn.q_proj.weight"][0]
         if (self._sync_hi - first) * 4 >= self._bucket_bytes:
+            lane = getattr(s, "wlane", None)
+            if lane is not None:
+                lane.join()   # the bucket's weight grads (side stream) are complete
             self._allreduce(first, self._sync_hi)
             self._sync_hi = first
 

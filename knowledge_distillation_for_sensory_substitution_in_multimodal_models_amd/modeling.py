@@ -287,6 +287,40 @@ class Saved(dict):
     """Per-layer activations kept for the backward."""
 
 
+class WgradLane:
+    """Weight-gradient work (dW GEMMs, bias column sums) on a side stream.
+
+    A linear layer's dW = dY^T X feeds only the optimizer, so it runs beside the dgrad
+    chain dX = dY W that the next layer waits for; the student's backward GEMMs (hidden
+    896, SigLIP 1152) fill 100-230 tiles of 256x256, fewer than the 256 CUs, so the two
+    streams fill each other's idle CUs.  `run` orders the side stream after everything
+    queued on the current stream, keeps its operands' memory alive for it (record_stream)
+    and returns an event the current stream waits on before it updates an operand in place;
+    `join` makes the current stream wait for all of it (before grads are read)."""
+
+    def __init__(self, device):
+        self.stream = torch.cuda.Stream(device=device)
+
+    def run(self, fn, *keep):
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            fn()
+        for t in keep:
+            if t is not None:
+                t.record_stream(self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    def join(self):
+        torch.cuda.current_stream().wait_stream(self.stream)
+
+
+def _wait(ev):
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
+
+
 # --------------------------------------------------------------------- model ----
 class LlavaOnevisionModel:
     """One LLaVA-OneVision instance (teacher or student) on a ParamStore."""
@@ -303,6 +337,8 @@ class LlavaOnevisionModel:
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         # which regions receive weight gradients (freeze masks, DT:468-523)
         self.train_vision = self.train_projector = self.train_language = trainable
+        self.wlane = WgradLane(self.device) if (trainable and self.device.type == "cuda") else None
+        self.tied_grad_event = None   # lm_head wgrad into the tied embedding grad (kd_module._backward)
 
     # -- freeze helpers mirroring DT:468-523 (applied to the student)
     def set_trainable(self, vision: bool, projector: bool, language: bool):
@@ -375,6 +411,7 @@ class LlavaOnevisionModel:
         NI = sv["NI"]
         NT = NI * V.n_patches
         gw = self.train_vision
+        W = self.wlane
         if dpost is not None:
             ops.norm_bwd(sv["x_last"], P[vp + "post_layernorm.weight"], dpost, sv["pm"], sv["pr"], dx=dx,
                          dx_accum=True,
@@ -385,43 +422,49 @@ class LlavaOnevisionModel:
             s = sv["layers"][i]
             W2 = P[p + "mlp.fc2.weight"]
             du = ops.gemm(dx, W2.t())
+            ev = None
             if gw:
-                ops.gemm(dx.t(), s["u"].t(), out=P.grad_view(p + "mlp.fc2.weight"), accumulate=True)
-                ops.colsum(dx, P.grad_view(p + "mlp.fc2.bias"))
+                ev = W.run(lambda: (ops.gemm(dx.t(), s["u"].t(), out=P.grad_view(p + "mlp.fc2.weight"), accumulate=True),
+                                    ops.colsum(dx, P.grad_view(p + "mlp.fc2.bias"))), dx, s["u"])
             dpre = ops.act_bwd(s["pre"], du, "gelu_tanh", out=du)
             dh2 = ops.gemm(dpre, P[p + "mlp.fc1.weight"].t())
             if gw:
-                ops.gemm(dpre.t(), s["h2"].t(), out=P.grad_view(p + "mlp.fc1.weight"), accumulate=True)
-                ops.colsum(dpre, P.grad_view(p + "mlp.fc1.bias"))
+                W.run(lambda: (ops.gemm(dpre.t(), s["h2"].t(), out=P.grad_view(p + "mlp.fc1.weight"), accumulate=True),
+                               ops.colsum(dpre, P.grad_view(p + "mlp.fc1.bias"))), dpre, s["h2"])
             del du, dpre
+            _wait(ev)   # dx is updated in place next
             ops.norm_bwd(s["x_mid"], P[p + "layer_norm2.weight"], dh2, s["m2"], s["r2"], dx=dx, dx_accum=True,
                          dweight=P.grad_view(p + "layer_norm2.weight") if gw else None,
                          dbias=P.grad_view(p + "layer_norm2.bias") if gw else None)
             do = ops.gemm(dx, P[p + "self_attn.out_proj.weight"].t())
             if gw:
-                ops.gemm(dx.t(), s["o"].t(), out=P.grad_view(p + "self_attn.out_proj.weight"), accumulate=True)
-                ops.colsum(dx, P.grad_view(p + "self_attn.out_proj.bias"))
+                ev = W.run(lambda: (ops.gemm(dx.t(), s["o"].t(), out=P.grad_view(p + "self_attn.out_proj.weight"),
+                                             accumulate=True),
+                                    ops.colsum(dx, P.grad_view(p + "self_attn.out_proj.bias"))), dx, s["o"])
             dq, dk, dv = ops.attn_bwd(s["q"], s["k"], s["v"], s["o"], do, s["lse"], V.hd, causal=False)
             dqkv = ops.qkv_merge(dq, dk, dv, NI, V.n_patches, V.heads, V.heads, V.hd, V.hdp)
             del dq, dk, dv, do
             Wqkv = P.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight", 3 * D, D)
             dh = ops.gemm(dqkv, Wqkv.t())
             if gw:
-                ops.gemm(dqkv.t(), s["h"].t(), out=P.grad_span(p + "self_attn.q_proj.weight",
-                                                                p + "self_attn.v_proj.weight", 3 * D, D),
-                         accumulate=True)
-                ops.colsum(dqkv, P.grad_span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1,
-                                             3 * D).view(-1))
+                W.run(lambda: (ops.gemm(dqkv.t(), s["h"].t(), out=P.grad_span(p + "self_attn.q_proj.weight",
+                                                                               p + "self_attn.v_proj.weight", 3 * D, D),
+                                        accumulate=True),
+                               ops.colsum(dqkv, P.grad_span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1,
+                                                            3 * D).view(-1))), dqkv, s["h"])
+            del dqkv
+            _wait(ev)
             ops.norm_bwd(s["x"], P[p + "layer_norm1.weight"], dh, s["m1"], s["r1"], dx=dx, dx_accum=True,
                          dweight=P.grad_view(p + "layer_norm1.weight") if gw else None,
                          dbias=P.grad_view(p + "layer_norm1.bias") if gw else None)
             sv["layers"][i] = None   # free activations as we go
         if gw:
-            ops.gemm(dx.t(), sv["rows"].t(), out=P.grad_view(vp + "embeddings.patch_embedding.weight"),
-                     accumulate=True)
-            ops.colsum(dx, P.grad_view(vp + "embeddings.patch_embedding.bias"))
-            ops.colsum(dx.view(NI, V.n_patches * D),
-                       P.grad_view(vp + "embeddings.position_embedding.weight").view(-1))
+            W.run(lambda: (ops.gemm(dx.t(), sv["rows"].t(), out=P.grad_view(vp + "embeddings.patch_embedding.weight"),
+                                    accumulate=True),
+                           ops.colsum(dx, P.grad_view(vp + "embeddings.patch_embedding.bias")),
+                           ops.colsum(dx.view(NI, V.n_patches * D),
+                                      P.grad_view(vp + "embeddings.position_embedding.weight").view(-1))),
+                  dx, sv["rows"])
 
     # =========================================================== projector ====
     def projector_forward(self, x_last, save: bool):
@@ -436,15 +479,17 @@ class LlavaOnevisionModel:
     def projector_backward(self, s, dfeats, need_dx: bool):
         P = self.P
         gw = self.train_projector
+        W = self.wlane
         dz = ops.gemm(dfeats, P["multi_modal_projector.linear_2.weight"].t())
         if gw:
-            ops.gemm(dfeats.t(), s["z"].t(), out=P.grad_view("multi_modal_projector.linear_2.weight"), accumulate=True)
-            ops.colsum(dfeats, P.grad_view("multi_modal_projector.linear_2.bias"))
+            W.run(lambda: (ops.gemm(dfeats.t(), s["z"].t(), out=P.grad_view("multi_modal_projector.linear_2.weight"),
+                                    accumulate=True),
+                           ops.colsum(dfeats, P.grad_view("multi_modal_projector.linear_2.bias"))), dfeats, s["z"])
         dpre = ops.act_bwd(s["pre"], dz, self.cfg.projector_act, out=dz)
         if gw:
-            ops.gemm(dpre.t(), s["x_last"].t(), out=P.grad_view("multi_modal_projector.linear_1.weight"),
-                     accumulate=True)
-            ops.colsum(dpre, P.grad_view("multi_modal_projector.linear_1.bias"))
+            W.run(lambda: (ops.gemm(dpre.t(), s["x_last"].t(), out=P.grad_view("multi_modal_projector.linear_1.weight"),
+                                    accumulate=True),
+                           ops.colsum(dpre, P.grad_view("multi_modal_projector.linear_1.bias"))), dpre, s["x_last"])
         if need_dx:
             return ops.gemm(dpre, P["multi_modal_projector.linear_1.weight"].t())
         return None
@@ -507,39 +552,49 @@ class LlavaOnevisionModel:
         cos, sin = self._rope_for(L)
         qd, kd = T.heads * T.head_dim, T.kv_heads * T.head_dim
         gw = self.train_language
+        W = self.wlane
         dx = ops.norm_bwd(sv["x_last"], P[lp + "norm.weight"], dhn, None, sv["rf"], rms=True,
                           dweight=P.grad_view(lp + "norm.weight") if gw else None)
         for i in reversed(range(T.layers)):
             p = f"{lp}layers.{i}."
             s = sv["layers"][i]
             da = ops.gemm(dx, P[p + "mlp.down_proj.weight"].t())
+            ev = None
             if gw:
-                ops.gemm(dx.t(), s["a"].t(), out=P.grad_view(p + "mlp.down_proj.weight"), accumulate=True)
+                ev = W.run(lambda: ops.gemm(dx.t(), s["a"].t(), out=P.grad_view(p + "mlp.down_proj.weight"),
+                                            accumulate=True), dx, s["a"])
             dgu = ops.swiglu_bwd(s["gu"], da, T.inter)
             del da
             Wgu = P.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight", 2 * T.inter, T.hidden)
             dh2 = ops.gemm(dgu, Wgu.t())
             if gw:
-                ops.gemm(dgu.t(), s["h2"].t(), out=P.grad_span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight",
-                                                                2 * T.inter, T.hidden), accumulate=True)
+                W.run(lambda: ops.gemm(dgu.t(), s["h2"].t(), out=P.grad_span(p + "mlp.gate_proj.weight",
+                                                                              p + "mlp.up_proj.weight",
+                                                                              2 * T.inter, T.hidden),
+                                       accumulate=True), dgu, s["h2"])
             del dgu
+            _wait(ev)   # dx is updated in place next
             ops.norm_bwd(s["x_mid"], P[p + "post_attention_layernorm.weight"], dh2, None, s["r2"], dx=dx,
                          dx_accum=True, rms=True,
                          dweight=P.grad_view(p + "post_attention_layernorm.weight") if gw else None)
             do = ops.gemm(dx, P[p + "self_attn.o_proj.weight"].t())
             if gw:
-                ops.gemm(dx.t(), s["o"].t(), out=P.grad_view(p + "self_attn.o_proj.weight"), accumulate=True)
+                ev = W.run(lambda: ops.gemm(dx.t(), s["o"].t(), out=P.grad_view(p + "self_attn.o_proj.weight"),
+                                            accumulate=True), dx, s["o"])
             dq, dk, dv = ops.attn_bwd(s["q"], s["k"], s["v"], s["o"], do, s["lse"], T.head_dim, causal=True)
             dqkv = ops.qkv_merge(dq, dk, dv, B, L, T.heads, T.kv_heads, T.head_dim, T.head_dim, cos, sin)
             del dq, dk, dv, do
             Wqkv = P.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight", qd + 2 * kd, T.hidden)
             dh = ops.gemm(dqkv, Wqkv.t())
             if gw:
-                ops.gemm(dqkv.t(), s["h"].t(), out=P.grad_span(p + "self_attn.q_proj.weight",
-                                                                p + "self_attn.v_proj.weight", qd + 2 * kd, T.hidden),
-                         accumulate=True)
-                ops.colsum(dqkv, P.grad_span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1,
-                                             qd + 2 * kd).view(-1))
+                W.run(lambda: (ops.gemm(dqkv.t(), s["h"].t(), out=P.grad_span(p + "self_attn.q_proj.weight",
+                                                                               p + "self_attn.v_proj.weight",
+                                                                               qd + 2 * kd, T.hidden),
+                                        accumulate=True),
+                               ops.colsum(dqkv, P.grad_span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1,
+                                                            qd + 2 * kd).view(-1))), dqkv, s["h"])
+            del dqkv
+            _wait(ev)
             ops.norm_bwd(s["x"], P[p + "input_layernorm.weight"], dh, None, s["r1"], dx=dx, dx_accum=True, rms=True,
                          dweight=P.grad_view(p + "input_layernorm.weight") if gw else None)
             sv["layers"][i] = None
@@ -576,6 +631,8 @@ class LlavaOnevisionModel:
         """Backward from d(final-norm hidden) and d(post-LN hook output) to every trainable grad."""
         T = self.cfg.text
         demb = self.lm_backward(fwd["lsave"], dhn, gscale, on_layer_done)
+        _wait(self.tied_grad_event)   # the tied lm_head wgrad accumulates into the embedding grad too
+        self.tied_grad_event = None
         NT = fwd["vsave"]["x_last"].shape[0] if fwd.get("vsave") else 0
         dfeats = torch.empty((NT, T.hidden), dtype=torch.bfloat16, device=self.device)
         ops.embed_bwd(fwd["ids"], fwd["src"], demb,
@@ -587,3 +644,5 @@ class LlavaOnevisionModel:
         dx_last = self.projector_backward(fwd["psave"], dfeats, need_dx=need_vision)
         if need_vision:
             self.vision_backward(fwd["vsave"], dx_last, dpost)
+        if self.wlane is not None:
+            self.wlane.join()
