@@ -279,6 +279,20 @@ __device__ __forceinline__ void stage2(char* tile, const bf16* ptr, int64_t ld, 
     }
 }
 
+// Transposed LDS read through inline asm. With the builtin, hipcc cannot tell the read
+// from the in-flight LDS-DMA writes of later stages and emits s_waitcnt vmcnt(0) before
+// the first one of every k-step, draining the whole prefetch ring (MN-major GEMMs ran
+// 30-65 % slower than K-major ones, SQ_WAIT_ANY 0.30 -> 0.50 of wave cycles). The asm
+// result is NOT tracked by the compiler's lgkmcnt waits: every caller retires these reads
+// with its own s_waitcnt lgkmcnt(0) before the fragments are used (v3: start of the next
+// step; v8: the step-end sync).
+template <int OFF>
+__device__ __forceinline__ bf16x4 ds_read_tr_asm(const char* lds) {
+    u32x2 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"((uint32_t)(uintptr_t)lds), "i"(OFF));
+    return __builtin_bit_cast(bf16x4, r);
+}
+
 template <int R, bool MN>
 __device__ __forceinline__ bf16x8 frag2(const char* tile, int rb, int lane) {
     if (!MN) {
@@ -289,11 +303,10 @@ __device__ __forceinline__ bf16x8 frag2(const char* tile, int rb, int lane) {
         constexpr int RB = R * 2;
         const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
         const int cc = (rb >> 3) + (p >> 1);
-        const int kr0 = 8 * g + q, kr1 = kr0 + 4;
+        const int kr0 = 8 * g + q;   // kr1 = kr0 + 4 has the same swizzle (sw_mn ignores bit 2)
         const char* a0 = tile + kr0 * RB + ((cc ^ (int)sw_mn(kr0)) << 4) + ((p & 1) << 3);
-        const char* a1 = tile + kr1 * RB + ((cc ^ (int)sw_mn(kr1)) << 4) + ((p & 1) << 3);
-        bf16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a0);
-        bf16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a1);
+        const bf16x4 h0 = ds_read_tr_asm<0>(a0);
+        const bf16x4 h1 = ds_read_tr_asm<4 * RB>(a0);
         bf16x8 r;
         r[0] = h0[0]; r[1] = h0[1]; r[2] = h0[2]; r[3] = h0[3];
         r[4] = h1[0]; r[5] = h1[1]; r[6] = h1[2]; r[7] = h1[3];
@@ -598,7 +611,8 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     }
     if (t < nk) KD_G3_STEP(aA, bA, aB, bB);
 #undef KD_G3_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // incl. the asm tr reads
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     epilogue2<BM, BN, WM, WN, TM, TN, MT, NT, NTH2, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
 }
@@ -873,11 +887,12 @@ __global__ void k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p) {
 
 // Kernel / tile / split-K plan. Cost model in microseconds: waves x (32-deep k-steps per
 // split x per-step tile cost + fixed per-tile prologue/epilogue), plus the fp32
-// partial-plane traffic of a split at ~6.2 TB/s. Candidates: v3 256x256 / 256x128 /
-// 128x256 (8 waves) and v8 256x256 (4 waves, K-major x K-major only). Constants fitted
-// (least squares on log time) to a kernel x tile x split sweep over all 42 GEMM shapes of
-// the c1 KD step (tools/tune_gemm.py, profiles/r01/gemm_tune.jsonl): the model's picks
-// are within 0.4% of the measured best per step (129.7 vs 129.3 ms of GEMM).
+// partial-plane traffic of a split. Candidates: v3 256x256 / 256x128 / 128x256 (8 waves)
+// and v8 256x256 (4 waves), each with its own constants for K-major x K-major operands
+// and for the layouts with an MN-major operand (tr_b16 fragment reads). Constants fitted
+// (least squares on log time, tools/fit_plan.py) to a kernel x tile x split sweep over all
+// 42 GEMM shapes of the c1 KD step (tools/tune_gemm.py, profiles/r01/gemm_tune.jsonl): the
+// model's picks are within 0.4% of the measured best per step.
 struct GemmPlan { int var; int split; int64_t kchunk; };   // var: 2/3/4 v3 tiles, 16 v8
 
 GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
@@ -885,10 +900,13 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t t256 = (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 256);
     const int64_t tiles[4] = {t256, (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 128),
                               (int64_t)ceil_div(d->M, 128) * ceil_div(d->N, 256), t256};
-    const double step[4] = {0.9848, 0.7656, 0.7569, 0.6844};   // v3 256x256, 256x128, 128x256; v8
-    const double fixed[4] = {3.968, 1.711, 1.166, 7.695};
-    const int vcode[4] = {2, 3, 4, 16};
     const bool kk = d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR;
+    // per variant (v3 256x256, 256x128, 128x256; v8): {K-major x K-major, MN-major operand}
+    static const double step_c[2][4] = {{0.7474, 0.5245, 0.5203, 0.6746}, {0.7874, 0.5727, 0.5746, 0.6120}};
+    static const double fixed_c[2][4] = {{7.537, 4.314, 3.730, 11.064}, {8.256, 4.529, 4.020, 12.656}};
+    const double* step = step_c[kk ? 0 : 1];
+    const double* fixed = fixed_c[kk ? 0 : 1];
+    const int vcode[4] = {2, 3, 4, 16};
     const int64_t nk = ceil_div(d->K, BK2);
     // forced: variants 2/5 v3 256x256, 3/6 256x128, 4/7 128x256, 16+ v8; 0 = model's choice
     const int fv = d->variant >= 16 ? 3 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
@@ -898,7 +916,6 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     double bt = 1e300;
     for (int v = 0; v < 4; ++v) {
         if (fv >= 0 && v != fv) continue;
-        if (v == 3 && !kk && fv != 3) continue;   // v8's MN-major paths are not competitive
         for (int S = 1; S <= 32; ++S) {
             if (d->split_k == 1 && S != 1) continue;
             if (d->split_k > 1 && S != d->split_k && S != 1) continue;
@@ -908,7 +925,7 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
             if (S > 1 && (uint64_t)S * M * N * 4 > ws_cap) continue;
             const int64_t waves = (tiles[v] * S + 255) / 256;
             double t = (double)waves * ((double)kcs * step[v] + fixed[v]);
-            if (S > 1) t += ((double)S * M * N * 8 + out_b) / 6.222e6;
+            if (S > 1) t += ((double)S * M * N * 8 + out_b) / 7.458e6;
             if (d->split_k > 1 && S == d->split_k) t = -1;              // forced
             if (t < bt) { bt = t; best = GemmPlan{vcode[v], S, kcs * BK2}; }
         }

@@ -277,7 +277,9 @@ __global__ void k_ovr_mask(const int* __restrict__ lab_last, const int* __restri
     const int kl = v < V ? klo_last[v] : -1, ll = v < V ? lab_last[v] : -1;
     const bool on = kl >= 0 || ll >= 0;
     const unsigned long long bits = __ballot(on);
-    if ((threadIdx.x & 63) == 0 && v < V + 63) mask[v >> 6] = bits;
+    // word k exists iff 64k < V (a "v < V + 63" bound wrote one word past the table when
+    // 64 | V, into ovr[0..1], racing with the block that owns them)
+    if ((threadIdx.x & 63) == 0 && v < V) mask[v >> 6] = bits;
     // klogits are written second (DT:185) and win over the label columns (DT:184)
     if (v < V) ovr[v] = kl >= 0 ? stats[kl].ovy : (ll >= 0 ? stats[ll].ovx : 0.f);
 }

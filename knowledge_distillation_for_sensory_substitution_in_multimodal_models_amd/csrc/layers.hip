@@ -192,18 +192,31 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
     }
 }
 
-// out[d] (+)= sum_p part[p][d]: 64 columns x 16 row lanes per 1024-thread block, LDS tree
+// out[d] (+)= sum_p part[p][d]: 16 columns x 64 row lanes per 1024-thread block, each lane
+// with RP_U independent loads in flight (the planes are L2/MALL-hot; with D = 896 a
+// 64-column block gave 14 workgroups whose lanes each waited out P/16 dependent loads),
+// then a fixed-order LDS tree (deterministic)
+constexpr int RP_C = 16, RP_R = 64, RP_U = 8;
 __global__ void __launch_bounds__(1024) k_reduce_parts(const float* __restrict__ part, int P, int D,
                                                        float* __restrict__ out, int accum) {
-    __shared__ float red[16][65];
-    const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-    const int d = blockIdx.x * 64 + cx;
+    __shared__ float red[RP_R][RP_C + 1];
+    const int cx = threadIdx.x % RP_C, ry = threadIdx.x / RP_C;
+    const int d = blockIdx.x * RP_C + cx;
     float s = 0.f;
-    if (d < D)
-        for (int p = ry; p < P; p += 16) s += part[(int64_t)p * D + d];
+    if (d < D) {
+        int p = ry;
+        for (; p + (RP_U - 1) * RP_R < P; p += RP_U * RP_R) {
+            float v[RP_U];
+#pragma unroll
+            for (int u = 0; u < RP_U; ++u) v[u] = part[(int64_t)(p + u * RP_R) * D + d];
+#pragma unroll
+            for (int u = 0; u < RP_U; ++u) s += v[u];
+        }
+        for (; p < P; p += RP_R) s += part[(int64_t)p * D + d];
+    }
     red[ry][cx] = s;
     __syncthreads();
-    for (int h = 8; h > 0; h >>= 1) {
+    for (int h = RP_R / 2; h > 0; h >>= 1) {
         if (ry < h) red[ry][cx] += red[ry + h][cx];
         __syncthreads();
     }
@@ -695,8 +708,8 @@ int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const vo
                             (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,
                             db ? dbp : nullptr, R, D, rows_per);
     KD_LAUNCH_CHECK("k_norm_bwd");
-    if (dw) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 63) / 64), dim3(1024), 0, st, dwp, nb, D, dw, accum_w);
-    if (db) hipLaunchKernelGGL(k_reduce_parts, dim3((D + 63) / 64), dim3(1024), 0, st, dbp, nb, D, db, accum_w);
+    if (dw) hipLaunchKernelGGL(k_reduce_parts, dim3((D + RP_C - 1) / RP_C), dim3(1024), 0, st, dwp, nb, D, dw, accum_w);
+    if (db) hipLaunchKernelGGL(k_reduce_parts, dim3((D + RP_C - 1) / RP_C), dim3(1024), 0, st, dbp, nb, D, db, accum_w);
     KD_LAUNCH_CHECK("k_reduce_parts");
     return KD_OK;
 }

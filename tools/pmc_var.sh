@@ -8,7 +8,7 @@ for v in ${VARS:-5 16}; do
              "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_MFMA" \
              "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
     i=$((i+1))
-    timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_v$v/p$i -o p -- python3 tools/gemm_one.py $M $N $K $v $LAY 5 > gpurun_out/pmc_v${v}_p$i.log 2>&1 || { echo "pmc v$v p$i failed"; tail -5 gpurun_out/pmc_v${v}_p$i.log; exit 1; }
+    timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_${LAY}_v$v/p$i -o p -- python3 tools/gemm_one.py $M $N $K $v $LAY 5 > gpurun_out/pmc_${LAY}_v${v}_p$i.log 2>&1 || { echo "pmc v$v p$i failed"; tail -5 gpurun_out/pmc_${LAY}_v${v}_p$i.log; exit 1; }
   done
 done
 echo pmc done
