@@ -151,6 +151,11 @@ typedef struct {
  * fp32 partials, and one reduce pass applies the epilogue above (deterministic). */
 size_t kd_gemm_workspace_size(const kd_gemm_desc* desc);
 
+/* The plan kd_gemm would run for `desc` (inspection only; no device work): kernel variant
+ * (1 v1, 2/3/4 v3 256x256 / 256x128 / 128x256, 16 v8), K splits, and how many leading
+ * tiles (whole waves of 256) run unsplit before the split tail (0 = every tile split). */
+int kd_gemm_plan(const kd_gemm_desc* desc, int32_t* variant, int32_t* split_k, int32_t* dp_tiles);
+
 int kd_gemm(const kd_gemm_desc* desc, void* stream);
 
 /* ------------------------------------------------------------- attention ---- */

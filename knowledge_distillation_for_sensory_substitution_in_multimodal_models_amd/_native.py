@@ -99,6 +99,7 @@ SIGNATURES = {
     "kd_attn_bwd": (_i32, [C.POINTER(KdAttnBwdDesc), _vp]),
     "kd_attn_bwd_workspace_size": (C.c_size_t, [C.POINTER(KdAttnBwdDesc)]),
     "kd_gemm_workspace_size": (C.c_size_t, [C.POINTER(KdGemmDesc)]),
+    "kd_gemm_plan": (_i32, [C.POINTER(KdGemmDesc), C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "kd_norm_fwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _f32, _vp]),
     "kd_norm_bwd_workspace_size": (_sz, [_i32, _i32]),
     "kd_norm_bwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _sz,

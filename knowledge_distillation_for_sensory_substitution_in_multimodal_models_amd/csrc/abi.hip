@@ -21,6 +21,7 @@ size_t kd_loss_ws(int B, int L, int V);
 int kd_loss_check_impl(const void* ws, void* stream);
 int launch_gemm(const kd_gemm_desc* d, void* stream);
 size_t gemm_workspace_size(const kd_gemm_desc* d);
+int gemm_plan_query(const kd_gemm_desc* d, int32_t* var, int32_t* split, int32_t* dp);
 int launch_attn_fwd(const kd_attn_desc* d, void* stream);
 int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream);
 size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d);
@@ -83,6 +84,9 @@ int kd_loss_check(const void* workspace, void* stream) { return kd::kd_loss_chec
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream) { return kd::launch_gemm(desc, stream); }
 size_t kd_gemm_workspace_size(const kd_gemm_desc* desc) { return kd::gemm_workspace_size(desc); }
+int kd_gemm_plan(const kd_gemm_desc* desc, int32_t* variant, int32_t* split_k, int32_t* dp_tiles) {
+    return kd::gemm_plan_query(desc, variant, split_k, dp_tiles);
+}
 int kd_attn_fwd(const kd_attn_desc* d, void* s) { return kd::launch_attn_fwd(d, s); }
 int kd_attn_bwd(const kd_attn_bwd_desc* d, void* s) { return kd::launch_attn_bwd(d, s); }
 size_t kd_attn_bwd_workspace_size(const kd_attn_bwd_desc* d) { return kd::attn_bwd_workspace_size(d); }

@@ -43,6 +43,7 @@ struct GemmP {
     int64_t kchunk;        // split-K: K elements per split (gridDim.y splits)
     int64_t split_stride;  // split-K: fp32 elements between consecutive partial planes
     int glu;               // SwiGLU epilogue (v8, K-major): I = N/2; B rows [0,I) gate, [I,2I) up; 0 = off
+    int tile0;             // first linear tile (grouped order) of this launch: the split tail of a hybrid plan
 };
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
@@ -134,20 +135,26 @@ __device__ __forceinline__ float apply_act(float x, int act) {
     }
 }
 
-// Block -> tile map: (1) XCD-aware bijective remap, so the blocks dispatched to one XCD
-// (b, b+8, ...) get consecutive ids; (2) grouped order, GM tile-rows at a time, so the
-// ~32 co-resident blocks of an XCD share GM A-panels and 32/GM B-panels in its L2.
-__device__ __forceinline__ void tile_of(int tiles_m, int tiles_n, int& tm, int& tn) {
-    const int nwg = gridDim.x, b = blockIdx.x;
-    const int q8 = nwg / 8, r8 = nwg % 8, x = b % 8;
-    const int wg = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + b / 8;
-    constexpr int GM = 8;
+// Linear tile id -> (tm, tn) in grouped order, GM tile-rows at a time, so the ~32
+// co-resident blocks of an XCD share GM A-panels and 32/GM B-panels in its L2.
+constexpr int GM_GROUP = 8;
+__host__ __device__ inline void tile_grouped(int wg, int tiles_m, int tiles_n, int& tm, int& tn) {
+    constexpr int GM = GM_GROUP;
     const int group = wg / (GM * tiles_n);
     const int first_m = group * GM;
     const int gm = min(tiles_m - first_m, GM);
     const int idx = wg - group * GM * tiles_n;
     tm = first_m + idx % gm;
     tn = idx / gm;
+}
+
+// Block -> tile map: XCD-aware bijective remap (the blocks dispatched to one XCD, b, b+8,
+// ..., get consecutive ids), offset by the launch's first tile, then the grouped order.
+__device__ __forceinline__ void tile_of(int tiles_m, int tiles_n, int& tm, int& tn, int tile0 = 0) {
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, x = b % 8;
+    const int wg = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + b / 8 + tile0;
+    tile_grouped(wg, tiles_m, tiles_n, tm, tn);
 }
 
 template <bool A_MN, bool B_MN>
@@ -547,7 +554,7 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     int tm, tn;
-    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
+    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn, p.tile0);
     const int m0 = tm * BM, n0 = tn * BN;
     __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
     if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
@@ -686,7 +693,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: LDS-DMA bases in SGPRs
     const int wm = wid >> 1, wn = wid & 1;
     int tm, tn;
-    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn);
+    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
     const int m0 = tm * 256, n0 = tn * 256;
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
@@ -842,18 +849,34 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
 }
 
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
-// (alpha, alpha_dev, bias, aux, act, residual, accumulate), 4 columns per thread
-__global__ void k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p) {
-    const int c4 = p.N / 4;
-    const int64_t total = (int64_t)p.M * c4;
+// (alpha, alpha_dev, bias, aux, act, residual, accumulate), over the split tiles only
+// (linear tiles [tile0, tile0 + gridDim.x) of a BM x BN tiling, grouped order as in the
+// GEMM launch); blockIdx.y takes a BM / gridDim.y row slab of its tile, 4 columns per
+// thread, the S partial loads of a chunk issued together.
+__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p, int BMr, int BNr) {
+    int tm, tn;
+    tile_grouped(p.tile0 + (int)blockIdx.x, (p.M + BMr - 1) / BMr, (p.N + BNr - 1) / BNr, tm, tn);
+    const int rows_per = BMr / (int)gridDim.y;
+    const int r0 = tm * BMr + (int)blockIdx.y * rows_per;
+    const int r1 = min(r0 + rows_per, p.M);
+    const int c0 = tn * BNr, cw = min(BNr, p.N - c0);
+    const int c4 = cw / 4;   // N % 8 == 0 on this path
     float alpha = p.alpha;
     if (p.alpha_dev) alpha *= *p.alpha_dev;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t row = idx / c4;
-        const int col = (int)(idx % c4) * 4;
+    for (int idx = threadIdx.x; idx < (r1 - r0) * c4; idx += 256) {
+        const int64_t row = r0 + idx / c4;
+        const int col = c0 + (idx % c4) * 4;
         const float* src = ws + row * p.N + col;
         f32x4 v = *(const f32x4*)src;
-        for (int s = 1; s < S; ++s) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
+        int s = 1;
+        for (; s + 3 < S; s += 4) {
+            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
+            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
+            const f32x4 c = *(const f32x4*)(src + (int64_t)(s + 2) * p.split_stride);
+            const f32x4 d = *(const f32x4*)(src + (int64_t)(s + 3) * p.split_stride);
+            v += a; v += b; v += c; v += d;
+        }
+        for (; s < S; ++s) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             float x = v[e] * alpha;
@@ -892,8 +915,12 @@ __global__ void k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p) {
 // and for the layouts with an MN-major operand (tr_b16 fragment reads). Constants fitted
 // (least squares on log time, tools/fit_plan.py) to a kernel x tile x split sweep over all
 // 42 GEMM shapes of the c1 KD step (tools/tune_gemm.py, profiles/r01/gemm_tune.jsonl): the
-// model's picks are within 0.4% of the measured best per step.
-struct GemmPlan { int var; int split; int64_t kchunk; };   // var: 2/3/4 v3 tiles, 16 v8
+// model's picks are within 0.4% of the measured best per step. A split can be confined to
+// the tiles past the last whole wave (hybrid: whole waves unsplit, then the tail tiles
+// x S splits), priced by the same constants.
+// var: 2/3/4 v3 tiles, 16 v8; split > 1 with dp_tiles > 0: the first dp_tiles tiles (whole
+// waves of 256) run unsplit with the full epilogue, only the tail tiles are split-K
+struct GemmPlan { int var; int split; int64_t kchunk; int dp_tiles; };
 
 GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t M = d->M, N = d->N;
@@ -910,9 +937,11 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t nk = ceil_div(d->K, BK2);
     // forced: variants 2/5 v3 256x256, 3/6 256x128, 4/7 128x256, 16+ v8; 0 = model's choice
     const int fv = d->variant >= 16 ? 3 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
-    const double out_b = (double)M * N * ((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
-                                          (d->residual ? 2 : 0) + (d->aux ? 2 : 0));
-    GemmPlan best{fv >= 0 ? vcode[fv] : 2, 1, d->K};
+    const double out_e = (double)((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
+                                  (d->residual ? 2 : 0) + (d->aux ? 2 : 0));   // epilogue bytes per element
+    const double out_b = (double)M * N * out_e;
+    const int tbm[4] = {256, 256, 128, 256}, tbn[4] = {256, 128, 256, 256};
+    GemmPlan best{fv >= 0 ? vcode[fv] : 2, 1, d->K, 0};
     double bt = 1e300;
     for (int v = 0; v < 4; ++v) {
         if (fv >= 0 && v != fv) continue;
@@ -927,7 +956,16 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
             double t = (double)waves * ((double)kcs * step[v] + fixed[v]);
             if (S > 1) t += ((double)S * M * N * 8 + out_b) / 7.458e6;
             if (d->split_k > 1 && S == d->split_k) t = -1;              // forced
-            if (t < bt) { bt = t; best = GemmPlan{vcode[v], S, kcs * BK2}; }
+            if (t < bt) { bt = t; best = GemmPlan{vcode[v], S, kcs * BK2, 0}; }
+            // hybrid: whole waves unsplit, the tail tiles split S ways (model's choice only)
+            const int64_t dp = (tiles[v] / 256) * 256, tail = tiles[v] - dp;
+            if (S > 1 && d->split_k <= 0 && dp > 0 && tail > 0) {
+                const double tb = (double)tbm[v] * tbn[v];
+                double th = (double)(dp / 256) * ((double)nk * step[v] + fixed[v]) +
+                            (double)((tail * S + 255) / 256) * ((double)kcs * step[v] + fixed[v]) +
+                            ((double)S * tail * tb * 8 + tail * tb * out_e) / 7.458e6;
+                if (th < bt) { bt = th; best = GemmPlan{vcode[v], S, kcs * BK2, (int)dp}; }
+            }
         }
     }
     return best;
@@ -975,7 +1013,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.c_f32 = d->c_dtype == KD_DTYPE_F32; p.accumulate = d->accumulate; p.bias_f32 = d->bias_dtype == KD_DTYPE_F32;
     p.act = d->act;
     p.res_mod = d->residual_row_mod;
-    p.kchunk = d->K; p.split_stride = 0; p.glu = 0;
+    p.kchunk = d->K; p.split_stride = 0; p.glu = 0; p.tile0 = 0;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
@@ -1002,62 +1040,71 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                                     // 16 v8 256x256 (4 waves, AGPR accumulators), 17-19 v8 diagnostics
     if (force != 1 && big_ok) {
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
-        GemmP pk = p;   // the tile kernels' parameters (split-K: plain fp32 partial planes)
-        if (pl.split > 1) {
-            KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
-                         "gemm: split-K workspace too small");
-            pk.C = d->workspace; pk.ldc = d->N; pk.c_f32 = 1; pk.accumulate = 0; pk.alpha = 1.f;
-            pk.alpha_dev = nullptr; pk.bias = nullptr; pk.aux = nullptr; pk.resid = nullptr; pk.act = KD_ACT_NONE;
-            pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N;
-        }
-        const unsigned gy = (unsigned)pl.split;
-        if (pl.var == 16) {   // v8; forced variants 17-19 are its diagnostic builds (EXP bits above)
-            const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256), gy);
-            const size_t lds = gemm2_lds<256, 256>();
+        const int tbm = pl.var == 4 ? 128 : 256, tbn = pl.var == 3 ? 128 : 256;
+        const int tiles = ceil_div(d->M, tbm) * ceil_div(d->N, tbn);
+        // one launch of the planned kernel over linear tiles [q.tile0, q.tile0 + nt), gy K splits
+        auto launch_tiles = [&](const GemmP& q, int nt, unsigned gy) {
+            const dim3 grid((unsigned)nt, gy);
+            if (pl.var == 16) {   // v8; forced variants 17-19 are its diagnostic builds (EXP bits above)
+                const size_t lds = gemm2_lds<256, 256>();
 #define L8(E)                                                                                                   \
     {                                                                                                           \
-        if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, pk);        \
-        else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, E>), grid, dim3(NTH8), lds, st, pk);     \
-        else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, E>), grid, dim3(NTH8), lds, st, pk);       \
-        else hipLaunchKernelGGL((k_gemm8<true, false, E>), grid, dim3(NTH8), lds, st, pk);                      \
+        if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, q);         \
+        else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, E>), grid, dim3(NTH8), lds, st, q);      \
+        else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, E>), grid, dim3(NTH8), lds, st, q);        \
+        else hipLaunchKernelGGL((k_gemm8<true, false, E>), grid, dim3(NTH8), lds, st, q);                       \
     }
 #define L8K(E)                                                                                                  \
     {                                                                                                           \
-        if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, pk);        \
+        if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, q);         \
         else L8(0)                                                                                              \
     }
-            switch (force) {   // the diagnostic builds exist for the forward (K-major x K-major) layout only
-                case 17: L8K(1) break;
-                case 18: L8K(2) break;
-                case 19: L8K(64) break;
-                default: L8(0) break;
-            }
+                switch (force) {   // the diagnostic builds exist for the forward (K-major x K-major) layout only
+                    case 17: L8K(1) break;
+                    case 18: L8K(2) break;
+                    case 19: L8K(64) break;
+                    default: L8(0) break;
+                }
 #undef L8K
 #undef L8
-            KD_LAUNCH_CHECK("k_gemm8");
-        } else {
-#define L3(BMv, BNv, AM, BMN)                                                                                     \
-    hipLaunchKernelGGL((k_gemm3<BMv, BNv, AM, BMN>), dim3(ceil_div(d->M, BMv) * ceil_div(d->N, BNv), gy),        \
-                       dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, pk)
+            } else {
+#define L3(BMv, BNv, AM, BMN) hipLaunchKernelGGL((k_gemm3<BMv, BNv, AM, BMN>), grid, dim3(NTH2), (gemm2_lds<BMv, BNv>()), st, q)
 #define L3SEL(BMv, BNv)                                     \
     if (!amn && !bmn) L3(BMv, BNv, false, false);           \
     else if (!amn && bmn) L3(BMv, BNv, false, true);        \
     else if (amn && bmn) L3(BMv, BNv, true, true);          \
     else L3(BMv, BNv, true, false);
-            if (pl.var == 2) { L3SEL(256, 256) }
-            else if (pl.var == 3) { L3SEL(256, 128) }
-            else { L3SEL(128, 256) }
+                if (pl.var == 2) { L3SEL(256, 256) }
+                else if (pl.var == 3) { L3SEL(256, 128) }
+                else { L3SEL(128, 256) }
 #undef L3SEL
 #undef L3
-            KD_LAUNCH_CHECK("k_gemm3");
+            }
+        };
+        if (pl.split <= 1) {
+            p.tile0 = 0;
+            launch_tiles(p, tiles, 1);
+            KD_LAUNCH_CHECK("k_gemm (tiles)");
+            return KD_OK;
         }
-        if (pl.split > 1) {
-            p.split_stride = (int64_t)d->M * d->N;
-            const int64_t work = (int64_t)d->M * d->N / 4;
-            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((work + 255) / 256, 16384)), dim3(256), 0,
-                               st, (const float*)d->workspace, pl.split, p);
-            KD_LAUNCH_CHECK("k_splitk_reduce");
+        KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
+                     "gemm: split-K workspace too small");
+        if (pl.dp_tiles > 0) {   // hybrid: whole waves unsplit with the full epilogue
+            p.tile0 = 0;
+            launch_tiles(p, pl.dp_tiles, 1);
+            KD_LAUNCH_CHECK("k_gemm (whole waves)");
         }
+        GemmP pk = p;   // the split tiles write plain fp32 partial planes
+        pk.C = d->workspace; pk.ldc = d->N; pk.c_f32 = 1; pk.accumulate = 0; pk.alpha = 1.f;
+        pk.alpha_dev = nullptr; pk.bias = nullptr; pk.aux = nullptr; pk.resid = nullptr; pk.act = KD_ACT_NONE;
+        pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N; pk.tile0 = pl.dp_tiles;
+        launch_tiles(pk, tiles - pl.dp_tiles, (unsigned)pl.split);
+        KD_LAUNCH_CHECK("k_gemm (split tiles)");
+        p.split_stride = (int64_t)d->M * d->N;
+        p.tile0 = pl.dp_tiles;
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)(tiles - pl.dp_tiles), (unsigned)(tbm / 32)), dim3(256), 0, st,
+                           (const float*)d->workspace, pl.split, p, tbm, tbn);
+        KD_LAUNCH_CHECK("k_splitk_reduce");
         return KD_OK;
     }
     const int tiles = ceil_div(d->M, BM) * ceil_div(d->N, BN);
@@ -1067,6 +1114,20 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     else if (amn && bmn) hipLaunchKernelGGL((k_gemm<true, true>), dim3(tiles), dim3(NTH), smem, st, p);
     else hipLaunchKernelGGL((k_gemm<true, false>), dim3(tiles), dim3(NTH), smem, st, p);
     KD_LAUNCH_CHECK("k_gemm");
+    return KD_OK;
+}
+
+int gemm_plan_query(const kd_gemm_desc* d, int32_t* var, int32_t* split, int32_t* dp) {
+    KD_CHECK_ARG(d && var && split && dp, "gemm_plan: null pointer");
+    KD_CHECK_SHAPE(d->M > 0 && d->N > 0 && d->K > 0, "gemm_plan: empty shape");
+    const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
+    const bool big_ok = d->N % 8 == 0 && d->M >= 128 && d->N >= 128 &&
+                        ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
+                        (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0);
+    if (d->act == KD_ACT_SWIGLU) { *var = 16; *split = 1; *dp = 0; return KD_OK; }
+    if (d->variant == 1 || !big_ok) { *var = 1; *split = 1; *dp = 0; return KD_OK; }
+    const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
+    *var = pl.var; *split = pl.split; *dp = pl.dp_tiles;
     return KD_OK;
 }
 

@@ -145,20 +145,8 @@ def _operand(x: torch.Tensor, name: str):
     raise RuntimeError(f"{name}: needs a unit stride in one dimension")
 
 
-def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
-         residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
-         out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0) -> torch.Tensor:
-    """out[M, N] = epilogue(alpha * a[M, K] @ b[N, K]^T).
-
-    split_k: 0 = library cost model (bounded by the cached GEMM_SPLITK_WS workspace),
-    1 = never split, >1 = forced number of K splits (tests).
-
-    `a`/`b` may be K-contiguous tensors or transposed views (x.t() of a contiguous tensor):
-    the kernel reads either layout directly (no transpose copies).
-
-    act="swiglu": b = [gate; up] ([2I, K]), out [M, I] = silu(gate) * up, aux (optional)
-    the [M, 2I] pre-activation (include/kdstep.h KD_ACT_SWIGLU).
-    """
+def _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate, out_dtype, residual_row_mod,
+               variant, split_k):
     M, K = a.shape
     N, K2 = b.shape
     if K != K2:
@@ -189,6 +177,37 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     if aux is not None:
         _require(aux, torch.bfloat16, "gemm.aux")
         d.aux, d.ld_aux = aux.data_ptr(), aux.stride(0)
+    return d, out, M, N, K, la, lb
+
+
+def gemm_plan(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
+              residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
+              out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0):
+    """(kernel variant, K splits, unsplit leading tiles) that gemm() with these arguments runs
+    (kd_gemm_plan; inspection only, nothing is launched)."""
+    d = _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate, out_dtype, residual_row_mod,
+                   variant, split_k)[0]
+    v, s_, dp = C.c_int32(), C.c_int32(), C.c_int32()
+    NV.call("kd_gemm_plan", C.byref(d), C.byref(v), C.byref(s_), C.byref(dp))
+    return v.value, s_.value, dp.value
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
+         residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
+         out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0) -> torch.Tensor:
+    """out[M, N] = epilogue(alpha * a[M, K] @ b[N, K]^T).
+
+    split_k: 0 = library cost model (bounded by the cached GEMM_SPLITK_WS workspace),
+    1 = never split, >1 = forced number of K splits (tests).
+
+    `a`/`b` may be K-contiguous tensors or transposed views (x.t() of a contiguous tensor):
+    the kernel reads either layout directly (no transpose copies).
+
+    act="swiglu": b = [gate; up] ([2I, K]), out [M, I] = silu(gate) * up, aux (optional)
+    the [M, 2I] pre-activation (include/kdstep.h KD_ACT_SWIGLU).
+    """
+    d, out, M, N, K, la, lb = _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate,
+                                         out_dtype, residual_row_mod, variant, split_k)
     if TIMER.enabled:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

@@ -65,3 +65,25 @@ def test_gemm_splitk_plan():
     assert ws(_gemm_desc(896, 896, 6144, 1, 1, split_k=1)) == 0
     assert ws(_gemm_desc(896, 896, 6144, 1, 1, variant=1)) == 0
     assert ws(_gemm_desc(896, 896, 6144, 1, 1, variant=16)) > 0   # forced 256x256 tile still splits
+
+
+def test_gemm_plan_hybrid_split_tail():
+    """kd_gemm_plan: a GEMM a little over one wave of 256x256 tiles (teacher down_proj,
+    6144 x 3584 x 18944: 336 tiles) runs its first 256 tiles unsplit and splits only the
+    80-tile tail; a many-wave GEMM is not split; a sub-wave one splits every tile."""
+    lib = N.lib()
+
+    def plan(d, ws=384 << 20):
+        d.A = d.B = d.C = 1 << 16
+        d.workspace, d.workspace_bytes = (1 << 20, ws) if ws else (None, 0)
+        v, s, dp = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        assert lib.kd_gemm_plan(ctypes.byref(d), ctypes.byref(v), ctypes.byref(s), ctypes.byref(dp)) == 0
+        return v.value, s.value, dp.value
+
+    var, split, dp = plan(_gemm_desc(6144, 3584, 18944, c_f32=0, acc=0))
+    assert split > 1 and dp == 256, (var, split, dp)
+    assert plan(_gemm_desc(6144, 37888, 3584, c_f32=0, acc=0))[1:] == (1, 0)
+    var, split, dp = plan(_gemm_desc(896, 896, 6144, 1, 1))
+    assert split > 1 and dp == 0
+    assert plan(_gemm_desc(6144, 3584, 18944, c_f32=0, acc=0), ws=0)[1] == 1   # no workspace: no split
+    assert plan(_gemm_desc(6144, 3584, 18944, c_f32=0, acc=0, split_k=4))[1:] == (4, 0)   # forced: every tile

@@ -192,6 +192,34 @@ def test_splitk_auto_wgrad(M, N, K, dev):
     assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
 
 
+def test_hybrid_split_tail(dev):
+    """Auto plan on a GEMM just over one wave of tiles: whole waves run unsplit with the
+    kernel epilogue, the tail tiles split-K with the reduce epilogue; both must give the
+    full epilogue (alpha, bias, aux, act, residual) and fp32 accumulate in every layout."""
+    ops = _ops()
+    M, N, K = 4608, 3840, 4096
+    a = _rand(M, K, dev=dev, seed=80, scale=0.2)
+    w = _rand(N, K, dev=dev, seed=81, scale=0.02)
+    bias = _rand(N, dev=dev, seed=82)
+    res = _rand(M, N, dev=dev, seed=83)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    var, split, dp = ops.gemm_plan(a, w)
+    assert split > 1 and 0 < dp < 18 * 15, (var, split, dp)
+    pre = 1.25 * (a.float() @ w.float().t()) + bias.float()
+    out = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=res, aux=aux, alpha=1.25)
+    _check(out, torch.nn.functional.gelu(pre, approximate="tanh") + res.float())
+    _check(aux, pre)
+    at = _rand(K, M, dev=dev, seed=84)
+    wt = _rand(K, N, dev=dev, seed=85, scale=0.05)
+    for A, B, ref in ((a, wt.t(), a.float() @ wt.float()), (at.t(), wt.t(), at.float().t() @ wt.float()),
+                      (at.t(), w, at.float().t() @ w.float().t())):
+        acc = torch.full((M, N), 0.5, dtype=torch.float32, device=dev)
+        assert ops.gemm_plan(A, B, out=acc, accumulate=True)[2] > 0
+        ops.gemm(A, B, out=acc, accumulate=True)
+        r = 0.5 + ref
+        assert (acc - r).abs().max().item() <= 1e-4 * r.abs().max().item() + 1e-3
+
+
 @pytest.mark.parametrize("M,I,K", [(300, 256, 96), (1536, 384, 896), (257, 128, 600), (512, 1280, 3584)])
 def test_swiglu_epilogue_bitexact(M, I, K, dev):
     """act='swiglu' (gate|up GEMM + silu(gate)*up fused, v8) == the unfused GEMM + k_swiglu_fwd,
