@@ -851,8 +851,9 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
 // (alpha, alpha_dev, bias, aux, act, residual, accumulate), over the split tiles only
 // (linear tiles [tile0, tile0 + gridDim.x) of a BM x BN tiling, grouped order as in the
-// GEMM launch); blockIdx.y takes a BM / gridDim.y row slab of its tile, 4 columns per
-// thread, the S partial loads of a chunk issued together.
+// GEMM launch); blockIdx.y takes a BM / gridDim.y row slab of its tile (one 4-column chunk
+// per thread: many blocks, every load of a block in flight at once), the S partial loads
+// of a chunk issued together.
 __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p, int BMr, int BNr) {
     int tm, tn;
     tile_grouped(p.tile0 + (int)blockIdx.x, (p.M + BMr - 1) / BMr, (p.N + BNr - 1) / BNr, tm, tn);
@@ -876,7 +877,13 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
             const f32x4 d = *(const f32x4*)(src + (int64_t)(s + 3) * p.split_stride);
             v += a; v += b; v += c; v += d;
         }
-        for (; s < S; ++s) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
+        if (s + 1 < S) {   // same summation order, both loads in flight
+            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
+            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
+            v += a; v += b;
+            s += 2;
+        }
+        if (s < S) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             float x = v[e] * alpha;
@@ -1102,7 +1109,8 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_LAUNCH_CHECK("k_gemm (split tiles)");
         p.split_stride = (int64_t)d->M * d->N;
         p.tile0 = pl.dp_tiles;
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)(tiles - pl.dp_tiles), (unsigned)(tbm / 32)), dim3(256), 0, st,
+        // one float4 column chunk per thread: BM / (1024 / BN) row slabs of 1024 / BN rows per tile
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)(tiles - pl.dp_tiles), (unsigned)(tbm * tbn / 1024)), dim3(256), 0, st,
                            (const float*)d->workspace, pl.split, p, tbm, tbn);
         KD_LAUNCH_CHECK("k_splitk_reduce");
         return KD_OK;
