@@ -140,7 +140,8 @@ typedef struct {
     int32_t residual_row_mod; /* >0: residual row index = m % residual_row_mod (SigLIP pos-emb) */
     int32_t variant;          /* 0 auto (cost model); forced (tests/tools): 1 128x128 4-wave; 2|5 / 3|6 / 4|7
                                  256x256 / 256x128 / 128x256 8-wave; 16 256x256 4-wave (AGPR accumulators);
-                                 17-19 diagnostic builds of 16 (tools/stamp_gemm.py, tools/ablate_gemm.py) */
+                                 17-19 diagnostic builds of 16 (tools/stamp_gemm.py, tools/ablate_gemm.py);
+                                 20 256x256 8-wave ping-pong (two wave groups alternate on each SIMD) */
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;

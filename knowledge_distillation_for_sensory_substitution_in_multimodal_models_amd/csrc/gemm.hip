@@ -848,6 +848,133 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     }
 }
 
+// =============================================================================
+// v9: 256x256 tile, EIGHT waves in two groups that ping-pong on every SIMD. Group g
+// (waves 4g..4g+3, one per SIMD) owns rows 128g..128g+127; wave 4g+c owns columns
+// 64c..64c+63, 8x4 MFMA 16x16x32 tiles whose accumulators stay in the AGPR file (asm
+// MFMA, as v8). Same 4-slot BK=32 LDS-DMA ring and stage images as v3/v8.
+// Group 1 runs one barrier behind group 0, so between consecutive barriers one group
+// issues its LDS reads and DMA while the other owns the SIMD's MFMA pipe (s_setprio 1):
+//   K-tile t, per wave: [reads of slot t%4 (12 fragments) ; DMA of K-tile t+3 (4 of the
+//   32 1-KiB wave-instructions) ; vmcnt(8) ; lgkmcnt(0)] barrier [32 MFMA] barrier
+// Barrier intervals: group 0 reads K-tile t in interval 2t, group 1 in 2t+1.
+// RAW: K-tile t+1's DMA is retired by every wave's vmcnt(8) in its load phase of K-tile t
+//   (issued then: t+1, t+2, t+3), before barrier 2t+1 (g0) / 2t+2 (g1); its first reader
+//   (g0) starts after barrier 2t+2.
+// WAR: K-tile t+3 goes into the slot of K-tile t-1, whose reads every wave retired
+//   (lgkmcnt 0) before barrier 2t (g1's is the later one); the DMA is issued in interval
+//   2t (g0) / 2t+1 (g1). Past the last K-tile the DMAs still run (all lanes out of range:
+//   zero-fill, no memory traffic) so the counts stay uniform.
+// =============================================================================
+constexpr int NTH9 = 512;
+
+template <bool A_MN, bool B_MN>
+__global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
+    GemmP p = p_;
+    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2, wc = wid & 3;
+    int tm, tn;
+    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int K = p.K;
+    const int nk = (K + BK2 - 1) / BK2;
+    const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (A_MN ? 0 : (int64_t)m0 * p.lda), A_MN ? 0u : rec_bytes(min(256, p.M - m0), p.lda));
+    const bool glu = !B_MN && p.glu != 0;   // gate rows [nb, nb+128) and up rows [I+nb, I+nb+128)
+    const int nb = tn * 128;
+    const __amdgpu_buffer_rsrc_t rsBk =
+        glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
+            : make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
+    // this wave's DMA share of a K-tile: A and B wave-instructions 2*wid, 2*wid+1 (of 16 each)
+    uint32_t va[2], vb[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        va[u] = voff8<A_MN>(wid * 2 + u, lane, p.lda, m0, p.M);
+        vb[u] = voff8<B_MN>(wid * 2 + u, lane, p.ldb, n0, p.N);
+        if (glu) {
+            const int row = 16 * (wid * 2 + u) + (lane >> 2);
+            const int gc = (lane & 3) ^ f4(row);
+            const int wrow = row < 128 ? nb + row : p.glu + nb + row - 128;
+            vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
+        }
+    }
+    auto dma = [&](int st, int u) {   // u: 0,1 operand A; 2,3 operand B
+        const bool isA = u < 2;
+        const bool mn = isA ? A_MN : B_MN;
+        const int i = wid * 2 + (u & 1);
+        char* dst = smem + (st & 3) * SS + (isA ? 0 : SA) + i * 1024;
+        uint32_t v = isA ? va[u & 1] : vb[u & 1];
+        if (!mn) {
+            int soff = st * BK2 * 2;
+            const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
+            if (kleft < BK2) {
+                const int row = 16 * i + (lane >> 2);
+                const int gc = (lane & 3) ^ f4(row);
+                if (gc * 8 >= kleft) v = OOB;
+                if (kleft <= 0) soff = 0;
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, v, soff, 0, 0);
+        } else {
+            const bf16* base = isA ? p.A + m0 : p.B + n0;
+            const int64_t ld = isA ? p.lda : p.ldb;
+            const int kv = max(0, min(BK2, K - st * BK2));
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)min(st * BK2, K) * ld, rec_bytes(kv, ld));
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)dst, 16, v, 0, 0, 0);
+        }
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int ra = grp * 128, cb = wc * 64;
+#pragma unroll
+    for (int st = 0; st < 3; ++st)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dma(st, u);
+    wait_vm<8>();   // K-tile 0 landed (1 and 2 stay in flight)
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
+    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < nk; ++t) {
+        const char* sl = smem + (t & 3) * SS;
+        bf16x8 fa[8], fb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag2<256, B_MN>(sl + SA, cb + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[i] = frag2<256, A_MN>(sl, ra + i * 16, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dma(t + 3, u);
+        wait_vm<8>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mfma_agpr(acc[i][j], fa[i], fb[j]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (!A_MN && !B_MN && glu) epilogue_glu<128, 64, 8, 4, NTH9>(p, acc, smem, m0, nb, grp, wc, lane, tid);
+    else epilogue2<256, 256, 2, 4, 128, 64, 8, 4, NTH9, !A_MN && !B_MN>(p, acc, smem, m0, n0, grp, wc, lane, tid);
+}
+
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
 // (alpha, alpha_dev, bias, aux, act, residual, accumulate), over the split tiles only
 // (linear tiles [tile0, tile0 + gridDim.x) of a BM x BN tiling, grouped order as in the
@@ -925,33 +1052,35 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
 // model's picks are within 0.4% of the measured best per step. A split can be confined to
 // the tiles past the last whole wave (hybrid: whole waves unsplit, then the tail tiles
 // x S splits), priced by the same constants.
-// var: 2/3/4 v3 tiles, 16 v8; split > 1 with dp_tiles > 0: the first dp_tiles tiles (whole
+// var: 2/3/4 v3 tiles, 16 v8, 20 v9; split > 1 with dp_tiles > 0: the first dp_tiles tiles (whole
 // waves of 256) run unsplit with the full epilogue, only the tail tiles are split-K
 struct GemmPlan { int var; int split; int64_t kchunk; int dp_tiles; };
 
 GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t M = d->M, N = d->N;
     const int64_t t256 = (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 256);
-    const int64_t tiles[4] = {t256, (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 128),
-                              (int64_t)ceil_div(d->M, 128) * ceil_div(d->N, 256), t256};
+    const int64_t tiles[5] = {t256, (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 128),
+                              (int64_t)ceil_div(d->M, 128) * ceil_div(d->N, 256), t256, t256};
     const bool kk = d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR;
-    // per variant (v3 256x256, 256x128, 128x256; v8): {K-major x K-major, MN-major operand}
-    static const double step_c[2][4] = {{0.7474, 0.5245, 0.5203, 0.6746}, {0.7874, 0.5727, 0.5746, 0.6120}};
-    static const double fixed_c[2][4] = {{7.537, 4.314, 3.730, 11.064}, {8.256, 4.529, 4.020, 12.656}};
+    // per variant (v3 256x256, 256x128, 128x256; v8; v9): {K-major x K-major, MN-major operand}
+    static const double step_c[2][5] = {{0.7474, 0.5245, 0.5203, 0.6746, 0.6746}, {0.7874, 0.5727, 0.5746, 0.6120, 0.6120}};
+    static const double fixed_c[2][5] = {{7.537, 4.314, 3.730, 11.064, 11.064}, {8.256, 4.529, 4.020, 12.656, 12.656}};
+    constexpr bool kV9Auto = false;   // v9 enters the model's choice once its constants are fitted
     const double* step = step_c[kk ? 0 : 1];
     const double* fixed = fixed_c[kk ? 0 : 1];
-    const int vcode[4] = {2, 3, 4, 16};
+    const int vcode[5] = {2, 3, 4, 16, 20};
     const int64_t nk = ceil_div(d->K, BK2);
     // forced: variants 2/5 v3 256x256, 3/6 256x128, 4/7 128x256, 16+ v8; 0 = model's choice
-    const int fv = d->variant >= 16 ? 3 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1));
+    const int fv = d->variant == 20 ? 4 : (d->variant >= 16 ? 3 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1)));
     const double out_e = (double)((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
                                   (d->residual ? 2 : 0) + (d->aux ? 2 : 0));   // epilogue bytes per element
     const double out_b = (double)M * N * out_e;
-    const int tbm[4] = {256, 256, 128, 256}, tbn[4] = {256, 128, 256, 256};
+    const int tbm[5] = {256, 256, 128, 256, 256}, tbn[5] = {256, 128, 256, 256, 256};
     GemmPlan best{fv >= 0 ? vcode[fv] : 2, 1, d->K, 0};
     double bt = 1e300;
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 5; ++v) {
         if (fv >= 0 && v != fv) continue;
+        if (v == 4 && !kV9Auto && fv != 4) continue;
         for (int S = 1; S <= 32; ++S) {
             if (d->split_k == 1 && S != 1) continue;
             if (d->split_k > 1 && S != d->split_k && S != 1) continue;
@@ -992,7 +1121,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->act == KD_ACT_NONE || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
                                           d->c_dtype == KD_DTYPE_BF16),
                  "gemm: an activation epilogue needs K-major operands and a bf16 output");
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 19), "gemm: unknown variant");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 20), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     KD_CHECK_SHAPE(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
@@ -1039,8 +1168,9 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         GemmP pk = p;
         pk.glu = d->N / 2; pk.act = KD_ACT_NONE;
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
-        hipLaunchKernelGGL((k_gemm8<false, false, 0>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
-        KD_LAUNCH_CHECK("k_gemm8<swiglu>");
+        if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
+        else hipLaunchKernelGGL((k_gemm8<false, false, 0>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        KD_LAUNCH_CHECK("k_gemm<swiglu>");
         return KD_OK;
     }
     const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,
@@ -1052,7 +1182,13 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         // one launch of the planned kernel over linear tiles [q.tile0, q.tile0 + nt), gy K splits
         auto launch_tiles = [&](const GemmP& q, int nt, unsigned gy) {
             const dim3 grid((unsigned)nt, gy);
-            if (pl.var == 16) {   // v8; forced variants 17-19 are its diagnostic builds (EXP bits above)
+            if (pl.var == 20) {   // v9
+                const size_t lds = gemm2_lds<256, 256>();
+                if (!amn && !bmn) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), lds, st, q);
+                else if (!amn && bmn) hipLaunchKernelGGL((k_gemm9<false, true>), grid, dim3(NTH9), lds, st, q);
+                else if (amn && bmn) hipLaunchKernelGGL((k_gemm9<true, true>), grid, dim3(NTH9), lds, st, q);
+                else hipLaunchKernelGGL((k_gemm9<true, false>), grid, dim3(NTH9), lds, st, q);
+            } else if (pl.var == 16) {   // v8; forced variants 17-19 are its diagnostic builds (EXP bits above)
                 const size_t lds = gemm2_lds<256, 256>();
 #define L8(E)                                                                                                   \
     {                                                                                                           \

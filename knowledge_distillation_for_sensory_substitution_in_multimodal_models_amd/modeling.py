@@ -19,6 +19,7 @@ a trainable model) in the transformers-4.45 state_dict order and names
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -300,10 +301,15 @@ class WgradLane:
 
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device)
+        # split-K default for the lane's GEMMs (0 = the library's cost model, which prices a
+        # GEMM as if it had the GPU to itself; 1 = never split: beside the dgrad chain an
+        # unsplit 76-150-tile dW GEMM leaves the other CUs to it and skips the fp32
+        # partial-plane round trip)
+        self.split_k = int(os.environ.get("KD_WGRAD_SPLIT_K", "0"))
 
     def run(self, fn, *keep):
         self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(self.stream), ops.gemm_split_default(self.split_k):
             fn()
         for t in keep:
             if t is not None:

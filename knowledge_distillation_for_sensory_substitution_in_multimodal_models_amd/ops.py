@@ -5,6 +5,7 @@ FLOP runs in libkdstep.so.  There is no CPU or torch fallback for any op.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import torch
@@ -192,6 +193,20 @@ def gemm_plan(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     return v.value, s_.value, dp.value
 
 
+_SPLIT_DEFAULT = [0]
+
+
+@contextlib.contextmanager
+def gemm_split_default(split_k: int):
+    """Within the block, gemm(split_k=0) calls use `split_k` instead (0 = cost model)."""
+    prev = _SPLIT_DEFAULT[0]
+    _SPLIT_DEFAULT[0] = int(split_k)
+    try:
+        yield
+    finally:
+        _SPLIT_DEFAULT[0] = prev
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
          residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
          out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0) -> torch.Tensor:
@@ -206,6 +221,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     act="swiglu": b = [gate; up] ([2I, K]), out [M, I] = silu(gate) * up, aux (optional)
     the [M, 2I] pre-activation (include/kdstep.h KD_ACT_SWIGLU).
     """
+    if split_k == 0:
+        split_k = _SPLIT_DEFAULT[0]
     d, out, M, N, K, la, lb = _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate,
                                          out_dtype, residual_row_mod, variant, split_k)
     if TIMER.enabled:

@@ -93,7 +93,8 @@ def test_epilogue_bias_act_residual_aux_accumulate(dev):
     assert (out - 0.5 * (a.float() @ w.float().t())).abs().max().item() < 1e-3
 
 
-VARIANTS = [1, 5, 6, 7, 16]   # 128x128 v1; v3 256x256 / 256x128 / 128x256 (8 waves); v8 256x256 (4 waves, AGPR acc)
+VARIANTS = [1, 5, 6, 7, 16, 20]   # 128x128 v1; v3 256x256 / 256x128 / 128x256 (8 waves); v8 256x256 (4 waves, AGPR acc);
+#                                  v9 256x256 (8 waves, ping-pong)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -119,7 +120,7 @@ def test_variants_all_layouts(variant, M, N, K, dev):
         _check(ops.gemm(at.t(), w, variant=variant), at.float().t() @ w.float().t())
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 16])
+@pytest.mark.parametrize("variant", [5, 6, 7, 16, 20])
 def test_variant_epilogue(variant, dev):
     ops = _ops()
     M, N, K = 1458, 1152, 192
@@ -139,7 +140,7 @@ def test_variant_epilogue(variant, dev):
 
 
 @pytest.mark.parametrize("split", [2, 3, 7])
-@pytest.mark.parametrize("variant", [0, 6, 7, 16])
+@pytest.mark.parametrize("variant", [0, 6, 7, 16, 20])
 @pytest.mark.parametrize("M,N,K", [(520, 384, 2248), (1152, 1152, 5832)])
 def test_splitk_all_layouts(split, variant, M, N, K, dev):
     """Forced K splits (fp32 partial planes + reduce) in every operand layout; K is not a
@@ -238,3 +239,23 @@ def test_swiglu_epilogue_bitexact(M, I, K, dev):
     assert torch.equal(ops.gemm(h, w, act="swiglu"), a_ref)
     g = gu_ref.float()
     _check(a, torch.nn.functional.silu(g[:, :I]) * g[:, I:])
+
+
+@pytest.mark.parametrize("M,N,K", [(6144 // 4, 896, 4864 // 2), (1456, 1152, 1152), (304, 520, 600), (4096, 4096, 4096)])
+def test_v9_bitexact_vs_v8(M, N, K, dev):
+    """v9 (8-wave ping-pong) accumulates every output element over the same k32 MFMA
+    sequence as v8, so the two agree bit for bit in every operand layout, with and without
+    the SwiGLU epilogue."""
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=90)
+    w = _rand(N, K, dev=dev, seed=91, scale=0.05)
+    at = _rand(K, M, dev=dev, seed=92)
+    wt = _rand(K, N, dev=dev, seed=93, scale=0.05)
+    for A, B in ((a, w), (a, wt.t()), (at.t(), w), (at.t(), wt.t())):
+        assert torch.equal(ops.gemm(A, B, variant=20, split_k=1), ops.gemm(A, B, variant=16, split_k=1))
+    if N % 256 == 0:
+        g9 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        g8 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        o9 = ops.gemm(a, w, act="swiglu", aux=g9, variant=20)
+        o8 = ops.gemm(a, w, act="swiglu", aux=g8, variant=16)
+        assert torch.equal(o9, o8) and torch.equal(g9, g8)

@@ -12,7 +12,8 @@ from scipy.optimize import least_squares
 
 rows = [json.loads(l) for l in open(sys.argv[1])]
 w = {r["shape"]: r["launches"] for r in json.load(open(sys.argv[2] if len(sys.argv) > 2 else "tools/step_shapes_c1.json"))}
-VI = {5: 0, 6: 1, 7: 2, 16: 3}
+VI = {5: 0, 6: 1, 7: 2, 16: 3, 20: 4}
+NV = 5
 
 
 def cd(a, b):
@@ -24,7 +25,8 @@ def feats(shape, v, S):
     M, N, K = map(int, p[1].split("x"))
     f32, acc = p[2] == "f32", len(p) > 3
     c = 0 if p[0] == "gemm_kk" else 1
-    tiles = [cd(M, 256) * cd(N, 256), cd(M, 256) * cd(N, 128), cd(M, 128) * cd(N, 256), cd(M, 256) * cd(N, 256)][v]
+    tiles = [cd(M, 256) * cd(N, 256), cd(M, 256) * cd(N, 128), cd(M, 128) * cd(N, 256), cd(M, 256) * cd(N, 256),
+             cd(M, 256) * cd(N, 256)][v]
     nk = cd(K, 32)
     kcs = cd(nk, S)
     waves = cd(tiles * S, 256)
@@ -42,20 +44,20 @@ for r in rows:
 
 def pred(x, shape, v, S):
     c, waves, kcs, traffic = feats(shape, v, S)
-    step, fixed = x[2 * (4 * c + v)], x[2 * (4 * c + v) + 1]
-    return waves * (kcs * step + fixed) + traffic / (x[16] * 1e6)
+    step, fixed = x[2 * (NV * c + v)], x[2 * (NV * c + v) + 1]
+    return waves * (kcs * step + fixed) + traffic / (x[4 * NV] * 1e6)
 
 
 def resid(x):
     return [math.log(max(pred(x, s, v, S), 1e-3)) - math.log(t) for s, v, S, t in data]
 
 
-x0 = np.array([0.8, 4.0] * 8 + [6.0])
-fit = least_squares(resid, x0, bounds=([0.05, 0.0] * 8 + [1.0], [5.0, 50.0] * 8 + [20.0]))
+x0 = np.array([0.8, 4.0] * (2 * NV) + [6.0])
+fit = least_squares(resid, x0, bounds=([0.05, 0.0] * (2 * NV) + [1.0], [5.0, 50.0] * (2 * NV) + [20.0]))
 x = fit.x
-print("step/fixed per class (kk, mn) x variant (v3 256x256, 256x128, 128x256, v8); BW TB/s", round(x[16], 3))
+print("step/fixed per class (kk, mn) x variant (v3 256x256, 256x128, 128x256, v8, v9); BW TB/s", round(x[4 * NV], 3))
 for c in range(2):
-    print(" ", ["kk", "mn"][c], [(round(x[2 * (4 * c + v)], 4), round(x[2 * (4 * c + v) + 1], 3)) for v in range(4)])
+    print(" ", ["kk", "mn"][c], [(round(x[2 * (NV * c + v)], 4), round(x[2 * (NV * c + v) + 1], 3)) for v in range(NV)])
 tot_best = tot_pick = 0.0
 for r in rows:
     meas = {(VI[int(k.split("/")[0])], int(k.split("/")[1])): t * 1e3 for k, t in r["all"].items()}

@@ -47,7 +47,7 @@ for sh in shapes:
     fl = 2.0 * M * N * K
     auto = timeit(lambda: ops.gemm(a, b, out=out, accumulate=acc))
     res = {}
-    VARS = (5, 6, 7, 16)
+    VARS = (5, 6, 7, 16, 20)
     for var in VARS:
         for sk in (1, 2, 3, 4, 6, 8, 12, 16):
             if sk > 1 and (K // 32) // sk < 4:
