@@ -143,6 +143,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timer", action="store_true", help="skip the serialized roofline pass (per-GEMM HIP events)")
+    ap.add_argument("--prefetch", action="store_true",
+                    help="run the next step's teacher forward one step ahead on its own stream (measured: no gain, "
+                         "the step is GPU-throughput-bound)")
     ap.add_argument("--serial", action="store_true",
                     help="student forward on the main stream (no overlap with the teacher forward)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
@@ -163,15 +166,25 @@ def main():
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
     m, opt = build(cfg, dev)
     m.concurrent_student = not a.serial
-    batch = synthetic_batch(B, dev, L=1536, seed=rank)
+    # two synthetic batches, alternated, so every step's teacher forward is a fresh one
+    batches = [synthetic_batch(B, dev, L=1536, seed=rank * 2 + j) for j in range(2)]
+    prefetch = [a.prefetch and not a.serial]
 
     def step(i):
-        loss = m.training_step(batch, i)
+        loss = m.training_step(batches[i % 2], i)
         loss.backward()
+        if prefetch[0]:   # the next step's teacher forward, beside this step's backward + AdamW
+            m.prefetch_teacher(batches[(i + 1) % 2])
         opt.step()
         opt.zero_grad()
         return loss
 
+    # the step's main stream at the same high priority as its side streams (the teacher
+    # prefetch stream stays at normal priority)
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import STREAM_PRIORITY_HIGH
+    hp = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
+    hp.wait_stream(torch.cuda.current_stream())
+    torch.cuda.set_stream(hp)
     for i in range(a.warmup):
         loss = step(i)
     torch.cuda.synchronize()
@@ -181,6 +194,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(a.warmup + i)
+    host_dt = time.perf_counter() - t0   # host enqueue time of the K steps (~dt: launch-bound)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -191,6 +205,8 @@ def main():
     # kernel's duration is its own and not shared with a concurrent stream
     if not a.no_timer:
         m.concurrent_student = False
+        prefetch[0] = False
+        m._prefetched = None   # the roofline steps run every teacher GEMM inline, on the main stream
         ops.TIMER.reset()
         ops.TIMER.enabled = True
         for i in range(2):
@@ -198,6 +214,7 @@ def main():
         torch.cuda.synchronize()
         ops.TIMER.enabled = False
         m.concurrent_student = not a.serial
+        prefetch[0] = a.prefetch and not a.serial
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -249,8 +266,10 @@ def main():
         "data": "synthetic (random 336x336 pixels, random token ids; random-init weights of the real architectures)",
         "config": {"workload": f"{a.config}: {cfg['desc']}", "model": "llava-onevision-qwen2-7b (teacher) -> 0.5b (student)",
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": 1536, "image": "336x336 (2 tiles, 1485 tokens)",
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "teacher_prefetch": bool(a.prefetch and not a.serial)},
         "mfu": round(value * tf_sample / world / PEAK_BF16_TFLOPS, 4),
+        "host_enqueue_ms_per_step": round(host_dt * 1e3 / a.steps, 2),
         "tflop_per_sample": round(tf_sample, 2),
         "loss": round(float(loss.item()), 5),
         "roofline": roof,

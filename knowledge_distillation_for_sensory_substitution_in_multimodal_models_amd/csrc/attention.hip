@@ -21,6 +21,8 @@
 //   dS goes through LDS once for dQ += dS K, accumulated with fp32 atomics.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace kd {
 namespace {
 
@@ -83,34 +85,60 @@ __device__ __forceinline__ bf16x4 tr_read(const char* lds, int r, int d) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a);
 }
 
-template <int HDP, bool CAUSAL>
+// The same transposed read through inline asm: with the builtin, hipcc cannot tell it from
+// the in-flight LDS-DMA of the next K/V tile and waits vmcnt(0) before the first one,
+// so the prefetch only overlapped QK^T + softmax, not PV. The caller retires these reads
+// with its own lgkmcnt(0) (+ sched_barrier) before the MFMAs that consume them.
+template <int RB>
+__device__ __forceinline__ bf16x4 tr_read_asm(const char* lds, int r, int d) {
+    const int c = d >> 3;
+    const char* a = lds + r * RB + ((c ^ swV<RB>(r)) << 4) + ((d & 4) << 1);
+    u32x2 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)a));
+    return __builtin_bit_cast(bf16x4, v);
+}
+
+// NQ query sub-tiles of 16 rows per wave (workgroup = 4 waves x 16·NQ rows): every K
+// fragment (b128) and V^T fragment (tr_b16) read from LDS feeds NQ MFMAs, so LDS bytes
+// per FLOP drop by NQ (at NQ = 1 the kernel was bound by its LDS reads: one 64-key tile =
+// 32 KiB of fragment reads per wave for a 16 x 64 block of scores).
+template <int HDP, bool CAUSAL, int NQ>
 __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
     constexpr int TILE = 64 * RB;
+    constexpr int QBLK = 64 * NQ;   // query rows per workgroup
     extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][K TILE | V TILE]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = lane >> 4, li = lane & 15;
-    const int nqb = (p.S + 63) / 64;
+    const int nqb = (p.S + QBLK - 1) / QBLK;
     const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
     const int h = blockIdx.y, b = blockIdx.z, kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const int q0 = qb * 64 + wid * 16;
-    const int myq = q0 + li;
-
-    bf16x8 qf[KS];
+    int myq[NQ];
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-        if (myq < p.S) qf[kk] = *(const bf16x8*)(Q + (int64_t)myq * HDP + kk * 32 + 8 * g);
-        else qf[kk] = (bf16x8){};
-    }
-    f32x4 o[DT];
-#pragma unroll
-    for (int d = 0; d < DT; ++d) o[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float m = -INFINITY, l = 0.f;
+    for (int j = 0; j < NQ; ++j) myq[j] = qb * QBLK + wid * 16 * NQ + j * 16 + li;
 
-    const int nkv = CAUSAL ? min(qb + 1, (p.S + 63) / 64) : (p.S + 63) / 64;
+    bf16x8 qf[NQ][KS];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j)
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            if (myq[j] < p.S) qf[j][kk] = *(const bf16x8*)(Q + (int64_t)myq[j] * HDP + kk * 32 + 8 * g);
+            else qf[j][kk] = (bf16x8){};
+        }
+    f32x4 o[NQ][DT];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j)
+#pragma unroll
+        for (int d = 0; d < DT; ++d) o[j][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float m[NQ], l[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
+
+    const int nkv_all = (p.S + 63) / 64;
+    const int nkv = CAUSAL ? min((qb + 1) * QBLK / 64, nkv_all) : nkv_all;
     stage_kv<HDP, false>(smem, K, 0, p.S, wid, lane);
     stage_kv<HDP, true>(smem + TILE, V, 0, p.S, wid, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -125,80 +153,112 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
         }
         const char* kt_l = smem + cur * 2 * TILE;
         const char* vt_l = kt_l + TILE;
-        // ---- S^T tiles: rows = keys 16kt + 4g + r, col = my query
-        f32x4 s[4];
+        // ---- S^T tiles: rows = keys 16kt + 4g + r, col = the lane's query of sub-tile j
+        f32x4 sc[NQ][4];
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
-            s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int kk = 0; kk < KS; ++kk)
-                s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(kt_l, 16 * kt + li, kk * 4 + g), qf[kk], s[kt], 0, 0, 0);
+            for (int j = 0; j < NQ; ++j) sc[j][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                const bf16x8 kf = k_frag<RB>(kt_l, 16 * kt + li, kk * 4 + g);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[j][kk], sc[j][kt], 0, 0, 0);
+            }
         }
-        float mt = -INFINITY;
+        // ---- online softmax in the log2 domain. The mask is applied only on tiles that
+        // cross the causal diagonal or the sequence end (wave-uniform test); the scale is
+        // folded into the exponent's fma; v_exp_f32 directly (exp2f adds range handling).
+        const int key0 = t * 64 + 4 * g;
+        bf16x8 pf[NQ][2];
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int j = 0; j < NQ; ++j) {
+            const int qlo = qb * QBLK + wid * 16 * NQ + j * 16;   // first query of this sub-tile
+            if (t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qlo)) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int key = t * 64 + 16 * kt + 4 * g + r;
-                float v = s[kt][r] * p.scale_log2;
-                if (key >= p.S || (CAUSAL && key > myq)) v = -INFINITY;
-                s[kt][r] = v;
-                mt = fmaxf(mt, v);
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int key = key0 + 16 * kt + r;
+                        if (key >= p.S || (CAUSAL && key > myq[j])) sc[j][kt][r] = -INFINITY;
+                    }
             }
-        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-        const float mn = fmaxf(m, mt);
-        const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
-        float ls = 0.f;
+            float mt = -INFINITY;
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+            for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float e = (mn == -INFINITY) ? 0.f : exp2f(s[kt][r] - mn);
-                s[kt][r] = e;
-                ls += e;
+                for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sc[j][kt][r]);
+            mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+            const float mn = fmaxf(m[j], mt * p.scale_log2);   // scale > 0: max commutes
+            const float mref = (mn == -INFINITY) ? 0.f : mn;
+            const float alpha = __builtin_amdgcn_exp2f(m[j] - mref);
+            float ls = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][kt][r], p.scale_log2, -mref));
+                    sc[j][kt][r] = e;
+                    ls += e;
+                }
+            l[j] = l[j] * alpha + ls;
+            m[j] = mn;
+            if (__ballot(alpha != 1.f)) {   // once the running max settles, most tiles skip it
+#pragma unroll
+                for (int d = 0; d < DT; ++d) o[j][d] *= alpha;
             }
-        l = l * alpha + ls;
-        m = mn;
 #pragma unroll
-        for (int d = 0; d < DT; ++d) o[d] *= alpha;
-        // ---- O^T += V^T P^T, two 32-key steps
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { pf[j][ks][r] = (bf16)sc[j][2 * ks][r]; pf[j][ks][4 + r] = (bf16)sc[j][2 * ks + 1][r]; }
+        }
+        // ---- O^T += V^T P^T, two 32-key steps; each V^T fragment feeds the NQ sub-tiles
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            bf16x8 pf;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { pf[r] = (bf16)s[2 * ks][r]; pf[4 + r] = (bf16)s[2 * ks + 1][r]; }
             const int kr = 32 * ks + 4 * g + (li >> 2);
+            bf16x4 v0[DT], v1[DT];
 #pragma unroll
             for (int d = 0; d < DT; ++d) {
                 const int dc = d * 16 + 4 * (li & 3);
-                bf16x4 v0 = tr_read<RB>(vt_l, kr, dc);
-                bf16x4 v1 = tr_read<RB>(vt_l, kr + 16, dc);
+                v0[d] = tr_read_asm<RB>(vt_l, kr, dc);
+                v1[d] = tr_read_asm<RB>(vt_l, kr + 16, dc);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
                 bf16x8 vf;
-                vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v0[2]; vf[3] = v0[3];
-                vf[4] = v1[0]; vf[5] = v1[1]; vf[6] = v1[2]; vf[7] = v1[3];
-                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[d], 0, 0, 0);
+                vf[0] = v0[d][0]; vf[1] = v0[d][1]; vf[2] = v0[d][2]; vf[3] = v0[d][3];
+                vf[4] = v1[d][0]; vf[5] = v1[d][1]; vf[6] = v1[d][2]; vf[7] = v1[d][3];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[j][ks], o[j][d], 0, 0, 0);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    if (myq < p.S) {
-        const float inv = 1.f / l;
-        bf16* orow = p.o + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
 #pragma unroll
-        for (int d = 0; d < DT; ++d) {
-            const int dd = d * 16 + 4 * g;
-            if (dd < p.hd) {
-                bf16x4 w;
+    for (int j = 0; j < NQ; ++j) {
+        float lj = l[j];
+        lj += __shfl_xor(lj, 16, 64);
+        lj += __shfl_xor(lj, 32, 64);
+        if (myq[j] < p.S) {
+            const float inv = 1.f / lj;
+            bf16* orow = p.o + (((int64_t)b * p.S + myq[j]) * p.H + h) * p.hd;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[d][r] * inv);
-                *(bf16x4*)(orow + dd) = w;
+            for (int d = 0; d < DT; ++d) {
+                const int dd = d * 16 + 4 * g;
+                if (dd < p.hd) {
+                    bf16x4 w;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[j][d][r] * inv);
+                    *(bf16x4*)(orow + dd) = w;
+                }
             }
+            if (g == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq[j]] = (m[j] + log2f(lj)) * 0.6931471805599453f;
         }
-        if (g == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq] = (m + log2f(l)) * 0.6931471805599453f;
     }
 }
 
@@ -506,19 +566,23 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     }
 }
 
-// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]
+// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]: one thread per (b, q, h) row, 16-B loads
+// (hd % 8 == 0; every row load of both tensors in flight at once). One wave per row with
+// a 2-B load per lane spent 38 us per call on 11 MB.
 __global__ void k_attn_delta(const bf16* __restrict__ O, const bf16* __restrict__ dO, float* __restrict__ delta,
                              int B, int H, int S, int hd) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per (b, q, h)
-    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= B * S * H) return;
     const int h = row % H, bq = row / H, q = bq % S, b = bq / S;
     const bf16* o = O + (int64_t)row * hd;
     const bf16* d = dO + (int64_t)row * hd;
     float acc = 0.f;
-    for (int i = lane; i < hd; i += 64) acc += (float)o[i] * (float)d[i];
-    acc = wave_sum(acc);
-    if (lane == 0) delta[((int64_t)b * H + h) * S + q] = acc;
+    for (int c = 0; c < hd; c += 8) {
+        const bf16x8 a = *(const bf16x8*)(o + c), g = *(const bf16x8*)(d + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += (float)a[e] * (float)g[e];
+    }
+    delta[((int64_t)b * H + h) * S + q] = acc;
 }
 
 }  // namespace
@@ -531,11 +595,17 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     KD_CHECK_SHAPE(!(d->hdp == 96 && d->hd > 80) && !(d->hdp == 64 && d->hd > 64), "attn_fwd: hd exceeds tile cover");
     AttnP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (bf16*)d->o, d->lse,
             d->B, d->H, d->HKV, d->S, d->hd, (float)(1.4426950408889634 / std::sqrt((double)d->hd))};
-    dim3 grid((d->S + 63) / 64, d->H, d->B);
+    // NQ query sub-tiles per wave (KD_ATTN_FWD_NQ=1 restores one, for A/B)
+    static const int nq = [] { const char* e = std::getenv("KD_ATTN_FWD_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
+    dim3 grid((d->S + 64 * nq - 1) / (64 * nq), d->H, d->B);
     hipStream_t st = as_stream(stream_);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem = 2 * 2 * 64 * rb;
-#define LAUNCH(HD, C) hipLaunchKernelGGL((k_attn_fwd<HD, C>), grid, dim3(256), smem, st, p)
+#define LAUNCH(HD, C)                                                                                \
+    do {                                                                                             \
+        if (nq == 2) hipLaunchKernelGGL((k_attn_fwd<HD, C, 2>), grid, dim3(256), smem, st, p);       \
+        else hipLaunchKernelGGL((k_attn_fwd<HD, C, 1>), grid, dim3(256), smem, st, p);               \
+    } while (0)
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }
     else if (d->hdp == 96) { if (d->causal) LAUNCH(96, true); else LAUNCH(96, false); }
     else { if (d->causal) LAUNCH(128, true); else LAUNCH(128, false); }
@@ -563,7 +633,7 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     hipStream_t st = as_stream(stream_);
     {
         const int rows = d->B * d->S * d->H;
-        hipLaunchKernelGGL(k_attn_delta, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16*)d->o,
+        hipLaunchKernelGGL(k_attn_delta, dim3((rows + 255) / 256), dim3(256), 0, st, (const bf16*)d->o,
                            (const bf16*)d->dO, d->delta, d->B, d->H, d->S, d->hd);
         KD_LAUNCH_CHECK("k_attn_delta");
     }

@@ -29,8 +29,18 @@ namespace {
 constexpr int NT = 256;  // threads per workgroup (row statistics, finalize)
 constexpr int NW = NT / 64;
 constexpr int RS_U = 4;  // 16-B chunks in flight per lane in k_row_stats
-constexpr int LG_NT = 1024, LG_NW = LG_NT / 64;   // k_loss_grad: one 16-wave workgroup per CU
-constexpr int LG_U = 2;  // chunk pairs in flight per lane in k_loss_grad
+#ifndef KD_LG_NT        // tuning overrides (tools/gpu_loss_cfg.sh builds variants with -D)
+#define KD_LG_NT 1024
+#endif
+#ifndef KD_LG_U
+#define KD_LG_U 2
+#endif
+#ifndef KD_LG_ROWS
+#define KD_LG_ROWS 256
+#endif
+constexpr int LG_NT = KD_LG_NT, LG_NW = LG_NT / 64;   // k_loss_grad: one 16-wave workgroup per CU
+constexpr int LG_U = KD_LG_U;      // chunk pairs in flight per lane in k_loss_grad
+constexpr int LG_ROWS = KD_LG_ROWS;   // rows in flight (workgroups) in k_loss_grad
 
 struct RowStats {
     float mt, zt;     // teacher max over [0,V_s) and sum exp((t-mt)/T)
@@ -72,12 +82,18 @@ inline Layout make_layout(int B, int L, int V) {
 __device__ __forceinline__ bool better(float a, int ia, float b, int ib) {
     return a > b || (a == b && ia < ib);
 }
+// Branch-free (selects only): the if/else-if form made hipcc keep (v1, i1, v2, i2) in a
+// scratch array indexed per lane (36 B of private memory, a scratch round trip per push
+// and per chunk test in k_row_stats' teacher loop).
 __device__ __forceinline__ void top2_push(float v, int i, float& v1, int& i1, float& v2, int& i2) {
-    if (better(v, i, v1, i1)) {
-        v2 = v1; i2 = i1; v1 = v; i1 = i;
-    } else if (better(v, i, v2, i2)) {
-        v2 = v; i2 = i;
-    }
+    const bool b1 = better(v, i, v1, i1);
+    const bool b2 = better(v, i, v2, i2);
+    const float nv2 = b1 ? v1 : (b2 ? v : v2);
+    const int ni2 = b1 ? i1 : (b2 ? i : i2);
+    v1 = b1 ? v : v1;
+    i1 = b1 ? i : i1;
+    v2 = nv2;
+    i2 = ni2;
 }
 
 // merge an online (max, sum-exp-at-invT) pair
@@ -546,7 +562,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     bf16* D_ = (bf16*)dlogits;
     // one 16-wave workgroup per CU: ~256 rows in flight, so pass B's re-read of a row (both
     // logits, 2 x 304 KB at V = 152K) is served by the 256 MB Infinity Cache, not HBM
-    const int lg_grid = rows < 256 ? rows : 256;
+    const int lg_grid = rows < LG_ROWS ? rows : LG_ROWS;
 #define KD_LAUNCH_LG(VAR)                                                                          \
     hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, \
                        V_s, rows, invT, p.clamp_min, stats, ovr, mask, kd_coef,                    \

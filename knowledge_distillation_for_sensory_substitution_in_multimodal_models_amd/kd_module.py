@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .modeling import (STUDENT_05B, TEACHER_7B, LlavaOnevisionModel, tiny_config)
+from .modeling import (STREAM_PRIORITY_HIGH, STUDENT_05B, TEACHER_7B, LlavaOnevisionModel, tiny_config)
 
 try:  # the reference's base class when installed; otherwise a minimal stand-in
     import pytorch_lightning as _pl  # noqa: F401
@@ -136,11 +136,17 @@ class _KDBase(_Base):
             self.load_kd_state_dict(state_dict)
         self.config = self.student_model.cfg
         self._anchor = nn.Parameter(torch.zeros((), device=dev))
-        self._opt_stream = torch.cuda.Stream(device=dev)
-        self._stu_stream = torch.cuda.Stream(device=dev)
+        # the step's own streams run at high priority; the teacher prefetch (off the critical
+        # path) at normal priority, so it fills the CUs the step leaves idle
+        self._opt_stream = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
+        self._stu_stream = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
         self.concurrent_student = True   # False: student forward on the main stream (bench.py --serial)
         self._opt_done = torch.cuda.Event()
         self._opt_pending = False
+        self._tch_stream = torch.cuda.Stream(device=dev, priority=0)
+        self.teacher_graphs = os.environ.get("KD_TEACHER_GRAPH", "0") == "1"   # measured slower on ROCm 7
+        self._tgraphs = {}
+        self._prefetched = None   # (batch key, teacher logits, post-LN features, event)
         self._ctx = None
         self.last_terms = None
         # data parallel
@@ -200,6 +206,88 @@ class _KDBase(_Base):
         return [opt], [sched]
 
     # ------------------------------------------------------------- the step ----
+    @staticmethod
+    def _batch_key(batch):
+        # the input tensors themselves (held, so their memory cannot be reused by another
+        # batch) and their version counters (an in-place edit invalidates the prefetch)
+        x, p, sz = batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"]
+        return (x, p, sz, x._version, p._version)
+
+    @staticmethod
+    def _same_key(k1, k2):
+        return all(a is b for a, b in zip(k1[:3], k2[:3])) and k1[3:] == k2[3:]
+
+    def _teacher_forward_eager(self, batch, need_feats):
+        tfwd = self.teacher_model.forward(batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"],
+                                          save=False, want_post_ln=need_feats)
+        t_logits = self.teacher_model.logits(tfwd["hn"])
+        del tfwd["hn"]
+        return t_logits, tfwd.get("post_ln")
+
+    def _teacher_forward(self, batch, need_feats):
+        """Teacher logits (+ post-LN vision features) for `batch` on the current stream.
+
+        The frozen teacher's forward is ~700 short host launches (~38 ms of Python + ctypes
+        per step, which left the step close to launch-bound); it is captured once per input
+        signature as a HIP graph (torch.cuda.CUDAGraph: every kernel is a libkdstep launch on
+        the capturing stream) and replayed: one launch. The inputs are copied into the
+        graph's static buffers; the outputs are the graph's static tensors (overwritten by
+        the next replay, which every consumer precedes on the stream order)."""
+        if not self.teacher_graphs:
+            return self._teacher_forward_eager(batch, need_feats)
+        ids, px, sz = batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"]
+        sizes = tuple(tuple(int(v) for v in hw) for hw in (sz.tolist() if hasattr(sz, "tolist") else sz))
+        key = (tuple(ids.shape), tuple(px.shape), px.dtype, sizes, bool(need_feats))
+        tg = self._tgraphs.get(key)
+        if tg is None:
+            out = self._teacher_forward_eager(batch, need_feats)   # warm-up: workspaces, maps, tables
+            sb = dict(batch)
+            sb["rgb_input_ids"], sb["rgb_pixel_values"] = ids.clone(), px.clone()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                logits, post = self._teacher_forward_eager(sb, need_feats)
+            self._tgraphs[key] = (g, sb["rgb_input_ids"], sb["rgb_pixel_values"], logits, post)
+            return out
+        g, s_ids, s_px, logits, post = tg
+        s_ids.copy_(ids)
+        s_px.copy_(px)
+        g.replay()
+        return logits, post
+
+    def prefetch_teacher(self, batch):
+        """Enqueue the frozen teacher's forward for `batch` (the NEXT training batch) on its own
+        stream, so it runs beside the current step's backward and optimizer; the
+        training_step that gets this batch waits on it instead of recomputing it. Optional:
+        without it the teacher runs inline. The teacher reads no student state, so the
+        result is identical either way."""
+        if not self.uses_teacher:
+            return
+        _, _, _, _, ctr_w = self._loss_spec()
+        ts = self._tch_stream
+        ts.wait_stream(torch.cuda.current_stream())   # the batch's inputs are ready
+        with torch.cuda.stream(ts):
+            t_logits, post_ln = self._teacher_forward(batch, ctr_w is not None)
+        ev = torch.cuda.Event()
+        ev.record(ts)
+        self._prefetched = (self._batch_key(batch), t_logits, post_ln, ev)
+
+    def _take_prefetched(self, batch, need_feats):
+        pf, self._prefetched = self._prefetched, None
+        if pf is None:
+            return None
+        _, t_logits, post_ln, ev = pf
+        main = torch.cuda.current_stream()
+        main.wait_event(ev)   # also when unused: an inline replay rewrites the same graph buffers
+        if not self._same_key(pf[0], self._batch_key(batch)) or (need_feats and post_ln is None):
+            return None
+        # consumed on the main stream from here on: keep the allocator from handing the
+        # blocks back to the teacher stream before those reads are done
+        if not self.teacher_graphs:
+            t_logits.record_stream(main)
+            if post_ln is not None:
+                post_ln.record_stream(main)
+        return t_logits, post_ln
+
     def forward(self, batch, train: bool = False):
         """The reference's forward(batch) (DT:206-271): total loss as a 0-d fp32 tensor."""
         variant, T, kd_w, ce_w, ctr_w = self._loss_spec()
@@ -212,23 +300,23 @@ class _KDBase(_Base):
         # student forward on its own stream beside the teacher forward. It first waits for
         # everything already queued on the main stream (so caching-allocator blocks the
         # previous step freed there are reusable) and for the previous optimizer step (the
-        # student weights); the main stream joins it before the loss.
+        # student weights); the main stream joins it before the loss. The teacher (the long
+        # pole, ~90 ms of large GEMMs that do not read student weights) is ENQUEUED first:
+        # the host spends ~20 ms launching the student's ~500 short kernels, and queued
+        # first they ran alone on the GPU while the teacher's launches waited behind them.
         side = self._stu_stream if self.concurrent_student else main
         side.wait_stream(main)
         if self._opt_pending:
             side.wait_event(self._opt_done)
             self._opt_pending = False
+        t_logits = t_post = None
+        if self.uses_teacher:
+            got = self._take_prefetched(batch, need_feats)
+            t_logits, t_post = got if got is not None else self._teacher_forward(batch, need_feats)
         with torch.cuda.stream(side):
             sfwd = s.forward(batch["depth_input_ids"], batch["depth_pixel_values"], image_sizes, save=train,
                              want_post_ln=need_feats)
             s_logits = s.logits(sfwd["hn"])
-        t_logits = None
-        tfwd = None
-        if self.uses_teacher:
-            tfwd = self.teacher_model.forward(batch["rgb_input_ids"], batch["rgb_pixel_values"], image_sizes,
-                                              save=False, want_post_ln=need_feats)
-            t_logits = self.teacher_model.logits(tfwd["hn"])
-            del tfwd["hn"]
         main.wait_stream(side)
         Vs = s_logits.shape[1]
         loss4, dlogits = ops.kd_loss_fwd_bwd(
@@ -240,7 +328,7 @@ class _KDBase(_Base):
         if need_feats:
             NI = sfwd["post_ln"].shape[0] // s.cfg.vision.n_patches
             ps = ops.row_group_mean(sfwd["post_ln"], NI, s.cfg.vision.n_patches)        # DT:243-244
-            pt = ops.row_group_mean(tfwd["post_ln"], NI, s.cfg.vision.n_patches)
+            pt = ops.row_group_mean(t_post, NI, s.cfg.vision.n_patches)
             ntx, dps = ops.ntxent(ps, pt, tau=0.07, weight=ctr_w, want_grad=train)      # DT:393-416
             total = total + ntx[0]
             self.last_ntxent = ntx

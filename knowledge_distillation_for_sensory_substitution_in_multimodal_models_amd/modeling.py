@@ -288,6 +288,11 @@ class Saved(dict):
     """Per-layer activations kept for the backward."""
 
 
+# priority of the training step's streams (lower = higher; 0 = default); the teacher
+# prefetch stream stays at 0 (KD_STREAM_PRIORITY=0 turns the distinction off)
+STREAM_PRIORITY_HIGH = int(os.environ.get("KD_STREAM_PRIORITY", "-1"))
+
+
 class WgradLane:
     """Weight-gradient work (dW GEMMs, bias column sums) on a side stream.
 
@@ -300,7 +305,7 @@ class WgradLane:
     `join` makes the current stream wait for all of it (before grads are read)."""
 
     def __init__(self, device):
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = torch.cuda.Stream(device=device, priority=STREAM_PRIORITY_HIGH)
         # split-K default for the lane's GEMMs (0 = the library's cost model, which prices a
         # GEMM as if it had the GPU to itself; 1 = never split: beside the dgrad chain an
         # unsplit 76-150-tile dW GEMM leaves the other CUs to it and skips the fp32

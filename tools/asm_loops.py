@@ -11,7 +11,7 @@ for i, l in enumerate(L):
     if not m or not pat.search(m.group(1)):
         continue
     end = i
-    while "s_endpgm" not in L[end]:
+    while not L[end].startswith(".Lfunc_end"):
         end += 1
     blocks, cur = [], ("entry", [])
     for x in L[i + 1:end]:
@@ -26,6 +26,6 @@ for i, l in enumerate(L):
     blocks.append(cur)
     for bn, ins in blocks:
         n = sum(1 for x in ins if x.startswith("v_mfma"))
-        if n >= 32:
+        if n >= int(__import__("os").environ.get("MINMFMA", "32")):
             v0 = sum(1 for x in ins if x.startswith("s_waitcnt") and "vmcnt(0)" in x)
             print(f"{m.group(1)[14:80]:66s} {bn:10s} mfma {n:4d} ins {len(ins):5d} vmcnt0 {v0}")
