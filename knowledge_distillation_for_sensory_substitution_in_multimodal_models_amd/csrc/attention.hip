@@ -311,6 +311,16 @@ __device__ __forceinline__ bf16x4 tr_read_k(const char* lds, int r, int d) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a);
 }
 
+// asm form of tr_read_k (see tr_read_asm): retired by the caller's lgkmcnt(0)
+template <int RB>
+__device__ __forceinline__ bf16x4 tr_read_k_asm(const char* lds, int r, int d) {
+    const int c = d >> 3;
+    const char* a = lds + r * RB + ((c ^ swK<RB>(r)) << 4) + ((d & 4) << 1);
+    u32x2 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)a));
+    return __builtin_bit_cast(bf16x4, v);
+}
+
 __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
     bf16x8 r;
     r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
@@ -390,13 +400,15 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
                 dp[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lO, 16 * qs + li, kk * 4 + g), vf[kk], dp[qs], 0, 0, 0);
             }
         }
+        // mask only where the tile crosses the diagonal or an edge (wave-uniform test)
+        const bool edge = q0 + 63 >= p.S || kb0 + wid * 16 + 15 >= p.S || (CAUSAL && kb0 + wid * 16 + 15 > q0);
 #pragma unroll
         for (int qs = 0; qs < 4; ++qs)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int ql = 16 * qs + 4 * g + r, q = q0 + ql;
-                float pv = exp2f(s[qs][r] * p.scale_log2 - lL[ql] * 1.4426950408889634f);
-                if (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q)) pv = 0.f;
+                float pv = __builtin_amdgcn_exp2f(fmaf(s[qs][r], p.scale_log2, -lL[ql] * 1.4426950408889634f));
+                if (edge && (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q))) pv = 0.f;
                 s[qs][r] = pv;
                 dp[qs][r] = pv * (dp[qs][r] - lD[ql]);
             }
@@ -410,13 +422,21 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
                 dsf[r] = (bf16)dp[2 * ks][r]; dsf[4 + r] = (bf16)dp[2 * ks + 1][r];
             }
             const int qr = 32 * ks + 4 * g + (li >> 2);
+            bf16x4 o0[DT], o1[DT], x0[DT], x1[DT];
 #pragma unroll
             for (int d = 0; d < DT; ++d) {
                 const int dc = d * 16 + 4 * (li & 3);
-                dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(tr_read_k<RB>(lO, qr, dc), tr_read_k<RB>(lO, qr + 16, dc)),
-                                                               pfr, dv[d], 0, 0, 0);
-                dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(tr_read_k<RB>(lQ, qr, dc), tr_read_k<RB>(lQ, qr + 16, dc)),
-                                                               dsf, dk[d], 0, 0, 0);
+                o0[d] = tr_read_k_asm<RB>(lO, qr, dc);
+                o1[d] = tr_read_k_asm<RB>(lO, qr + 16, dc);
+                x0[d] = tr_read_k_asm<RB>(lQ, qr, dc);
+                x1[d] = tr_read_k_asm<RB>(lQ, qr + 16, dc);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
+                dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(o0[d], o1[d]), pfr, dv[d], 0, 0, 0);
+                dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(x0[d], x1[d]), dsf, dk[d], 0, 0, 0);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -534,13 +554,15 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
                 dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lV, 16 * kt + li, kk * 4 + g), df[kk], dp[kt], 0, 0, 0);
             }
         }
+        const int qlo = qb * 64 + wid * 16;   // first query of this wave
+        const bool edge = qlo + 15 >= p.S || t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qlo);
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int key = t * 64 + 16 * kt + 4 * g + r;
-                float pv = exp2f(s[kt][r] * p.scale_log2 - lse2);
-                if (!qok || key >= p.S || (CAUSAL && key > myq)) pv = 0.f;
+                float pv = __builtin_amdgcn_exp2f(fmaf(s[kt][r], p.scale_log2, -lse2));
+                if (edge && (!qok || key >= p.S || (CAUSAL && key > myq))) pv = 0.f;
                 dp[kt][r] = pv * (dp[kt][r] - dl);
             }
 #pragma unroll
@@ -549,12 +571,18 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) { dsf[r] = (bf16)dp[2 * ks][r]; dsf[4 + r] = (bf16)dp[2 * ks + 1][r]; }
             const int kr = 32 * ks + 4 * g + (li >> 2);
+            bf16x4 k0[DT], k1[DT];
 #pragma unroll
             for (int d = 0; d < DT; ++d) {
                 const int dc = d * 16 + 4 * (li & 3);
-                acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(tr_read_k<RB>(lK, kr, dc), tr_read_k<RB>(lK, kr + 16, dc)),
-                                                                dsf, acc[d], 0, 0, 0);
+                k0[d] = tr_read_k_asm<RB>(lK, kr, dc);
+                k1[d] = tr_read_k_asm<RB>(lK, kr + 16, dc);
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int d = 0; d < DT; ++d)
+                acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(k0[d], k1[d]), dsf, acc[d], 0, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
