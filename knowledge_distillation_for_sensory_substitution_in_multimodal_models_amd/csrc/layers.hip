@@ -18,6 +18,8 @@
 //   sumsq               gradient norm
 #include "common.h"
 
+#include <cstdlib>
+
 namespace kd {
 namespace {
 
@@ -103,23 +105,24 @@ __global__ void __launch_bounds__(NT) k_norm_fwd(const bf16* __restrict__ x, int
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat))   (LayerNorm)
 // dx = rstd * (w*dy - xhat * mean(w*dy*xhat))                (RMSNorm, xhat = x*rstd)
 // dw/db partial sums over the rows a workgroup handles -> fp32 [gridDim.x, D].
-// One wave per row, two passes over the row (the second re-reads x/dy from L2).
-constexpr int BWD_IT = 4;  // D <= 64 lanes * 8 * BWD_IT = 2048
-template <bool RMS>
+// One wave per row; IT = ceil(D / 512) 16-B chunks per lane. The rows of a wave go through
+// a two-deep register pipeline: x, dy, the previous dx (accumulate) and the row's stats of
+// row i+1 are in flight while row i is reduced and written (one row at a time, with the
+// dx re-load after the reduction, the kernel ran at ~1.5 TB/s).
+constexpr int NW_NORM = NT / 64;   // waves per k_norm_bwd workgroup
+template <bool RMS, int IT>
 __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
                                                  const bf16* __restrict__ dy, int64_t lddy,
                                                  const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                  bf16* __restrict__ dx, int64_t lddx, int dx_accum,
                                                  float* __restrict__ dw_part, float* __restrict__ db_part,
                                                  int R, int D, int rows_per_block) {
-    extern __shared__ __attribute__((aligned(16))) float sacc[];  // [2][D] per workgroup
+    extern __shared__ __attribute__((aligned(16))) float sacc[];  // [4 waves][2][D] per workgroup
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nch = D / 8;
-    for (int i = threadIdx.x; i < 2 * D; i += NT) sacc[i] = 0.f;
-    __syncthreads();
-    float pw[BWD_IT][8], pb[BWD_IT][8], wr[BWD_IT][8];
+    float pw[IT][8], pb[IT][8], wr[IT][8];
 #pragma unroll
-    for (int it = 0; it < BWD_IT; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int c = lane + it * 64;
 #pragma unroll
         for (int j = 0; j < 8; ++j) { pw[it][j] = 0.f; pb[it][j] = 0.f; wr[it][j] = 0.f; }
@@ -127,23 +130,34 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
     }
     const int r_begin = blockIdx.x * rows_per_block;
     const int r_end = min(R, r_begin + rows_per_block);
-    for (int row = r_begin + wv; row < r_end; row += 4) {
+    struct Row { bf16x8 x[IT], g[IT], p[IT]; float mean, rstd; };
+    // every load is unconditional (row and chunk clamped into range, dx read even when not
+    // accumulated): with a data-dependent number of loads in flight hipcc can only wait
+    // vmcnt(0), which drains the next row's loads and undoes the pipeline
+    auto load = [&](Row& t, int row_) {
+        const int row = min(row_, R - 1);
         const bf16* xr = x + (int64_t)row * ldx;
         const bf16* gr = dy + (int64_t)row * lddy;
-        const float mean = RMS ? 0.f : mean_in[row], rstd = rstd_in[row];
-        bf16x8 xs[BWD_IT], gs[BWD_IT];   // the row stays in registers for the second pass
+        const bf16* pr = dx + (int64_t)row * lddx;
 #pragma unroll
-        for (int it = 0; it < BWD_IT; ++it) {
-            const int c = lane + it * 64;
-            if (c < nch) { xs[it] = *(const bf16x8*)(xr + c * 8); gs[it] = *(const bf16x8*)(gr + c * 8); }
-            else { xs[it] = (bf16x8){}; gs[it] = (bf16x8){}; }
+        for (int it = 0; it < IT; ++it) {
+            const int c = min(lane + it * 64, nch - 1);
+            t.x[it] = *(const bf16x8*)(xr + c * 8);
+            t.g[it] = *(const bf16x8*)(gr + c * 8);
+            t.p[it] = *(const bf16x8*)(pr + c * 8);
         }
+        t.mean = RMS ? 0.f : mean_in[row];
+        t.rstd = rstd_in[row];
+    };
+    auto process = [&](const Row& t, int row) {
+        const float mean = t.mean, rstd = t.rstd;
         float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-        for (int it = 0; it < BWD_IT; ++it) {
+        for (int it = 0; it < IT; ++it) {
+            if (lane + it * 64 >= nch) continue;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float xv = (float)xs[it][j], dv = (float)gs[it][j];
+                const float xv = (float)t.x[it][j], dv = (float)t.g[it][j];
                 const float xh = (xv - mean) * rstd;
                 const float g = dv * wr[it][j];
                 a1 += g;
@@ -156,39 +170,49 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
         a2 = wave_sum(a2) / D;
         bf16* dxr = dx + (int64_t)row * lddx;
 #pragma unroll
-        for (int it = 0; it < BWD_IT; ++it) {
+        for (int it = 0; it < IT; ++it) {
             const int c = lane + it * 64;
             if (c < nch) {
                 float o[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float xh = ((float)xs[it][j] - mean) * rstd;
-                    o[j] = rstd * ((float)gs[it][j] * wr[it][j] - (RMS ? 0.f : a1) - xh * a2);
-                }
-                if (dx_accum) {
-                    float prev[8];
-                    load8(dxr + c * 8, prev);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) o[j] += prev[j];
+                    const float xh = ((float)t.x[it][j] - mean) * rstd;
+                    o[j] = rstd * ((float)t.g[it][j] * wr[it][j] - (RMS ? 0.f : a1) - xh * a2);
+                    if (dx_accum) o[j] += (float)t.p[it][j];
                 }
                 store8(dxr + c * 8, o);
             }
         }
+    };
+    Row r0, r1;
+    int row = r_begin + wv;
+    load(r0, row);
+    for (; row < r_end; row += 8) {   // two rows per trip: the buffers stay compile-time named
+        load(r1, row + 4);
+        process(r0, row);
+        if (row + 4 >= r_end) break;
+        load(r0, row + 8);
+        process(r1, row + 4);
     }
+    // block sum of the 4 waves' dw/db partials: each wave stores its own [2][D] slice (16-B
+    // stores, no LDS atomics: ds_add_f32 at a 32-B lane stride was 16-way bank-conflicted),
+    // then every thread adds the 4 slices of its columns in a fixed order
+    float* mine = sacc + (size_t)wv * 2 * D;
 #pragma unroll
-    for (int it = 0; it < BWD_IT; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int c = lane + it * 64;
-        if (c < nch)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                atomicAdd(&sacc[c * 8 + j], pw[it][j]);
-                atomicAdd(&sacc[D + c * 8 + j], pb[it][j]);
-            }
+        if (c < nch) {
+            *(f32x4*)(mine + c * 8) = (f32x4){pw[it][0], pw[it][1], pw[it][2], pw[it][3]};
+            *(f32x4*)(mine + c * 8 + 4) = (f32x4){pw[it][4], pw[it][5], pw[it][6], pw[it][7]};
+            *(f32x4*)(mine + D + c * 8) = (f32x4){pb[it][0], pb[it][1], pb[it][2], pb[it][3]};
+            *(f32x4*)(mine + D + c * 8 + 4) = (f32x4){pb[it][4], pb[it][5], pb[it][6], pb[it][7]};
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < D; i += NT) {
-        if (dw_part) dw_part[(int64_t)blockIdx.x * D + i] = sacc[i];
-        if (db_part) db_part[(int64_t)blockIdx.x * D + i] = sacc[D + i];
+        if (dw_part) dw_part[(int64_t)blockIdx.x * D + i] = ((sacc[i] + sacc[2 * D + i]) + sacc[4 * D + i]) + sacc[6 * D + i];
+        if (db_part)
+            db_part[(int64_t)blockIdx.x * D + i] = ((sacc[D + i] + sacc[3 * D + i]) + sacc[5 * D + i]) + sacc[7 * D + i];
     }
 }
 
@@ -683,7 +707,10 @@ int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const vo
 }
 
 // workgroups of k_norm_bwd: ~8 rows each (2 per wave), at most 512 (2 per CU)
-static int norm_bwd_blocks(int R) { return std::max(1, std::min(512, (R + 7) / 8)); }
+static int norm_bwd_blocks(int R) {
+    static const int cap = [] { const char* e = std::getenv("KD_NORM_BWD_BLOCKS"); return e ? std::atoi(e) : 512; }();
+    return std::max(1, std::min(cap, (R + 7) / 8));
+}
 
 size_t norm_bwd_ws(int R, int D) {
     return (size_t)norm_bwd_blocks(R) * D * 4 * 2;
@@ -700,13 +727,18 @@ int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const vo
     float* dwp = (float*)ws;
     float* dbp = dwp + (size_t)nb * D;
     hipStream_t st = as_stream(stream);
-    const size_t smem = 2 * D * 4;
-    if (rms) hipLaunchKernelGGL(k_norm_bwd<true>, dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx, (const bf16*)w,
-                                (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,
-                                nullptr, R, D, rows_per);
-    else hipLaunchKernelGGL(k_norm_bwd<false>, dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx, (const bf16*)w,
-                            (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,
-                            db ? dbp : nullptr, R, D, rows_per);
+    const size_t smem = (size_t)NW_NORM * 2 * D * 4;
+#define KD_NB(RMSV, ITV)                                                                                        \
+    hipLaunchKernelGGL((k_norm_bwd<RMSV, ITV>), dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx, (const bf16*)w,    \
+                       (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,              \
+                       (RMSV || !db) ? nullptr : dbp, R, D, rows_per)
+    const int it = (D + 511) / 512;
+    if (rms) {
+        if (it == 1) KD_NB(true, 1); else if (it == 2) KD_NB(true, 2); else if (it == 3) KD_NB(true, 3); else KD_NB(true, 4);
+    } else {
+        if (it == 1) KD_NB(false, 1); else if (it == 2) KD_NB(false, 2); else if (it == 3) KD_NB(false, 3); else KD_NB(false, 4);
+    }
+#undef KD_NB
     KD_LAUNCH_CHECK("k_norm_bwd");
     if (dw) hipLaunchKernelGGL(k_reduce_parts, dim3((D + RP_C - 1) / RP_C), dim3(1024), 0, st, dwp, nb, D, dw, accum_w);
     if (db) hipLaunchKernelGGL(k_reduce_parts, dim3((D + RP_C - 1) / RP_C), dim3(1024), 0, st, dbp, nb, D, db, accum_w);
