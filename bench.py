@@ -224,7 +224,7 @@ def main():
     tf_sample = step_tflops_per_sample(cfg["kind"], cfg["phase"])
     roof = None
     br = {}
-    for kind in ("gemm_kk", "gemm_kn", "gemm_nn"):
+    for kind in ("gemm_kk_swiglu", "gemm_kk", "gemm_kn", "gemm_nn"):
         s = ops.TIMER.summary(kind)
         if s:
             br[kind] = dict(launches=s["launches"], avg_us=round(s["avg_ms"] * 1e3, 2),
@@ -233,17 +233,20 @@ def main():
     if a.shapes and rank == 0 and ops.TIMER.records:
         with open(a.shapes, "w") as f:
             json.dump(ops.TIMER.by_shape(top=200), f, indent=1)
-    fwd = ops.TIMER.summary("gemm_kk")
+    # the roofline kernel: the fused gate|up + SwiGLU GEMM (k_gemm8<K-major,K-major> SwiGLU build,
+    # one launch per call, 28 + 24 calls per step, ~40% of the step's GEMM time) -- a kernel of
+    # its own, so the rocprofv3 kernel trace's average for it is directly comparable
+    fwd = ops.TIMER.summary("gemm_kk_swiglu")
     traffic = None   # PMC HBM bytes per forward-GEMM launch (tools/pmc_bench.sh, committed under profiles/)
     tpath = REPO / "profiles" / "r01" / "pmc_traffic.json"
     if tpath.exists():
-        fg = json.load(open(tpath)).get("forward_gemm")
+        fg = json.load(open(tpath)).get("roofline_kernel")
         if fg:
             traffic = round(fg["traffic_bytes"])
     if fwd:
         ach = fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12
-        roof = dict(bound="mfma", kernel="k_gemm<K-major,K-major> (forward bf16 GEMM: every nn.Linear of teacher "
-                                           "and student forward)",
+        roof = dict(bound="mfma", kernel="k_gemm8<false, false, 4> (fused gate|up GEMM + SwiGLU epilogue of every "
+                                           "teacher and student MLP, bf16)",
                     achieved=round(ach, 1), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s", frac=round(ach / PEAK_BF16_TFLOPS, 4),
                     traffic=traffic, traffic_unit="bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                    "profiles/r01/pmc_traffic.json)",

@@ -667,7 +667,9 @@ __device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, i
     }
 }
 
-// EXP (diagnostic variants 17-19 only; production = 0): bit 0 writes per-wave s_memtime
+// EXP: bit 2 = the fused SwiGLU build (KD_ACT_SWIGLU: gathered gate|up B rows, GLU epilogue;
+// its own kernel, so its launches are exactly the gate|up GEMMs in a kernel trace; the
+// production non-GLU build carries no GLU code). Diagnostic variants 17-19 only: bit 0 writes per-wave s_memtime
 // cycle totals (step-end sync, MFMA units, prologue, epilogue) as uint32 to p.aux (which
 // then carries no pre-activation output); bit 1 drops the in-loop DMA (timing ablation:
 // WRONG results); bit 6 re-reads stage 0 for every stage (same addresses, L2-hot:
@@ -698,7 +700,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
     const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (A_MN ? 0 : (int64_t)m0 * p.lda), A_MN ? 0u : rec_bytes(min(256, p.M - m0), p.lda));
-    const bool glu = !B_MN && p.glu != 0;   // gate rows [nb, nb+128) and up rows [I+nb, I+nb+128)
+    constexpr bool glu = !B_MN && (EXP & 4);   // gate rows [nb, nb+128) and up rows [I+nb, I+nb+128)
     const int nb = tn * 128;
     const __amdgpu_buffer_rsrc_t rsBk =
         glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
@@ -1169,7 +1171,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         pk.glu = d->N / 2; pk.act = KD_ACT_NONE;
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
-        else hipLaunchKernelGGL((k_gemm8<false, false, 0>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
         return KD_OK;
     }

@@ -230,7 +230,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
         e0.record()
         NV.call("kd_gemm", C.byref(d), _stream())
         e1.record()
-        kind = f"gemm_{'kn'[la]}{'kn'[lb]}"
+        kind = "gemm_kk_swiglu" if act == "swiglu" else f"gemm_{'kn'[la]}{'kn'[lb]}"
         TIMER.records.append((kind, 2.0 * M * N * K, e0, e1,
                               f"{kind}:{M}x{N}x{K}:{'f32' if out.dtype == torch.float32 else 'bf16'}"
                               f"{':acc' if accumulate else ''}"))

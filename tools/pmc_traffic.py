@@ -30,8 +30,8 @@ def short(n):
     return n.replace("kd::(anonymous namespace)::", "").split("(")[0][:100]
 
 
-def is_fwd_gemm(n):   # the K-major x K-major GEMM kernels: v8 production build and v3 tiles
-    return "k_gemm8<false, false, 0>" in n or ("k_gemm3<" in n and ", false, false, 4>" in n)
+def is_roofline_kernel(n):   # bench.py's roofline kernel: the fused gate|up + SwiGLU GEMM (v8 GLU build)
+    return "k_gemm8<false, false, 4>" in n
 
 
 fetch, write = load("p1", "FETCH_SIZE"), load("p2", "WRITE_SIZE")
@@ -45,11 +45,11 @@ for n in sorted(set(fetch) | set(write)):
     e["launches"] = max(len(f), len(w))
     e["fetch_bytes"] = 2.0 * sum(f) / max(len(f), 1)
     e["write_bytes"] = sum(w) / max(len(w), 1)
-    if is_fwd_gemm(n):
+    if is_roofline_kernel(n):
         fw_f += f
         fw_w += w
 if fw_f:
     fb = 2.0 * sum(fw_f) / len(fw_f)
     wb = sum(fw_w) / max(len(fw_w), 1)
-    out["forward_gemm"] = dict(launches=len(fw_f), fetch_bytes=fb, write_bytes=wb, traffic_bytes=fb + wb)
+    out["roofline_kernel"] = dict(launches=len(fw_f), fetch_bytes=fb, write_bytes=wb, traffic_bytes=fb + wb)
 json.dump(out, sys.stdout, indent=1)
