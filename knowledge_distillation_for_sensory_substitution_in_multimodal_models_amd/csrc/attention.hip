@@ -494,41 +494,51 @@ __global__ void k_attn_group_sum(const float* __restrict__ dkp, const float* __r
     }
 }
 
-// dQ for 64 query rows of one head (4 waves x 16 rows, query on the lane), the forward's
-// structure: K / V tiles double-buffered through LDS-DMA, S^T = K Q^T and dP^T = V dO^T
-// recomputed, dS^T in registers feeds dQ^T += K^T dS^T (A = transposed K reads).
+// dQ for 64·NQ query rows of one head (4 waves x NQ sub-tiles of 16 rows, query on the
+// lane), the forward's structure: K / V tiles double-buffered through LDS-DMA, S^T = K Q^T
+// and dP^T = V dO^T recomputed, dS^T in registers feeds dQ^T += K^T dS^T (A = transposed K
+// reads). Every K / V / K^T fragment read from LDS feeds the NQ sub-tiles.
 // No atomics: each workgroup owns its rows of dQ.
-template <int HDP, bool CAUSAL>
+template <int HDP, bool CAUSAL, int NQ>
 __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
     constexpr int TILE = 64 * RB;
+    constexpr int QBLK = 64 * NQ;
     extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][K TILE | V TILE]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = lane >> 4, li = lane & 15;
-    const int nqb = (p.S + 63) / 64;
+    const int nqb = (p.S + QBLK - 1) / QBLK;
     const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
     const int h = blockIdx.y, b = blockIdx.z, kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const int myq = qb * 64 + wid * 16 + li;
-    const bool qok = myq < p.S;
-
-    bf16x8 qf[KS], df[KS];
-    const bf16* dOr = p.dO + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
+    int myq[NQ];
+    bool qok[NQ];
+    bf16x8 qf[NQ][KS], df[NQ][KS];
+    float lse2[NQ], dl[NQ];
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-        const int d0 = kk * 32 + 8 * g;
-        qf[kk] = qok ? *(const bf16x8*)(Q + (int64_t)myq * HDP + d0) : (bf16x8){};
-        df[kk] = (qok && d0 < p.hd) ? *(const bf16x8*)(dOr + d0) : (bf16x8){};
+    for (int j = 0; j < NQ; ++j) {
+        myq[j] = qb * QBLK + wid * 16 * NQ + j * 16 + li;
+        qok[j] = myq[j] < p.S;
+        const bf16* dOr = p.dO + (((int64_t)b * p.S + myq[j]) * p.H + h) * p.hd;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            const int d0 = kk * 32 + 8 * g;
+            qf[j][kk] = qok[j] ? *(const bf16x8*)(Q + (int64_t)myq[j] * HDP + d0) : (bf16x8){};
+            df[j][kk] = (qok[j] && d0 < p.hd) ? *(const bf16x8*)(dOr + d0) : (bf16x8){};
+        }
+        lse2[j] = qok[j] ? p.lse[((int64_t)b * p.H + h) * p.S + myq[j]] * 1.4426950408889634f : 0.f;
+        dl[j] = qok[j] ? p.delta[((int64_t)b * p.H + h) * p.S + myq[j]] : 0.f;
     }
-    const float lse2 = qok ? p.lse[((int64_t)b * p.H + h) * p.S + myq] * 1.4426950408889634f : 0.f;
-    const float dl = qok ? p.delta[((int64_t)b * p.H + h) * p.S + myq] : 0.f;
-    f32x4 acc[DT];
+    f32x4 acc[NQ][DT];
 #pragma unroll
-    for (int d = 0; d < DT; ++d) acc[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NQ; ++j)
+#pragma unroll
+        for (int d = 0; d < DT; ++d) acc[j][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    const int nkv = CAUSAL ? min(qb + 1, nqb) : nqb;
+    const int nkv_all = (p.S + 63) / 64;
+    const int nkv = CAUSAL ? min((qb + 1) * QBLK / 64, nkv_all) : nkv_all;
     stage_kv<HDP, false>(smem, K, 0, p.S, wid, lane);
     stage_kv<HDP, false>(smem + TILE, V, 0, p.S, wid, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -542,34 +552,44 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
         }
         const char* lK = smem + cur * 2 * TILE;
         const char* lV = lK + TILE;
-        // S^T, dP^T tiles: rows = keys 16kt + 4g + r, col = my query
-        f32x4 s[4], dp[4];
+        // S^T, dP^T tiles: rows = keys 16kt + 4g + r, col = the lane's query of sub-tile j
+        f32x4 sc[NQ][4], dp[NQ][4];
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
-            s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-            dp[kt] = s[kt];
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) { sc[j][kt] = (f32x4){0.f, 0.f, 0.f, 0.f}; dp[j][kt] = sc[j][kt]; }
 #pragma unroll
             for (int kk = 0; kk < KS; ++kk) {
-                s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lK, 16 * kt + li, kk * 4 + g), qf[kk], s[kt], 0, 0, 0);
-                dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lV, 16 * kt + li, kk * 4 + g), df[kk], dp[kt], 0, 0, 0);
+                const bf16x8 kf = k_frag<RB>(lK, 16 * kt + li, kk * 4 + g);
+                const bf16x8 vf = k_frag<RB>(lV, 16 * kt + li, kk * 4 + g);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[j][kk], sc[j][kt], 0, 0, 0);
+                    dp[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[j][kk], dp[j][kt], 0, 0, 0);
+                }
             }
         }
-        const int qlo = qb * 64 + wid * 16;   // first query of this wave
-        const bool edge = qlo + 15 >= p.S || t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qlo);
+        bf16x8 dsf[NQ][2];
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int j = 0; j < NQ; ++j) {
+            const int qlo = qb * QBLK + wid * 16 * NQ + j * 16;   // first query of this sub-tile
+            const bool edge = qlo + 15 >= p.S || t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qlo);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int key = t * 64 + 16 * kt + 4 * g + r;
-                float pv = __builtin_amdgcn_exp2f(fmaf(s[kt][r], p.scale_log2, -lse2));
-                if (edge && (!qok || key >= p.S || (CAUSAL && key > myq))) pv = 0.f;
-                dp[kt][r] = pv * (dp[kt][r] - dl);
-            }
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = t * 64 + 16 * kt + 4 * g + r;
+                    float pv = __builtin_amdgcn_exp2f(fmaf(sc[j][kt][r], p.scale_log2, -lse2[j]));
+                    if (edge && (!qok[j] || key >= p.S || (CAUSAL && key > myq[j]))) pv = 0.f;
+                    dp[j][kt][r] = pv * (dp[j][kt][r] - dl[j]);
+                }
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { dsf[j][ks][r] = (bf16)dp[j][2 * ks][r]; dsf[j][ks][4 + r] = (bf16)dp[j][2 * ks + 1][r]; }
+        }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            bf16x8 dsf;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { dsf[r] = (bf16)dp[2 * ks][r]; dsf[4 + r] = (bf16)dp[2 * ks + 1][r]; }
             const int kr = 32 * ks + 4 * g + (li >> 2);
             bf16x4 k0[DT], k1[DT];
 #pragma unroll
@@ -581,17 +601,22 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int d = 0; d < DT; ++d)
-                acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat4(k0[d], k1[d]), dsf, acc[d], 0, 0, 0);
+            for (int d = 0; d < DT; ++d) {
+                const bf16x8 kt8 = cat4(k0[d], k1[d]);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) acc[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt8, dsf[j][ks], acc[j][d], 0, 0, 0);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    if (qok) {
-        float* dQr = p.dq + ((int64_t)(b * p.H + h) * p.S + myq) * HDP;
 #pragma unroll
-        for (int d = 0; d < DT; ++d) *(f32x4*)(dQr + d * 16 + 4 * g) = acc[d] * p.scale;
-    }
+    for (int j = 0; j < NQ; ++j)
+        if (qok[j]) {
+            float* dQr = p.dq + ((int64_t)(b * p.H + h) * p.S + myq[j]) * HDP;
+#pragma unroll
+            for (int d = 0; d < DT; ++d) *(f32x4*)(dQr + d * 16 + 4 * g) = acc[j][d] * p.scale;
+        }
 }
 
 // delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]: one thread per (b, q, h) row, 16-B loads
@@ -672,6 +697,8 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
                (float)(sc * 1.4426950408889634)};
     dim3 grid((d->S + 63) / 64, d->H, d->B);
+    static const int nq_dq = [] { const char* e = std::getenv("KD_ATTN_DQ_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
+    dim3 grid_q((d->S + 64 * nq_dq - 1) / (64 * nq_dq), d->H, d->B);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem_kv = 2 * (2 * 64 * rb + 512);
     const size_t smem_q = 2 * 2 * 64 * rb;
@@ -679,7 +706,8 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     do {                                                                                      \
         hipLaunchKernelGGL((k_attn_bwd_dkdv<HD, C>), grid, dim3(256), smem_kv, st, p);       \
         KD_LAUNCH_CHECK("k_attn_bwd_dkdv");                                                   \
-        hipLaunchKernelGGL((k_attn_bwd_dq<HD, C>), grid, dim3(256), smem_q, st, p);          \
+        if (nq_dq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p); \
+        else hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 1>), grid_q, dim3(256), smem_q, st, p);            \
         KD_LAUNCH_CHECK("k_attn_bwd_dq");                                                     \
     } while (0)
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }
