@@ -244,6 +244,18 @@ int kd_adamw(float* param, void* param_bf16, const float* grad, float* exp_avg, 
 int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 
+/* ------------------------------------------------------ depth transform ---- */
+/* Depth image -> 3-channel uint8 image (normalised depth, Prewitt gradient magnitude,
+ * Prewitt gradient angle), replacing CustomSUNRGBDDatasetOneVision.
+ * convert_depth_image_into_3D (dataset/dataloader/OneVision/CustomSUNRGBDDatasetOneVision.py:64-112:
+ * per-image min/max normalisation to uint8, scipy.ndimage.convolve with the Prewitt kernels in
+ * mode='reflect', sqrt / arctan2, safe_normalize to uint8, np.dstack).
+ * depth: [B, H, W] of dtype 0 = uint16 (the PNG's 16-bit samples), 1 = int32 (PIL mode "I"),
+ * 2 = float32; out: [B, H, W, 3] uint8.  Each image is normalised by its own range. */
+size_t kd_depth_to_3ch_workspace_size(int B, int H, int W);
+int kd_depth_to_3ch(const void* depth, int dtype, int B, int H, int W, uint8_t* out, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,6 +120,8 @@ SIGNATURES = {
     "kd_adamw": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
     "kd_sumsq": (_i32, [_vp, _i64, _vp, _vp]),
     "kd_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
+    "kd_depth_to_3ch_workspace_size": (_sz, [_i32, _i32, _i32]),
+    "kd_depth_to_3ch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp]),
 }
 
 _lib = None

@@ -55,6 +55,9 @@ int launch_sumsq(const float* x, int64_t n, float* out, void* stream);
 int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, const int* map, int map_ld,
                          const int* map_len, int* src, int* err, void* stream);
 int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+size_t depth3_ws(int B, int H, int W);
+int launch_depth3(const void* depth, int dtype, int B, int H, int W, void* out, void* ws, size_t ws_bytes,
+                  void* stream);
 
 }  // namespace kd
 
@@ -150,5 +153,10 @@ int kd_image_src_map(const int64_t* ids, int B, int L, int64_t tok, const int32_
     return kd::launch_image_src_map(ids, B, L, tok, map, ld, len, src, err, s);
 }
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* s) { return kd::launch_cast_f32_bf16(x, y, n, s); }
+size_t kd_depth_to_3ch_workspace_size(int B, int H, int W) { return kd::depth3_ws(B, H, W); }
+int kd_depth_to_3ch(const void* depth, int dtype, int B, int H, int W, uint8_t* out, void* ws, size_t ws_bytes,
+                    void* s) {
+    return kd::launch_depth3(depth, dtype, B, H, W, out, ws, ws_bytes, s);
+}
 
 }  // extern "C"

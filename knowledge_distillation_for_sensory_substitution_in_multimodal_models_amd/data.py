@@ -45,3 +45,38 @@ def synthetic_batch(B: int, device, L: int = 1536, image_hw=(336, 336), seed: in
         "labels": ids.clone(),
         "question_id": question_id,
     }
+
+
+def convert_depth_image_into_3D(depth_image, device="cuda") -> torch.Tensor:
+    """GPU counterpart of CustomSUNRGBDDatasetOneVision.convert_depth_image_into_3D
+    (dataset/dataloader/OneVision/CustomSUNRGBDDatasetOneVision.py:64-112).
+
+    `depth_image` is a path to the depth PNG (read as PIL mode "I", DS:86) or an [H, W]
+    array / tensor of depth samples.  Returns the uint8 [H, W, 3] image (normalised depth,
+    Prewitt magnitude, Prewitt angle) on `device` — what __getitem__ holds as
+    `np.array(depth_image)` (DS:194-195).  Every pixel is computed by kd_depth_to_3ch."""
+    from . import ops
+    if isinstance(depth_image, (str, bytes)) or hasattr(depth_image, "__fspath__"):
+        from PIL import Image
+        import numpy as np
+        depth_image = np.array(Image.open(depth_image).convert("I"))      # int32, DS:86
+    t = depth_image if isinstance(depth_image, torch.Tensor) else torch.from_numpy(depth_image)
+    if t.dtype not in (torch.uint16, torch.int32, torch.float32):
+        t = t.to(torch.int32) if not t.is_floating_point() else t.to(torch.float32)
+    return ops.depth_to_3ch(t.to(device, non_blocking=True))
+
+
+def convert_depth_batch(depth_images, device="cuda") -> list:
+    """A list of [H, W] depth maps (ragged sizes allowed) -> list of uint8 [H, W, 3] device
+    tensors; maps of equal size share one batched launch."""
+    from . import ops
+    ts = [d if isinstance(d, torch.Tensor) else torch.from_numpy(d) for d in depth_images]
+    out: list = [None] * len(ts)
+    groups: dict = {}
+    for i, t in enumerate(ts):
+        groups.setdefault((tuple(t.shape), t.dtype), []).append(i)
+    for (_, _), idx in groups.items():
+        y = ops.depth_to_3ch(torch.stack([ts[i] for i in idx]).to(device, non_blocking=True))
+        for k, i in enumerate(idx):
+            out[i] = y[k]
+    return out

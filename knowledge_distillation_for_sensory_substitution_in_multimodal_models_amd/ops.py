@@ -420,3 +420,29 @@ def image_src_map(ids, image_token: int, maps, map_len, err):
     NV.call("kd_image_src_map", ids.contiguous().data_ptr(), B, L, int(image_token), maps.data_ptr(), maps.shape[1],
             map_len.data_ptr(), src.data_ptr(), err.data_ptr(), _stream())
     return src
+
+
+_DEPTH_DTYPES = {torch.uint16: 0, torch.int32: 1, torch.float32: 2}
+
+
+def depth_to_3ch(depth: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """depth [B, H, W] or [H, W] (uint16 / int32 / float32, device) -> uint8 [..., H, W, 3]
+    (kd_depth_to_3ch: normalised depth, Prewitt magnitude, Prewitt angle; each image
+    normalised by its own range)."""
+    if not depth.is_cuda:
+        raise RuntimeError("depth_to_3ch: expected a device tensor (no CPU path)")
+    if depth.dtype not in _DEPTH_DTYPES:
+        raise RuntimeError(f"depth_to_3ch: dtype {depth.dtype} not in uint16/int32/float32")
+    if depth.dim() not in (2, 3):
+        raise RuntimeError(f"depth_to_3ch: expected [H, W] or [B, H, W], got {tuple(depth.shape)}")
+    d = depth.contiguous()
+    B, H, W = (1, *d.shape) if d.dim() == 2 else d.shape
+    if out is None:
+        out = torch.empty((*d.shape, 3), dtype=torch.uint8, device=d.device)
+    elif out.shape != (*d.shape, 3) or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise RuntimeError("depth_to_3ch: out must be a contiguous uint8 [..., H, W, 3] tensor")
+    nbytes = NV.lib().kd_depth_to_3ch_workspace_size(B, H, W)
+    ws = _workspace(("depth3", _stream()), nbytes, d.device)
+    NV.call("kd_depth_to_3ch", d.data_ptr(), _DEPTH_DTYPES[d.dtype], B, H, W, out.data_ptr(), ws.data_ptr(),
+            ws.numel(), _stream())
+    return out
