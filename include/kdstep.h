@@ -256,6 +256,25 @@ size_t kd_depth_to_3ch_workspace_size(int B, int H, int W);
 int kd_depth_to_3ch(const void* depth, int dtype, int B, int H, int W, uint8_t* out, void* workspace,
                     size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------ image preprocessing ---- */
+/* The image half of the reference's collate_fn (DM:124-146, the LLaVA-OneVision processor on the
+ * RGB / 3-channel depth uint8 images = transformers LlavaOnevisionImageProcessor._preprocess,
+ * PIL backend).
+ * kd_image_resize_u8: PIL Image.resize((out_w, out_h), BICUBIC) of an [H, W, 3] uint8 image
+ *   (Pillow libImaging/Resample.c: int32 taps with 22 fraction bits, horizontal then vertical
+ *   8-bit pass), bit-exact.  Same size = copy.  Downscale factor <= 15.
+ * kd_anyres_tiles: pixel_values [n_out, 3, patch, patch] (float32 or bf16) of one image:
+ *   tile 0 from `base` (the image resized to patch x patch), tiles 1..(bh/patch)*(bw/patch) cut
+ *   from the (bh, bw) canvas holding `resized` ([nh, nw, 3], the aspect-preserving resize)
+ *   centred on zeros (get_image_patches / _pad_for_patching / divide_to_patches), rescaled by
+ *   1/255 and normalised with mean_std_host = {mean[3], std[3]}; tiles past the image's own
+ *   count are zero (_pad_for_batching).  out_dtype: 0 = float32, 1 = bf16. */
+size_t kd_image_resize_workspace_size(int H, int W, int out_h, int out_w);
+int kd_image_resize_u8(const uint8_t* in, int H, int W, uint8_t* out, int out_h, int out_w, void* workspace,
+                       size_t workspace_bytes, void* stream);
+int kd_anyres_tiles(const uint8_t* base, const uint8_t* resized, int nh, int nw, int bh, int bw, int patch,
+                    int n_out, const float* mean_std_host, void* out, int out_dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

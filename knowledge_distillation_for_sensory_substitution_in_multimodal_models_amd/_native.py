@@ -122,6 +122,9 @@ SIGNATURES = {
     "kd_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
     "kd_depth_to_3ch_workspace_size": (_sz, [_i32, _i32, _i32]),
     "kd_depth_to_3ch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp]),
+    "kd_image_resize_workspace_size": (_sz, [_i32, _i32, _i32, _i32]),
+    "kd_image_resize_u8": (_i32, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _sz, _vp]),
+    "kd_anyres_tiles": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp]),
 }
 
 _lib = None

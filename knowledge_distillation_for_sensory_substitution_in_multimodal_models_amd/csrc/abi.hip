@@ -56,6 +56,11 @@ int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, 
                          const int* map_len, int* src, int* err, void* stream);
 int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 size_t depth3_ws(int B, int H, int W);
+size_t image_resize_ws(int H, int W, int oh, int ow);
+int launch_image_resize(const uint8_t* in, int H, int W, uint8_t* out, int oh, int ow, void* ws, size_t ws_bytes,
+                        void* stream);
+int launch_anyres_tiles(const uint8_t* base, const uint8_t* resized, int nh, int nw, int bh, int bw, int patch,
+                        int n_out, const float* mean_std_host, void* out, int out_dtype, void* stream);
 int launch_depth3(const void* depth, int dtype, int B, int H, int W, void* out, void* ws, size_t ws_bytes,
                   void* stream);
 
@@ -157,6 +162,15 @@ size_t kd_depth_to_3ch_workspace_size(int B, int H, int W) { return kd::depth3_w
 int kd_depth_to_3ch(const void* depth, int dtype, int B, int H, int W, uint8_t* out, void* ws, size_t ws_bytes,
                     void* s) {
     return kd::launch_depth3(depth, dtype, B, H, W, out, ws, ws_bytes, s);
+}
+size_t kd_image_resize_workspace_size(int H, int W, int oh, int ow) { return kd::image_resize_ws(H, W, oh, ow); }
+int kd_image_resize_u8(const uint8_t* in, int H, int W, uint8_t* out, int oh, int ow, void* ws, size_t ws_bytes,
+                       void* s) {
+    return kd::launch_image_resize(in, H, W, out, oh, ow, ws, ws_bytes, s);
+}
+int kd_anyres_tiles(const uint8_t* base, const uint8_t* resized, int nh, int nw, int bh, int bw, int patch, int n_out,
+                    const float* mean_std_host, void* out, int out_dtype, void* s) {
+    return kd::launch_anyres_tiles(base, resized, nh, nw, bh, bw, patch, n_out, mean_std_host, out, out_dtype, s);
 }
 
 }  // extern "C"

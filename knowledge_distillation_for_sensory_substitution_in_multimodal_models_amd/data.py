@@ -80,3 +80,42 @@ def convert_depth_batch(depth_images, device="cuda") -> list:
         for k, i in enumerate(idx):
             out[i] = y[k]
     return out
+
+
+SIGLIP_MEAN = SIGLIP_STD = (0.5, 0.5, 0.5)   # image_mean / image_std of the llava-onevision-*-ov-hf checkpoints
+
+
+def patch_output_size(h: int, w: int, th: int, tw: int):
+    """transformers get_patch_output_size: aspect-preserving size inside (th, tw)."""
+    import math
+    sw, sh = tw / w, th / h
+    if sw < sh:
+        return min(math.ceil(h * sw), th), tw
+    return th, min(math.ceil(w * sh), tw)
+
+
+def process_images(images, device="cuda", image_mean=SIGLIP_MEAN, image_std=SIGLIP_STD,
+                   dtype=torch.float32, patch: int = 384, pinpoints=anyres.DEFAULT_PINPOINTS) -> dict:
+    """GPU counterpart of the image half of the processor call in the reference's collate_fn
+    (DM:124-146; transformers LlavaOnevisionImageProcessor._preprocess): a list of [H, W, 3]
+    uint8 images (numpy or tensors; RGB, or the 3-channel depth image) ->
+    {"pixel_values": [B, P_max, 3, patch, patch] (dtype), "image_sizes": [B, 2] int64}.
+    The plan (best pinpoint resolution, resize sizes) is host arithmetic on the image sizes;
+    every pixel is computed by kd_image_resize_u8 / kd_anyres_tiles."""
+    from . import ops
+    ims = [(i if isinstance(i, torch.Tensor) else torch.from_numpy(i)).to(device, non_blocking=True) for i in images]
+    plans = []
+    for im in ims:
+        if im.dtype != torch.uint8 or im.dim() != 3 or im.shape[2] != 3:
+            raise RuntimeError(f"process_images: expected uint8 [H, W, 3], got {im.dtype} {tuple(im.shape)}")
+        H, W = int(im.shape[0]), int(im.shape[1])
+        bh, bw = anyres.select_best_resolution((H, W), pinpoints)
+        plans.append((H, W, bh, bw, patch_output_size(H, W, bh, bw)))
+    p_max = max(1 + (bh // patch) * (bw // patch) for _, _, bh, bw, _ in plans)
+    pv = torch.empty((len(ims), p_max, 3, patch, patch), dtype=dtype, device=ims[0].device)
+    for b, (im, (H, W, bh, bw, (nh, nw))) in enumerate(zip(ims, plans)):
+        resized = ops.image_resize_u8(im, nh, nw)                    # _resize_for_patching
+        base = ops.image_resize_u8(im, patch, patch)                 # resized_original_image
+        ops.anyres_tiles(base, resized, (bh, bw), p_max, image_mean, image_std, dtype=dtype, patch=patch, out=pv[b])
+    sizes = torch.tensor([[H, W] for H, W, *_ in plans], dtype=torch.int64)
+    return {"pixel_values": pv, "image_sizes": sizes}

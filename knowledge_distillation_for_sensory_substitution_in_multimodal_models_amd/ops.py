@@ -446,3 +446,40 @@ def depth_to_3ch(depth: torch.Tensor, out: torch.Tensor | None = None) -> torch.
     NV.call("kd_depth_to_3ch", d.data_ptr(), _DEPTH_DTYPES[d.dtype], B, H, W, out.data_ptr(), ws.data_ptr(),
             ws.numel(), _stream())
     return out
+
+
+def image_resize_u8(img: torch.Tensor, out_h: int, out_w: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """[H, W, 3] uint8 (device) -> [out_h, out_w, 3] uint8: PIL Image.resize(BICUBIC), bit-exact
+    (kd_image_resize_u8)."""
+    _require(img, torch.uint8, "image_resize_u8")
+    if img.dim() != 3 or img.shape[2] != 3:
+        raise RuntimeError(f"image_resize_u8: expected [H, W, 3], got {tuple(img.shape)}")
+    x = img.contiguous()
+    H, W = int(x.shape[0]), int(x.shape[1])
+    if out is None:
+        out = torch.empty((out_h, out_w, 3), dtype=torch.uint8, device=x.device)
+    nbytes = NV.lib().kd_image_resize_workspace_size(H, W, out_h, out_w)
+    ws = _workspace(("image_resize", _stream()), nbytes, x.device)
+    NV.call("kd_image_resize_u8", x.data_ptr(), H, W, out.data_ptr(), int(out_h), int(out_w), ws.data_ptr(),
+            ws.numel(), _stream())
+    return out
+
+
+def anyres_tiles(base: torch.Tensor, resized: torch.Tensor, best_hw, n_out: int, mean, std,
+                 dtype=torch.float32, patch: int = 384, out: torch.Tensor | None = None) -> torch.Tensor:
+    """pixel_values [n_out, 3, patch, patch] of one image from its base resize and its
+    aspect-preserving resize (kd_anyres_tiles)."""
+    _require(base, torch.uint8, "anyres_tiles")
+    _require(resized, torch.uint8, "anyres_tiles")
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise RuntimeError(f"anyres_tiles: dtype {dtype} not float32/bfloat16")
+    if tuple(base.shape) != (patch, patch, 3):
+        raise RuntimeError(f"anyres_tiles: base must be [{patch}, {patch}, 3], got {tuple(base.shape)}")
+    bh, bw = int(best_hw[0]), int(best_hw[1])
+    nh, nw = int(resized.shape[0]), int(resized.shape[1])
+    if out is None:
+        out = torch.empty((n_out, 3, patch, patch), dtype=dtype, device=base.device)
+    ms = (C.c_float * 6)(*[float(v) for v in mean], *[float(v) for v in std])
+    NV.call("kd_anyres_tiles", base.contiguous().data_ptr(), resized.contiguous().data_ptr(), nh, nw, bh, bw, patch,
+            int(n_out), C.cast(ms, C.c_void_p), out.data_ptr(), 0 if dtype == torch.float32 else 1, _stream())
+    return out
