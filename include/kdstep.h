@@ -275,6 +275,21 @@ int kd_image_resize_u8(const uint8_t* in, int H, int W, uint8_t* out, int out_h,
 int kd_anyres_tiles(const uint8_t* base, const uint8_t* resized, int nh, int nw, int bh, int bw, int patch,
                     int n_out, const float* mean_std_host, void* out, int out_dtype, void* stream);
 
+/* ------------------------------------------------------------ generate() ---- */
+/* Student generate() (evaluation/onevisionv3/evaluate_onevision.py:185-195: greedy,
+ * max_new_tokens=32, repetition_penalty=1.2, no_repeat_ngram_size=2).
+ * kd_attn_decode: SDPA of one new token per head against the KV cache of a layer:
+ *   q [H, hdp] bf16 (head-major, RoPE applied), k/v caches [HKV, smax, hdp] bf16 holding n valid
+ *   positions (the new token's included), o [H, hd] bf16; scale hd^-0.5, fp32 softmax.
+ * kd_gen_select: RepetitionPenaltyLogitsProcessor + NoRepeatNGramLogitsProcessor + greedy argmax
+ *   (lowest index on ties) over one row of bf16 logits [V]; seq [len + 1] int64 device holds the
+ *   sequence so far (prompt + generated) and receives the new token at seq[len]; out (optional)
+ *   also receives it.  workspace >= V bytes. */
+int kd_attn_decode(const void* q, const void* k_cache, const void* v_cache, void* o, int H, int HKV, int hd,
+                   int hdp, int smax, int n, void* stream);
+int kd_gen_select(const void* logits, int V, int64_t* seq, int len, float repetition_penalty, int no_repeat_ngram,
+                  void* workspace, size_t workspace_bytes, int64_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

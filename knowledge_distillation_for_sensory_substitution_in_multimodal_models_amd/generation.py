@@ -1,0 +1,99 @@
+"""Student generate(): prefill + KV-cache greedy decode on the HIP kernels.
+
+Drop-in for the call the reference's evaluation makes on the trained student
+(evaluation/onevisionv3/evaluate_onevision.py:185-195):
+
+    model.generate(**inputs, max_new_tokens=32, pad_token_id=pad_token_id,
+                   repetition_penalty=1.2, no_repeat_ngram_size=2, temperature=0.7)
+
+`do_sample` is not set there, so decoding is greedy and `temperature` has no effect (transformers
+only applies it when sampling).  The prompt runs through the same forward as training
+(LlavaOnevisionModel.forward: SigLIP, projector, anyres pack, Qwen2), whose roped keys and values
+seed a per-layer KV cache [HKV, L + max_new_tokens, hd]; each new token then runs one row through
+every layer (kd_norm_fwd, kd_gemm, kd_qkv_split at its position, kd_attn_decode, fused SwiGLU
+kd_gemm) and kd_gen_select picks it on the device.  Returns prompt + generated ids like
+transformers' generate (B = 1, as the evaluation runs it).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+EOS_TOKEN_IDS = (151645,)   # <|im_end|>: generation_config.eos_token_id of the -ov-hf chat checkpoints
+
+
+@torch.no_grad()
+def generate(model, input_ids: torch.Tensor, pixel_values: torch.Tensor, image_sizes, max_new_tokens: int = 32,
+             repetition_penalty: float = 1.0, no_repeat_ngram_size: int = 0, eos_token_id=EOS_TOKEN_IDS,
+             pad_token_id: int | None = None, temperature: float | None = None, return_logits: bool = False):
+    """-> int64 [1, L + n_new] on the device (and the bf16 logits row of every step if
+    return_logits).  `temperature` is accepted for signature parity and ignored (greedy)."""
+    del temperature, pad_token_id   # greedy, batch of one: no padding of finished rows
+    if input_ids.dim() != 2 or input_ids.shape[0] != 1:
+        raise ValueError("generate: batch size 1 (as evaluate_onevision.py runs it)")
+    T, P = model.cfg.text, model.P
+    dev = model.device
+    L = int(input_ids.shape[1])
+    smax = L + int(max_new_tokens)
+    eos = {int(e) for e in ([eos_token_id] if isinstance(eos_token_id, int) else (eos_token_id or ()))}
+    nq, nkv, hd = T.heads, T.kv_heads, T.head_dim
+    qd, kd = nq * hd, nkv * hd
+    lp = "language_model.model."
+
+    # ---- prefill: the training forward, its roped k/v kept
+    kv = []
+    fwd = model.forward(input_ids, pixel_values, image_sizes, save=False, kv_out=kv)
+    kc = torch.empty((T.layers, nkv, smax, hd), dtype=torch.bfloat16, device=dev)
+    vc = torch.empty_like(kc)
+    for i, (k, v) in enumerate(kv):
+        kc[i, :, :L].copy_(k[0])
+        vc[i, :, :L].copy_(v[0])
+    del kv
+    seq = torch.empty(smax, dtype=torch.int64, device=dev)
+    seq[:L].copy_(input_ids[0])
+    logits = model.logits(fwd["hn"][L - 1:L])
+    del fwd
+    steps = [logits] if return_logits else None
+    ops.gen_select(logits, seq, L, repetition_penalty, no_repeat_ngram_size)
+
+    cos, sin = model._rope_for(smax)
+    src = torch.full((1,), -2, dtype=torch.int32, device=dev)   # token embedding (kd_embed_assemble)
+    table = P[lp + "embed_tokens.weight"]
+    layers = []
+    for i in range(T.layers):
+        p = f"{lp}layers.{i}."
+        layers.append((P[p + "input_layernorm.weight"],
+                       P.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight", qd + 2 * kd, T.hidden),
+                       P.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1, qd + 2 * kd).view(-1),
+                       P[p + "self_attn.o_proj.weight"], P[p + "post_attention_layernorm.weight"],
+                       P.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight", 2 * T.inter, T.hidden),
+                       P[p + "mlp.down_proj.weight"]))
+    n = L + 1
+    while n < smax:
+        if eos and int(seq[n - 1]) in eos:   # one host read per token: transformers stops on EOS
+            break
+        pos = n - 1
+        x = ops.embed_assemble(seq[pos:pos + 1], src, table, None, None, model.err)
+        for i, (w_in, Wqkv, bqkv, Wo, w_post, Wgu, Wdown) in enumerate(layers):
+            h, _, _ = ops.norm_fwd(x, w_in, None, T.eps, rms=True, save_stats=False)
+            qkv = ops.gemm(h, Wqkv, bias=bqkv)
+            q, k, v = ops.qkv_split(qkv, 1, 1, nq, nkv, hd, hd, cos[pos:pos + 1], sin[pos:pos + 1])
+            kc[i, :, pos].copy_(k[0, :, 0])
+            vc[i, :, pos].copy_(v[0, :, 0])
+            o = ops.attn_decode(q.view(nq, hd), kc[i], vc[i], n, hd)
+            x_mid = ops.gemm(o, Wo, residual=x)
+            h2, _, _ = ops.norm_fwd(x_mid, w_post, None, T.eps, rms=True, save_stats=False)
+            if T.inter % 128 == 0:
+                a = ops.gemm(h2, Wgu, act="swiglu")
+            else:
+                a = ops.swiglu_fwd(ops.gemm(h2, Wgu), T.inter)
+            x = ops.gemm(a, Wdown, residual=x_mid)
+        hn, _, _ = ops.norm_fwd(x, P[lp + "norm.weight"], None, T.eps, rms=True, save_stats=False)
+        logits = model.logits(hn)
+        if return_logits:
+            steps.append(logits)
+        ops.gen_select(logits, seq, n, repetition_penalty, no_repeat_ngram_size)
+        n += 1
+    out = seq[:n].view(1, n)
+    return (out, steps) if return_logits else out

@@ -506,7 +506,7 @@ class LlavaOnevisionModel:
         return None
 
     # ============================================================ language ====
-    def lm_forward(self, embeds, B, L, save: bool):
+    def lm_forward(self, embeds, B, L, save: bool, kv_out: list | None = None):
         T, P = self.cfg.text, self.P
         M = B * L
         cos, sin = self._rope_for(L)
@@ -522,6 +522,8 @@ class LlavaOnevisionModel:
             qkv = ops.gemm(h, Wqkv, bias=bqkv)
             q, k, v = ops.qkv_split(qkv, B, L, T.heads, T.kv_heads, T.head_dim, T.head_dim, cos, sin)
             del qkv
+            if kv_out is not None:   # generate(): the prefill's roped keys / values seed the KV cache
+                kv_out.append((k, v))
             o, lse = ops.attn_fwd(q, k, v, T.head_dim, causal=True, want_lse=save)
             o2 = o.view(M, qd)
             x_mid = ops.gemm(o2, P[p + "self_attn.o_proj.weight"], residual=x)
@@ -614,7 +616,8 @@ class LlavaOnevisionModel:
         return dx
 
     # ========================================================= full model ====
-    def forward(self, input_ids, pixel_values, image_sizes, save: bool = False, want_post_ln: bool = False):
+    def forward(self, input_ids, pixel_values, image_sizes, save: bool = False, want_post_ln: bool = False,
+                kv_out: list | None = None):
         """LlavaOnevisionForConditionalGeneration.forward up to the final norm.
 
         input_ids [B, L] int64 (device), pixel_values [B, P, 3, 384, 384], image_sizes
@@ -630,7 +633,7 @@ class LlavaOnevisionModel:
         emb = ops.embed_assemble(input_ids.reshape(-1), src, self.P["language_model.model.embed_tokens.weight"], feats,
                                  self.P["image_newline"], self.err)
         del feats
-        hn, lsave = self.lm_forward(emb, B, L, save=save)
+        hn, lsave = self.lm_forward(emb, B, L, save=save, kv_out=kv_out)
         out = dict(hn=hn, src=src, ids=input_ids.reshape(-1))
         if want_post_ln:
             out["post_ln"] = post

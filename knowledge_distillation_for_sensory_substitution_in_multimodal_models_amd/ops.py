@@ -483,3 +483,26 @@ def anyres_tiles(base: torch.Tensor, resized: torch.Tensor, best_hw, n_out: int,
     NV.call("kd_anyres_tiles", base.contiguous().data_ptr(), resized.contiguous().data_ptr(), nh, nw, bh, bw, patch,
             int(n_out), C.cast(ms, C.c_void_p), out.data_ptr(), 0 if dtype == torch.float32 else 1, _stream())
     return out
+
+
+def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n: int, hd: int,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """One token's attention against the first n cached positions (kd_attn_decode).
+    q [H, hdp], caches [HKV, smax, hdp] bf16 -> o [1, H*hd] bf16 (token-major, what o_proj reads)."""
+    H, hdp = q.shape
+    HKV, smax, _ = k_cache.shape
+    if out is None:
+        out = torch.empty((1, H * hd), dtype=torch.bfloat16, device=q.device)
+    NV.call("kd_attn_decode", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), H, HKV, hd, hdp,
+            smax, int(n), _stream())
+    return out
+
+
+def gen_select(logits: torch.Tensor, seq: torch.Tensor, length: int, repetition_penalty: float = 1.0,
+               no_repeat_ngram_size: int = 0, out: torch.Tensor | None = None) -> None:
+    """Greedy next token of one bf16 logits row with the repetition-penalty / no-repeat-n-gram
+    processors; written to seq[length] (kd_gen_select)."""
+    V = logits.shape[-1]
+    ws = _workspace(("gen_select", _stream()), V, logits.device)
+    NV.call("kd_gen_select", logits.data_ptr(), V, seq.data_ptr(), int(length), float(repetition_penalty),
+            int(no_repeat_ngram_size), ws.data_ptr(), ws.numel(), _ptr(out), _stream())
