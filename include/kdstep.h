@@ -278,17 +278,31 @@ int kd_anyres_tiles(const uint8_t* base, const uint8_t* resized, int nh, int nw,
 /* ------------------------------------------------------------ generate() ---- */
 /* Student generate() (evaluation/onevisionv3/evaluate_onevision.py:185-195: greedy,
  * max_new_tokens=32, repetition_penalty=1.2, no_repeat_ngram_size=2).
+ * The sequence length may live on the device (cur_dev, int32: tokens in the sequence, the one
+ * being decoded included) so that a decode step has fixed arguments and replays from one HIP
+ * graph; with cur_dev NULL the host value (n / len) is used.
  * kd_attn_decode: SDPA of one new token per head against the KV cache of a layer:
- *   q [H, hdp] bf16 (head-major, RoPE applied), k/v caches [HKV, smax, hdp] bf16 holding n valid
- *   positions (the new token's included), o [H, hd] bf16; scale hd^-0.5, fp32 softmax.
+ *   q [H, hdp] bf16 (head-major, RoPE applied), k_new/v_new [HKV, hdp] the token's own key/value
+ *   (stored into the caches at position n - 1), caches [HKV, smax, hdp] bf16, o [H, hd] bf16;
+ *   scale hd^-0.5, fp32 softmax over positions [0, n).
  * kd_gen_select: RepetitionPenaltyLogitsProcessor + NoRepeatNGramLogitsProcessor + greedy argmax
- *   (lowest index on ties) over one row of bf16 logits [V]; seq [len + 1] int64 device holds the
- *   sequence so far (prompt + generated) and receives the new token at seq[len]; out (optional)
- *   also receives it.  workspace >= V bytes. */
-int kd_attn_decode(const void* q, const void* k_cache, const void* v_cache, void* o, int H, int HKV, int hd,
-                   int hdp, int smax, int n, void* stream);
-int kd_gen_select(const void* logits, int V, int64_t* seq, int len, float repetition_penalty, int no_repeat_ngram,
-                  void* workspace, size_t workspace_bytes, int64_t* out, void* stream);
+ *   (lowest index on ties) over one row of bf16 logits [V]; seq (int64, device) holds the len ids
+ *   so far (prompt + generated) and receives the new token at seq[len]; out (optional) also
+ *   receives it; *cur_dev (if given) supplies len and is incremented.  workspace >= V bytes.
+ * kd_rope_row: cos/sin row of position *cur_dev - 1 ([.., hh] tables) into one-row buffers. */
+size_t kd_attn_decode_workspace_size(int H, int hd, int smax);
+int kd_attn_decode(const void* q, const void* k_new, const void* v_new, void* k_cache, void* v_cache, void* o,
+                   int H, int HKV, int hd, int hdp, int smax, int n, const int32_t* cur_dev, void* workspace,
+                   size_t workspace_bytes, void* stream);
+/* Decode GEMV (one token row through an nn.Linear): y[N] bf16 = epilogue(W[N, K] x[K]), fp32
+ * accumulation; epilogue 0 none, 1 + bias[N], 2 + residual[N] (both in `extra`), 3 SwiGLU over the
+ * adjacent gate|up weight: y[n] = silu(W[n] x) * (W[inter + n] x), N = inter. */
+int kd_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epilogue,
+            int inter, void* stream);
+int kd_gen_select(const void* logits, int V, int64_t* seq, int len, int32_t* cur_dev, float repetition_penalty,
+                  int no_repeat_ngram, void* workspace, size_t workspace_bytes, int64_t* out, void* stream);
+int kd_rope_row(const float* cos_table, const float* sin_table, int hh, const int32_t* cur_dev, float* cos_row,
+                float* sin_row, void* stream);
 
 #ifdef __cplusplus
 }

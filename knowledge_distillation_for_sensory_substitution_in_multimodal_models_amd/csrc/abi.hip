@@ -57,10 +57,16 @@ int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, 
 int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 size_t depth3_ws(int B, int H, int W);
 size_t image_resize_ws(int H, int W, int oh, int ow);
-int launch_attn_decode(const void* q, const void* kc, const void* vc, void* o, int H, int HKV, int hd, int hdp,
-                       int smax, int n, void* stream);
-int launch_gen_select(const void* logits, int V, int64_t* seq, int len, float penalty, int ngram, void* flags_ws,
-                      size_t ws_bytes, int64_t* out, void* stream);
+size_t attn_decode_ws(int H, int hd, int smax);
+int launch_attn_decode(const void* q, const void* k_new, const void* v_new, void* kc, void* vc, void* o, int H,
+                       int HKV, int hd, int hdp, int smax, int n, const int* cur_dev, void* ws, size_t ws_bytes,
+                       void* stream);
+int launch_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epi, int I,
+                void* stream);
+int launch_gen_select(const void* logits, int V, int64_t* seq, int len, int* cur_dev, float penalty, int ngram,
+                      void* flags_ws, size_t ws_bytes, int64_t* out, void* stream);
+int launch_rope_row(const float* cos_t, const float* sin_t, int hh, const int* cur_dev, float* cos_row, float* sin_row,
+                    void* stream);
 int launch_image_resize(const uint8_t* in, int H, int W, uint8_t* out, int oh, int ow, void* ws, size_t ws_bytes,
                         void* stream);
 int launch_anyres_tiles(const uint8_t* base, const uint8_t* resized, int nh, int nw, int bh, int bw, int patch,
@@ -167,13 +173,21 @@ int kd_depth_to_3ch(const void* depth, int dtype, int B, int H, int W, uint8_t* 
                     void* s) {
     return kd::launch_depth3(depth, dtype, B, H, W, out, ws, ws_bytes, s);
 }
-int kd_attn_decode(const void* q, const void* kc, const void* vc, void* o, int H, int HKV, int hd, int hdp, int smax,
-                   int n, void* s) {
-    return kd::launch_attn_decode(q, kc, vc, o, H, HKV, hd, hdp, smax, n, s);
+size_t kd_attn_decode_workspace_size(int H, int hd, int smax) { return kd::attn_decode_ws(H, hd, smax); }
+int kd_attn_decode(const void* q, const void* kn, const void* vn, void* kc, void* vc, void* o, int H, int HKV, int hd,
+                   int hdp, int smax, int n, const int32_t* cur, void* ws, size_t wsb, void* s) {
+    return kd::launch_attn_decode(q, kn, vn, kc, vc, o, H, HKV, hd, hdp, smax, n, cur, ws, wsb, s);
 }
-int kd_gen_select(const void* logits, int V, int64_t* seq, int len, float penalty, int ngram, void* ws, size_t wsb,
-                  int64_t* out, void* s) {
-    return kd::launch_gen_select(logits, V, seq, len, penalty, ngram, ws, wsb, out, s);
+int kd_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epi, int I,
+            void* s) {
+    return kd::launch_gemv(x, W, ldw, extra, y, N, K, epi, I, s);
+}
+int kd_gen_select(const void* logits, int V, int64_t* seq, int len, int32_t* cur, float penalty, int ngram, void* ws,
+                  size_t wsb, int64_t* out, void* s) {
+    return kd::launch_gen_select(logits, V, seq, len, cur, penalty, ngram, ws, wsb, out, s);
+}
+int kd_rope_row(const float* c, const float* sn, int hh, const int32_t* cur, float* cr, float* sr, void* s) {
+    return kd::launch_rope_row(c, sn, hh, cur, cr, sr, s);
 }
 size_t kd_image_resize_workspace_size(int H, int W, int oh, int ow) { return kd::image_resize_ws(H, W, oh, ow); }
 int kd_image_resize_u8(const uint8_t* in, int H, int W, uint8_t* out, int oh, int ow, void* ws, size_t ws_bytes,

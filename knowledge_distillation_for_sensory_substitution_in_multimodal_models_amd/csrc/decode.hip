@@ -20,65 +20,146 @@ namespace {
 
 constexpr int NT = 256;
 
-// One workgroup per query head.  q [H, hdp] bf16 (head-major, one token), caches
-// [HKV, smax, hdp] bf16, o [H, hd] bf16.  Scores for all n keys live in LDS (n <= smax).
+// Split-KV decode attention (flash-decoding): workgroup (h, c) handles keys [c*CH, c*CH + CH)
+// of query head h and writes its partial (max, sum, unnormalised output) to the workspace;
+// k_attn_decode_combine merges the partials of a head.  Chunks at or past n exit after writing
+// an empty partial, so the grid depends only on smax (fixed under graph capture).
+// The step's own key/value row (k_new/v_new [HKV, hdp]) stands in for cache position n - 1 and
+// is stored there by chunk 0 of the first query head of each KV group (read by later steps only).
+// n = *cur_dev when cur_dev is given: the position lives on the device.
+constexpr int CH = 64;   // keys per workgroup: 4 lanes per key for the scores, 4 key groups for P.V
+
 template <int HD>
-__global__ void __launch_bounds__(NT) k_attn_decode(const bf16* __restrict__ q, const bf16* __restrict__ kc,
-                                                    const bf16* __restrict__ vc, bf16* __restrict__ o, int H,
-                                                    int HKV, int hdp, int smax, int n, float scale) {
-    extern __shared__ float sh[];   // [n] scores, then [NT / HD][HD] partial outputs
+__global__ void __launch_bounds__(NT) k_attn_decode_part(const bf16* __restrict__ q, const bf16* __restrict__ k_new,
+                                                         const bf16* __restrict__ v_new, bf16* __restrict__ kc,
+                                                         bf16* __restrict__ vc, float* __restrict__ part, int H,
+                                                         int HKV, int hdp, int smax, int n,
+                                                         const int* __restrict__ cur_dev, float scale) {
+    __shared__ float p_s[CH];
     __shared__ float red[8];
-    const int h = blockIdx.x, kvh = h / (H / HKV);
-    const bf16* qh = q + (size_t)h * hdp;
-    const bf16* K = kc + (size_t)kvh * smax * hdp;
-    const bf16* V = vc + (size_t)kvh * smax * hdp;
-    float qv[HD];
-#pragma unroll
-    for (int d = 0; d < HD; ++d) qv[d] = (float)qh[d];
-    float mx = -INFINITY;
-    for (int j = threadIdx.x; j < n; j += NT) {
-        const bf16* kr = K + (size_t)j * hdp;
-        float s = 0.f;
-#pragma unroll
-        for (int d = 0; d < HD; d += 8) {
-            const bf16x8 kv8 = *(const bf16x8*)(kr + d);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) s += qv[d + e] * (float)kv8[e];
+    __shared__ float acc_s[NT];
+    if (cur_dev) n = *cur_dev;
+    const int h = blockIdx.x, c = blockIdx.y, nch = gridDim.y, kvh = h / (H / HKV);
+    float* pp = part + ((size_t)h * nch + c) * (HD + 2);
+    const int j0 = c * CH;
+    bf16* K = kc + (size_t)kvh * smax * hdp;
+    bf16* V = vc + (size_t)kvh * smax * hdp;
+    const bf16* kn = k_new + (size_t)kvh * hdp;
+    const bf16* vn = v_new + (size_t)kvh * hdp;
+    if (c == 0 && h % (H / HKV) == 0)
+        for (int d = threadIdx.x; d < hdp; d += NT) {
+            K[(size_t)(n - 1) * hdp + d] = kn[d];
+            V[(size_t)(n - 1) * hdp + d] = vn[d];
         }
-        s *= scale;
-        sh[j] = s;
-        mx = fmaxf(mx, s);
+    if (j0 >= n) {   // empty chunk
+        if (threadIdx.x == 0) { pp[0] = -INFINITY; pp[1] = 0.f; }
+        if (threadIdx.x < HD) pp[2 + threadIdx.x] = 0.f;
+        return;
     }
-    mx = block_max<NT / 64>(mx, red);
-    float sum = 0.f;
-    for (int j = threadIdx.x; j < n; j += NT) {
-        const float p = __expf(sh[j] - mx);
-        sh[j] = p;
-        sum += p;
+    // scores: key j0 + threadIdx/4, lane quarter (threadIdx & 3) covers HD/4 dims
+    constexpr int DQ = HD / 4;
+    const int kj = j0 + (threadIdx.x >> 2), qd = (threadIdx.x & 3) * DQ;
+    float s = -INFINITY;
+    if (kj < n) {
+        const bf16* kr = (kj == n - 1 ? kn : K + (size_t)kj * hdp) + qd;
+        const bf16* qh = q + (size_t)h * hdp + qd;
+        float a = 0.f;
+#pragma unroll
+        for (int d = 0; d < DQ; d += 8) {
+            const bf16x8 k8 = *(const bf16x8*)(kr + d);
+            const bf16x8 q8 = *(const bf16x8*)(qh + d);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a += (float)q8[e] * (float)k8[e];
+        }
+        a += __shfl_xor(a, 1, 64);
+        a += __shfl_xor(a, 2, 64);
+        s = a * scale;
     }
-    sum = block_sum<NT / 64>(sum, red);   // its barriers also publish sh[]
-    constexpr int G = NT / HD;            // key groups
+    const float m = block_max<NT / 64>(s, red);
+    const float pv = kj < n ? __expf(s - m) : 0.f;
+    if ((threadIdx.x & 3) == 0) p_s[threadIdx.x >> 2] = pv;
+    const float l = block_sum<NT / 64>((threadIdx.x & 3) == 0 ? pv : 0.f, red);   // barriers publish p_s
+    constexpr int G = NT / HD;
     const int d = threadIdx.x % HD, g = threadIdx.x / HD;
     float acc = 0.f;
-    for (int j = g; j < n; j += G) acc += sh[j] * (float)V[(size_t)j * hdp + d];
-    float* part = sh + ((n + 3) & ~3);
-    part[g * HD + d] = acc;
+    const int jend = min(CH, n - j0);
+    for (int jj = g; jj < jend; jj += G) {
+        const int j = j0 + jj;
+        acc += p_s[jj] * (float)(j == n - 1 ? vn[d] : V[(size_t)j * hdp + d]);
+    }
+    acc_s[threadIdx.x] = acc;
     __syncthreads();
     if (g == 0) {
-        float t = 0.f;
+        float tsum = 0.f;
 #pragma unroll
-        for (int i = 0; i < G; ++i) t += part[i * HD + d];
-        o[(size_t)h * HD + d] = (bf16)(t / sum);
+        for (int i = 0; i < G; ++i) tsum += acc_s[i * HD + d];
+        pp[2 + d] = tsum;
+        if (d == 0) { pp[0] = m; pp[1] = l; }
+    }
+}
+
+template <int HD>
+__global__ void __launch_bounds__(HD) k_attn_decode_combine(const float* __restrict__ part, int nch,
+                                                            bf16* __restrict__ o) {
+    const int h = blockIdx.x, d = threadIdx.x;
+    const float* pp = part + (size_t)h * nch * (HD + 2);
+    float m = -INFINITY;
+    for (int c = 0; c < nch; ++c) m = fmaxf(m, pp[(size_t)c * (HD + 2)]);
+    float l = 0.f, acc = 0.f;
+    for (int c = 0; c < nch; ++c) {
+        const float* q = pp + (size_t)c * (HD + 2);
+        if (q[0] == -INFINITY) continue;
+        const float w = __expf(q[0] - m);
+        l += w * q[1];
+        acc += w * q[2 + d];
+    }
+    o[(size_t)h * HD + d] = (bf16)(acc / l);
+}
+
+// Decode GEMV: y[n] = epilogue(sum_k x[k] * W[n][k]) for one token row, one wave per output
+// (two weight rows, n and I + n, for the SwiGLU form).  Weight rows are read once, 16 B per lane,
+// so the decode step streams its weights at HBM rate instead of running 256-row GEMM tiles at
+// M = 1.  EPI: 0 none, 1 + bias[n], 2 + residual[n], 3 silu(row n) * (row I + n).
+template <int EPI>
+__global__ void __launch_bounds__(NT) k_gemv(const bf16* __restrict__ x, const bf16* __restrict__ W, int64_t ldw,
+                                             const bf16* __restrict__ extra, bf16* __restrict__ y, int N, int K,
+                                             int I) {
+    extern __shared__ float xs[];
+    for (int k = threadIdx.x; k < K; k += NT) xs[k] = (float)x[k];
+    __syncthreads();
+    const int n = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (n >= N) return;
+    const bf16* r0 = W + (size_t)n * ldw;
+    const bf16* r1 = W + (size_t)(I + n) * ldw;
+    float a0 = 0.f, a1 = 0.f;
+    for (int k = lane * 8; k < K; k += 512) {
+        const bf16x8 w0 = *(const bf16x8*)(r0 + k);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a0 += xs[k + e] * (float)w0[e];
+        if constexpr (EPI == 3) {
+            const bf16x8 w1 = *(const bf16x8*)(r1 + k);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a1 += xs[k + e] * (float)w1[e];
+        }
+    }
+    a0 = wave_sum(a0);
+    if constexpr (EPI == 3) a1 = wave_sum(a1);
+    if (lane == 0) {
+        float v = a0;
+        if constexpr (EPI == 1 || EPI == 2) v += (float)extra[n];
+        if constexpr (EPI == 3) v = a0 / (1.f + __expf(-a0)) * a1;
+        y[n] = (bf16)v;
     }
 }
 
 // One workgroup of 1024 threads: flags in the workspace (bit 0 = seen, bit 1 = banned), then
 // the processed-score argmax.  seq [len + 1] int64 (the new token is written at seq[len]).
 __global__ void __launch_bounds__(1024) k_gen_select(const bf16* __restrict__ logits, int V, int64_t* __restrict__ seq,
-                                                     int len, float penalty, int ngram, uint8_t* __restrict__ flags,
-                                                     int64_t* __restrict__ out) {
+                                                     int len, int* __restrict__ cur_dev, float penalty, int ngram,
+                                                     uint8_t* __restrict__ flags, int64_t* __restrict__ out) {
     __shared__ float sv[16];
     __shared__ int si[16];
+    if (cur_dev) len = *cur_dev;
     for (int i = threadIdx.x; i < V; i += blockDim.x) flags[i] = 0;
     __syncthreads();
     // RepetitionPenaltyLogitsProcessor: every id of the sequence (prompt + generated)
@@ -87,6 +168,7 @@ __global__ void __launch_bounds__(1024) k_gen_select(const bf16* __restrict__ lo
             const int64_t t = seq[i];
             if (t >= 0 && t < V) flags[t] |= 1;
         }
+    __syncthreads();   // the two processors OR different bits into the same bytes
     // NoRepeatNGramLogitsProcessor: the last (ngram - 1) tokens as a prefix; ban the token that
     // followed every earlier occurrence of that prefix (only once cur_len + 1 >= ngram)
     if (ngram > 0 && len + 1 >= ngram)
@@ -123,41 +205,94 @@ __global__ void __launch_bounds__(1024) k_gen_select(const bf16* __restrict__ lo
         if (bi == 0x7fffffff) bi = 0;   // every score -inf: torch.argmax returns 0
         seq[len] = bi;
         if (out) *out = bi;
+        if (cur_dev) *cur_dev = len + 1;
+    }
+}
+
+// cos/sin row of position *cur_dev - 1 into fixed one-row buffers (what kd_qkv_split reads).
+__global__ void k_rope_row(const float* __restrict__ cos_t, const float* __restrict__ sin_t, int hh,
+                           const int* __restrict__ cur_dev, float* __restrict__ cos_row, float* __restrict__ sin_row) {
+    const int pos = *cur_dev - 1;
+    for (int i = threadIdx.x; i < hh; i += blockDim.x) {
+        cos_row[i] = cos_t[(size_t)pos * hh + i];
+        sin_row[i] = sin_t[(size_t)pos * hh + i];
     }
 }
 
 }  // namespace
 
-int launch_attn_decode(const void* q, const void* kc, const void* vc, void* o, int H, int HKV, int hd, int hdp,
-                       int smax, int n, void* stream) {
-    KD_CHECK_ARG(q && kc && vc && o, "attn_decode: null pointer");
+int launch_rope_row(const float* cos_t, const float* sin_t, int hh, const int* cur_dev, float* cos_row, float* sin_row,
+                    void* stream) {
+    KD_CHECK_ARG(cos_t && sin_t && cur_dev && cos_row && sin_row, "rope_row: null pointer");
+    KD_CHECK_SHAPE(hh > 0, "rope_row: hh must be positive");
+    hipLaunchKernelGGL(k_rope_row, dim3(1), dim3(256), 0, as_stream(stream), cos_t, sin_t, hh, cur_dev, cos_row,
+                       sin_row);
+    KD_LAUNCH_CHECK("k_rope_row");
+    return KD_OK;
+}
+
+size_t attn_decode_ws(int H, int hd, int smax) {
+    return (size_t)H * ((smax + CH - 1) / CH) * (hd + 2) * sizeof(float);
+}
+
+int launch_attn_decode(const void* q, const void* k_new, const void* v_new, void* kc, void* vc, void* o, int H,
+                       int HKV, int hd, int hdp, int smax, int n, const int* cur_dev, void* ws, size_t ws_bytes,
+                       void* stream) {
+    KD_CHECK_ARG(q && k_new && v_new && kc && vc && o && ws, "attn_decode: null pointer");
     KD_CHECK_SHAPE(hd == 64 || hd == 128, "attn_decode: head dim must be 64 or 128");
     KD_CHECK_SHAPE(hdp >= hd && hdp % 8 == 0, "attn_decode: hdp must be >= hd and a multiple of 8");
     KD_CHECK_SHAPE(H > 0 && HKV > 0 && H % HKV == 0, "attn_decode: heads must be a multiple of kv heads");
-    KD_CHECK_SHAPE(n > 0 && n <= smax && n <= 30000, "attn_decode: 0 < n <= smax <= 30000");
+    KD_CHECK_SHAPE(smax > 0 && (cur_dev || (n > 0 && n <= smax)), "attn_decode: need 0 < n <= smax");
     KD_CHECK_ALIGN(q, 16, "attn_decode: q misaligned");
     KD_CHECK_ALIGN(kc, 16, "attn_decode: k cache misaligned");
-    const size_t lds = (size_t)(((n + 3) & ~3) + NT) * sizeof(float);
+    KD_CHECK_ALIGN(k_new, 16, "attn_decode: k_new misaligned");
+    if (ws_bytes < attn_decode_ws(H, hd, smax)) return fail(KD_ERR_WORKSPACE, "attn_decode: workspace too small");
+    const int nch = (smax + CH - 1) / CH;
     const float scale = 1.0f / sqrtf((float)hd);
     hipStream_t s = as_stream(stream);
-    if (hd == 64)
-        hipLaunchKernelGGL(k_attn_decode<64>, dim3(H), dim3(NT), lds, s, (const bf16*)q, (const bf16*)kc,
-                           (const bf16*)vc, (bf16*)o, H, HKV, hdp, smax, n, scale);
-    else
-        hipLaunchKernelGGL(k_attn_decode<128>, dim3(H), dim3(NT), lds, s, (const bf16*)q, (const bf16*)kc,
-                           (const bf16*)vc, (bf16*)o, H, HKV, hdp, smax, n, scale);
+    float* part = (float*)ws;
+    if (hd == 64) {
+        hipLaunchKernelGGL(k_attn_decode_part<64>, dim3(H, nch), dim3(NT), 0, s, (const bf16*)q, (const bf16*)k_new,
+                           (const bf16*)v_new, (bf16*)kc, (bf16*)vc, part, H, HKV, hdp, smax, n, cur_dev, scale);
+        hipLaunchKernelGGL(k_attn_decode_combine<64>, dim3(H), dim3(64), 0, s, part, nch, (bf16*)o);
+    } else {
+        hipLaunchKernelGGL(k_attn_decode_part<128>, dim3(H, nch), dim3(NT), 0, s, (const bf16*)q, (const bf16*)k_new,
+                           (const bf16*)v_new, (bf16*)kc, (bf16*)vc, part, H, HKV, hdp, smax, n, cur_dev, scale);
+        hipLaunchKernelGGL(k_attn_decode_combine<128>, dim3(H), dim3(128), 0, s, part, nch, (bf16*)o);
+    }
     KD_LAUNCH_CHECK("k_attn_decode");
     return KD_OK;
 }
 
-int launch_gen_select(const void* logits, int V, int64_t* seq, int len, float penalty, int ngram, void* flags_ws,
-                      size_t ws_bytes, int64_t* out, void* stream) {
+int launch_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epi, int I,
+                void* stream) {
+    KD_CHECK_ARG(x && W && y, "gemv: null pointer");
+    KD_CHECK_ARG(epi >= 0 && epi <= 3 && (epi == 0 || epi == 3 || extra), "gemv: epilogue 0..3 (1, 2 need extra)");
+    KD_CHECK_SHAPE(N > 0 && K > 0 && K % 8 == 0 && K <= 16384 && ldw >= K && ldw % 8 == 0,
+                   "gemv: K must be a multiple of 8 (<= 16384), ldw >= K and a multiple of 8");
+    KD_CHECK_ALIGN(W, 16, "gemv: W misaligned");
+    const dim3 grid((N + NT / 64 - 1) / (NT / 64));
+    const size_t lds = (size_t)K * sizeof(float);
+    hipStream_t s = as_stream(stream);
+    const bf16 *xb = (const bf16*)x, *Wb = (const bf16*)W, *eb = (const bf16*)extra;
+    switch (epi) {
+        case 0: hipLaunchKernelGGL(k_gemv<0>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
+        case 1: hipLaunchKernelGGL(k_gemv<1>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
+        case 2: hipLaunchKernelGGL(k_gemv<2>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
+        default: hipLaunchKernelGGL(k_gemv<3>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I);
+    }
+    KD_LAUNCH_CHECK("k_gemv");
+    return KD_OK;
+}
+
+int launch_gen_select(const void* logits, int V, int64_t* seq, int len, int* cur_dev, float penalty, int ngram,
+                      void* flags_ws, size_t ws_bytes, int64_t* out, void* stream) {
     KD_CHECK_ARG(logits && seq && flags_ws, "gen_select: null pointer");
-    KD_CHECK_SHAPE(V > 0 && len > 0, "gen_select: V and len must be positive");
+    KD_CHECK_SHAPE(V > 0 && (cur_dev || len > 0), "gen_select: V and len must be positive");
     KD_CHECK_ARG(penalty > 0.f && ngram >= 0, "gen_select: penalty must be > 0 and ngram >= 0");
     if (ws_bytes < (size_t)V) return fail(KD_ERR_WORKSPACE, "gen_select: workspace must hold V bytes");
     hipLaunchKernelGGL(k_gen_select, dim3(1), dim3(1024), 0, as_stream(stream), (const bf16*)logits, V, seq, len,
-                       penalty, ngram, (uint8_t*)flags_ws, out);
+                       cur_dev, penalty, ngram, (uint8_t*)flags_ws, out);
     KD_LAUNCH_CHECK("k_gen_select");
     return KD_OK;
 }

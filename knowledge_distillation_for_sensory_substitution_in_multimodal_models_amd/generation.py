@@ -10,8 +10,11 @@ Drop-in for the call the reference's evaluation makes on the trained student
 only applies it when sampling).  The prompt runs through the same forward as training
 (LlavaOnevisionModel.forward: SigLIP, projector, anyres pack, Qwen2), whose roped keys and values
 seed a per-layer KV cache [HKV, L + max_new_tokens, hd]; each new token then runs one row through
-every layer (kd_norm_fwd, kd_gemm, kd_qkv_split at its position, kd_attn_decode, fused SwiGLU
-kd_gemm) and kd_gen_select picks it on the device.  Returns prompt + generated ids like
+every layer (kd_norm_fwd, kd_gemv with bias / residual / SwiGLU epilogues, kd_qkv_split with its
+RoPE row, split-KV kd_attn_decode) and kd_gen_select picks it on the device.  The position lives in a device counter, so
+every launch of a step has fixed arguments: the first step runs eagerly, the step is captured
+once as a HIP graph (torch.cuda.CUDAGraph) and replayed for the rest; steps past an EOS are
+discarded afterwards (one host read at the end instead of one per token).  Returns prompt + generated ids like
 transformers' generate (B = 1, as the evaluation runs it).
 """
 from __future__ import annotations
@@ -26,7 +29,8 @@ EOS_TOKEN_IDS = (151645,)   # <|im_end|>: generation_config.eos_token_id of the 
 @torch.no_grad()
 def generate(model, input_ids: torch.Tensor, pixel_values: torch.Tensor, image_sizes, max_new_tokens: int = 32,
              repetition_penalty: float = 1.0, no_repeat_ngram_size: int = 0, eos_token_id=EOS_TOKEN_IDS,
-             pad_token_id: int | None = None, temperature: float | None = None, return_logits: bool = False):
+             pad_token_id: int | None = None, temperature: float | None = None, return_logits: bool = False,
+             graph: bool = True):
     """-> int64 [1, L + n_new] on the device (and the bf16 logits row of every step if
     return_logits).  `temperature` is accepted for signature parity and ignored (greedy)."""
     del temperature, pad_token_id   # greedy, batch of one: no padding of finished rows
@@ -69,31 +73,53 @@ def generate(model, input_ids: torch.Tensor, pixel_values: torch.Tensor, image_s
                        P[p + "self_attn.o_proj.weight"], P[p + "post_attention_layernorm.weight"],
                        P.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight", 2 * T.inter, T.hidden),
                        P[p + "mlp.down_proj.weight"]))
-    n = L + 1
-    while n < smax:
-        if eos and int(seq[n - 1]) in eos:   # one host read per token: transformers stops on EOS
-            break
-        pos = n - 1
-        x = ops.embed_assemble(seq[pos:pos + 1], src, table, None, None, model.err)
+    # device-resident step state: the sequence length (tokens so far, the one being decoded
+    # included), the token being decoded and its RoPE row -> every launch of a step has fixed
+    # arguments and the step replays from one captured HIP graph
+    cur = torch.full((1,), L + 1, dtype=torch.int32, device=dev)
+    tok = seq[L:L + 1].clone()   # the token being decoded (kd_gen_select rewrites it each step)
+    cos_row = torch.empty((1, cos.shape[1]), dtype=torch.float32, device=dev)
+    sin_row = torch.empty_like(cos_row)
+
+    def step():
+        ops.rope_row(cos, sin, cur, cos_row, sin_row)
+        x = ops.embed_assemble(tok, src, table, None, None, model.err)
         for i, (w_in, Wqkv, bqkv, Wo, w_post, Wgu, Wdown) in enumerate(layers):
             h, _, _ = ops.norm_fwd(x, w_in, None, T.eps, rms=True, save_stats=False)
-            qkv = ops.gemm(h, Wqkv, bias=bqkv)
-            q, k, v = ops.qkv_split(qkv, 1, 1, nq, nkv, hd, hd, cos[pos:pos + 1], sin[pos:pos + 1])
-            kc[i, :, pos].copy_(k[0, :, 0])
-            vc[i, :, pos].copy_(v[0, :, 0])
-            o = ops.attn_decode(q.view(nq, hd), kc[i], vc[i], n, hd)
-            x_mid = ops.gemm(o, Wo, residual=x)
+            qkv = ops.gemv(h, Wqkv, bias=bqkv)
+            q, k, v = ops.qkv_split(qkv, 1, 1, nq, nkv, hd, hd, cos_row, sin_row)
+            o = ops.attn_decode(q.view(nq, hd), k.view(nkv, hd), v.view(nkv, hd), kc[i], vc[i], 0, hd, cur=cur)
+            x_mid = ops.gemv(o, Wo, residual=x)
             h2, _, _ = ops.norm_fwd(x_mid, w_post, None, T.eps, rms=True, save_stats=False)
-            if T.inter % 128 == 0:
-                a = ops.gemm(h2, Wgu, act="swiglu")
-            else:
-                a = ops.swiglu_fwd(ops.gemm(h2, Wgu), T.inter)
-            x = ops.gemm(a, Wdown, residual=x_mid)
+            a = ops.gemv(h2, Wgu, swiglu_inter=T.inter)
+            x = ops.gemv(a, Wdown, residual=x_mid)
         hn, _, _ = ops.norm_fwd(x, P[lp + "norm.weight"], None, T.eps, rms=True, save_stats=False)
-        logits = model.logits(hn)
+        lg = ops.gemv(hn, model.lm_head_weight())
+        ops.gen_select(lg, seq, 0, repetition_penalty, no_repeat_ngram_size, out=tok, cur=cur)
+        return lg
+
+    n_steps = smax - (L + 1)
+    graph_obj = None
+    for t_ in range(n_steps):
+        if graph and t_ == 1:   # step 0 ran eagerly (warm-up: allocations, workspaces); capture the rest
+            graph_obj = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph_obj):
+                lg_static = step()
+        if graph_obj is not None:
+            graph_obj.replay()
+            lg = lg_static
+        else:
+            lg = step()
         if return_logits:
-            steps.append(logits)
-        ops.gen_select(logits, seq, n, repetition_penalty, no_repeat_ngram_size)
-        n += 1
+            steps.append(lg.clone())
+    n = smax
+    if eos:   # transformers stops after the first EOS; the steps past it are discarded
+        gen = seq[L:smax].tolist()
+        for j, t_ in enumerate(gen):
+            if t_ in eos:
+                n = L + j + 1
+                break
+        if return_logits:
+            steps = steps[:n - L]
     out = seq[:n].view(1, n)
     return (out, steps) if return_logits else out

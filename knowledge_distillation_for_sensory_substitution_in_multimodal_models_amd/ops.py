@@ -485,24 +485,55 @@ def anyres_tiles(base: torch.Tensor, resized: torch.Tensor, best_hw, n_out: int,
     return out
 
 
-def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n: int, hd: int,
+def attn_decode(q: torch.Tensor, k_new: torch.Tensor, v_new: torch.Tensor, k_cache: torch.Tensor,
+                v_cache: torch.Tensor, n: int, hd: int, cur: torch.Tensor | None = None,
                 out: torch.Tensor | None = None) -> torch.Tensor:
-    """One token's attention against the first n cached positions (kd_attn_decode).
+    """One token's attention against cache positions [0, n) (kd_attn_decode); the token's own
+    k_new/v_new [HKV, hdp] are stored at position n - 1.  n = cur[0] (device int32) when given.
     q [H, hdp], caches [HKV, smax, hdp] bf16 -> o [1, H*hd] bf16 (token-major, what o_proj reads)."""
     H, hdp = q.shape
     HKV, smax, _ = k_cache.shape
     if out is None:
         out = torch.empty((1, H * hd), dtype=torch.bfloat16, device=q.device)
-    NV.call("kd_attn_decode", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), H, HKV, hd, hdp,
-            smax, int(n), _stream())
+    nbytes = NV.lib().kd_attn_decode_workspace_size(H, hd, smax)
+    ws = _workspace(("attn_decode", _stream()), nbytes, q.device)
+    NV.call("kd_attn_decode", q.data_ptr(), k_new.data_ptr(), v_new.data_ptr(), k_cache.data_ptr(),
+            v_cache.data_ptr(), out.data_ptr(), H, HKV, hd, hdp, smax, int(n), _ptr(cur), ws.data_ptr(), ws.numel(),
+            _stream())
     return out
 
 
+def gemv(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, swiglu_inter: int = 0) -> torch.Tensor:
+    """One token row through a linear layer (kd_gemv): x [1, K] bf16, w [N, K] (row stride may
+    exceed K) -> [1, N] bf16 with an optional bias / residual / SwiGLU (w = gate|up, N = 2*inter)."""
+    K = x.shape[-1]
+    epi, extra = 0, None
+    if swiglu_inter:
+        epi, N = 3, int(swiglu_inter)
+    else:
+        N = w.shape[0]
+        if bias is not None:
+            epi, extra = 1, bias
+        elif residual is not None:
+            epi, extra = 2, residual
+    y = torch.empty((1, N), dtype=torch.bfloat16, device=x.device)
+    NV.call("kd_gemv", x.data_ptr(), w.data_ptr(), w.stride(0), _ptr(extra), y.data_ptr(), N, K, epi,
+            int(swiglu_inter), _stream())
+    return y
+
+
 def gen_select(logits: torch.Tensor, seq: torch.Tensor, length: int, repetition_penalty: float = 1.0,
-               no_repeat_ngram_size: int = 0, out: torch.Tensor | None = None) -> None:
+               no_repeat_ngram_size: int = 0, out: torch.Tensor | None = None, cur: torch.Tensor | None = None) -> None:
     """Greedy next token of one bf16 logits row with the repetition-penalty / no-repeat-n-gram
-    processors; written to seq[length] (kd_gen_select)."""
+    processors; written to seq[length] (length = cur[0], then incremented, when cur is given)
+    (kd_gen_select)."""
     V = logits.shape[-1]
     ws = _workspace(("gen_select", _stream()), V, logits.device)
-    NV.call("kd_gen_select", logits.data_ptr(), V, seq.data_ptr(), int(length), float(repetition_penalty),
+    NV.call("kd_gen_select", logits.data_ptr(), V, seq.data_ptr(), int(length), _ptr(cur), float(repetition_penalty),
             int(no_repeat_ngram_size), ws.data_ptr(), ws.numel(), _ptr(out), _stream())
+
+
+def rope_row(cos: torch.Tensor, sin: torch.Tensor, cur: torch.Tensor, cos_row: torch.Tensor, sin_row: torch.Tensor):
+    """cos/sin row of position cur[0] - 1 into the one-row buffers (kd_rope_row)."""
+    NV.call("kd_rope_row", cos.data_ptr(), sin.data_ptr(), cos.shape[1], cur.data_ptr(), cos_row.data_ptr(),
+            sin_row.data_ptr(), _stream())

@@ -41,8 +41,9 @@ def test_oracle_matches_transformers_processors(penalty, ngram):
 def test_abi_rejects_bad_arguments():
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import _native as N
     lib = N.lib()
-    assert lib.kd_gen_select(None, 10, None, 1, 1.2, 2, None, 0, None, None) == 7
-    assert lib.kd_attn_decode(None, None, None, None, 2, 1, 64, 64, 8, 4, None) == 7
+    assert lib.kd_gen_select(None, 10, None, 1, None, 1.2, 2, None, 0, None, None) == 7
+    assert lib.kd_attn_decode(None, None, None, None, None, None, 2, 1, 64, 64, 8, 4, None, None, 0, None) == 7
+    assert lib.kd_gemv(None, None, 8, None, None, 4, 8, 0, 0, None) == 7
 
 
 # ----------------------------------------------------------------------------- GPU ----
@@ -56,7 +57,12 @@ def test_gpu_gen_select_matches_oracle(penalty, ngram, dev):
         lg = torch.from_numpy(scores).bfloat16()
         s = torch.tensor(seq + [0], dtype=torch.int64, device=dev)
         out = torch.empty(1, dtype=torch.int64, device=dev)
-        ops.gen_select(lg.to(dev)[None], s, len(seq), penalty, ngram, out=out)
+        if seed % 2:   # the device-counter form used inside the captured decode step
+            cur = torch.tensor([len(seq)], dtype=torch.int32, device=dev)
+            ops.gen_select(lg.to(dev)[None], s, 0, penalty, ngram, out=out, cur=cur)
+            assert int(cur) == len(seq) + 1
+        else:
+            ops.gen_select(lg.to(dev)[None], s, len(seq), penalty, ngram, out=out)
         want = G.select(lg.float().numpy(), seq, penalty, ngram)
         assert int(out) == want == int(s[-1])
 
@@ -70,7 +76,12 @@ def test_gpu_attn_decode_matches_torch(hd, H, HKV, n, dev):
     q = torch.randn(H, hd, generator=g).bfloat16()
     kc = torch.randn(HKV, smax, hd, generator=g).bfloat16()
     vc = torch.randn(HKV, smax, hd, generator=g).bfloat16()
-    o = ops.attn_decode(q.to(dev), kc.to(dev), vc.to(dev), n, hd).float().cpu().view(H, hd)
+    kcd, vcd = kc.to(dev), vc.to(dev)
+    kn, vn = kc[:, n - 1].to(dev), vc[:, n - 1].to(dev)
+    kcd[:, n - 1] = 0     # the kernel must take the token's own row from k_new / v_new ...
+    vcd[:, n - 1] = 0
+    o = ops.attn_decode(q.to(dev), kn, vn, kcd, vcd, n, hd).float().cpu().view(H, hd)
+    assert torch.equal(kcd[:, n - 1].cpu(), kc[:, n - 1]) and torch.equal(vcd[:, n - 1].cpu(), vc[:, n - 1])  # ... and store it
     rep = H // HKV
     k = kc[:, :n].float().repeat_interleave(rep, 0)
     v = vc[:, :n].float().repeat_interleave(rep, 0)
@@ -95,6 +106,11 @@ def test_gpu_generate_matches_oracle_teacher_forced(dev):
     b = synthetic_batch(1, dev, L=1536, seed=9, pixel_dtype=torch.bfloat16, cpu_rng=True)
     out, steps = generate(model, b["depth_input_ids"], b["depth_pixel_values"], b["image_sizes"], max_new_tokens=12,
                           repetition_penalty=1.2, no_repeat_ngram_size=2, eos_token_id=(), return_logits=True)
+    out_e, steps_e = generate(model, b["depth_input_ids"], b["depth_pixel_values"], b["image_sizes"], max_new_tokens=12,
+                              repetition_penalty=1.2, no_repeat_ngram_size=2, eos_token_id=(), return_logits=True,
+                              graph=False)
+    assert torch.equal(out, out_e)                       # graph replay == eager launches, bit for bit
+    assert all(torch.equal(a, b_) for a, b_ in zip(steps, steps_e))
     seq = out[0].cpu().tolist()
     L = 1536
     assert len(seq) == L + 12 and len(steps) == 12
@@ -107,3 +123,46 @@ def test_gpu_generate_matches_oracle_teacher_forced(dev):
         assert cos > 0.999, (t, float(cos))
         assert (got - want).abs().max() < 0.05 * want.abs().max() + 0.05, t
         assert seq[L + t] == G.select(lg.float().cpu()[0].numpy(), seq[:L + t], 1.2, 2), t
+
+
+@pytest.mark.gpu
+def test_gpu_generate_stops_after_eos(dev):
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.generation import generate
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import (
+        LlavaOnevisionModel, tiny_config)
+    model = LlavaOnevisionModel(tiny_config(False), dev, seed=5, cpu_rng=True)
+    b = synthetic_batch(1, dev, L=1536, seed=9, pixel_dtype=torch.bfloat16, cpu_rng=True)
+    full = generate(model, b["depth_input_ids"], b["depth_pixel_values"], b["image_sizes"], max_new_tokens=8,
+                    repetition_penalty=1.2, no_repeat_ngram_size=2, eos_token_id=())[0].cpu().tolist()
+    eos = full[1536 + 3]   # pretend the 4th generated token is EOS
+    cut = generate(model, b["depth_input_ids"], b["depth_pixel_values"], b["image_sizes"], max_new_tokens=8,
+                   repetition_penalty=1.2, no_repeat_ngram_size=2, eos_token_id=(eos,))[0].cpu().tolist()
+    first = full[1536:].index(eos)
+    assert cut == full[:1536 + first + 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K,epi", [(1152, 896, "bias"), (896, 896, "residual"), (4864, 896, "swiglu"),
+                                      (896, 4864, "residual"), (151936, 896, "none"), (5, 24, "none")])
+def test_gpu_gemv_matches_torch(N, K, epi, dev):
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(N + K)
+    rows = 2 * N if epi == "swiglu" else N
+    w = (torch.randn(rows, K + 8, generator=g) * 0.05).bfloat16()[:, :K]   # row stride > K (span views)
+    x = torch.randn(1, K, generator=g).bfloat16()
+    e = torch.randn(1, N, generator=g).bfloat16()
+    acc = x.float() @ w.float().t()
+    if epi == "swiglu":
+        ref = torch.nn.functional.silu(acc[:, :N]) * acc[:, N:]
+        got = ops.gemv(x.to(dev), w.to(dev), swiglu_inter=N)
+    elif epi == "bias":
+        ref = acc + e.float()
+        got = ops.gemv(x.to(dev), w.to(dev), bias=e.view(-1).to(dev))
+    elif epi == "residual":
+        ref = acc + e.float()
+        got = ops.gemv(x.to(dev), w.to(dev), residual=e.to(dev))
+    else:
+        ref = acc
+        got = ops.gemv(x.to(dev), w.to(dev))
+    torch.testing.assert_close(got.float().cpu(), ref, rtol=1e-2, atol=1e-2)
