@@ -98,22 +98,41 @@ __global__ void __launch_bounds__(NT) k_attn_decode_part(const bf16* __restrict_
     }
 }
 
+constexpr int MAX_CH = 512;   // chunks per head (smax <= 32768)
+
+// Merge the nch partials of head h: chunk maxima and weights staged in LDS (one load round
+// trip), then 256 threads = HD dims x (256 / HD) chunk groups accumulate in parallel.
 template <int HD>
-__global__ void __launch_bounds__(HD) k_attn_decode_combine(const float* __restrict__ part, int nch,
+__global__ void __launch_bounds__(NT) k_attn_decode_combine(const float* __restrict__ part, int nch,
                                                             bf16* __restrict__ o) {
-    const int h = blockIdx.x, d = threadIdx.x;
+    __shared__ float ms[MAX_CH], red[8], acc_s[NT];
+    const int h = blockIdx.x;
     const float* pp = part + (size_t)h * nch * (HD + 2);
     float m = -INFINITY;
-    for (int c = 0; c < nch; ++c) m = fmaxf(m, pp[(size_t)c * (HD + 2)]);
-    float l = 0.f, acc = 0.f;
-    for (int c = 0; c < nch; ++c) {
-        const float* q = pp + (size_t)c * (HD + 2);
-        if (q[0] == -INFINITY) continue;
-        const float w = __expf(q[0] - m);
-        l += w * q[1];
-        acc += w * q[2 + d];
+    for (int c = threadIdx.x; c < nch; c += NT) {
+        ms[c] = pp[(size_t)c * (HD + 2)];
+        m = fmaxf(m, ms[c]);
     }
-    o[(size_t)h * HD + d] = (bf16)(acc / l);
+    m = block_max<NT / 64>(m, red);
+    float l = 0.f;
+    for (int c = threadIdx.x; c < nch; c += NT) {
+        const float w = ms[c] == -INFINITY ? 0.f : __expf(ms[c] - m);
+        ms[c] = w;
+        l += w * pp[(size_t)c * (HD + 2) + 1];
+    }
+    l = block_sum<NT / 64>(l, red);   // barriers publish the weights in ms[]
+    constexpr int G = NT / HD;
+    const int d = threadIdx.x % HD, g = threadIdx.x / HD;
+    float acc = 0.f;
+    for (int c = g; c < nch; c += G) acc += ms[c] * pp[(size_t)c * (HD + 2) + 2 + d];
+    acc_s[threadIdx.x] = acc;
+    __syncthreads();
+    if (g == 0) {
+        float tsum = 0.f;
+#pragma unroll
+        for (int i = 0; i < G; ++i) tsum += acc_s[i * HD + d];
+        o[(size_t)h * HD + d] = (bf16)(tsum / l);
+    }
 }
 
 // Decode GEMV: y[n] = epilogue(sum_k x[k] * W[n][k]) for one token row, one wave per output
@@ -152,6 +171,38 @@ __global__ void __launch_bounds__(NT) k_gemv(const bf16* __restrict__ x, const b
     }
 }
 
+// Row-per-workgroup form of k_gemv for few output rows with long K (o_proj / down_proj of the
+// 0.5B student: N = 896, K up to 4864): 256 threads split K, block reduction, so N workgroups
+// instead of N / 4 keep every CU streaming.
+template <int EPI>
+__global__ void __launch_bounds__(NT) k_gemv_rows(const bf16* __restrict__ x, const bf16* __restrict__ W, int64_t ldw,
+                                                  const bf16* __restrict__ extra, bf16* __restrict__ y, int K, int I) {
+    __shared__ float red[8];
+    const int n = blockIdx.x;
+    const bf16* r0 = W + (size_t)n * ldw;
+    const bf16* r1 = W + (size_t)(I + n) * ldw;
+    float a0 = 0.f, a1 = 0.f;
+    for (int k = threadIdx.x * 8; k < K; k += NT * 8) {
+        const bf16x8 xv = *(const bf16x8*)(x + k);
+        const bf16x8 w0 = *(const bf16x8*)(r0 + k);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a0 += (float)xv[e] * (float)w0[e];
+        if constexpr (EPI == 3) {
+            const bf16x8 w1 = *(const bf16x8*)(r1 + k);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a1 += (float)xv[e] * (float)w1[e];
+        }
+    }
+    a0 = block_sum<NT / 64>(a0, red);
+    if constexpr (EPI == 3) a1 = block_sum<NT / 64>(a1, red);
+    if (threadIdx.x == 0) {
+        float v = a0;
+        if constexpr (EPI == 1 || EPI == 2) v += (float)extra[n];
+        if constexpr (EPI == 3) v = a0 / (1.f + __expf(-a0)) * a1;
+        y[n] = (bf16)v;
+    }
+}
+
 // One workgroup of 1024 threads: flags in the workspace (bit 0 = seen, bit 1 = banned), then
 // the processed-score argmax.  seq [len + 1] int64 (the new token is written at seq[len]).
 __global__ void __launch_bounds__(1024) k_gen_select(const bf16* __restrict__ logits, int V, int64_t* __restrict__ seq,
@@ -160,7 +211,11 @@ __global__ void __launch_bounds__(1024) k_gen_select(const bf16* __restrict__ lo
     __shared__ float sv[16];
     __shared__ int si[16];
     if (cur_dev) len = *cur_dev;
-    for (int i = threadIdx.x; i < V; i += blockDim.x) flags[i] = 0;
+    {   // clear the flags, 16 B per store (flags is 256-B aligned workspace)
+        const int v16 = V >> 4;
+        for (int i = threadIdx.x; i < v16; i += blockDim.x) ((u32x4*)flags)[i] = u32x4{0u, 0u, 0u, 0u};
+        for (int i = (v16 << 4) + threadIdx.x; i < V; i += blockDim.x) flags[i] = 0;
+    }
     __syncthreads();
     // RepetitionPenaltyLogitsProcessor: every id of the sequence (prompt + generated)
     if (penalty != 1.0f)
@@ -183,13 +238,19 @@ __global__ void __launch_bounds__(1024) k_gen_select(const bf16* __restrict__ lo
     __syncthreads();
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < V; i += blockDim.x) {
-        float s = (float)logits[i];
-        const uint8_t f = flags[i];
+    auto consider = [&](int i, float s, uint32_t f) {
         if (f & 1) s = s < 0.f ? __fmul_rn(s, penalty) : __fdiv_rn(s, penalty);
         if (f & 2) s = -INFINITY;
         if (s > best || (s == best && i < bi)) { best = s; bi = i; }   // NaN never wins
+    };
+    const int v8 = ((uintptr_t)logits & 15) == 0 ? V >> 3 : 0;   // 8 logits (16 B) + 8 flags per step
+    for (int c = threadIdx.x; c < v8; c += blockDim.x) {
+        const bf16x8 lv = ((const bf16x8*)logits)[c];
+        const u32x2 fv = ((const u32x2*)flags)[c];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) consider(c * 8 + e, (float)lv[e], ((e < 4 ? fv.x : fv.y) >> (8 * (e & 3))) & 255u);
     }
+    for (int i = (v8 << 3) + threadIdx.x; i < V; i += blockDim.x) consider(i, (float)logits[i], flags[i]);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const float ov = __shfl_xor(best, off, 64);
@@ -242,7 +303,8 @@ int launch_attn_decode(const void* q, const void* k_new, const void* v_new, void
     KD_CHECK_SHAPE(hd == 64 || hd == 128, "attn_decode: head dim must be 64 or 128");
     KD_CHECK_SHAPE(hdp >= hd && hdp % 8 == 0, "attn_decode: hdp must be >= hd and a multiple of 8");
     KD_CHECK_SHAPE(H > 0 && HKV > 0 && H % HKV == 0, "attn_decode: heads must be a multiple of kv heads");
-    KD_CHECK_SHAPE(smax > 0 && (cur_dev || (n > 0 && n <= smax)), "attn_decode: need 0 < n <= smax");
+    KD_CHECK_SHAPE(smax > 0 && smax <= MAX_CH * CH && (cur_dev || (n > 0 && n <= smax)),
+                   "attn_decode: need 0 < n <= smax <= 32768");
     KD_CHECK_ALIGN(q, 16, "attn_decode: q misaligned");
     KD_CHECK_ALIGN(kc, 16, "attn_decode: k cache misaligned");
     KD_CHECK_ALIGN(k_new, 16, "attn_decode: k_new misaligned");
@@ -254,11 +316,11 @@ int launch_attn_decode(const void* q, const void* k_new, const void* v_new, void
     if (hd == 64) {
         hipLaunchKernelGGL(k_attn_decode_part<64>, dim3(H, nch), dim3(NT), 0, s, (const bf16*)q, (const bf16*)k_new,
                            (const bf16*)v_new, (bf16*)kc, (bf16*)vc, part, H, HKV, hdp, smax, n, cur_dev, scale);
-        hipLaunchKernelGGL(k_attn_decode_combine<64>, dim3(H), dim3(64), 0, s, part, nch, (bf16*)o);
+        hipLaunchKernelGGL(k_attn_decode_combine<64>, dim3(H), dim3(NT), 0, s, part, nch, (bf16*)o);
     } else {
         hipLaunchKernelGGL(k_attn_decode_part<128>, dim3(H, nch), dim3(NT), 0, s, (const bf16*)q, (const bf16*)k_new,
                            (const bf16*)v_new, (bf16*)kc, (bf16*)vc, part, H, HKV, hdp, smax, n, cur_dev, scale);
-        hipLaunchKernelGGL(k_attn_decode_combine<128>, dim3(H), dim3(128), 0, s, part, nch, (bf16*)o);
+        hipLaunchKernelGGL(k_attn_decode_combine<128>, dim3(H), dim3(NT), 0, s, part, nch, (bf16*)o);
     }
     KD_LAUNCH_CHECK("k_attn_decode");
     return KD_OK;
@@ -275,6 +337,17 @@ int launch_gemv(const void* x, const void* W, int64_t ldw, const void* extra, vo
     const size_t lds = (size_t)K * sizeof(float);
     hipStream_t s = as_stream(stream);
     const bf16 *xb = (const bf16*)x, *Wb = (const bf16*)W, *eb = (const bf16*)extra;
+    if (N < 4096 && K >= 512) {   // few rows: one workgroup per row, K split over 256 threads
+        KD_CHECK_ALIGN(x, 16, "gemv: x misaligned");
+        switch (epi) {
+            case 0: hipLaunchKernelGGL(k_gemv_rows<0>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I); break;
+            case 1: hipLaunchKernelGGL(k_gemv_rows<1>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I); break;
+            case 2: hipLaunchKernelGGL(k_gemv_rows<2>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I); break;
+            default: hipLaunchKernelGGL(k_gemv_rows<3>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I);
+        }
+        KD_LAUNCH_CHECK("k_gemv_rows");
+        return KD_OK;
+    }
     switch (epi) {
         case 0: hipLaunchKernelGGL(k_gemv<0>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
         case 1: hipLaunchKernelGGL(k_gemv<1>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
