@@ -294,11 +294,12 @@ size_t kd_attn_decode_workspace_size(int H, int hd, int smax);
 int kd_attn_decode(const void* q, const void* k_new, const void* v_new, void* k_cache, void* v_cache, void* o,
                    int H, int HKV, int hd, int hdp, int smax, int n, const int32_t* cur_dev, void* workspace,
                    size_t workspace_bytes, void* stream);
-/* Decode GEMV (one token row through an nn.Linear): y[N] bf16 = epilogue(W[N, K] x[K]), fp32
+/* Decode GEMV (one token row through an nn.Linear): y[N] bf16 = epilogue(W[N, K] x'[K]), fp32
  * accumulation; epilogue 0 none, 1 + bias[N], 2 + residual[N] (both in `extra`), 3 SwiGLU over the
- * adjacent gate|up weight: y[n] = silu(W[n] x) * (W[inter + n] x), N = inter. */
+ * adjacent gate|up weight: y[n] = silu(W[n] x') * (W[inter + n] x'), N = inter.  x' = x, or with
+ * norm_w the Qwen2RMSNorm of x (weight norm_w, eps) as kd_norm_fwd computes it (fused prologue). */
 int kd_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epilogue,
-            int inter, void* stream);
+            int inter, const void* norm_w, float eps, void* stream);
 int kd_gen_select(const void* logits, int V, int64_t* seq, int len, int32_t* cur_dev, float repetition_penalty,
                   int no_repeat_ngram, void* workspace, size_t workspace_bytes, int64_t* out, void* stream);
 int kd_rope_row(const float* cos_table, const float* sin_table, int hh, const int32_t* cur_dev, float* cos_row,

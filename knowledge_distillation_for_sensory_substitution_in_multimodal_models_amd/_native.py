@@ -125,7 +125,7 @@ SIGNATURES = {
     "kd_image_resize_workspace_size": (_sz, [_i32, _i32, _i32, _i32]),
     "kd_attn_decode_workspace_size": (_sz, [_i32, _i32, _i32]),
     "kd_attn_decode": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp]),
-    "kd_gemv": (_i32, [_vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
+    "kd_gemv": (_i32, [_vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _f32, _vp]),
     "kd_gen_select": (_i32, [_vp, _i32, _vp, _i32, _vp, _f32, _i32, _vp, _sz, _vp, _vp]),
     "kd_rope_row": (_i32, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "kd_image_resize_u8": (_i32, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _sz, _vp]),

@@ -62,7 +62,7 @@ int launch_attn_decode(const void* q, const void* k_new, const void* v_new, void
                        int HKV, int hd, int hdp, int smax, int n, const int* cur_dev, void* ws, size_t ws_bytes,
                        void* stream);
 int launch_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epi, int I,
-                void* stream);
+                const void* norm_w, float eps, void* stream);
 int launch_gen_select(const void* logits, int V, int64_t* seq, int len, int* cur_dev, float penalty, int ngram,
                       void* flags_ws, size_t ws_bytes, int64_t* out, void* stream);
 int launch_rope_row(const float* cos_t, const float* sin_t, int hh, const int* cur_dev, float* cos_row, float* sin_row,
@@ -179,8 +179,8 @@ int kd_attn_decode(const void* q, const void* kn, const void* vn, void* kc, void
     return kd::launch_attn_decode(q, kn, vn, kc, vc, o, H, HKV, hd, hdp, smax, n, cur, ws, wsb, s);
 }
 int kd_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epi, int I,
-            void* s) {
-    return kd::launch_gemv(x, W, ldw, extra, y, N, K, epi, I, s);
+            const void* norm_w, float eps, void* s) {
+    return kd::launch_gemv(x, W, ldw, extra, y, N, K, epi, I, norm_w, eps, s);
 }
 int kd_gen_select(const void* logits, int V, int64_t* seq, int len, int32_t* cur, float penalty, int ngram, void* ws,
                   size_t wsb, int64_t* out, void* s) {

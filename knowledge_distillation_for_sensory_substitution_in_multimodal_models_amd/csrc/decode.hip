@@ -135,6 +135,24 @@ __global__ void __launch_bounds__(NT) k_attn_decode_combine(const float* __restr
     }
 }
 
+// Stage the token row x[K] into LDS as fp32; with norm_w, as kd_norm_fwd's RMSNorm output
+// (bf16(x * rsqrt(mean(x^2) + eps) * w), rounded to bf16 as the unfused kernel stores it), so the
+// norm costs no launch of its own.
+__device__ __forceinline__ void stage_x(const bf16* __restrict__ x, const bf16* __restrict__ norm_w, float eps, int K,
+                                        float* xs, float* red) {
+    float ss = 0.f;
+    for (int k = threadIdx.x; k < K; k += NT) {
+        const float v = (float)x[k];
+        xs[k] = v;
+        ss += v * v;
+    }
+    if (norm_w) {
+        const float rstd = rsqrtf(block_sum<NT / 64>(ss, red) / K + eps);
+        for (int k = threadIdx.x; k < K; k += NT) xs[k] = (float)(bf16)(xs[k] * rstd * (float)norm_w[k]);
+    }
+    __syncthreads();
+}
+
 // Decode GEMV: y[n] = epilogue(sum_k x[k] * W[n][k]) for one token row, one wave per output
 // (two weight rows, n and I + n, for the SwiGLU form).  Weight rows are read once, 16 B per lane,
 // so the decode step streams its weights at HBM rate instead of running 256-row GEMM tiles at
@@ -142,10 +160,10 @@ __global__ void __launch_bounds__(NT) k_attn_decode_combine(const float* __restr
 template <int EPI>
 __global__ void __launch_bounds__(NT) k_gemv(const bf16* __restrict__ x, const bf16* __restrict__ W, int64_t ldw,
                                              const bf16* __restrict__ extra, bf16* __restrict__ y, int N, int K,
-                                             int I) {
+                                             int I, const bf16* __restrict__ norm_w, float eps) {
     extern __shared__ float xs[];
-    for (int k = threadIdx.x; k < K; k += NT) xs[k] = (float)x[k];
-    __syncthreads();
+    __shared__ float red[8];
+    stage_x(x, norm_w, eps, K, xs, red);
     const int n = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (n >= N) return;
     const bf16* r0 = W + (size_t)n * ldw;
@@ -176,21 +194,23 @@ __global__ void __launch_bounds__(NT) k_gemv(const bf16* __restrict__ x, const b
 // instead of N / 4 keep every CU streaming.
 template <int EPI>
 __global__ void __launch_bounds__(NT) k_gemv_rows(const bf16* __restrict__ x, const bf16* __restrict__ W, int64_t ldw,
-                                                  const bf16* __restrict__ extra, bf16* __restrict__ y, int K, int I) {
+                                                  const bf16* __restrict__ extra, bf16* __restrict__ y, int K, int I,
+                                                  const bf16* __restrict__ norm_w, float eps) {
+    extern __shared__ float xs[];
     __shared__ float red[8];
+    stage_x(x, norm_w, eps, K, xs, red);
     const int n = blockIdx.x;
     const bf16* r0 = W + (size_t)n * ldw;
     const bf16* r1 = W + (size_t)(I + n) * ldw;
     float a0 = 0.f, a1 = 0.f;
     for (int k = threadIdx.x * 8; k < K; k += NT * 8) {
-        const bf16x8 xv = *(const bf16x8*)(x + k);
         const bf16x8 w0 = *(const bf16x8*)(r0 + k);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) a0 += (float)xv[e] * (float)w0[e];
+        for (int e = 0; e < 8; ++e) a0 += xs[k + e] * (float)w0[e];
         if constexpr (EPI == 3) {
             const bf16x8 w1 = *(const bf16x8*)(r1 + k);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) a1 += (float)xv[e] * (float)w1[e];
+            for (int e = 0; e < 8; ++e) a1 += xs[k + e] * (float)w1[e];
         }
     }
     a0 = block_sum<NT / 64>(a0, red);
@@ -327,7 +347,7 @@ int launch_attn_decode(const void* q, const void* k_new, const void* v_new, void
 }
 
 int launch_gemv(const void* x, const void* W, int64_t ldw, const void* extra, void* y, int N, int K, int epi, int I,
-                void* stream) {
+                const void* norm_w, float eps, void* stream) {
     KD_CHECK_ARG(x && W && y, "gemv: null pointer");
     KD_CHECK_ARG(epi >= 0 && epi <= 3 && (epi == 0 || epi == 3 || extra), "gemv: epilogue 0..3 (1, 2 need extra)");
     KD_CHECK_SHAPE(N > 0 && K > 0 && K % 8 == 0 && K <= 16384 && ldw >= K && ldw % 8 == 0,
@@ -336,23 +356,22 @@ int launch_gemv(const void* x, const void* W, int64_t ldw, const void* extra, vo
     const dim3 grid((N + NT / 64 - 1) / (NT / 64));
     const size_t lds = (size_t)K * sizeof(float);
     hipStream_t s = as_stream(stream);
-    const bf16 *xb = (const bf16*)x, *Wb = (const bf16*)W, *eb = (const bf16*)extra;
+    const bf16 *xb = (const bf16*)x, *Wb = (const bf16*)W, *eb = (const bf16*)extra, *nw = (const bf16*)norm_w;
     if (N < 4096 && K >= 512) {   // few rows: one workgroup per row, K split over 256 threads
-        KD_CHECK_ALIGN(x, 16, "gemv: x misaligned");
         switch (epi) {
-            case 0: hipLaunchKernelGGL(k_gemv_rows<0>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I); break;
-            case 1: hipLaunchKernelGGL(k_gemv_rows<1>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I); break;
-            case 2: hipLaunchKernelGGL(k_gemv_rows<2>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I); break;
-            default: hipLaunchKernelGGL(k_gemv_rows<3>, dim3(N), dim3(NT), 0, s, xb, Wb, ldw, eb, (bf16*)y, K, I);
+            case 0: hipLaunchKernelGGL(k_gemv_rows<0>, dim3(N), dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, K, I, nw, eps); break;
+            case 1: hipLaunchKernelGGL(k_gemv_rows<1>, dim3(N), dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, K, I, nw, eps); break;
+            case 2: hipLaunchKernelGGL(k_gemv_rows<2>, dim3(N), dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, K, I, nw, eps); break;
+            default: hipLaunchKernelGGL(k_gemv_rows<3>, dim3(N), dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, K, I, nw, eps);
         }
         KD_LAUNCH_CHECK("k_gemv_rows");
         return KD_OK;
     }
     switch (epi) {
-        case 0: hipLaunchKernelGGL(k_gemv<0>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
-        case 1: hipLaunchKernelGGL(k_gemv<1>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
-        case 2: hipLaunchKernelGGL(k_gemv<2>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I); break;
-        default: hipLaunchKernelGGL(k_gemv<3>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I);
+        case 0: hipLaunchKernelGGL(k_gemv<0>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I, nw, eps); break;
+        case 1: hipLaunchKernelGGL(k_gemv<1>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I, nw, eps); break;
+        case 2: hipLaunchKernelGGL(k_gemv<2>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I, nw, eps); break;
+        default: hipLaunchKernelGGL(k_gemv<3>, grid, dim3(NT), lds, s, xb, Wb, ldw, eb, (bf16*)y, N, K, I, nw, eps);
     }
     KD_LAUNCH_CHECK("k_gemv");
     return KD_OK;

@@ -10,7 +10,7 @@ Drop-in for the call the reference's evaluation makes on the trained student
 only applies it when sampling).  The prompt runs through the same forward as training
 (LlavaOnevisionModel.forward: SigLIP, projector, anyres pack, Qwen2), whose roped keys and values
 seed a per-layer KV cache [HKV, L + max_new_tokens, hd]; each new token then runs one row through
-every layer (kd_norm_fwd, kd_gemv with bias / residual / SwiGLU epilogues, kd_qkv_split with its
+every layer (kd_gemv with the RMSNorms fused in front and bias / residual / SwiGLU epilogues, kd_qkv_split with its
 RoPE row, split-KV kd_attn_decode) and kd_gen_select picks it on the device.  The position lives in a device counter, so
 every launch of a step has fixed arguments: the first step runs eagerly, the step is captured
 once as a HIP graph (torch.cuda.CUDAGraph) and replayed for the rest; steps past an EOS are
@@ -23,7 +23,10 @@ import torch
 
 from . import ops
 
-EOS_TOKEN_IDS = (151645,)   # <|im_end|>: generation_config.eos_token_id of the -ov-hf chat checkpoints
+import os
+
+EOS_TOKEN_IDS = (151645,)
+FUSE_NORM = os.environ.get("KD_DECODE_FUSE_NORM", "1") != "0"   # RMSNorm fused into the decode GEMVs (A/B knob)   # <|im_end|>: generation_config.eos_token_id of the -ov-hf chat checkpoints
 
 
 @torch.no_grad()
@@ -85,14 +88,22 @@ def generate(model, input_ids: torch.Tensor, pixel_values: torch.Tensor, image_s
         ops.rope_row(cos, sin, cur, cos_row, sin_row)
         x = ops.embed_assemble(tok, src, table, None, None, model.err)
         for i, (w_in, Wqkv, bqkv, Wo, w_post, Wgu, Wdown) in enumerate(layers):
-            h, _, _ = ops.norm_fwd(x, w_in, None, T.eps, rms=True, save_stats=False)
-            qkv = ops.gemv(h, Wqkv, bias=bqkv)
+            if FUSE_NORM:
+                qkv = ops.gemv(x, Wqkv, bias=bqkv, norm_w=w_in, eps=T.eps)      # input_layernorm fused
+            else:
+                h, _, _ = ops.norm_fwd(x, w_in, None, T.eps, rms=True, save_stats=False)
+                qkv = ops.gemv(h, Wqkv, bias=bqkv)
             q, k, v = ops.qkv_split(qkv, 1, 1, nq, nkv, hd, hd, cos_row, sin_row)
             o = ops.attn_decode(q.view(nq, hd), k.view(nkv, hd), v.view(nkv, hd), kc[i], vc[i], 0, hd, cur=cur)
             x_mid = ops.gemv(o, Wo, residual=x)
-            h2, _, _ = ops.norm_fwd(x_mid, w_post, None, T.eps, rms=True, save_stats=False)
-            a = ops.gemv(h2, Wgu, swiglu_inter=T.inter)
+            if FUSE_NORM:
+                a = ops.gemv(x_mid, Wgu, swiglu_inter=T.inter, norm_w=w_post, eps=T.eps)  # post_attention_layernorm
+            else:
+                h2, _, _ = ops.norm_fwd(x_mid, w_post, None, T.eps, rms=True, save_stats=False)
+                a = ops.gemv(h2, Wgu, swiglu_inter=T.inter)
             x = ops.gemv(a, Wdown, residual=x_mid)
+        # final norm as its own launch: fused into the 38k-workgroup lm_head GEMV it would be recomputed
+        # by every workgroup (measured slower)
         hn, _, _ = ops.norm_fwd(x, P[lp + "norm.weight"], None, T.eps, rms=True, save_stats=False)
         lg = ops.gemv(hn, model.lm_head_weight())
         ops.gen_select(lg, seq, 0, repetition_penalty, no_repeat_ngram_size, out=tok, cur=cur)

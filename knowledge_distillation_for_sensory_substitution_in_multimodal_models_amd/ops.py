@@ -503,9 +503,11 @@ def attn_decode(q: torch.Tensor, k_new: torch.Tensor, v_new: torch.Tensor, k_cac
     return out
 
 
-def gemv(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, swiglu_inter: int = 0) -> torch.Tensor:
+def gemv(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, swiglu_inter: int = 0, norm_w=None,
+         eps: float = 1e-6) -> torch.Tensor:
     """One token row through a linear layer (kd_gemv): x [1, K] bf16, w [N, K] (row stride may
-    exceed K) -> [1, N] bf16 with an optional bias / residual / SwiGLU (w = gate|up, N = 2*inter)."""
+    exceed K) -> [1, N] bf16 with an optional bias / residual / SwiGLU (w = gate|up, N = 2*inter),
+    and with norm_w the RMSNorm of x fused in front."""
     K = x.shape[-1]
     epi, extra = 0, None
     if swiglu_inter:
@@ -518,7 +520,7 @@ def gemv(x: torch.Tensor, w: torch.Tensor, *, bias=None, residual=None, swiglu_i
             epi, extra = 2, residual
     y = torch.empty((1, N), dtype=torch.bfloat16, device=x.device)
     NV.call("kd_gemv", x.data_ptr(), w.data_ptr(), w.stride(0), _ptr(extra), y.data_ptr(), N, K, epi,
-            int(swiglu_inter), _stream())
+            int(swiglu_inter), _ptr(norm_w), float(eps), _stream())
     return y
 
 

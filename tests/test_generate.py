@@ -43,7 +43,7 @@ def test_abi_rejects_bad_arguments():
     lib = N.lib()
     assert lib.kd_gen_select(None, 10, None, 1, None, 1.2, 2, None, 0, None, None) == 7
     assert lib.kd_attn_decode(None, None, None, None, None, None, 2, 1, 64, 64, 8, 4, None, None, 0, None) == 7
-    assert lib.kd_gemv(None, None, 8, None, None, 4, 8, 0, 0, None) == 7
+    assert lib.kd_gemv(None, None, 8, None, None, 4, 8, 0, 0, None, 1e-6, None) == 7
 
 
 # ----------------------------------------------------------------------------- GPU ----
@@ -166,3 +166,18 @@ def test_gpu_gemv_matches_torch(N, K, epi, dev):
         ref = acc
         got = ops.gemv(x.to(dev), w.to(dev))
     torch.testing.assert_close(got.float().cpu(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K", [(1152, 896), (151936, 896), (4864, 896)])
+def test_gpu_gemv_fused_rmsnorm_matches_norm_then_gemv(N, K, dev):
+    """The fused RMSNorm prologue against kd_norm_fwd followed by the plain GEMV."""
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(K + N)
+    x = (torch.randn(1, K, generator=g) * 3).bfloat16().to(dev)
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).bfloat16().to(dev)
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16().to(dev)
+    h, _, _ = ops.norm_fwd(x, nw, None, 1e-6, rms=True, save_stats=False)
+    ref = ops.gemv(h, w).float()
+    got = ops.gemv(x, w, norm_w=nw, eps=1e-6).float()
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
