@@ -623,14 +623,39 @@ __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const floa
                         float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
                         float bc1, float bc2, const float* __restrict__ gscale) {
     const float gs = gscale ? *gscale : 1.f;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = g[i] * gs;
-        float pi = p[i] * (1.f - lr * wd);
-        const float mi = b1 * m[i] + (1.f - b1) * gi;
-        const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    auto step = [&](float& pi, float& mi, float& vi, float graw) {
+        const float gi = graw * gs;
+        pi = pi * (1.f - lr * wd);
+        mi = b1 * mi + (1.f - b1) * gi;
+        vi = b2 * vi + (1.f - b2) * gi * gi;
+        pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+    };
+    // 4 parameters per thread and iteration: 16-B loads / stores of p, g, m, v, 8-B bf16 stores
+    // (same per-element arithmetic as the scalar tail)
+    const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 && ((uintptr_t)pb & 7) == 0;
+    const int64_t n4 = vec ? n >> 2 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        f32x4 pv = ((const f32x4*)p)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
+        const f32x4 gv = ((const f32x4*)g)[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float pe = pv[e], me = mv[e], ve = vv[e];
+            step(pe, me, ve, gv[e]);
+            pv[e] = pe;
+            mv[e] = me;
+            vv[e] = ve;
+        }
+        ((f32x4*)m)[i] = mv;
+        ((f32x4*)v)[i] = vv;
+        ((f32x4*)p)[i] = pv;
+        ((bf16x4*)pb)[i] = bf16x4{(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
+    }
+    for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float pi = p[i], mi = m[i], vi = v[i];
+        step(pi, mi, vi, g[i]);
         m[i] = mi;
         v[i] = vi;
-        pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
         p[i] = pi;
         pb[i] = (bf16)pi;
     }

@@ -206,22 +206,25 @@ def test_ntxent_matches_oracle(dev):
     assert torch.allclose(dfs.cpu(), x.grad, rtol=1e-3, atol=1e-7)
 
 
-def test_adamw_matches_torch(dev):
+@pytest.mark.parametrize("n,off", [(10000, 0), (10003, 1)])   # 16-B vector path; unaligned scalar path
+def test_adamw_matches_torch(n, off, dev):
     ops = _ops()
-    n = 10000
     g = torch.Generator().manual_seed(23)
     p0 = torch.randn(n, generator=g)
     grads = [torch.randn(n, generator=g) for _ in range(3)]
     ref = p0.clone().requires_grad_(True)
     opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=0.01)
-    p = p0.clone().to(dev)
-    pb = torch.empty(n, dtype=torch.bfloat16, device=dev)
-    m = torch.zeros(n, device=dev)
-    v = torch.zeros(n, device=dev)
+    p = torch.empty(n + off, device=dev)[off:]
+    p.copy_(p0.to(dev))
+    pb = torch.empty(n + off, dtype=torch.bfloat16, device=dev)[off:]
+    m = torch.zeros(n + off, device=dev)[off:]
+    v = torch.zeros(n + off, device=dev)[off:]
+    gd = torch.empty(n + off, device=dev)[off:]
     for step, gr in enumerate(grads, 1):
         ref.grad = gr.clone()
         opt.step()
-        ops.adamw(p, pb, gr.to(dev), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+        gd.copy_(gr.to(dev))
+        ops.adamw(p, pb, gd, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
     assert torch.allclose(p.cpu(), ref.detach(), rtol=1e-6, atol=1e-7)
     assert torch.equal(pb.cpu(), ref.detach().bfloat16())
     out = torch.zeros(1, device=dev)
