@@ -1,6 +1,6 @@
 """KD training-step throughput on MI355X (BASELINE.json metric), one JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4] [--no-cpu-baseline] [--cpu-full]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 A step = one `training_step(batch)` + `loss.backward()` + `optimizer.step()` +
@@ -75,63 +75,161 @@ def build(cfg, dev):
     return m, opt
 
 
-def cpu_baseline(kind: str, phase: int, threads: int):
-    """Oracle (CPU fp32 restatement, `port`) KD step at bs=1, L=1536: full-width teacher and
-    student at depth 1 and 3 of every tower (depth 1 timed twice, after and before the
-    depth-3 run, min taken: the first run pays allocator/thread-pool warm-up), extrapolated
-    to 28/26 + 24/26 layers by the per-layer FLOP share of the depth 1 -> 3 delta (a
-    bounded ~40 s sample of the same workload)."""
+def host_cpu_info():
+    """(threads usable by this process, machine CPU count, CPU model): the process's
+    affinity capped by its cgroup CPU quota (a GPU box shares its host; OMP_NUM_THREADS
+    there is the box's CPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except Exception:
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp:
+        n = min(n, omp)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return n, os.cpu_count(), model
+
+
+def _oracle_step_time(kind, phase, depth, dtype, batch):
+    """One oracle KD step (fwd + bwd) at `depth` layers of every tower, full widths."""
     import torch
+    from dataclasses import replace
     from oracle.model import OracleLlava, kd_step_losses
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import (
         STUDENT_05B, TEACHER_7B, param_specs)
-    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
-    from dataclasses import replace
-    torch.set_num_threads(threads)
-    batch = synthetic_batch(1, "cpu", L=1536, seed=0, pixel_dtype=torch.float32, cpu_rng=True)
 
     def weights(cfg, seed):
         g = torch.Generator().manual_seed(seed)
         sd = {}
-        for s in param_specs(cfg):
-            shape = s.ckpt_shape or s.shape
-            if s.init == "ones":
-                sd[s.name] = torch.ones(shape)
-            elif s.init == "zeros":
-                sd[s.name] = torch.zeros(shape)
+        for s_ in param_specs(cfg):
+            shape = s_.ckpt_shape or s_.shape
+            if s_.init == "ones":
+                sd[s_.name] = torch.ones(shape, dtype=dtype)
+            elif s_.init == "zeros":
+                sd[s_.name] = torch.zeros(shape, dtype=dtype)
             else:
-                sd[s.name] = torch.empty(shape).normal_(0, 0.02, generator=g)
+                sd[s_.name] = torch.empty(shape).normal_(0, 0.02, generator=g).to(dtype)
         return sd
 
-    times = {}
-    for d in (1, 3, 1):
-        tc = replace(TEACHER_7B, vision=replace(TEACHER_7B.vision, layers=d), text=replace(TEACHER_7B.text, layers=d))
-        sc = replace(STUDENT_05B, vision=replace(STUDENT_05B.vision, layers=d), text=replace(STUDENT_05B.text, layers=d))
-        tsd, ssd = weights(tc, 1), weights(sc, 2)
-        train_vision = not (kind == "dt" and phase == 2)
-        for k, v in ssd.items():
-            v.requires_grad_(train_vision or not k.startswith("vision"))
-        teacher, student = OracleLlava(tsd, tc), OracleLlava(ssd, sc)
-        t0 = time.perf_counter()
-        total, _ = kd_step_losses(kind, teacher, student, batch, phase=phase)
-        total.backward()
-        times[d] = min(times.get(d, 1e30), time.perf_counter() - t0)
-        del tsd, ssd, teacher, student, total
-    # per-layer FLOP shares (fwd teacher, fwd+bwd student), L = 1536
-    L, NV = 1536, 1458
-    vit_layer = 2 * NV * (4 * 1152 ** 2 + 2 * 1152 * 4304) + 4 * 2 * 729 ** 2 * 1152
+    tc, sc = TEACHER_7B, STUDENT_05B
+    if depth is not None:
+        tc = replace(tc, vision=replace(tc.vision, layers=depth), text=replace(tc.text, layers=depth))
+        sc = replace(sc, vision=replace(sc.vision, layers=depth), text=replace(sc.text, layers=depth))
+    tsd, ssd = weights(tc, 1), weights(sc, 2)
+    train_vision = not (kind == "dt" and phase == 2)
+    for k, v in ssd.items():
+        v.requires_grad_(train_vision or not k.startswith("vision"))
+    b = dict(batch)
+    for k in ("rgb_pixel_values", "depth_pixel_values"):
+        b[k] = b[k].to(dtype)
+    teacher, student = OracleLlava(tsd, tc), OracleLlava(ssd, sc)
+    t0 = time.perf_counter()
+    total, _ = kd_step_losses(kind, teacher, student, b, phase=phase)
+    total.float().backward()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(kind: str, phase: int, threads: int, full: bool = False):
+    """The oracle (CPU torch restatement of the reference's step, kind `port`) at bs=1,
+    L=1536, full widths, in fp32 and bf16.  Default (bounded, ~1 min): depth 1 and 3 of
+    every tower, each timed twice (min), extrapolated to the full 26/28 + 26/24 layers by
+    the per-layer FLOP share of the depth 1 -> 3 delta.  full=True: one full-depth step."""
+    import torch
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    torch.set_num_threads(threads)
+    batch = synthetic_batch(1, "cpu", L=1536, seed=0, pixel_dtype=torch.float32, cpu_rng=True)
+    L = 1536
+    vit_layer = 2 * 1458 * (4 * 1152 ** 2 + 2 * 1152 * 4304) + 4 * 2 * 729 ** 2 * 1152
     t_layer = 2 * L * (2 * 3584 ** 2 + 2 * 3584 * 512 + 3 * 3584 * 18944) + 2 * L * L * 3584
     s_layer = 3 * (2 * L * (2 * 896 ** 2 + 2 * 896 * 128 + 3 * 896 * 4864) + 2 * L * L * 896)
-    s_vit = (3 if not (kind == "dt" and phase == 2) else 1) * vit_layer
-    parts = dict(t_vit=vit_layer, t_lm=t_layer, s_vit=s_vit, s_lm=s_layer)
+    parts = dict(t_vit=vit_layer, t_lm=t_layer, s_vit=(3 if not (kind == "dt" and phase == 2) else 1) * vit_layer,
+                 s_lm=s_layer)
     tot = sum(parts.values())
-    delta = max((times[3] - times[1]) / 2, 1e-6)   # one layer of every tower
     extra = {"t_vit": 25, "t_lm": 27, "s_vit": 25, "s_lm": 23}
-    t_full = times[1] + sum(delta * parts[k] / tot * extra[k] for k in parts)
-    return dict(value=round(1.0 / t_full, 5), unit="samples/s", cores=threads, kind="port",
-                sample=(f"oracle (CPU fp32 torch restatement) KD step bs=1 L=1536, measured at depth 1 "
-                        f"({times[1]:.2f} s, min of 2) and 3 ({times[3]:.2f} s) of every tower, extrapolated to the "
-                        f"full 28/26 + 24/26 layers by per-layer FLOP share: {t_full:.1f} s/sample"))
+    res = {}
+    for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        if full:   # one full-depth step (7B + 0.5B weights in host memory)
+            res[name] = dict(s_per_sample=round(_oracle_step_time(kind, phase, None, dt, batch), 2),
+                             measured="full depth")
+            continue
+        times = {}
+        for d in (1, 3, 1, 3):
+            times[d] = min(times.get(d, 1e30), _oracle_step_time(kind, phase, d, dt, batch))
+        delta = max((times[3] - times[1]) / 2, 1e-6)   # one layer of every tower
+        t_full = times[1] + sum(delta * parts[k] / tot * extra[k] for k in parts)
+        res[name] = dict(s_per_sample=round(t_full, 2), depth1_s=round(times[1], 2), depth3_s=round(times[3], 2))
+    n, ncpu, model = host_cpu_info()
+    v = res["fp32"]["s_per_sample"]
+    return dict(value=round(1.0 / v, 5), unit="samples/s", cores=threads, kind="port",
+                cpu_model=model, machine_cpus=ncpu, bf16=dict(value=round(1.0 / res["bf16"]["s_per_sample"], 5), **res["bf16"]),
+                fp32=res["fp32"],
+                sample=(f"oracle (CPU torch restatement of the reference step, pinned to its fixtures) KD step, bs=1, "
+                        f"L=1536, full widths, {threads} threads on {model}: "
+                        + ("one full-depth step" if full else
+                           "measured at depth 1 and 3 of every tower (min of 2 each), extrapolated to the full "
+                           "26/28 + 26/24 layers by per-layer FLOP share")
+                        + f"; value = fp32 ({v:.1f} s/sample), bf16 alongside ({res['bf16']['s_per_sample']:.1f} s/sample)"))
+
+
+def kd_loss_delta(m, batch, variant_T):
+    """The BASELINE metric's second half: this step's own GPU logits (copied to the host)
+    through the CPU oracle's loss functions vs the fused kernel's terms."""
+    import torch
+    from oracle import kd_losses as O
+    s3, t3 = m.last_logits
+    gpu = m.last_terms.tolist()
+    labels = batch["labels"].cpu()
+    s = s3.float().cpu()
+    t = t3.float().cpu() if t3 is not None else None
+    m.last_logits = None
+    variant, T = variant_T
+    out = {}
+    ce = float(O.causal_lm_ce(s, labels))
+    out["student_ce"] = (gpu[1], ce)
+    if t is not None:
+        out["teacher_ce"] = (gpu[2], float(O.causal_lm_ce(t, labels)))
+        if variant == "loca":
+            kd = float(O.loca_kd_term(t, s, labels, T=T))
+        elif variant == "kl":
+            kd = float(O.kl_mean_term(t, s, T))
+        else:
+            kd = float(O.kl_logtarget_term(t, s, T))
+        out["kd_term"] = (gpu[0], kd)
+    del s, t
+    return {k: dict(gpu=g, cpu=c, abs=abs(g - c), rel=abs(g - c) / abs(c) if c else None) for k, (g, c) in out.items()}
+
+
+def teacher_forward_rate(m, batch, reps=3):
+    """The north-star's teacher-forward fraction: the 7B teacher forward alone (vision,
+    projector, LM, lm_head), serialized on one stream, HIP events around it."""
+    import torch
+    B = batch["rgb_input_ids"].shape[0]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    with torch.no_grad():
+        m._teacher_forward(batch, False)
+        for e0, e1 in ev:
+            e0.record()
+            out = m._teacher_forward(batch, False)
+            e1.record()
+            del out
+    torch.cuda.synchronize()
+    ms = min(e0.elapsed_time(e1) for e0, e1 in ev)
+    L = 1536
+    vit = 2 * 1458 * 395.8e6 + 4 * 2 * 729 ** 2 * 1152 * 26 + 2 * 1458 * 0.677e6
+    fl = B * (vit + 2 * 1458 * (1152 * 3584 + 3584 * 3584) + 2 * L * 7070.6e6 + 2 * L * L * 3584 * 28)
+    tf = fl / (ms * 1e-3) / 1e12
+    return dict(ms=round(ms, 2), tflop=round(fl / 1e12, 2), tflops=round(tf, 1), frac_of_peak=round(tf / PEAK_BF16_TFLOPS, 4),
+                target_frac=0.40, measured="min of 3 serialized teacher forwards, HIP events on the main stream")
 
 
 def main():
@@ -142,10 +240,9 @@ def main():
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true", help="cpu_baseline: one full-depth step instead of depth 1/3")
     ap.add_argument("--no-timer", action="store_true", help="skip the serialized roofline pass (per-GEMM HIP events)")
-    ap.add_argument("--prefetch", action="store_true",
-                    help="run the next step's teacher forward one step ahead on its own stream (measured: no gain, "
-                         "the step is GPU-throughput-bound)")
+    ap.add_argument("--no-delta", action="store_true", help="skip kd_loss_delta (the CPU oracle on this step's logits)")
     ap.add_argument("--serial", action="store_true",
                     help="student forward on the main stream (no overlap with the teacher forward)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
@@ -168,19 +265,15 @@ def main():
     m.concurrent_student = not a.serial
     # two synthetic batches, alternated, so every step's teacher forward is a fresh one
     batches = [synthetic_batch(B, dev, L=1536, seed=rank * 2 + j) for j in range(2)]
-    prefetch = [a.prefetch and not a.serial]
 
     def step(i):
         loss = m.training_step(batches[i % 2], i)
         loss.backward()
-        if prefetch[0]:   # the next step's teacher forward, beside this step's backward + AdamW
-            m.prefetch_teacher(batches[(i + 1) % 2])
         opt.step()
         opt.zero_grad()
         return loss
 
-    # the step's main stream at the same high priority as its side streams (the teacher
-    # prefetch stream stays at normal priority)
+    # the step's main stream at the same high priority as its side streams
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import STREAM_PRIORITY_HIGH
     hp = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
     hp.wait_stream(torch.cuda.current_stream())
@@ -194,19 +287,22 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(a.warmup + i)
-    host_dt = time.perf_counter() - t0   # host enqueue time of the K steps (~dt: launch-bound)
+    host_dt = time.perf_counter() - t0   # host enqueue time of the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # roofline pass (untimed): two steps with the student forward serialized behind the
-    # teacher forward, every GEMM bracketed by HIP events on its launch stream, so a
-    # kernel's duration is its own and not shared with a concurrent stream
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    loss_v = float(loss.item())
+    # ---- after the timed region: roofline pass (two steps with the student forward
+    # serialized behind the teacher forward, every GEMM bracketed by HIP events on its launch
+    # stream, so a kernel's duration is its own and not shared with a concurrent stream)
     if not a.no_timer:
         m.concurrent_student = False
-        prefetch[0] = False
-        m._prefetched = None   # the roofline steps run every teacher GEMM inline, on the main stream
         ops.TIMER.reset()
         ops.TIMER.enabled = True
         for i in range(2):
@@ -214,11 +310,6 @@ def main():
         torch.cuda.synchronize()
         ops.TIMER.enabled = False
         m.concurrent_student = not a.serial
-        prefetch[0] = a.prefetch and not a.serial
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     samples = world * B * a.steps
     value = samples / dt
     tf_sample = step_tflops_per_sample(cfg["kind"], cfg["phase"])
@@ -234,26 +325,29 @@ def main():
         with open(a.shapes, "w") as f:
             json.dump(ops.TIMER.by_shape(top=200), f, indent=1)
     # the roofline kernel: the fused gate|up + SwiGLU GEMM (k_gemm8<K-major,K-major> SwiGLU build,
-    # one launch per call, 28 + 24 calls per step, ~40% of the step's GEMM time) -- a kernel of
-    # its own, so the rocprofv3 kernel trace's average for it is directly comparable
+    # one launch per call, 28 + 24 calls per step) -- a kernel of its own, so the rocprofv3
+    # kernel trace's average for it is directly comparable
     fwd = ops.TIMER.summary("gemm_kk_swiglu")
-    traffic = None   # PMC HBM bytes per forward-GEMM launch (tools/pmc_bench.sh, committed under profiles/)
-    tpath = REPO / "profiles" / "r01" / "pmc_traffic.json"
-    if tpath.exists():
-        fg = json.load(open(tpath)).get("roofline_kernel")
-        if fg:
-            traffic = round(fg["traffic_bytes"])
+    traffic = None   # PMC HBM bytes per launch of that kernel (tools/pmc_bench.sh -> profiles/)
+    for rd in ("r02", "r01"):
+        tpath = REPO / "profiles" / rd / "pmc_traffic.json"
+        if tpath.exists():
+            fg = json.load(open(tpath)).get("roofline_kernel")
+            if fg:
+                traffic = round(fg["traffic_bytes"])
+                break
     if fwd:
         ach = fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12
         roof = dict(bound="mfma", kernel="k_gemm8<false, false, 4> (fused gate|up GEMM + SwiGLU epilogue of every "
                                            "teacher and student MLP, bf16)",
                     achieved=round(ach, 1), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s", frac=round(ach / PEAK_BF16_TFLOPS, 4),
                     traffic=traffic, traffic_unit="bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
-                                                   "profiles/r01/pmc_traffic.json)",
+                                                   "profiles/*/pmc_traffic.json)",
                     flops_per_launch=round(fwd["flops_per_launch"] / 1e9, 2),
                     avg_launch_us=round(fwd["avg_ms"] * 1e3, 2),
                     measured="HIP events on the launch stream over 2 serialized steps after the timed region "
                              "(bench.py --serial under rocprofv3 gives the matching kernel trace)")
+    tfwd = teacher_forward_rate(m, batches[0]) if m.teacher_model is not None else None
     out = {
         "metric": "KD samples/sec/step (7B->0.5B, 336x336)",
         "value": round(value, 4),
@@ -269,20 +363,33 @@ def main():
         "data": "synthetic (random 336x336 pixels, random token ids; random-init weights of the real architectures)",
         "config": {"workload": f"{a.config}: {cfg['desc']}", "model": "llava-onevision-qwen2-7b (teacher) -> 0.5b (student)",
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": 1536, "image": "336x336 (2 tiles, 1485 tokens)",
-                   "parallelism": f"dp{world}",
-                   "teacher_prefetch": bool(a.prefetch and not a.serial)},
+                   "parallelism": f"dp{world}"},
         "mfu": round(value * tf_sample / world / PEAK_BF16_TFLOPS, 4),
         "host_enqueue_ms_per_step": round(host_dt * 1e3 / a.steps, 2),
         "tflop_per_sample": round(tf_sample, 2),
-        "loss": round(float(loss.item()), 5),
+        "loss": round(loss_v, 5),
+        "teacher_fwd": tfwd,
         "roofline": roof,
         "gemm_breakdown": br,
+        "kd_loss_delta": None,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    if rank == 0 and not a.no_delta:
+        # one more step with its logits kept: the fused loss kernel's terms vs the CPU oracle
+        # on the same (bf16) logits
+        m.keep_logits = True
+        step(a.warmup + a.steps + 2)
+        torch.cuda.synchronize()
+        m.keep_logits = False
+        variant, T = m._loss_spec()[:2]
         try:
-            out["cpu_baseline"] = cpu_baseline(cfg["kind"], cfg["phase"], threads)
+            out["kd_loss_delta"] = kd_loss_delta(m, batches[(a.warmup + a.steps + 2) % 2], (variant, T))
+        except Exception as e:  # report, never hide
+            out["kd_loss_delta"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = host_cpu_info()[0]
+        try:
+            out["cpu_baseline"] = cpu_baseline(cfg["kind"], cfg["phase"], threads, full=a.cpu_full)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

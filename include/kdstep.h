@@ -47,7 +47,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 1
+#define KD_ABI_VERSION 2
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -79,6 +79,14 @@ typedef struct {
     float grad_scale;       /* dlogits multiplier (upstream dL/dtotal, e.g. 1/accum)    */
     float clamp_min;        /* LoCa clamp of p_S before log (1e-8, DT:161-162)           */
     int32_t teacher_ce;     /* 1: also compute the teacher's (unused) CE side output    */
+    float out_scale;        /* loss_out receives out_scale * value (set 1 for plain use) */
+    int32_t out_accumulate; /* 1: loss_out += out_scale * value (loss groups, §8e)      */
+    int32_t* err_out;       /* optional device int32[4], caller-zeroed, never reset here:
+                               [0] |= 1 LoCa gather label outside [0, V_s) (DT:166),
+                                      2 CE target outside {-100} u [0, V_s);
+                               [1] first offending label, [2] its row + row_base,
+                               [3] claim flag                                          */
+    int32_t row_base;       /* added to the row reported in err_out[2]                   */
 } kd_loss_params;
 
 /* loss_out (device float[4]): [0] KD term (mean, incl. T^2, unweighted)
@@ -86,7 +94,8 @@ typedef struct {
  * dlogits: d(total)/d(student_logits) * grad_scale, bf16 [B*L, ld_d] (may be NULL).
  * labels: int64 [B, L] (row-major).  LoCa requires every label in [0, V_s): a label
  * outside raises KD_ERR_LABEL_RANGE from kd_loss_check() (the reference raises
- * RuntimeError from gather, DT:166).  teacher may be NULL for KD_LOSS_NONE.
+ * RuntimeError from gather, DT:166) and is recorded in params.err_out (read
+ * asynchronously by the caller, no device sync).  teacher may be NULL for KD_LOSS_NONE.
  * V_t >= V_s: the teacher is sliced to its first V_s columns (DT:155). */
 size_t kd_loss_workspace_size(int B, int L, int V_s);
 int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t,

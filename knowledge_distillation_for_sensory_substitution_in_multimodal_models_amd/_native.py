@@ -17,6 +17,7 @@ LIB_PATH = Path(os.environ.get("KDSTEP_LIB", _PKG / "libkdstep.so"))
 HEADER = _PKG.parent / "include" / "kdstep.h"
 
 KD_OK = 0
+ABI_VERSION = 2
 STATUS_NAMES = {
     0: "KD_OK", 1: "KD_ERR_SHAPE", 2: "KD_ERR_DTYPE", 3: "KD_ERR_ALIGN", 4: "KD_ERR_ARCH",
     5: "KD_ERR_LABEL_RANGE", 6: "KD_ERR_LAUNCH", 7: "KD_ERR_ARG", 8: "KD_ERR_WORKSPACE",
@@ -36,6 +37,10 @@ class KdLossParams(C.Structure):
         ("grad_scale", C.c_float),
         ("clamp_min", C.c_float),
         ("teacher_ce", C.c_int32),
+        ("out_scale", C.c_float),
+        ("out_accumulate", C.c_int32),
+        ("err_out", C.c_void_p),
+        ("row_base", C.c_int32),
     ]
 
 
@@ -148,7 +153,7 @@ def lib() -> C.CDLL:
             f = getattr(l, name)
             f.restype = res
             f.argtypes = args
-        if l.kd_abi_version() != 1:
+        if l.kd_abi_version() != ABI_VERSION:
             raise ImportError("libkdstep.so ABI version mismatch")
         _lib = l
     return _lib

@@ -104,13 +104,26 @@ __device__ __forceinline__ void lse_merge(float& m, float& z, float m2, float z2
     else        { z = z + z2 * __expf((m2 - m) * invT); }
 }
 
+// error word of the workspace (kd_loss_check) and, when given, the caller's err_out
+// (read asynchronously by the host): bits, first offending label and its row
+__device__ __forceinline__ void report_label(int* err, int* err_ext, int bit, int64_t lab, int row) {
+    atomicOr(err, 1);
+    if (err_ext != nullptr) {
+        atomicOr(err_ext, bit);
+        if (atomicCAS(err_ext + 3, 0, 1) == 0) {
+            err_ext[1] = (int)lab;
+            err_ext[2] = row;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(NT)
 k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
             const bf16* __restrict__ S_, int64_t ld_s, int V_s,
             const int64_t* __restrict__ labels, int L, int rows,
             int variant, float invT, float alpha, int want_tce,
             RowStats* __restrict__ stats, int* __restrict__ lab_last,
-            int* __restrict__ klo_last, int* __restrict__ err) {
+            int* __restrict__ klo_last, int* __restrict__ err, int* __restrict__ err_ext, int row_base) {
     __shared__ float sm[NW * 8];
     __shared__ int si[NW * 2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -255,7 +268,7 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
             st.lab_next = (int)labn;
             // student / teacher CE on the shifted label
             const bool labn_ok = (labn == -100) || (labn >= 0 && labn < V_s);
-            if (!labn_ok) atomicOr(err, 1);
+            if (!labn_ok) report_label(err, err_ext, 2, labn, r + 1 + row_base);
             st.valid = (labn >= 0 && labn < V_s) ? 1 : 0;
             st.ce = 0.f; st.tce = 0.f;
             if (st.valid) {
@@ -266,7 +279,7 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
             st.ovx = 0.f; st.ovy = 0.f;
             if (variant == KD_LOSS_LOCA) {
                 if (lab < 0 || lab >= V_s) {
-                    atomicOr(err, 1);  // reference: gather index out of bounds (DT:166)
+                    report_label(err, err_ext, 1, lab, r + row_base);  // reference: gather out of bounds (DT:166)
                 } else {
                     // p_gt, p_k (DT:166, :174), sigma, s (DT:177-180)
                     const float p_gt = __expf(((float)trow[lab] - Mt) * invT) / Zt;
@@ -439,7 +452,7 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
 
 __global__ void k_finalize(const RowStats* __restrict__ stats, const float* __restrict__ part_kl,
                            int rows, double kl_scale, float kd_weight, float ce_weight,
-                           float* __restrict__ out) {
+                           float out_scale, int out_acc, float* __restrict__ out) {
     __shared__ double red[4][NW];
     double kl = 0, ce = 0, tce = 0, nv = 0;
     for (int r = threadIdx.x; r < rows; r += NT) {
@@ -457,10 +470,8 @@ __global__ void k_finalize(const RowStats* __restrict__ stats, const float* __re
         const double kd = a * kl_scale;
         // HF CE: mean over valid targets (NaN when there are none, as torch's mean of empty)
         const double ce_m = b / n, tce_m = c / n;
-        out[0] = (float)kd;
-        out[1] = (float)ce_m;
-        out[2] = (float)tce_m;
-        out[3] = (float)(kd_weight * kd + ce_weight * ce_m);
+        const double v[4] = {kd, ce_m, tce_m, kd_weight * kd + ce_weight * ce_m};
+        for (int i = 0; i < 4; ++i) out[i] = (out_acc ? out[i] : 0.f) + (float)(out_scale * v[i]);
     }
 }
 
@@ -544,7 +555,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     const int grid = rows < 2048 ? rows : 2048;
     hipLaunchKernelGGL(k_row_stats, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
                        V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
-                       lab_last, klo_last, err);
+                       lab_last, klo_last, err, p.err_out, p.row_base);
     KD_LAUNCH_CHECK("k_row_stats");
     if (variant == KD_LOSS_LOCA) {
         const int nb = (V_s + 255) / 256;
@@ -577,7 +588,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     KD_LAUNCH_CHECK("k_loss_grad");
     const double kl_scale = (variant == KD_LOSS_NONE) ? 0.0 : (double)T * T / N;
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(NT), 0, stream, stats, part_kl, rows, kl_scale,
-                       p.kd_weight, p.ce_weight, loss_out);
+                       p.kd_weight, p.ce_weight, p.out_scale, p.out_accumulate ? 1 : 0, loss_out);
     KD_LAUNCH_CHECK("k_finalize");
     return KD_OK;
 }

@@ -1,0 +1,89 @@
+"""Data-parallel gradient synchronisation of the student.
+
+One process per GPU; the student's trainable gradient is one contiguous range of a flat
+fp32 buffer (modeling.ParamStore), so the all-reduce (mean over ranks) is a handful of
+large buckets, launched as soon as the backward has made a range final (LM layers
+top-down), overlapping the rest of the backward; RCCL over xGMI on GPUs (backend "nccl"),
+gloo in the CPU tests.
+
+Gradient accumulation (the reference trains with accumulate_grad_batches=64, DT1T:70,
+:155): only the LAST micro-batch's backward of an optimizer step reduces, DDP `no_sync`
+style — the earlier ones only accumulate locally.  No collective is ever in flight while
+a backward writes the buffer: `begin()` retires pending work first.  With every
+micro-batch's loss scaled by 1/k (Lightning), the reduced buffer is the mean over ranks of
+the sum over micro-batches, i.e. the gradient of the global mean loss.
+"""
+from __future__ import annotations
+
+
+class GradSync:
+    """Bucketed all-reduce of `grad` (a flat tensor) over the default process group.
+
+    Protocol per backward:   begin(sync) -> layer_done(first)* -> end(lo, hi)
+    before the optimizer:    finish(lo, hi)
+    """
+
+    def __init__(self, dist, grad, bucket_bytes: int = 256 << 20):
+        self.dist = dist
+        self.grad = grad
+        self.bucket_bytes = int(bucket_bytes)
+        self.works = []          # (work, range view to divide after wait (gloo) | None)
+        self.hi = None           # high-water mark: [first, hi) already launched this backward
+        self.active = False      # this backward reduces
+        self.unsynced = False    # local grads accumulated since the last reduction
+        self.world = dist.get_world_size()
+        self.avg_in_collective = dist.get_backend() == "nccl"   # RCCL AVG; gloo has no AVG
+
+    # -------------------------------------------------------------- backward ----
+    def begin(self, sync: bool):
+        self.wait()              # nothing in flight while this backward accumulates into grad
+        self.active = bool(sync)
+        self.hi = None
+
+    def layer_done(self, first: int, before_launch=None):
+        """Everything from flat offset `first` to the high-water mark is final."""
+        if not self.active:
+            return
+        if self.hi is None:
+            self.hi = self.grad.numel()
+        if (self.hi - first) * self.grad.element_size() >= self.bucket_bytes:
+            if before_launch is not None:
+                before_launch()  # e.g. join the weight-gradient stream
+            self._launch(first, self.hi)
+            self.hi = first
+
+    def end(self, lo: int, hi: int):
+        """The backward is complete: reduce what is left of the trainable range [lo, hi)."""
+        if self.active:
+            top = hi if self.hi is None else min(hi, self.hi)
+            if top > lo:
+                self._launch(lo, top)
+            self.unsynced = False
+        else:
+            self.unsynced = True
+        self.active = False
+        self.hi = None
+
+    # ------------------------------------------------------------- optimizer ----
+    def finish(self, lo: int, hi: int):
+        """Before the optimizer reads grad: reduce grads accumulated without a sync (an
+        optimizer step taken before the accumulation boundary) and retire all work."""
+        if self.unsynced and hi > lo:
+            self._launch(lo, hi)
+        self.unsynced = False
+        self.wait()
+
+    def wait(self):
+        for w, g in self.works:
+            w.wait()
+            if g is not None:
+                g.div_(self.world)
+        self.works = []
+
+    def _launch(self, lo: int, hi: int):
+        g = self.grad[lo:hi]
+        d = self.dist
+        if self.avg_in_collective:
+            self.works.append((d.all_reduce(g, op=d.ReduceOp.AVG, async_op=True), None))
+        else:   # SUM, divided once after the wait (each range is reduced exactly once per sync)
+            self.works.append((d.all_reduce(g, op=d.ReduceOp.SUM, async_op=True), g))

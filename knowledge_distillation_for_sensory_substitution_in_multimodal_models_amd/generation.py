@@ -25,18 +25,24 @@ from . import ops
 
 import os
 
-EOS_TOKEN_IDS = (151645,)
-FUSE_NORM = os.environ.get("KD_DECODE_FUSE_NORM", "1") != "0"   # RMSNorm fused into the decode GEMVs (A/B knob)   # <|im_end|>: generation_config.eos_token_id of the -ov-hf chat checkpoints
+EOS_TOKEN_IDS = (151645,)   # <|im_end|>: generation_config.eos_token_id of the -ov-hf chat checkpoints
+
+
+def _fuse_norm_default() -> bool:
+    """RMSNorm fused into the decode GEMVs unless KD_DECODE_FUSE_NORM=0 (A/B knob; read per call)."""
+    return os.environ.get("KD_DECODE_FUSE_NORM", "1") != "0"
 
 
 @torch.no_grad()
 def generate(model, input_ids: torch.Tensor, pixel_values: torch.Tensor, image_sizes, max_new_tokens: int = 32,
              repetition_penalty: float = 1.0, no_repeat_ngram_size: int = 0, eos_token_id=EOS_TOKEN_IDS,
              pad_token_id: int | None = None, temperature: float | None = None, return_logits: bool = False,
-             graph: bool = True):
+             graph: bool = True, fuse_norm: bool | None = None):
     """-> int64 [1, L + n_new] on the device (and the bf16 logits row of every step if
-    return_logits).  `temperature` is accepted for signature parity and ignored (greedy)."""
+    return_logits).  `temperature` is accepted for signature parity and ignored (greedy).
+    fuse_norm: RMSNorm fused into the q|k|v and gate|up GEMVs (default: KD_DECODE_FUSE_NORM)."""
     del temperature, pad_token_id   # greedy, batch of one: no padding of finished rows
+    FUSE_NORM = _fuse_norm_default() if fuse_norm is None else bool(fuse_norm)
     if input_ids.dim() != 2 or input_ids.shape[0] != 1:
         raise ValueError("generate: batch size 1 (as evaluate_onevision.py runs it)")
     T, P = model.cfg.text, model.P

@@ -23,14 +23,14 @@ forward of step t+1 (the student forward of step t+1 waits for them).
 """
 from __future__ import annotations
 
-import math
-import os
-import re
+import contextlib
+import inspect
 
 import torch
 import torch.nn as nn
 
 from . import ops
+from .dp import GradSync
 from .modeling import (STREAM_PRIORITY_HIGH, STUDENT_05B, TEACHER_7B, LlavaOnevisionModel, tiny_config)
 
 try:  # the reference's base class when installed; otherwise a minimal stand-in
@@ -88,10 +88,16 @@ class FusedAdamW(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         m = self.module
         g = self.param_groups[0]
-        self.step_count += 1
-        m._finish_grad_sync()
-        P = m.student_model.P
+        # a batch the reference would have rejected (label out of range, DT:166) must not
+        # update the weights: the step's loss kernel has long finished by now, so this
+        # host wait costs nothing in steady state
+        m._check_errors(block=True)
         lo, hi = m._trainable_range()
+        if m._gsync is not None:
+            m._gsync.finish(lo, hi)
+        m._micro = 0
+        self.step_count += 1
+        P = m.student_model.P
         if hi > lo:
             side = m._opt_stream
             side.wait_stream(torch.cuda.current_stream())
@@ -113,17 +119,90 @@ class FusedAdamW(torch.optim.Optimizer):
             m.student_model.P.grad[lo:hi].zero_()
 
 
+class _ErrorWatch:
+    """Device error words of a step (label range in the KD loss, token ids / image-token
+    count in the embedding assembly), copied asynchronously into pinned host slots and
+    read when their event has completed — no device sync on the step's path.  The
+    reference raises at the offending call (gather, DT:166; embedding / masked_scatter);
+    here the error surfaces at the next optimizer.step() (before any weight update) or
+    the next training_step."""
+
+    SLOTS = 4
+
+    def __init__(self, dev):
+        self.kd = torch.zeros(4, dtype=torch.int32, device=dev)    # kd_loss_params.err_out
+        self.host = torch.zeros((self.SLOTS, 6), dtype=torch.int32).pin_memory()
+        self.pending = []    # (event, slot, info)
+        self.next = 0
+
+    def record(self, student_err, teacher_err, info):
+        """Enqueue the copies on the current stream (after the step's loss), then reset."""
+        if len(self.pending) >= self.SLOTS:
+            self.check(block=True, upto=1)
+        slot = self.next
+        self.next = (self.next + 1) % self.SLOTS
+        h = self.host[slot]
+        h[4:6].zero_()
+        h[0:4].copy_(self.kd, non_blocking=True)
+        h[4:5].copy_(student_err, non_blocking=True)
+        if teacher_err is not None:
+            h[5:6].copy_(teacher_err, non_blocking=True)
+        self.kd.zero_()
+        student_err.zero_()
+        if teacher_err is not None:
+            teacher_err.zero_()
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((ev, slot, info))
+
+    def check(self, block: bool, upto: int | None = None):
+        keep = []
+        for i, (ev, slot, info) in enumerate(self.pending):
+            if (block and (upto is None or i < upto)) or ev.query():
+                ev.synchronize()
+                self._raise_if(self.host[slot].tolist(), info)
+            else:
+                keep.append((ev, slot, info))
+        self.pending = keep
+
+    @staticmethod
+    def _raise_if(h, info):
+        bits, lab, row, _, serr, terr = h
+        L, V = info["L"], info["V"]
+        if bits & 1:
+            raise RuntimeError(f"compute_loca_loss: index {lab} is out of bounds for dimension 2 with size {V} "
+                               f"(label at batch {row // L}, position {row % L}; the reference's gather, DT:166)")
+        if bits & 2:
+            raise RuntimeError(f"student CE: target {lab} is out of bounds (not -100 and not in [0, {V})) "
+                               f"at batch {row // L}, position {row % L}")
+        for who, e in (("student", serr), ("teacher", terr)):
+            if e & 1:
+                raise RuntimeError(f"{who} embed_tokens: input id outside the vocabulary")
+            if e & 2:
+                raise RuntimeError(f"{who}: image-token count does not match the image features "
+                                   f"(masked_scatter size mismatch)")
+
+
 class _KDBase(_Base):
     # subclass hooks
     uses_teacher = True
+    ckpt_student_prefix = "student_model."
 
     def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1,
-                 seed_teacher: int = 1, seed_student: int = 2, state_dict=None, world=None):
+                 seed_teacher: int = 1, seed_student: int = 2, state_dict=None, loss_group_size: int | None = None,
+                 accumulate_grad_batches: int = 1, **_ignored):
         super().__init__()
         self.phase = phase
         self.learning_rate = learning_rate
         self.processor = processor
         self.model_name_student, self.model_name_teacher = model_name_student, model_name_teacher
+        # samples whose losses are coupled in one loss call (LoCa's column overrides, NT-Xent
+        # negatives; SURVEY §8e).  None = the whole per-rank micro-batch; 1 = the reference's
+        # batch_size=1 x accumulate_grad_batches semantics (DT1T:70, :155).
+        self.loss_group_size = loss_group_size
+        # micro-batches per optimizer step (Lightning's accumulate_grad_batches): only the last
+        # backward of a step all-reduces (DP); see also no_sync()
+        self.accumulate_grad_batches = int(accumulate_grad_batches)
         dev = _device()
         small = model_name_student.startswith("tiny")
         self.student_model = LlavaOnevisionModel(MODEL_CONFIGS[model_name_student], dev, trainable=True,
@@ -136,31 +215,30 @@ class _KDBase(_Base):
             self.load_kd_state_dict(state_dict)
         self.config = self.student_model.cfg
         self._anchor = nn.Parameter(torch.zeros((), device=dev))
-        # the step's own streams run at high priority; the teacher prefetch (off the critical
-        # path) at normal priority, so it fills the CUs the step leaves idle
         self._opt_stream = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
         self._stu_stream = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
         self.concurrent_student = True   # False: student forward on the main stream (bench.py --serial)
         self._opt_done = torch.cuda.Event()
         self._opt_pending = False
-        self._tch_stream = torch.cuda.Stream(device=dev, priority=0)
-        self.teacher_graphs = os.environ.get("KD_TEACHER_GRAPH", "0") == "1"   # measured slower on ROCm 7
-        self._tgraphs = {}
-        self._prefetched = None   # (batch key, teacher logits, post-LN features, event)
         self._ctx = None
+        self._errors = _ErrorWatch(dev)
+        self.keep_logits = False         # tests: keep the step's logits in last_logits
         self.last_terms = None
+        self.last_ntxent = None
+        self.last_logits = None
+        self._micro = 0                  # backward passes since the last optimizer step
+        self._no_sync_depth = 0
         # data parallel
         import torch.distributed as dist
         self._dist = dist if (dist.is_available() and dist.is_initialized()) else None
-        self._works = []
-        self._sync_hi = None
-        self._bucket_bytes = 256 << 20
-        if self._dist is not None and self.uses_teacher:
-            # teacher weights broadcast once from rank 0, then read-only in every GPU's HBM
-            self._dist.broadcast(self.teacher_model.P.flat, src=0)
+        self._gsync = None
         if self._dist is not None:
+            if self.uses_teacher:
+                # teacher weights broadcast once from rank 0, then read-only in every GPU's HBM
+                self._dist.broadcast(self.teacher_model.P.flat, src=0)
             self._dist.broadcast(self.student_model.P.flat, src=0)
             self.student_model.P.master.copy_(self.student_model.P.flat.float())
+            self._gsync = GradSync(self._dist, self.student_model.P.grad)
 
     # ------------------------------------------------------------- freezing ----
     def _trainable_range(self):
@@ -206,87 +284,18 @@ class _KDBase(_Base):
         return [opt], [sched]
 
     # ------------------------------------------------------------- the step ----
-    @staticmethod
-    def _batch_key(batch):
-        # the input tensors themselves (held, so their memory cannot be reused by another
-        # batch) and their version counters (an in-place edit invalidates the prefetch)
-        x, p, sz = batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"]
-        return (x, p, sz, x._version, p._version)
-
-    @staticmethod
-    def _same_key(k1, k2):
-        return all(a is b for a, b in zip(k1[:3], k2[:3])) and k1[3:] == k2[3:]
-
-    def _teacher_forward_eager(self, batch, need_feats):
+    def _teacher_forward(self, batch, need_feats):
         tfwd = self.teacher_model.forward(batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"],
                                           save=False, want_post_ln=need_feats)
         t_logits = self.teacher_model.logits(tfwd["hn"])
         del tfwd["hn"]
         return t_logits, tfwd.get("post_ln")
 
-    def _teacher_forward(self, batch, need_feats):
-        """Teacher logits (+ post-LN vision features) for `batch` on the current stream.
-
-        The frozen teacher's forward is ~700 short host launches (~38 ms of Python + ctypes
-        per step, which left the step close to launch-bound); it is captured once per input
-        signature as a HIP graph (torch.cuda.CUDAGraph: every kernel is a libkdstep launch on
-        the capturing stream) and replayed: one launch. The inputs are copied into the
-        graph's static buffers; the outputs are the graph's static tensors (overwritten by
-        the next replay, which every consumer precedes on the stream order)."""
-        if not self.teacher_graphs:
-            return self._teacher_forward_eager(batch, need_feats)
-        ids, px, sz = batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"]
-        sizes = tuple(tuple(int(v) for v in hw) for hw in (sz.tolist() if hasattr(sz, "tolist") else sz))
-        key = (tuple(ids.shape), tuple(px.shape), px.dtype, sizes, bool(need_feats))
-        tg = self._tgraphs.get(key)
-        if tg is None:
-            out = self._teacher_forward_eager(batch, need_feats)   # warm-up: workspaces, maps, tables
-            sb = dict(batch)
-            sb["rgb_input_ids"], sb["rgb_pixel_values"] = ids.clone(), px.clone()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                logits, post = self._teacher_forward_eager(sb, need_feats)
-            self._tgraphs[key] = (g, sb["rgb_input_ids"], sb["rgb_pixel_values"], logits, post)
-            return out
-        g, s_ids, s_px, logits, post = tg
-        s_ids.copy_(ids)
-        s_px.copy_(px)
-        g.replay()
-        return logits, post
-
-    def prefetch_teacher(self, batch):
-        """Enqueue the frozen teacher's forward for `batch` (the NEXT training batch) on its own
-        stream, so it runs beside the current step's backward and optimizer; the
-        training_step that gets this batch waits on it instead of recomputing it. Optional:
-        without it the teacher runs inline. The teacher reads no student state, so the
-        result is identical either way."""
-        if not self.uses_teacher:
-            return
-        _, _, _, _, ctr_w = self._loss_spec()
-        ts = self._tch_stream
-        ts.wait_stream(torch.cuda.current_stream())   # the batch's inputs are ready
-        with torch.cuda.stream(ts):
-            t_logits, post_ln = self._teacher_forward(batch, ctr_w is not None)
-        ev = torch.cuda.Event()
-        ev.record(ts)
-        self._prefetched = (self._batch_key(batch), t_logits, post_ln, ev)
-
-    def _take_prefetched(self, batch, need_feats):
-        pf, self._prefetched = self._prefetched, None
-        if pf is None:
-            return None
-        _, t_logits, post_ln, ev = pf
-        main = torch.cuda.current_stream()
-        main.wait_event(ev)   # also when unused: an inline replay rewrites the same graph buffers
-        if not self._same_key(pf[0], self._batch_key(batch)) or (need_feats and post_ln is None):
-            return None
-        # consumed on the main stream from here on: keep the allocator from handing the
-        # blocks back to the teacher stream before those reads are done
-        if not self.teacher_graphs:
-            t_logits.record_stream(main)
-            if post_ln is not None:
-                post_ln.record_stream(main)
-        return t_logits, post_ln
+    def _groups(self, B):
+        G = self.loss_group_size or B
+        if G <= 0 or B % G:
+            raise ValueError(f"loss_group_size {G} must divide the per-rank batch {B}")
+        return G, B // G
 
     def forward(self, batch, train: bool = False):
         """The reference's forward(batch) (DT:206-271): total loss as a 0-d fp32 tensor."""
@@ -294,6 +303,7 @@ class _KDBase(_Base):
         labels = batch["labels"]
         image_sizes = batch["image_sizes"]
         B, L = batch["depth_input_ids"].shape
+        G, ng = self._groups(B)
         need_feats = ctr_w is not None
         main = torch.cuda.current_stream()
         s = self.student_model
@@ -301,9 +311,7 @@ class _KDBase(_Base):
         # everything already queued on the main stream (so caching-allocator blocks the
         # previous step freed there are reusable) and for the previous optimizer step (the
         # student weights); the main stream joins it before the loss. The teacher (the long
-        # pole, ~90 ms of large GEMMs that do not read student weights) is ENQUEUED first:
-        # the host spends ~20 ms launching the student's ~500 short kernels, and queued
-        # first they ran alone on the GPU while the teacher's launches waited behind them.
+        # pole, large GEMMs that do not read student weights) is ENQUEUED first.
         side = self._stu_stream if self.concurrent_student else main
         side.wait_stream(main)
         if self._opt_pending:
@@ -311,28 +319,47 @@ class _KDBase(_Base):
             self._opt_pending = False
         t_logits = t_post = None
         if self.uses_teacher:
-            got = self._take_prefetched(batch, need_feats)
-            t_logits, t_post = got if got is not None else self._teacher_forward(batch, need_feats)
+            t_logits, t_post = self._teacher_forward(batch, need_feats)
         with torch.cuda.stream(side):
             sfwd = s.forward(batch["depth_input_ids"], batch["depth_pixel_values"], image_sizes, save=train,
                              want_post_ln=need_feats)
             s_logits = s.logits(sfwd["hn"])
         main.wait_stream(side)
         Vs = s_logits.shape[1]
-        loss4, dlogits = ops.kd_loss_fwd_bwd(
-            s_logits.view(B, L, Vs), None if t_logits is None else t_logits.view(B, L, -1), labels, variant,
-            temperature=T, alpha=0.8, kd_weight=kd_w, ce_weight=ce_w, want_grad=train)
-        del s_logits, t_logits
+        s3 = s_logits.view(B, L, Vs)
+        t3 = None if t_logits is None else t_logits.view(B, L, -1)
+        loss4 = torch.empty(4, dtype=torch.float32, device=s_logits.device)
+        dlogits = torch.empty((B, L, Vs), dtype=torch.bfloat16, device=s_logits.device) if train else None
+        for g in range(ng):   # loss groups: mean over groups of each group's loss
+            sl = slice(g * G, (g + 1) * G)
+            ops.kd_loss_fwd_bwd(s3[sl], None if t3 is None else t3[sl], labels[sl], variant,
+                                temperature=T, alpha=0.8, kd_weight=kd_w, ce_weight=ce_w, grad_scale=1.0 / ng,
+                                want_grad=train, loss_out=loss4, out_scale=1.0 / ng, accumulate=g > 0,
+                                dlogits_out=None if dlogits is None else dlogits[sl], err_out=self._errors.kd,
+                                row_base=g * G * L)
+        if self.keep_logits:
+            self.last_logits = (s3, t3)
+        del s_logits, t_logits, s3, t3
         total = loss4[3]
         dps = None
         if need_feats:
-            NI = sfwd["post_ln"].shape[0] // s.cfg.vision.n_patches
-            ps = ops.row_group_mean(sfwd["post_ln"], NI, s.cfg.vision.n_patches)        # DT:243-244
-            pt = ops.row_group_mean(t_post, NI, s.cfg.vision.n_patches)
-            ntx, dps = ops.ntxent(ps, pt, tau=0.07, weight=ctr_w, want_grad=train)      # DT:393-416
+            NP = s.cfg.vision.n_patches
+            NI = sfwd["post_ln"].shape[0] // NP
+            ps = ops.row_group_mean(sfwd["post_ln"], NI, NP)        # DT:243-244
+            pt = ops.row_group_mean(t_post, NI, NP)
+            rpg = NI // B * G                                        # pooled tile rows per group
+            ntx_rows = torch.empty((ng, 2), dtype=torch.float32, device=ps.device)
+            dps = torch.empty_like(ps) if train else None
+            for g in range(ng):                                      # DT:393-416 per group
+                r = slice(g * rpg, (g + 1) * rpg)
+                ops.ntxent(ps[r], pt[r], tau=0.07, weight=ctr_w / ng, want_grad=train, loss_out=ntx_rows[g],
+                           dfs_out=None if dps is None else dps[r])
+            ntx = ntx_rows.sum(0) if ng > 1 else ntx_rows[0]
             total = total + ntx[0]
-            self.last_ntxent = ntx
+            self.last_ntxent = (ntx[0], ntx_rows[:, 1].mean() if ng > 1 else ntx_rows[0, 1])
         self.last_terms = loss4
+        self._errors.record(s.err, None if self.teacher_model is None else self.teacher_model.err,
+                            dict(L=L, V=Vs))
         if train:
             self._ctx = dict(sfwd=sfwd, dlogits=dlogits, dps=dps)
         return total
@@ -340,6 +367,11 @@ class _KDBase(_Base):
     def _backward(self, gscale):
         ctx, self._ctx = self._ctx, None
         s = self.student_model
+        self._micro += 1
+        sync = self._gsync is not None and self._no_sync_depth == 0 and \
+            self._micro % max(1, self.accumulate_grad_batches) == 0
+        if self._gsync is not None:
+            self._gsync.begin(sync)
         sf = ctx["sfwd"]
         hn = sf["hn"]
         W = s.lm_head_weight()
@@ -354,8 +386,19 @@ class _KDBase(_Base):
         dpost = None
         if ctx["dps"] is not None and s.train_vision:
             dpost = ops.row_group_mean_bwd(ctx["dps"], s.cfg.vision.n_patches, scale_dev=gscale)
-        s.backward(sf, dhn, dpost, on_layer_done=self._on_layer_done if self._dist else None)
-        self._launch_grad_sync(final=True)
+        s.backward(sf, dhn, dpost, on_layer_done=self._on_layer_done if sync else None)
+        if self._gsync is not None:
+            self._gsync.end(*self._trainable_range())
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside the block accumulate locally without the DP all-reduce
+        (DDP no_sync); the optimizer step reduces whatever is left unsynced."""
+        self._no_sync_depth += 1
+        try:
+            yield
+        finally:
+            self._no_sync_depth -= 1
 
     # ------------------------------------------------------- data parallel ----
     def _on_layer_done(self, i):
@@ -363,48 +406,21 @@ class _KDBase(_Base):
 
         Flat layout [vision | projector | embed, layers 0..N-1, norm(, lm_head)]; the backward
         finishes the tail first (lm_head, norm), then layers N-1..0, then embed / projector /
-        vision.  Everything from layer i's first parameter to the current high-water mark is
-        final once layer i is done."""
+        vision.  Everything from layer i's first parameter to the high-water mark is final
+        once layer i is done."""
         s = self.student_model
         if not s.train_language:
             return
-        P = s.P
-        if self._sync_hi is None:
-            self._sync_hi = P.numel
-        first = P.offsets[f"language_model.model.layers.{i}.self_attn.q_proj.weight"][0]
-        if (self._sync_hi - first) * 4 >= self._bucket_bytes:
-            lane = getattr(s, "wlane", None)
-            if lane is not None:
-                lane.join()   # the bucket's weight grads (side stream) are complete
-            self._allreduce(first, self._sync_hi)
-            self._sync_hi = first
+        first = s.P.offsets[f"language_model.model.layers.{i}.self_attn.q_proj.weight"][0]
+        lane = getattr(s, "wlane", None)
+        self._gsync.layer_done(first, before_launch=lane.join if lane is not None else None)
 
-    def _launch_grad_sync(self, final: bool):
-        if self._dist is None:
-            return
-        lo, hi = self._trainable_range()
-        top = hi if self._sync_hi is None else min(hi, self._sync_hi)
-        if top > lo:
-            self._allreduce(lo, top)
-        self._sync_hi = None
-
-    def _allreduce(self, lo, hi):
-        g = self.student_model.P.grad[lo:hi]
-        if self._dist.get_backend() == "nccl":   # RCCL: AVG in the collective
-            self._works.append((self._dist.all_reduce(g, op=self._dist.ReduceOp.AVG, async_op=True), None))
-        else:                                      # gloo (CPU tests): SUM, divided after the wait
-            self._works.append((self._dist.all_reduce(g, op=self._dist.ReduceOp.SUM, async_op=True), g))
-
-    def _finish_grad_sync(self):
-        ws = self._dist.get_world_size() if self._dist is not None else 1
-        for w, g in self._works:
-            w.wait()
-            if g is not None:
-                g.div_(ws)
-        self._works = []
+    def _check_errors(self, block: bool):
+        self._errors.check(block=block)
 
     # ---------------------------------------------------------- Lightning API ----
     def training_step(self, batch, batch_idx):           # DT:123-131
+        self._check_errors(block=False)
         total = self.forward(batch, train=True)
         loss = _KDStepFn.apply(self._anchor, total, self)
         self.log("train_loss", loss, on_step=True, on_epoch=True, prog_bar=True, logger=True)
@@ -413,6 +429,7 @@ class _KDBase(_Base):
     def validation_step(self, batch, batch_idx):         # DT:133-138
         with torch.no_grad():
             loss = self.forward(batch, train=False)
+        self._check_errors(block=True)
         self.log("val_loss", loss, on_step=False, on_epoch=True, prog_bar=True, logger=True)
         return loss
 
@@ -420,33 +437,45 @@ class _KDBase(_Base):
     def kd_state_dict(self):
         if self._opt_pending:   # weights of a queued optimizer step
             torch.cuda.current_stream().wait_event(self._opt_done)
-        sd = {f"student_model.{k}": v for k, v in self.student_model.P.state_dict().items()}
+        sd = {f"{self.ckpt_student_prefix}{k}": v for k, v in self.student_model.P.state_dict().items()}
         if self.teacher_model is not None:
             sd.update({f"teacher_model.{k}": v for k, v in self.teacher_model.P.state_dict().items()})
         return sd
 
     def load_kd_state_dict(self, sd):
-        self.student_model.P.load_state_dict(sd, prefix="student_model.")
+        self.student_model.P.load_state_dict(sd, prefix=self.ckpt_student_prefix)
         if self.teacher_model is not None and any(k.startswith("teacher_model.") for k in sd):
             self.teacher_model.P.load_state_dict(sd, prefix="teacher_model.")
+
+    def _hparams(self):
+        return {"model_name_student": self.model_name_student, "model_name_teacher": self.model_name_teacher,
+                "learning_rate": self.learning_rate, "phase": self.phase}
 
     def save_checkpoint(self, path, epoch: int = 0, global_step: int = 0):
         """Lightning-style .ckpt: {'state_dict': {student_model.*, teacher_model.*}, ...}."""
         sd = {k: v.detach().cpu() for k, v in self.kd_state_dict().items()}
         torch.save({"state_dict": sd, "epoch": epoch, "global_step": global_step,
-                    "pytorch-lightning_version": "2.4.0",
-                    "hyper_parameters": {"model_name_student": self.model_name_student,
-                                         "model_name_teacher": self.model_name_teacher,
-                                         "learning_rate": self.learning_rate, "phase": self.phase}}, path)
+                    "pytorch-lightning_version": "2.4.0", "hyper_parameters": self._hparams()}, path)
 
     @classmethod
-    def load_from_checkpoint(cls, checkpoint_path, model_name_student=None, model_name_teacher=None, processor=None,
-                             map_location=None, **kw):
+    def load_from_checkpoint(cls, checkpoint_path, map_location=None, **kw):
+        """LightningModule.load_from_checkpoint: the constructor arguments come from the
+        keywords given here (the reference passes model names, processor, torch_dtype,
+        map_location, phase: evaluate_onevision.py:65-73, BDT:86-91), falling back to the
+        checkpoint's saved hyper-parameters; then the state_dict is loaded."""
         ck = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
-        hp = ck.get("hyper_parameters", {})
-        return cls(model_name_student or hp["model_name_student"], model_name_teacher or hp["model_name_teacher"],
-                   processor, learning_rate=kw.pop("learning_rate", hp.get("learning_rate", 1e-5)),
-                   state_dict=ck["state_dict"], **{k: v for k, v in kw.items() if k in ("phase",)})
+        hp = dict(ck.get("hyper_parameters", {}))
+        sig = inspect.signature(cls.__init__)
+        args = {}
+        for name, prm in list(sig.parameters.items())[1:]:
+            if prm.kind in (prm.VAR_KEYWORD, prm.VAR_POSITIONAL):
+                continue
+            if name in kw:
+                args[name] = kw.pop(name)
+            elif name in hp:
+                args[name] = hp[name]
+        kw.pop("torch_dtype", None)   # the build's weights are bf16 in HBM whatever the caller's dtype
+        return cls(**args, state_dict=ck["state_dict"], **kw)
 
 
 class OnlineKnowledgeDistillationLLavaOneVision(_KDBase):
@@ -499,12 +528,18 @@ class FeatureBasedKD(_KDBase):
 
 
 class LlavaOnevisionModule(_KDBase):
-    """Depth-student SFT baseline (BD:6-138): loss = the student's CE only."""
+    """Depth-student SFT baseline (BD:6-138): loss = the student's CE only.  Its Lightning
+    checkpoint holds the student under `model.*` (the reference's attribute, BD:15)."""
     uses_teacher = False
+    ckpt_student_prefix = "model."
 
     def __init__(self, model_name, processor=None, learning_rate=2e-5, **kw):
         super().__init__(model_name, None, processor, learning_rate, phase=0, **kw)
+        self.model_name = model_name
         self.model = self.student_model
+
+    def _hparams(self):
+        return {"model_name": self.model_name, "learning_rate": self.learning_rate}
 
     def _loss_spec(self):
         return "none", 1.0, 0.0, 1.0, None

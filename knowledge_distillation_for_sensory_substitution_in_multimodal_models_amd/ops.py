@@ -89,12 +89,19 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
                     labels: torch.Tensor, variant: str, temperature: float = 1.0, alpha: float = 0.8,
                     kd_weight: float = 1.0, ce_weight: float = 1.0, grad_scale: float = 1.0,
                     clamp_min: float = 1e-8, teacher_ce: bool = True, want_grad: bool = True,
-                    check: bool = False):
+                    check: bool = False, loss_out: torch.Tensor | None = None, out_scale: float = 1.0,
+                    accumulate: bool = False, dlogits_out: torch.Tensor | None = None,
+                    err_out: torch.Tensor | None = None, row_base: int = 0):
     """Fused KD-loss forward + backward (include/kdstep.h kd_loss_fwd_bwd).
 
     student_logits [B, L, V_s] bf16 (last dim contiguous), teacher_logits [B, L, V_t] bf16,
     labels [B, L] int64.  Returns (loss4, dlogits): loss4 = fp32 [4] =
     (kd_term, student_ce, teacher_ce, total); dlogits bf16 [B, L, V_s] or None.
+
+    Loss groups: loss_out / out_scale / accumulate let consecutive calls on
+    sub-batches average their terms on the device; dlogits_out receives the gradient rows
+    of this call.  err_out (device int32[4], caller-zeroed) collects label-range errors
+    without a host sync (kd_loss_params.err_out).
     """
     B, L, V_s = student_logits.shape
     _require(student_logits, torch.bfloat16, "student_logits")
@@ -113,12 +120,20 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
             raise RuntimeError(f"kd_loss variant {variant} needs teacher logits")
         V_t, ld_t = 0, 0
     dev = student_logits.device
-    loss = torch.empty(4, dtype=torch.float32, device=dev)
-    dl = torch.empty((B, L, V_s), dtype=torch.bfloat16, device=dev) if want_grad else None
+    loss = loss_out if loss_out is not None else torch.empty(4, dtype=torch.float32, device=dev)
+    if want_grad:
+        dl = dlogits_out if dlogits_out is not None else torch.empty((B, L, V_s), dtype=torch.bfloat16, device=dev)
+        if dl.shape[-1] != V_s or dl.stride(-1) != 1 or dl.numel() != B * L * V_s:
+            raise RuntimeError("dlogits_out: expected a contiguous [B, L, V_s] view")
+    else:
+        dl = None
+    if err_out is not None:
+        _require(err_out, torch.int32, "err_out")
     nbytes = NV.lib().kd_loss_workspace_size(B, L, V_s)
     ws = _workspace("kd_loss", nbytes, dev)
     prm = NV.KdLossParams(v, float(temperature), float(alpha), float(kd_weight), float(ce_weight),
-                         float(grad_scale), float(clamp_min), 1 if teacher_ce else 0)
+                         float(grad_scale), float(clamp_min), 1 if teacher_ce else 0, float(out_scale),
+                         1 if accumulate else 0, _ptr(err_out), int(row_base))
     NV.call("kd_loss_fwd_bwd", _ptr(teacher_logits), ld_t, V_t, _ptr(student_logits),
            student_logits.stride(1), V_s, _ptr(labels), B, L, prm, _ptr(loss), _ptr(dl),
            V_s, _ptr(ws), ws.numel(), _stream())
@@ -388,11 +403,12 @@ def row_group_mean_bwd(dpool, P: int, out=None, scale_dev=None):
     return out
 
 
-def ntxent(fs, ft, tau: float = 0.07, weight: float = 1.0, want_grad: bool = True, grad_scale: float = 1.0):
+def ntxent(fs, ft, tau: float = 0.07, weight: float = 1.0, want_grad: bool = True, grad_scale: float = 1.0,
+           loss_out=None, dfs_out=None):
     """fs/ft: pooled features [n, D] fp32.  Returns (loss2 [weighted, raw], dfs | None)."""
     n, D = fs.shape
-    loss = torch.empty(2, dtype=torch.float32, device=fs.device)
-    dfs = torch.empty_like(fs) if want_grad else None
+    loss = loss_out if loss_out is not None else torch.empty(2, dtype=torch.float32, device=fs.device)
+    dfs = (dfs_out if dfs_out is not None else torch.empty_like(fs)) if want_grad else None
     NV.call("kd_ntxent", fs.contiguous().data_ptr(), ft.contiguous().data_ptr(), n, D, float(tau), float(weight),
             loss.data_ptr(), _ptr(dfs), float(grad_scale), _stream())
     return loss, dfs

@@ -50,13 +50,13 @@ def _log_softmax_T(logits: torch.Tensor, T: float) -> torch.Tensor:
 
 def top2_second_index(probs: torch.Tensor) -> torch.Tensor:
     """Index of the second most probable class (DT:170-171), ties -> lowest index."""
+    # = the second entry of a stable sort by -value (index order among ties), in two linear
+    # passes: torch.argmax returns the FIRST maximal index, so masking it and taking the
+    # argmax again gives the lowest-index runner-up (the tie partner when the max is tied)
     v = probs.detach()
-    n = v.shape[-1]
-    idx = torch.arange(n, device=v.device).expand_as(v)
-    # sort by (-value, index): stable sort on -value keeps index order among ties
-    order = torch.sort(-v, dim=-1, stable=True).indices
-    del idx
-    return order[..., 1]
+    i1 = torch.argmax(v, dim=-1, keepdim=True)
+    masked = v.scatter(-1, i1, float("-inf"))
+    return torch.argmax(masked, dim=-1)
 
 
 def last_position_table(ids: np.ndarray, V: int) -> np.ndarray:

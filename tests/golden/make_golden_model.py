@@ -73,6 +73,57 @@ def hf5_to_445(name):
     return None
 
 
+# rows of the student logits recorded in full (first / image / last text positions of each sample)
+LOGIT_ROWS = (0, 23, 24, 700, 1508, 1509, 1534, 1535)
+LOGIT_COL_STRIDE = 37      # ... at every 37th vocab column (4107 of 151936)
+
+
+class _Recorder:
+    """Captures the per-term values of the reference's forward without editing it: the
+    HF models' outputs (forward hooks: logits, in-model CE), every F.kl_div the loss
+    functions call (the KD term before its T^2 factor) and contrastive_loss's value."""
+
+    def __init__(self):
+        self.kl, self.ntx, self.out = [], [], {}
+
+    def __enter__(self):
+        import torch.nn.functional as F
+        self._F = F
+        self._kl = F.kl_div
+
+        def kl_rec(*a, **k):
+            v = self._kl(*a, **k)
+            self.kl.append(float(v))
+            return v
+        F.kl_div = kl_rec
+        return self
+
+    def __exit__(self, *exc):
+        self._F.kl_div = self._kl
+
+    def hook(self, name):
+        def fn(mod, args, out):
+            self.out[name] = out
+        return fn
+
+    def wrap_contrastive(self, obj):
+        orig = obj.contrastive_loss
+
+        def rec(*a, **k):
+            v = orig(*a, **k)
+            self.ntx.append(float(v))
+            return v
+        obj.contrastive_loss = rec
+
+
+def logit_stats(logits):
+    """Per-row logsumexp and sum (fp64) of [B, L, V] logits, plus rows LOGIT_ROWS sampled at
+    every LOGIT_COL_STRIDE-th column."""
+    x = logits.detach().double()
+    return (torch.logsumexp(x, -1).reshape(-1).numpy(), x.sum(-1).reshape(-1).numpy(),
+            x[:, list(LOGIT_ROWS), ::LOGIT_COL_STRIDE].float().numpy())
+
+
 def run(kind, phase, teacher_sd, student_sd, out_name):
     from transformers import LlavaOnevisionForConditionalGeneration  # noqa: F401
     MG._install_stub()
@@ -84,33 +135,40 @@ def run(kind, phase, teacher_sd, student_sd, out_name):
     student = hf_model(scfg, student_sd)
     teacher = hf_model(tcfg, teacher_sd) if kind != "bd" else None
     batch = batch_cpu()
-    if kind == "bd":
-        obj = MG._bare(BD, model=student)
-        student.train()
-        loss = obj.training_step(batch, 0)
-        terms = dict(total=loss.item())
-    else:
-        cls, hp = {"dt": (DT, dict(T=0.8, gamma=0.8, soft_target_loss_weight=0.1, ce_loss_weight=0.5, phase=phase)),
-                   "lb": (LB, dict(T=1, soft_target_loss_weight=0.5, ce_loss_weight=0.5)),
-                   "fb": (FB, dict(T=0.8, soft_target_loss_weight=0.1, ce_loss_weight=0.8))}[kind]
-        obj = MG._bare(cls, teacher_model=teacher, student_model=student, **hp)
-        teacher.eval()
-        for p in teacher.parameters():
-            p.requires_grad = False
-        # the reference's own hook functions, at the transformers-5 module path (DT:110-121)
-        teacher.model.vision_tower.post_layernorm.register_forward_hook(obj.hook_fn_teacher)
-        student.model.vision_tower.post_layernorm.register_forward_hook(obj.hook_fn_student)
-        if kind == "dt" and phase == 1:     # DT1T:105/111: freeze_student_language_layers
-            for p in student.model.language_model.parameters():
+    rec = _Recorder()
+    student.register_forward_hook(rec.hook("student"))
+    if teacher is not None:
+        teacher.register_forward_hook(rec.hook("teacher"))
+    T = 1.0
+    with rec:
+        if kind == "bd":
+            obj = MG._bare(BD, model=student)
+            student.train()
+            loss = obj.training_step(batch, 0)
+        else:
+            cls, hp = {"dt": (DT, dict(T=0.8, gamma=0.8, soft_target_loss_weight=0.1, ce_loss_weight=0.5, phase=phase)),
+                       "lb": (LB, dict(T=1, soft_target_loss_weight=0.5, ce_loss_weight=0.5)),
+                       "fb": (FB, dict(T=0.8, soft_target_loss_weight=0.1, ce_loss_weight=0.8))}[kind]
+            T = float(hp["T"])
+            obj = MG._bare(cls, teacher_model=teacher, student_model=student, **hp)
+            rec.wrap_contrastive(obj)
+            teacher.eval()
+            for p in teacher.parameters():
                 p.requires_grad = False
-            for p in student.lm_head.parameters():
-                p.requires_grad = False
-        if kind == "dt" and phase == 2:     # DT2T:106/112: freeze_student_vision_layers
-            for p in student.model.vision_tower.parameters():
-                p.requires_grad = False
-        student.train()
-        loss = obj.training_step(batch, 0)
-        terms = dict(total=loss.item())
+            # the reference's own hook functions, at the transformers-5 module path (DT:110-121)
+            teacher.model.vision_tower.post_layernorm.register_forward_hook(obj.hook_fn_teacher)
+            student.model.vision_tower.post_layernorm.register_forward_hook(obj.hook_fn_student)
+            if kind == "dt" and phase == 1:     # DT1T:105/111: freeze_student_language_layers
+                for p in student.model.language_model.parameters():
+                    p.requires_grad = False
+                for p in student.lm_head.parameters():
+                    p.requires_grad = False
+            if kind == "dt" and phase == 2:     # DT2T:106/112: freeze_student_vision_layers
+                for p in student.model.vision_tower.parameters():
+                    p.requires_grad = False
+            student.train()
+            loss = obj.training_step(batch, 0)
+    assert len(rec.kl) <= 1 and len(rec.ntx) <= 1, (rec.kl, rec.ntx)
     loss.backward()
     grads = {}
     for n, p in student.named_parameters():
@@ -123,7 +181,19 @@ def run(kind, phase, teacher_sd, student_sd, out_name):
         if k445 in grads:
             raise RuntimeError(k445)
         grads[k445] = g
-    out = dict(total=np.float64(terms["total"]))
+    so = rec.out["student"]
+    out = dict(total=np.float64(loss.item()),
+               # per-term values of the reference's own forward (NaN = the term is absent)
+               kd_term=np.float64(rec.kl[0] * T * T if rec.kl else np.nan),     # kl_div(...) * T**2
+               student_ce=np.float64(so.loss.item()),
+               teacher_ce=np.float64(rec.out["teacher"].loss.item() if "teacher" in rec.out else np.nan),
+               ntxent=np.float64(rec.ntx[0] if rec.ntx else np.nan))
+    lse, rsum, rows = logit_stats(so.logits)
+    out.update(s_logit_lse=lse, s_logit_rowsum=rsum, s_logit_rows=rows, logit_rows=np.array(LOGIT_ROWS),
+               logit_col_stride=np.int64(LOGIT_COL_STRIDE))
+    if "teacher" in rec.out:
+        tl, ts, _ = logit_stats(rec.out["teacher"].logits)
+        out.update(t_logit_lse=tl, t_logit_rowsum=ts)
     names = sorted(grads)
     out["grad_names"] = np.array(names)
     out["grad_norms"] = np.array([float(grads[n].norm()) for n in names])
@@ -132,7 +202,8 @@ def run(kind, phase, teacher_sd, student_sd, out_name):
     out["grad_total_norm"] = np.float64(math_sqrt(tot))
     meta = dict(kind=kind, phase=phase, B=B, L=L, seed_t=SEED_T, seed_s=SEED_S, seed_data=SEED_DATA)
     np.savez_compressed(HERE / f"model_{out_name}.npz", meta=json.dumps(meta), **out)
-    print(out_name, "total", terms["total"], "grad norm", out["grad_total_norm"], "n_grads", len(names))
+    print(out_name, {k: float(out[k]) for k in ("total", "kd_term", "student_ce", "teacher_ce", "ntxent")},
+          "grad norm", out["grad_total_norm"], "n_grads", len(names))
 
 
 def math_sqrt(x):

@@ -1,0 +1,160 @@
+"""Property tests at the bench configuration's real shapes (c1: B = 4, L = 1536).
+
+The kernels' size-dependent paths (XCD remap and tile grouping at 24 x 148 tiles, the
+hybrid split tail at 336 tiles, buffer-descriptor ranges on the 1.87 GB logits, causal
+GQA attention at 28q/4kv hd 128 over 4 x 1536 tokens) are checked against torch fp32 on
+the same bf16 inputs: every output row of a sample of rows and every row of a sample of
+columns (a full fp32 product of these sizes would not fit a test's time budget).
+
+Tolerance (bf16 output of an fp32 accumulation): |err| <= 1e-2 |ref| + 1e-2 rms(ref).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+M = 4 * 1536   # c1 tokens per model
+
+
+def _ops():
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
+    return ops
+
+
+def _rand(*shape, dev, scale=1.0, seed=0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=dev) * scale).to(torch.bfloat16)
+
+
+def _check(out, ref, rtol=1e-2, what=""):
+    ref = ref.float()
+    err = (out.float() - ref).abs()
+    tol = rtol * ref.abs() + rtol * ref.pow(2).mean().sqrt()
+    bad = int((err > tol).sum())
+    assert bad == 0, f"{what}: {bad} elements out of tolerance, max err {err.max().item():.3e}"
+
+
+def _samples(n, k, dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.randperm(n, generator=g)[:k - 2]
+    return torch.cat([idx, torch.tensor([0, n - 1])]).sort().values.to(dev)
+
+
+@pytest.mark.parametrize("name,N,K", [("teacher lm_head", 152064, 3584), ("teacher o_proj", 3584, 3584),
+                                      ("teacher down_proj (hybrid split tail)", 3584, 18944),
+                                      ("student lm_head", 151936, 896)])
+def test_forward_gemm_bench_shapes(name, N, K, dev):
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=1)
+    w = _rand(N, K, dev=dev, seed=2, scale=0.02)
+    out = ops.gemm(a, w)
+    rows, cols = _samples(M, 48, dev, 3), _samples(N, 48, dev, 4)
+    _check(out[rows], a[rows].float() @ w.float().t(), what=f"{name} rows")
+    _check(out[:, cols], a.float() @ w[cols].float().t(), what=f"{name} cols")
+
+
+def test_swiglu_gate_up_teacher_shape(dev):
+    """Fused gate|up GEMM + SwiGLU epilogue at 6144 x 37888 x 3584 (the roofline kernel)."""
+    ops = _ops()
+    I, K = 18944, 3584
+    a = _rand(M, K, dev=dev, seed=5)
+    w = _rand(2 * I, K, dev=dev, seed=6, scale=0.02)
+    aux = torch.empty((M, 2 * I), dtype=torch.bfloat16, device=dev)
+    h = ops.gemm(a, w, act="swiglu", aux=aux)
+    rows, cols = _samples(M, 32, dev, 7), _samples(I, 32, dev, 8)
+
+    def ref(x, wg, wu):
+        g = (x.float() @ wg.float().t()).bfloat16().float()     # the epilogue rounds v to bf16 first
+        u = (x.float() @ wu.float().t()).bfloat16().float()
+        return torch.nn.functional.silu(g) * u, g, u
+    r, g, u = ref(a[rows], w[:I], w[I:])
+    _check(h[rows], r, what="swiglu rows")
+    _check(aux[rows, :I], g, what="aux gate rows")
+    _check(aux[rows, I:], u, what="aux up rows")
+    rc, _, _ = ref(a, w[cols], w[I + cols])
+    _check(h[:, cols], rc, what="swiglu cols")
+
+
+def test_student_lm_head_backward_shapes(dev):
+    """lm_head dgrad (K = 151936) and tied-embedding wgrad (fp32 accumulate, K = 6144 tokens)."""
+    ops = _ops()
+    V, H = 151936, 896
+    dl = _rand(M, V, dev=dev, seed=9, scale=1e-3)
+    w = _rand(V, H, dev=dev, seed=10, scale=0.02)
+    hn = _rand(M, H, dev=dev, seed=11)
+    dhn = ops.gemm(dl, w.t())                                     # [M, H]
+    rows = _samples(M, 48, dev, 12)
+    _check(dhn[rows], dl[rows].float() @ w.float(), what="dgrad rows")
+    gw = torch.full((V, H), 0.25, dtype=torch.float32, device=dev)
+    ops.gemm(dl.t(), hn.t(), out=gw, accumulate=True)             # gw += dl^T hn
+    vrows = _samples(V, 48, dev, 13)
+    ref = 0.25 + dl[:, vrows].float().t() @ hn.float()
+    err = (gw[vrows] - ref).abs()
+    assert float(err.max()) <= 1e-4 * float(ref.abs().max()) + 1e-6
+
+
+@pytest.mark.parametrize("B,H,HKV,hd,causal", [(4, 28, 4, 128, True), (4, 14, 2, 64, True)])
+def test_attention_bench_shape(B, H, HKV, hd, causal, dev):
+    """Teacher (28q/4kv, hd 128) and student (14q/2kv, hd 64) causal attention, B = 4, S = 1536;
+    the student's backward too."""
+    ops = _ops()
+    S = 1536
+    q = _rand(B, H, S, hd, dev=dev, seed=14)
+    k = _rand(B, HKV, S, hd, dev=dev, seed=15)
+    v = _rand(B, HKV, S, hd, dev=dev, seed=16)
+    o, lse = ops.attn_fwd(q, k, v, hd, causal)
+    rep = H // HKV
+    heads = [0, H // 2, H - 1]
+    mask = torch.triu(torch.ones(S, S, dtype=torch.bool, device=dev), 1)
+    for b in (0, B - 1):
+        for h in heads:
+            s = q[b, h].float() @ k[b, h // rep].float().t() / math.sqrt(hd)
+            s = s.masked_fill(mask, float("-inf"))
+            ro = torch.softmax(s, -1) @ v[b, h // rep].float()
+            err = (o[b, :, h].float() - ro).abs()
+            assert float(err.max()) <= 2e-2 * float(ro.pow(2).mean().sqrt()) + 1e-2 * float(ro.abs().max())
+            assert float((lse[b, h] - torch.logsumexp(s, -1)).abs().max()) < 1e-3
+    if hd == 64:   # the student's backward
+        g = torch.Generator(device=dev).manual_seed(17)
+        do = (torch.randn(B, S, H, hd, generator=g, device=dev)).to(torch.bfloat16)
+        dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, hd, causal)
+        b, kvh = B - 1, HKV - 1
+        qf = q[b, kvh * rep:(kvh + 1) * rep].float().requires_grad_(True)
+        kf = k[b, kvh].float().requires_grad_(True)
+        vf = v[b, kvh].float().requires_grad_(True)
+        s = (qf @ kf.t() / math.sqrt(hd)).masked_fill(mask, float("-inf"))
+        ro = torch.softmax(s, -1) @ vf
+        ro.backward(do[b, :, kvh * rep:(kvh + 1) * rep].float().permute(1, 0, 2))
+        for got, ref in ((dq[b, kvh * rep:(kvh + 1) * rep], qf.grad), (dk[b, kvh], kf.grad), (dv[b, kvh], vf.grad)):
+            err = (got.float() - ref).abs()
+            bound = 8e-2 * ref.pow(2).mean().sqrt() + 3e-2 * ref.abs()
+            assert bool((err <= bound).all()), f"max err {err.max().item():.3e}"
+
+
+def test_kd_loss_bench_shape_properties(dev):
+    """The fused KD loss at c1's full size ([4, 1536, 151936] student, 152064 teacher):
+    the loss terms equal the oracle on sampled rows' contributions (exact per-row sums are
+    size independent), dlogits rows sum to ~0 (softmax gradients), and LoCa with labels
+    in range reports no error."""
+    ops = _ops()
+    B, L, Vs, Vt = 4, 1536, 151936, 152064
+    g = torch.Generator(device=dev).manual_seed(18)
+    t = (torch.randn(B, L, Vt, generator=g, device=dev) * 2).to(torch.bfloat16)
+    s = (torch.randn(B, L, Vs, generator=g, device=dev) * 2).to(torch.bfloat16)
+    labels = torch.randint(0, 151643, (B, L), generator=g, device=dev)
+    err = torch.zeros(4, dtype=torch.int32, device=dev)
+    loss, dl = ops.kd_loss_fwd_bwd(s, t, labels, "loca", temperature=1.0, err_out=err)
+    torch.cuda.synchronize()
+    assert int(err[0]) == 0
+    kd, ce, tce, tot = loss.tolist()
+    # CE = mean over rows of lse(s) - s[label]: computed here in fp64 over all rows
+    sf = s.double()
+    lse = torch.logsumexp(sf, -1)
+    tgt = labels[:, 1:]
+    ref_ce = float((lse[:, :-1] - sf[:, :-1].gather(-1, tgt[..., None])[..., 0]).mean())
+    assert abs(ce - ref_ce) <= 1e-4 * abs(ref_ce)
+    assert kd > 0 and math.isfinite(kd) and abs(tot - (kd + ce)) <= 1e-5 * abs(tot)
+    rs = dl.double().sum(-1)                      # each row's gradient sums to 0 (up to bf16 rounding
+    assert float(rs.abs().max()) < 4e-3 * float(dl.float().abs().amax())   # of its largest element)

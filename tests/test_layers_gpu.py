@@ -192,12 +192,13 @@ def test_colsum_and_group_mean(dev):
     assert torch.allclose(dx.float().view(4, 729, 1152), pm[:, None].expand(4, 729, 1152) / 729, rtol=1e-2, atol=1e-8)
 
 
-def test_ntxent_matches_oracle(dev):
+@pytest.mark.parametrize("n", [8, 16, 64])   # c1 (2B = 8 tiles), c2 (2B = 16), the kernel's limit
+def test_ntxent_matches_oracle(n, dev):
     from oracle import kd_losses as O
     ops = _ops()
     g = torch.Generator().manual_seed(22)
-    fs = torch.randn(8, 1152, generator=g)
-    ft = torch.randn(8, 1152, generator=g) + 0.3 * fs
+    fs = torch.randn(n, 1152, generator=g)
+    ft = torch.randn(n, 1152, generator=g) + 0.3 * fs
     loss, dfs = ops.ntxent(fs.to(dev), ft.to(dev), weight=0.5)
     x = fs.clone().requires_grad_(True)
     ref = O.nt_xent(O.l2_normalize(x), O.l2_normalize(ft))

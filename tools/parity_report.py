@@ -1,0 +1,95 @@
+"""End-to-end parity report: every per-term value of the HIP training_step vs the
+reference's own forward (tests/golden/model_*.npz), as measured deltas.
+
+    python tools/parity_report.py [--out profiles/r02/parity.json]
+
+For each module kind: KD term, student CE, teacher CE, NT-Xent, total (|Δ|, rel Δ and
+whether |Δ| <= 1e-4 + 1e-3 |ref|, the north-star tolerance); student logits per-row
+logsumexp and sampled rows; the student gradient's total norm.  GPU only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "tests"))
+sys.path.insert(0, str(REPO / "tests" / "golden"))
+
+ATOL, RTOL = 1e-4, 1e-3
+
+
+def _d(got, ref):
+    ad = abs(got - ref)
+    return dict(got=got, ref=ref, abs=ad, rel=ad / abs(ref) if ref else None, ok=bool(ad <= ATOL + RTOL * abs(ref)))
+
+
+def measure(name, dev):
+    import numpy as np
+    import torch
+    from model_fixtures import KINDS, batch, load
+    from test_kd_step_gpu import _module
+    meta, exp = load(name)
+    kind, phase = KINDS[name]
+    m = _module(kind, phase)
+    m.keep_logits = True
+    b = batch(meta, dev)
+    loss = m.training_step(b, 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    kd, ce, tce, tot = m.last_terms.tolist()
+    out = {"total": _d(loss.item(), float(exp["total"])), "student_ce": _d(ce, float(exp["student_ce"]))}
+    if not math.isnan(float(exp["teacher_ce"])):
+        out["teacher_ce"] = _d(tce, float(exp["teacher_ce"]))
+    if not math.isnan(float(exp["kd_term"])):
+        out["kd_term"] = _d(kd, float(exp["kd_term"]))
+    if not math.isnan(float(exp["ntxent"])):
+        out["ntxent"] = _d(float(m.last_ntxent[1]), float(exp["ntxent"]))
+    s3, _ = m.last_logits
+    lse = torch.logsumexp(s3.double(), -1).reshape(-1).cpu().numpy()
+    dl = np.abs(lse - exp["s_logit_lse"])
+    out["s_logit_lse"] = dict(max_abs=float(dl.max()), max_rel=float((dl / np.abs(exp["s_logit_lse"])).max()),
+                              ok=bool((dl <= ATOL + RTOL * np.abs(exp["s_logit_lse"])).all()))
+    rows = exp["logit_rows"].tolist()
+    st = int(exp["logit_col_stride"])
+    got = s3[:, rows, ::st].float().cpu().numpy()
+    ref = exp["s_logit_rows"]
+    err = np.abs(got - ref)
+    out["s_logit_rows"] = dict(max_abs=float(err.max()), rms_ref=float(np.sqrt((ref ** 2).mean())),
+                               max_rel_to_rms=float(err.max() / np.sqrt((ref ** 2).mean())),
+                               frac_within_north_star=float((err <= ATOL + RTOL * np.abs(ref)).mean()))
+    P = m.student_model.P
+    names = [str(n) for n in exp["grad_names"]]
+    tot2 = 0.0
+    for n in names:
+        g = P.grad_view(n)
+        spec = next(s for s in P.specs if s.name == n)
+        if spec.ckpt_shape is not None:
+            g = g[:, :int(np.prod(spec.ckpt_shape[1:]))]
+        tot2 += float(g.double().pow(2).sum())
+    out["grad_total_norm"] = _d(math.sqrt(tot2), float(exp["grad_total_norm"]))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    from model_fixtures import KINDS
+    dev = torch.device("cuda:0")
+    rep = {"tolerance": f"|d| <= {ATOL} + {RTOL} |ref| (north_star)"}
+    for name in KINDS:
+        rep[name] = measure(name, dev)
+        print(name, json.dumps(rep[name]), flush=True)
+    if a.out:
+        Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(a.out).write_text(json.dumps(rep, indent=1))
+
+
+if __name__ == "__main__":
+    main()
