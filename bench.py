@@ -321,7 +321,7 @@ def main():
             br[kind] = dict(launches=s["launches"], avg_us=round(s["avg_ms"] * 1e3, 2),
                             tflops=round(s["flops"] / (s["total_ms"] * 1e-3) / 1e12, 1),
                             share_of_step=round(s["total_ms"] / 2 * 1e-3 / (dt / a.steps), 3))
-    if a.shapes and rank == 0 and ops.TIMER.records:
+    if a.shapes and rank == 0:
         with open(a.shapes, "w") as f:
             json.dump(ops.TIMER.by_shape(top=200), f, indent=1)
     # the roofline kernel: the fused gate|up + SwiGLU GEMM (k_gemm8<K-major,K-major> SwiGLU build,

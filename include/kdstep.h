@@ -47,7 +47,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 2
+#define KD_ABI_VERSION 3
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -313,6 +313,83 @@ int kd_gen_select(const void* logits, int V, int64_t* seq, int len, int32_t* cur
                   int no_repeat_ngram, void* workspace, size_t workspace_bytes, int64_t* out, void* stream);
 int kd_rope_row(const float* cos_table, const float* sin_table, int hh, const int32_t* cur_dev, float* cos_row,
                 float* sin_row, void* stream);
+
+/* --------------------------------------------------------- model runtime ---- */
+/* One LLaVA-OneVision instance (SigLIP -> projector -> anyres pack -> Qwen2 -> lm_head)
+ * whose forward and backward layer loops run in the library (SURVEY §8b "teacher forward"
+ * / "student forward and backward with saved-activation workspace handles").  Replaces
+ * the reference's model calls
+ *   self.teacher_model(input_ids=, pixel_values=, image_sizes=, labels=)   DT:228 (no_grad)
+ *   self.student_model(input_ids=, pixel_values=, image_sizes=, labels=)   DT:238
+ * and the autograd backward Lightning runs through the student for `loss` (DT:123-131).
+ * The arithmetic is transformers' (HF5 siglip :116-357, llava_onevision :131-150,
+ * :280-343, :510-513, qwen2 :35-300).
+ *
+ * Weights: one flat bf16 buffer in the transformers-4.45 state_dict order whose layout
+ * kd_model_param_info() defines (every tensor 16-B aligned; fused q|k|v and gate|up are
+ * adjacent); gradients (trainable models): a flat fp32 buffer of the same layout,
+ * accumulated into (+=).  The caller owns both; the handle only keeps the pointers. */
+typedef struct {
+    int32_t v_hidden, v_inter, v_layers, v_heads, v_patch, v_image;   /* SigLIP          */
+    float v_eps;
+    int32_t t_hidden, t_inter, t_layers, t_heads, t_kv_heads, t_head_dim, t_vocab, t_tie; /* Qwen2 */
+    float t_rope_theta, t_eps;
+    int64_t image_token_id;                                            /* 151646           */
+    int32_t projector_act;                                             /* kd_act (GELU_ERF)*/
+} kd_model_config;
+
+/* Parameter layout: count, then per index the 4.45 name, flat offset and element count
+ * (storage shape rows x cols; cols = 0 for 1-D).  The SigLIP conv weight is stored
+ * im2col-flattened [hidden, 3*patch*patch padded to a multiple of 8]. */
+int kd_model_param_count(const kd_model_config* cfg);
+int64_t kd_model_param_numel(const kd_model_config* cfg);          /* flat length (padded) */
+int kd_model_param_info(const kd_model_config* cfg, int index, char* name, int name_cap, int64_t* offset,
+                        int64_t* numel, int64_t* rows, int64_t* cols);
+
+typedef struct kd_model kd_model;
+int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad, kd_model** out);
+void kd_model_destroy(kd_model* m);
+/* freeze masks (DT:468-523): which regions receive weight gradients */
+int kd_model_set_trainable(kd_model* m, int vision, int projector, int language);
+
+/* Forward.  ids int64 [B, L]; pixels [B*tiles, 3, image, image] (kd_dtype); src int32 [B*L]
+ * from kd_image_src_map; rope_cos/rope_sin fp32 [L, head_dim/2] (Qwen2RotaryEmbedding:
+ * inv_freq = 1 / theta^(2i/hd) in fp32, angle = pos * inv_freq).  save = 1 keeps every
+ * activation the backward reads in `workspace` (the saved-activation handle: pass the
+ * same pointer to kd_model_backward and leave it untouched until then).
+ * Outputs: hn bf16 [B*L, t_hidden] (final-norm hidden state); post_ln (optional) bf16
+ * [B*tiles*np, v_hidden] (the vision post_layernorm output the reference hooks, DT:100-121);
+ * logits (optional) bf16 [B*L, vocab] (lm_head); kv_k / kv_v (optional, host arrays of
+ * t_layers device pointers) receive each layer's roped keys / values [B, kv_heads, L,
+ * head_dim] (generate()'s prefill).  err: kd_embed_assemble's error word. */
+size_t kd_model_forward_workspace_size(const kd_model* m, int B, int L, int tiles, int save);
+int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pixel_dtype, const int32_t* src,
+                     const float* rope_cos, const float* rope_sin, int B, int L, int tiles, int save,
+                     void* workspace, size_t workspace_bytes, void* hn, void* post_ln, void* logits,
+                     void* const* kv_k, void* const* kv_v, int32_t* err, void* stream);
+
+/* Backward of a save = 1 forward (fwd_workspace) from dhn (bf16 [B*L, t_hidden], grad of
+ * hn) and dpost (optional bf16 grad of post_ln) into the grad buffer (+=).  Weight
+ * gradients run on wgrad_stream beside the dgrad chain on `stream`; `stream` waits for
+ * all of it before returning.  Work already queued on wgrad_stream (e.g. the caller's
+ * lm_head wgrad into a tied embedding) is ordered before the embedding backward.
+ * on_layer_done (optional) is called after each Qwen2 layer's backward is enqueued,
+ * top-down (bucketed data-parallel all-reduce). */
+typedef void (*kd_layer_cb)(void* user, int layer);
+size_t kd_model_backward_workspace_size(const kd_model* m, int B, int L, int tiles);
+int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids, const int32_t* src,
+                      const float* rope_cos, const float* rope_sin, int B, int L, int tiles,
+                      const void* dhn, const void* dpost, void* workspace, size_t workspace_bytes,
+                      void* stream, void* wgrad_stream, kd_layer_cb on_layer_done, void* user);
+
+/* GEMM timer (measurement): while enabled, every kd_gemm launch (the ABI entry and the
+ * model runtime's) is bracketed by HIP events on its stream.  kd_timer_read synchronises
+ * record i's end event and returns its key "<kind>:<M>x<N>x<K>:<f32|bf16>[:acc]", kind =
+ * gemm_{k|n}{k|n} (A / B layout) or gemm_kk_swiglu, its FLOPs and milliseconds. */
+void kd_timer_enable(int on);
+int kd_timer_count(void);
+int kd_timer_read(int i, char* key, int key_cap, double* flops, float* ms);
+void kd_timer_reset(void);
 
 #ifdef __cplusplus
 }

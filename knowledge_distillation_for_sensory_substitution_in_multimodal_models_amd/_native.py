@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("KDSTEP_LIB", _PKG / "libkdstep.so"))
 HEADER = _PKG.parent / "include" / "kdstep.h"
 
 KD_OK = 0
-ABI_VERSION = 2
+ABI_VERSION = 3
 STATUS_NAMES = {
     0: "KD_OK", 1: "KD_ERR_SHAPE", 2: "KD_ERR_DTYPE", 3: "KD_ERR_ALIGN", 4: "KD_ERR_ARCH",
     5: "KD_ERR_LABEL_RANGE", 6: "KD_ERR_LAUNCH", 7: "KD_ERR_ARG", 8: "KD_ERR_WORKSPACE",
@@ -82,6 +82,19 @@ class KdAttnBwdDesc(C.Structure):
                 ("hdp", C.c_int32), ("causal", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64)]
 
 
+class KdModelConfig(C.Structure):
+    _fields_ = [("v_hidden", C.c_int32), ("v_inter", C.c_int32), ("v_layers", C.c_int32), ("v_heads", C.c_int32),
+                ("v_patch", C.c_int32), ("v_image", C.c_int32), ("v_eps", C.c_float),
+                ("t_hidden", C.c_int32), ("t_inter", C.c_int32), ("t_layers", C.c_int32), ("t_heads", C.c_int32),
+                ("t_kv_heads", C.c_int32), ("t_head_dim", C.c_int32), ("t_vocab", C.c_int32), ("t_tie", C.c_int32),
+                ("t_rope_theta", C.c_float), ("t_eps", C.c_float),
+                ("image_token_id", C.c_int64), ("projector_act", C.c_int32)]
+
+
+# void (*kd_layer_cb)(void* user, int layer)
+LAYER_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
+
+
 class KdError(RuntimeError):
     def __init__(self, fn: str, code: int, msg: str):
         super().__init__(f"{fn}: {STATUS_NAMES.get(code, code)}: {msg}")
@@ -135,6 +148,23 @@ SIGNATURES = {
     "kd_rope_row": (_i32, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "kd_image_resize_u8": (_i32, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _sz, _vp]),
     "kd_anyres_tiles": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp]),
+    "kd_model_param_count": (_i32, [C.POINTER(KdModelConfig)]),
+    "kd_model_param_numel": (_i64, [C.POINTER(KdModelConfig)]),
+    "kd_model_param_info": (_i32, [C.POINTER(KdModelConfig), _i32, C.c_char_p, _i32, C.POINTER(_i64),
+                                   C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
+    "kd_model_create": (_i32, [C.POINTER(KdModelConfig), _vp, _vp, C.POINTER(_vp)]),
+    "kd_model_destroy": (None, [_vp]),
+    "kd_model_set_trainable": (_i32, [_vp, _i32, _i32, _i32]),
+    "kd_model_forward_workspace_size": (_sz, [_vp, _i32, _i32, _i32, _i32]),
+    "kd_model_forward": (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _sz, _vp, _vp, _vp,
+                                _vp, _vp, _vp, _vp]),
+    "kd_model_backward_workspace_size": (_sz, [_vp, _i32, _i32, _i32]),
+    "kd_model_backward": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp, _vp,
+                                 LAYER_CB, _vp]),
+    "kd_timer_enable": (None, [_i32]),
+    "kd_timer_count": (_i32, []),
+    "kd_timer_read": (_i32, [_i32, C.c_char_p, _i32, C.POINTER(C.c_double), C.POINTER(_f32)]),
+    "kd_timer_reset": (None, []),
 }
 
 _lib = None

@@ -531,14 +531,24 @@ __global__ void k_row_group_mean_bwd(const float* __restrict__ dpool, int G, int
 // one workgroup; n <= 64 features of dim D.  fs/ft pooled (pre-normalisation) student /
 // teacher features.  DT:246-248 normalises once, contrastive_loss normalises again
 // (idempotent up to rounding; both applied).  loss = CE(S T^T / tau, arange).
+// FEATS_LDS: the normalised features are staged in LDS (2 n D floats, n <= 16 at D = 1152);
+// otherwise every read recomputes x / n1 / n2 from the (L2-resident) inputs — the same
+// arithmetic, so both builds give identical results.
+template <bool FEATS_LDS>
 __global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, const float* __restrict__ ft, int n, int D,
                                                float tau, float weight, float* __restrict__ loss_out,
                                                float* __restrict__ dfs, float grad_scale) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];  // s_hat[n][D], t_hat[n][D], logits[n][n], norms
-    float* sh = sm;
-    float* th = sh + n * D;
-    float* lg = th + n * D;
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // logits[n][n], norms[4n](, s_hat[n][D], t_hat[n][D])
+    float* lg = sm;
     float* nrm = lg + n * n;  // [4n]: |fs|, |s1|, |ft|, |t1|
+    float* sh = nrm + 4 * n;
+    float* th = sh + n * D;
+    auto SH = [&](int i, int d) -> float {
+        return FEATS_LDS ? sh[i * D + d] : fs[(int64_t)i * D + d] / nrm[i] / nrm[n + i];
+    };
+    auto TH = [&](int j, int d) -> float {
+        return FEATS_LDS ? th[j * D + d] : ft[(int64_t)j * D + d] / nrm[2 * n + j] / nrm[3 * n + j];
+    };
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // norms (two normalisations, each x / max(|x|, 1e-12))
     for (int r = w; r < 2 * n; r += 4) {
@@ -551,8 +561,10 @@ __global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, con
         for (int d = lane; d < D; d += 64) { const float y = src[d] / n1; s3 += y * y; }
         s3 = wave_sum(s3);
         const float n2 = fmaxf(sqrtf(s3), 1e-12f);
-        float* dst = r < n ? sh + r * D : th + (r - n) * D;
-        for (int d = lane; d < D; d += 64) dst[d] = src[d] / n1 / n2;
+        if (FEATS_LDS) {
+            float* dst = r < n ? sh + r * D : th + (r - n) * D;
+            for (int d = lane; d < D; d += 64) dst[d] = src[d] / n1 / n2;
+        }
         if (lane == 0) {
             if (r < n) { nrm[r] = n1; nrm[n + r] = n2; }
             else { nrm[2 * n + r - n] = n1; nrm[3 * n + r - n] = n2; }
@@ -562,7 +574,7 @@ __global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, con
     for (int e = w; e < n * n; e += 4) {
         const int i = e / n, j = e % n;
         float s = 0.f;
-        for (int d = lane; d < D; d += 64) s += sh[i * D + d] * th[j * D + d];
+        for (int d = lane; d < D; d += 64) s += SH(i, d) * TH(j, d);
         s = wave_sum(s);
         if (lane == 0) lg[e] = s / tau;
     }
@@ -594,23 +606,23 @@ __global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, con
         float yg = 0.f;
         for (int d = lane; d < D; d += 64) {
             float g = 0.f;
-            for (int j = 0; j < n; ++j) g += lg[i * n + j] * th[j * D + d];
+            for (int j = 0; j < n; ++j) g += lg[i * n + j] * TH(j, d);
             g /= tau;
             dfs[(int64_t)i * D + d] = g;  // scratch
-            yg += g * sh[i * D + d];
+            yg += g * SH(i, d);
         }
         yg = wave_sum(yg);
         const float n1 = nrm[i], n2 = nrm[n + i];
         float uq = 0.f;
         for (int d = lane; d < D; d += 64) {
-            const float y = sh[i * D + d];
+            const float y = SH(i, d);
             const float gu = (dfs[(int64_t)i * D + d] - y * yg) / n2;
             dfs[(int64_t)i * D + d] = gu;
             uq += gu * (y * n2);  // u = y * n2
         }
         uq = wave_sum(uq);
         for (int d = lane; d < D; d += 64) {
-            const float u = sh[i * D + d] * n2;
+            const float u = SH(i, d) * n2;
             dfs[(int64_t)i * D + d] = (dfs[(int64_t)i * D + d] - u * uq) / n1;
         }
     }
@@ -908,10 +920,14 @@ int launch_ntxent(const float* fs, const float* ft, int n, int D, float tau, flo
                   float grad_scale, void* stream) {
     KD_CHECK_ARG(fs && ft && loss_out, "ntxent: null pointer");
     KD_CHECK_SHAPE(n >= 1 && n <= 64, "ntxent: 1 <= n <= 64");
-    const size_t smem = ((size_t)2 * n * D + n * n + 4 * n) * 4;
-    KD_CHECK_SHAPE(smem <= 160 * 1024, "ntxent: n * D too large for LDS");
-    hipLaunchKernelGGL(k_ntxent, dim3(1), dim3(NT), smem, as_stream(stream), fs, ft, n, D, tau, weight, loss_out, dfs,
-                       grad_scale);
+    KD_CHECK_SHAPE(D >= 1, "ntxent: D >= 1");
+    const size_t small = ((size_t)n * n + 4 * n) * 4, full = small + (size_t)2 * n * D * 4;
+    if (full <= 160 * 1024)
+        hipLaunchKernelGGL(k_ntxent<true>, dim3(1), dim3(NT), full, as_stream(stream), fs, ft, n, D, tau, weight,
+                           loss_out, dfs, grad_scale);
+    else
+        hipLaunchKernelGGL(k_ntxent<false>, dim3(1), dim3(NT), small, as_stream(stream), fs, ft, n, D, tau, weight,
+                           loss_out, dfs, grad_scale);
     KD_LAUNCH_CHECK("k_ntxent");
     return KD_OK;
 }

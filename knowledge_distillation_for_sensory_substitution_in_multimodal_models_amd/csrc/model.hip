@@ -1,0 +1,959 @@
+// Model runtime: the LLaVA-OneVision forward and backward layer loops in C++ (include/kdstep.h
+// "model runtime").  The reference calls transformers' LlavaOnevisionForConditionalGeneration
+// for the teacher under no_grad (DT:228) and for the student (DT:238), and Lightning's
+// autograd runs the student backward; here both loops issue the library's kernels straight
+// from C++ onto the caller's HIP streams (one host call per model per step instead of
+// ~700-1000 Python launches).
+//
+// Memory: the caller hands in one workspace per call, sized by the *_workspace_size
+// queries; a bump allocator carves it in a fixed order, so the backward re-derives every
+// saved activation's address from the forward's workspace pointer alone.  save = 1 keeps
+// one buffer per layer for each activation the backward reads; save = 0 reuses one set of
+// buffers across layers (stream order makes the reuse safe).
+//
+// Weight gradients (dW = dY^T X and bias column sums) run on a second stream beside the
+// dgrad chain (dX = dY W), which is what the next layer waits for: the student's small-N
+// backward GEMMs (hidden 896, SigLIP 1152) leave CUs idle that the other stream fills.
+// The dgrad chain waits on the lane only before it updates dx in place (the lane reads
+// dx); every other buffer the lane reads is rewritten only after such a wait (see
+// lm_backward), so single buffers suffice.
+#include "common.h"
+#include "launchers.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace kd {
+
+// ================================================================ GEMM timer ====
+namespace {
+struct TimerRec {
+    std::string key;
+    double flops;
+    hipEvent_t e0, e1;
+};
+std::mutex g_timer_mu;
+std::vector<TimerRec> g_timer;
+bool g_timer_on = false;
+}  // namespace
+
+int gemm_timed(const kd_gemm_desc* d, void* stream) {
+    if (!g_timer_on) return launch_gemm(d, stream);
+    TimerRec r;
+    const bool swiglu = d->act == KD_ACT_SWIGLU;
+    r.key = swiglu ? std::string("gemm_kk_swiglu")
+                   : std::string("gemm_") + (d->a_layout ? 'n' : 'k') + (d->b_layout ? 'n' : 'k');
+    r.key += ":" + std::to_string(d->M) + "x" + std::to_string(d->N) + "x" + std::to_string(d->K) + ":" +
+             (d->c_dtype == KD_DTYPE_F32 ? "f32" : "bf16") + (d->accumulate ? ":acc" : "");
+    r.flops = 2.0 * d->M * d->N * d->K;
+    hipEventCreate(&r.e0);
+    hipEventCreate(&r.e1);
+    hipEventRecord(r.e0, as_stream(stream));
+    const int st = launch_gemm(d, stream);
+    hipEventRecord(r.e1, as_stream(stream));
+    std::lock_guard<std::mutex> g(g_timer_mu);
+    g_timer.push_back(r);
+    return st;
+}
+
+// ============================================================ parameter layout ====
+namespace {
+
+struct Spec {
+    std::string name;
+    int64_t rows, cols;   // storage shape (cols = 0: 1-D)
+    int64_t offset, numel;
+};
+
+struct Cfg {
+    kd_model_config c;
+    int v_hd() const { return c.v_hidden / c.v_heads; }
+    int v_hdp() const { return v_hd() <= 64 ? 64 : (v_hd() <= 80 ? 96 : 128); }   // attention head-dim padding
+    int grid() const { return c.v_image / c.v_patch; }
+    int np() const { return grid() * grid(); }
+    int kpatch() const { return (3 * c.v_patch * c.v_patch + 7) / 8 * 8; }
+    int qd() const { return c.t_heads * c.t_head_dim; }
+    int kvd() const { return c.t_kv_heads * c.t_head_dim; }
+};
+
+// The order of modeling.param_specs (transformers-4.45 state_dict order), offsets aligned to
+// 8 elements (16 B).
+std::vector<Spec> make_specs(const Cfg& C, int64_t* total) {
+    const kd_model_config& c = C.c;
+    std::vector<Spec> S;
+    int64_t off = 0;
+    auto add = [&](const std::string& n, int64_t r, int64_t cl) {
+        off = (off + 7) / 8 * 8;
+        const int64_t ne = cl ? r * cl : r;
+        S.push_back({n, r, cl, off, ne});
+        off += ne;
+    };
+    const std::string vp = "vision_tower.vision_model.";
+    const int64_t D = c.v_hidden, I = c.v_inter;
+    add(vp + "embeddings.patch_embedding.weight", D, C.kpatch());
+    add(vp + "embeddings.patch_embedding.bias", D, 0);
+    add(vp + "embeddings.position_embedding.weight", C.np(), D);
+    for (int i = 0; i < c.v_layers; ++i) {
+        const std::string p = vp + "encoder.layers." + std::to_string(i) + ".";
+        for (const char* n : {"q", "k", "v"}) add(p + "self_attn." + n + "_proj.weight", D, D);
+        for (const char* n : {"q", "k", "v"}) add(p + "self_attn." + n + "_proj.bias", D, 0);
+        add(p + "self_attn.out_proj.weight", D, D);
+        add(p + "self_attn.out_proj.bias", D, 0);
+        add(p + "layer_norm1.weight", D, 0);
+        add(p + "layer_norm1.bias", D, 0);
+        add(p + "mlp.fc1.weight", I, D);
+        add(p + "mlp.fc1.bias", I, 0);
+        add(p + "mlp.fc2.weight", D, I);
+        add(p + "mlp.fc2.bias", D, 0);
+        add(p + "layer_norm2.weight", D, 0);
+        add(p + "layer_norm2.bias", D, 0);
+    }
+    add(vp + "post_layernorm.weight", D, 0);
+    add(vp + "post_layernorm.bias", D, 0);
+    const int64_t H = c.t_hidden, TI = c.t_inter, qd = C.qd(), kd = C.kvd();
+    add("multi_modal_projector.linear_1.weight", H, D);
+    add("multi_modal_projector.linear_1.bias", H, 0);
+    add("multi_modal_projector.linear_2.weight", H, H);
+    add("multi_modal_projector.linear_2.bias", H, 0);
+    add("image_newline", H, 0);
+    const std::string lp = "language_model.model.";
+    add(lp + "embed_tokens.weight", c.t_vocab, H);
+    for (int i = 0; i < c.t_layers; ++i) {
+        const std::string p = lp + "layers." + std::to_string(i) + ".";
+        add(p + "self_attn.q_proj.weight", qd, H);
+        add(p + "self_attn.k_proj.weight", kd, H);
+        add(p + "self_attn.v_proj.weight", kd, H);
+        add(p + "self_attn.q_proj.bias", qd, 0);
+        add(p + "self_attn.k_proj.bias", kd, 0);
+        add(p + "self_attn.v_proj.bias", kd, 0);
+        add(p + "self_attn.o_proj.weight", H, qd);
+        add(p + "mlp.gate_proj.weight", TI, H);
+        add(p + "mlp.up_proj.weight", TI, H);
+        add(p + "mlp.down_proj.weight", H, TI);
+        add(p + "input_layernorm.weight", H, 0);
+        add(p + "post_attention_layernorm.weight", H, 0);
+    }
+    add(lp + "norm.weight", H, 0);
+    if (!c.t_tie) add("language_model.lm_head.weight", c.t_vocab, H);
+    *total = (off + 7) / 8 * 8;
+    return S;
+}
+
+bool cfg_ok(const kd_model_config* c) {
+    return c && c->v_hidden > 0 && c->v_heads > 0 && c->v_hidden % c->v_heads == 0 && c->v_layers >= 0 &&
+           c->v_patch > 0 && c->v_image >= c->v_patch && c->t_hidden > 0 && c->t_heads > 0 &&
+           c->t_kv_heads > 0 && c->t_heads % c->t_kv_heads == 0 && c->t_layers >= 0 && c->t_vocab > 0 &&
+           (c->t_head_dim == 64 || c->t_head_dim == 128) && c->v_hidden / c->v_heads <= 128;
+}
+
+// per-layer parameter indices into the spec list
+enum VisField { VQW, VKW, VVW, VQB, VKB, VVB, VOW, VOB, VLN1W, VLN1B, VFC1W, VFC1B, VFC2W, VFC2B, VLN2W, VLN2B, VNF };
+enum LmField { LQW, LKW, LVW, LQB, LKB, LVB, LOW, LGW, LUW, LDW, LINW, LPOSTW, LNF };
+
+}  // namespace
+
+}  // namespace kd
+
+struct kd_model {
+    kd::Cfg C;
+    std::vector<kd::Spec> specs;
+    int64_t numel = 0;
+    const kd::bf16* w = nullptr;
+    float* g = nullptr;
+    int train_vision = 0, train_projector = 0, train_language = 0;
+    int lane_split_k = 0;     // split-K of the lane's GEMMs (KD_WGRAD_SPLIT_K; 0 = cost model)
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_next = 0;
+    // spec indices
+    int i_patch_w = 0, i_patch_b = 1, i_pos = 2, i_vis0 = 3, i_post_w, i_post_b, i_p1w, i_p1b, i_p2w, i_p2b, i_newline,
+        i_embed, i_lm0, i_norm, i_head;
+
+    int64_t off(int idx) const { return specs[idx].offset; }
+    const kd::bf16* W(int idx) const { return w + off(idx); }
+    float* G(int idx) const { return g + off(idx); }
+    int vis(int layer, int f) const { return i_vis0 + layer * kd::VNF + f; }
+    int lm(int layer, int f) const { return i_lm0 + layer * kd::LNF + f; }
+    hipEvent_t event() {   // reused round-robin: a wait is enqueued long before its event comes round again
+        if (ev_pool.empty()) {
+            ev_pool.resize(1024);
+            for (auto& e : ev_pool) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        }
+        return ev_pool[ev_next++ % ev_pool.size()];
+    }
+};
+
+namespace kd {
+namespace {
+
+constexpr size_t SPLITK_WS = (size_t)384 << 20;   // fp32 split-K partial planes per stream (ops.py GEMM_SPLITK_WS)
+
+// bump allocator over a caller workspace; base == nullptr: sizing pass
+struct Arena {
+    char* base;
+    size_t off = 0;
+    explicit Arena(void* b) : base((char*)b) {}
+    template <class T>
+    T* take(size_t n) {
+        off = (off + 255) & ~(size_t)255;
+        T* p = base ? (T*)(base + off) : nullptr;
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+// ------------------------------------------------------------- GEMM helpers ----
+struct Op {   // one GEMM operand: pointer, leading dim, layout
+    const void* p;
+    int64_t ld;
+    int layout;
+};
+inline Op km(const void* p, int64_t ld) { return {p, ld, KD_LAYOUT_K_MAJOR}; }   // [rows][k]
+inline Op mn(const void* p, int64_t ld) { return {p, ld, KD_LAYOUT_MN_MAJOR}; }  // stored [k][rows]
+
+struct GemmArgs {
+    const void* bias = nullptr;
+    int act = KD_ACT_NONE;
+    const void* residual = nullptr;
+    int64_t ldr = 0;
+    void* aux = nullptr;
+    int64_t ld_aux = 0;
+    int residual_row_mod = 0;
+    int accumulate = 0;
+    int c_f32 = 0;
+    int bias_f32 = 0;
+    int split_k = 0;
+};
+
+int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int64_t ldc, const GemmArgs& g) {
+    kd_gemm_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.M = M; d.N = N; d.K = K;
+    d.a_layout = a.layout; d.b_layout = b.layout;
+    d.A = a.p; d.lda = a.ld; d.B = b.p; d.ldb = b.ld;
+    d.C = C; d.ldc = ldc;
+    d.c_dtype = g.c_f32 ? KD_DTYPE_F32 : KD_DTYPE_BF16;
+    d.accumulate = g.accumulate;
+    d.alpha = 1.f;
+    d.bias = g.bias; d.bias_dtype = g.bias_f32 ? KD_DTYPE_F32 : KD_DTYPE_BF16;
+    d.act = g.act;
+    d.residual = g.residual; d.ldr = g.ldr;
+    d.aux = g.aux; d.ld_aux = g.ld_aux;
+    d.residual_row_mod = g.residual_row_mod;
+    d.split_k = g.split_k;
+    if (g.split_k != 1 && ws) { d.workspace = ws; d.workspace_bytes = SPLITK_WS; }
+    return gemm_timed(&d, s);
+}
+
+#define KD_TRY(x)                    \
+    do {                             \
+        const int st__ = (x);        \
+        if (st__ != KD_OK) return st__; \
+    } while (0)
+
+// the weight-gradient lane: a second stream ordered after the dgrad chain at each hand-off
+struct Lane {
+    kd_model* m;
+    hipStream_t main, lane;
+    void* ws;
+    void begin() {   // lane waits for everything queued on the main stream so far
+        hipEvent_t e = m->event();
+        hipEventRecord(e, main);
+        hipStreamWaitEvent(lane, e, 0);
+    }
+    hipEvent_t end() {
+        hipEvent_t e = m->event();
+        hipEventRecord(e, lane);
+        return e;
+    }
+    // dW[N_out, K_in] (fp32 +=) = dy[M, N_out]^T x[M, K_in]
+    int wgrad(int M, int Nout, int Kin, const void* dy, int64_t lddy, const void* x, int64_t ldx, float* dW) {
+        GemmArgs g;
+        g.accumulate = 1;
+        g.c_f32 = 1;
+        g.split_k = m->lane_split_k;
+        return gemm(lane, ws, Nout, Kin, M, mn(dy, lddy), mn(x, ldx), dW, Kin, g);
+    }
+    int colsum(const void* dy, int64_t ld, int M, int N, float* out) {
+        return launch_colsum(dy, ld, M, N, out, 1, lane);
+    }
+};
+inline void wait(hipStream_t s, hipEvent_t e) {
+    if (e) hipStreamWaitEvent(s, e, 0);
+}
+
+// ------------------------------------------------------ forward buffer plan ----
+struct VisLayerBufs {
+    bf16 *x, *h, *q, *k, *v, *o, *x_mid, *h2, *pre, *u;
+    float *m1, *r1, *lse, *m2, *r2;
+};
+struct LmLayerBufs {
+    bf16 *x, *h, *q, *k, *v, *o, *x_mid, *h2, *gu, *a;
+    float *r1, *lse, *r2;
+};
+struct FwdPlan {
+    bf16* rows;
+    std::vector<VisLayerBufs> vl;
+    bf16 *x_vis_last, *qkv_v;     // x_vis_last = vl.back() output (saved) / ping-pong
+    bf16* x_vis[2];               // save = 0 ping-pong
+    float *pm, *pr;
+    bf16 *ppre, *z, *feats;
+    std::vector<LmLayerBufs> ll;
+    bf16 *x_lm_last, *qkv_t;
+    bf16* x_lm[2];
+    float* rf;
+    void* splitk;
+    size_t bytes;
+};
+
+FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void* base) {
+    const Cfg& C = m->C;
+    const kd_model_config& c = C.c;
+    Arena A(base);
+    FwdPlan P;
+    const int NI = B * tiles, np = C.np();
+    const int64_t NT = (int64_t)NI * np, D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp();
+    const int64_t M = (int64_t)B * L, H = c.t_hidden, TI = c.t_inter, qd = C.qd(), kvd = C.kvd(), hd = c.t_head_dim;
+    P.rows = A.take<bf16>(NT * C.kpatch());
+    // vision
+    P.vl.resize(c.v_layers);
+    P.qkv_v = A.take<bf16>(NT * 3 * D);
+    if (save) {
+        for (int i = 0; i < c.v_layers; ++i) {
+            VisLayerBufs& b = P.vl[i];
+            b.x = A.take<bf16>(NT * D);
+            b.h = A.take<bf16>(NT * D);
+            b.q = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+            b.k = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+            b.v = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+            b.o = A.take<bf16>(NT * D);
+            b.x_mid = A.take<bf16>(NT * D);
+            b.h2 = A.take<bf16>(NT * D);
+            b.pre = A.take<bf16>(NT * Iv);
+            b.u = A.take<bf16>(NT * Iv);
+            b.m1 = A.take<float>(NT);
+            b.r1 = A.take<float>(NT);
+            b.lse = A.take<float>((int64_t)NI * c.v_heads * np);
+            b.m2 = A.take<float>(NT);
+            b.r2 = A.take<float>(NT);
+        }
+        P.x_vis_last = A.take<bf16>(NT * D);
+        P.x_vis[0] = P.x_vis[1] = nullptr;
+    } else {
+        VisLayerBufs b{};
+        P.x_vis[0] = A.take<bf16>(NT * D);
+        P.x_vis[1] = A.take<bf16>(NT * D);
+        b.h = A.take<bf16>(NT * D);
+        b.q = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+        b.k = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+        b.v = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+        b.o = A.take<bf16>(NT * D);
+        b.x_mid = A.take<bf16>(NT * D);
+        b.h2 = A.take<bf16>(NT * D);
+        b.u = A.take<bf16>(NT * Iv);
+        for (int i = 0; i < c.v_layers; ++i) {
+            P.vl[i] = b;
+            P.vl[i].x = P.x_vis[i & 1];
+        }
+        P.x_vis_last = P.x_vis[c.v_layers & 1];
+    }
+    P.pm = A.take<float>(NT);
+    P.pr = A.take<float>(NT);
+    // projector
+    P.ppre = save ? A.take<bf16>(NT * H) : nullptr;
+    P.z = A.take<bf16>(NT * H);
+    P.feats = A.take<bf16>(NT * H);
+    // language model
+    P.ll.resize(c.t_layers);
+    P.qkv_t = A.take<bf16>(M * (qd + 2 * kvd));
+    const bool fused_swiglu = TI % 128 == 0;
+    if (save) {
+        for (int i = 0; i < c.t_layers; ++i) {
+            LmLayerBufs& b = P.ll[i];
+            b.x = A.take<bf16>(M * H);
+            b.h = A.take<bf16>(M * H);
+            b.q = A.take<bf16>(M * qd);
+            b.k = A.take<bf16>(M * kvd);
+            b.v = A.take<bf16>(M * kvd);
+            b.o = A.take<bf16>(M * qd);
+            b.x_mid = A.take<bf16>(M * H);
+            b.h2 = A.take<bf16>(M * H);
+            b.gu = A.take<bf16>(M * 2 * TI);
+            b.a = A.take<bf16>(M * TI);
+            b.r1 = A.take<float>(M);
+            b.lse = A.take<float>((int64_t)B * c.t_heads * L);
+            b.r2 = A.take<float>(M);
+        }
+        P.x_lm_last = A.take<bf16>(M * H);
+        P.x_lm[0] = P.x_lm[1] = nullptr;
+    } else {
+        LmLayerBufs b{};
+        P.x_lm[0] = A.take<bf16>(M * H);
+        P.x_lm[1] = A.take<bf16>(M * H);
+        b.h = A.take<bf16>(M * H);
+        b.q = A.take<bf16>(M * qd);
+        b.k = A.take<bf16>(M * kvd);
+        b.v = A.take<bf16>(M * kvd);
+        b.o = A.take<bf16>(M * qd);
+        b.x_mid = A.take<bf16>(M * H);
+        b.h2 = A.take<bf16>(M * H);
+        b.gu = fused_swiglu ? nullptr : A.take<bf16>(M * 2 * TI);
+        b.a = A.take<bf16>(M * TI);
+        for (int i = 0; i < c.t_layers; ++i) {
+            P.ll[i] = b;
+            P.ll[i].x = P.x_lm[i & 1];
+        }
+        P.x_lm_last = P.x_lm[c.t_layers & 1];
+    }
+    P.rf = A.take<float>(M);
+    (void)hd;
+    P.splitk = A.take<char>(SPLITK_WS);
+    P.bytes = A.off + 256;
+    return P;
+}
+
+// ------------------------------------------------------------------ forward ----
+int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dtype, int NI, int save, void* post,
+                   hipStream_t s) {
+    const Cfg& C = m->C;
+    const kd_model_config& c = C.c;
+    const int np = C.np(), D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp(), hd = C.v_hd();
+    const int NT = NI * np;
+    KD_TRY(launch_patchify(pixels, px_dtype, P.rows, NI, c.v_image, c.v_patch, C.kpatch(), s));
+    bf16* x0 = c.v_layers ? P.vl[0].x : P.x_vis_last;
+    {
+        GemmArgs g;
+        g.bias = m->W(m->i_patch_b);
+        g.residual = m->W(m->i_pos);
+        g.ldr = D;
+        g.residual_row_mod = np;
+        KD_TRY(gemm(s, P.splitk, NT, D, C.kpatch(), km(P.rows, C.kpatch()), km(m->W(m->i_patch_w), C.kpatch()), x0, D, g));
+    }
+    for (int i = 0; i < c.v_layers; ++i) {
+        const VisLayerBufs& b = P.vl[i];
+        bf16* x_out = (i + 1 < c.v_layers) ? P.vl[i + 1].x : P.x_vis_last;
+        KD_TRY(launch_norm_fwd(0, b.x, D, m->W(m->vis(i, VLN1W)), m->W(m->vis(i, VLN1B)), b.h, D, save ? b.m1 : nullptr,
+                               save ? b.r1 : nullptr, NT, D, c.v_eps, s));
+        {
+            GemmArgs g;
+            g.bias = m->W(m->vis(i, VQB));
+            KD_TRY(gemm(s, P.splitk, NT, 3 * D, D, km(b.h, D), km(m->W(m->vis(i, VQW)), D), P.qkv_v, 3 * D, g));
+        }
+        KD_TRY(launch_qkv_split(P.qkv_v, 3 * D, b.q, b.k, b.v, nullptr, nullptr, NI, np, c.v_heads, c.v_heads, hd, hdp, s));
+        {
+            kd_attn_desc a{b.q, b.k, b.v, b.o, save ? b.lse : nullptr, NI, c.v_heads, c.v_heads, np, hd, hdp, 0};
+            KD_TRY(launch_attn_fwd(&a, s));
+        }
+        {
+            GemmArgs g;
+            g.bias = m->W(m->vis(i, VOB));
+            g.residual = b.x;
+            g.ldr = D;
+            KD_TRY(gemm(s, P.splitk, NT, D, D, km(b.o, D), km(m->W(m->vis(i, VOW)), D), b.x_mid, D, g));
+        }
+        KD_TRY(launch_norm_fwd(0, b.x_mid, D, m->W(m->vis(i, VLN2W)), m->W(m->vis(i, VLN2B)), b.h2, D,
+                               save ? b.m2 : nullptr, save ? b.r2 : nullptr, NT, D, c.v_eps, s));
+        {
+            GemmArgs g;
+            g.bias = m->W(m->vis(i, VFC1B));
+            g.act = KD_ACT_GELU_TANH;
+            g.aux = save ? b.pre : nullptr;
+            g.ld_aux = Iv;
+            KD_TRY(gemm(s, P.splitk, NT, Iv, D, km(b.h2, D), km(m->W(m->vis(i, VFC1W)), D), b.u, Iv, g));
+        }
+        {
+            GemmArgs g;
+            g.bias = m->W(m->vis(i, VFC2B));
+            g.residual = b.x_mid;
+            g.ldr = D;
+            KD_TRY(gemm(s, P.splitk, NT, D, Iv, km(b.u, Iv), km(m->W(m->vis(i, VFC2W)), Iv), x_out, D, g));
+        }
+    }
+    if (post)
+        KD_TRY(launch_norm_fwd(0, P.x_vis_last, D, m->W(m->i_post_w), m->W(m->i_post_b), post, D, save ? P.pm : nullptr,
+                               save ? P.pr : nullptr, NT, D, c.v_eps, s));
+    return KD_OK;
+}
+
+int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, int B, int L, int save, void* hn,
+               void* const* kv_k, void* const* kv_v, hipStream_t s) {
+    const kd_model_config& c = m->C.c;
+    const int M = B * L, H = c.t_hidden, TI = c.t_inter, qd = m->C.qd(), kvd = m->C.kvd(), hd = c.t_head_dim;
+    const bool fused = TI % 128 == 0;
+    for (int i = 0; i < c.t_layers; ++i) {
+        const LmLayerBufs& b = P.ll[i];
+        bf16* x_out = (i + 1 < c.t_layers) ? P.ll[i + 1].x : P.x_lm_last;
+        KD_TRY(launch_norm_fwd(1, b.x, H, m->W(m->lm(i, LINW)), nullptr, b.h, H, nullptr, save ? b.r1 : nullptr, M, H,
+                               c.t_eps, s));
+        {
+            GemmArgs g;
+            g.bias = m->W(m->lm(i, LQB));
+            KD_TRY(gemm(s, P.splitk, M, qd + 2 * kvd, H, km(b.h, H), km(m->W(m->lm(i, LQW)), H), P.qkv_t, qd + 2 * kvd, g));
+        }
+        void* k = kv_k ? kv_k[i] : b.k;
+        void* v = kv_v ? kv_v[i] : b.v;
+        KD_TRY(launch_qkv_split(P.qkv_t, qd + 2 * kvd, b.q, k, v, cs, sn, B, L, c.t_heads, c.t_kv_heads, hd, hd, s));
+        {
+            kd_attn_desc a{b.q, k, v, b.o, save ? b.lse : nullptr, B, c.t_heads, c.t_kv_heads, L, hd, hd, 1};
+            KD_TRY(launch_attn_fwd(&a, s));
+        }
+        {
+            GemmArgs g;
+            g.residual = b.x;
+            g.ldr = H;
+            KD_TRY(gemm(s, P.splitk, M, H, qd, km(b.o, qd), km(m->W(m->lm(i, LOW)), qd), b.x_mid, H, g));
+        }
+        KD_TRY(launch_norm_fwd(1, b.x_mid, H, m->W(m->lm(i, LPOSTW)), nullptr, b.h2, H, nullptr, save ? b.r2 : nullptr, M,
+                               H, c.t_eps, s));
+        if (fused) {   // SwiGLU in the gate|up GEMM's epilogue; gate|up kept only for the backward
+            GemmArgs g;
+            g.act = KD_ACT_SWIGLU;
+            g.aux = save ? b.gu : nullptr;
+            g.ld_aux = 2 * TI;
+            KD_TRY(gemm(s, P.splitk, M, 2 * TI, H, km(b.h2, H), km(m->W(m->lm(i, LGW)), H), b.a, TI, g));
+        } else {
+            GemmArgs g;
+            KD_TRY(gemm(s, P.splitk, M, 2 * TI, H, km(b.h2, H), km(m->W(m->lm(i, LGW)), H), b.gu, 2 * TI, g));
+            KD_TRY(launch_swiglu_fwd(b.gu, 2 * TI, b.a, TI, M, TI, s));
+        }
+        {
+            GemmArgs g;
+            g.residual = b.x_mid;
+            g.ldr = H;
+            KD_TRY(gemm(s, P.splitk, M, H, TI, km(b.a, TI), km(m->W(m->lm(i, LDW)), TI), x_out, H, g));
+        }
+    }
+    return launch_norm_fwd(1, P.x_lm_last, H, m->W(m->i_norm), nullptr, hn, H, nullptr, save ? P.rf : nullptr, M, H,
+                           c.t_eps, s);
+}
+
+// ---------------------------------------------------------- backward plan ----
+struct BwdPlan {
+    bf16 *dx, *da, *dgu, *dh2, *do_, *dk, *dv, *dqkv, *dh, *demb;   // language model
+    float *dq, *delta;
+    bf16 *dfeats, *dz, *dxv, *du, *dh2v, *dov, *dkv, *dvv, *dqkvv, *dhv;   // projector / vision
+    float *dqv, *deltav;
+    void *attn_ws, *attn_ws_v, *norm_ws;
+    size_t attn_ws_bytes, attn_ws_v_bytes, norm_ws_bytes;
+    void *splitk_main, *splitk_lane;
+    size_t bytes;
+};
+
+kd_attn_bwd_desc lm_attn_desc(const kd_model* m, int B, int L) {
+    const kd_model_config& c = m->C.c;
+    kd_attn_bwd_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.B = B; d.H = c.t_heads; d.HKV = c.t_kv_heads; d.S = L; d.hd = c.t_head_dim; d.hdp = c.t_head_dim; d.causal = 1;
+    return d;
+}
+kd_attn_bwd_desc vis_attn_desc(const kd_model* m, int NI) {
+    const kd_model_config& c = m->C.c;
+    kd_attn_bwd_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.B = NI; d.H = c.v_heads; d.HKV = c.v_heads; d.S = m->C.np(); d.hd = m->C.v_hd(); d.hdp = m->C.v_hdp(); d.causal = 0;
+    return d;
+}
+
+BwdPlan plan_backward(const kd_model* m, int B, int L, int tiles, void* base) {
+    const Cfg& C = m->C;
+    const kd_model_config& c = C.c;
+    Arena A(base);
+    BwdPlan P;
+    const int NI = B * tiles, np = C.np();
+    const int64_t NT = (int64_t)NI * np, D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp();
+    const int64_t M = (int64_t)B * L, H = c.t_hidden, TI = c.t_inter, qd = C.qd(), kvd = C.kvd();
+    P.dx = A.take<bf16>(M * H);
+    P.da = A.take<bf16>(M * TI);
+    P.dgu = A.take<bf16>(M * 2 * TI);
+    P.dh2 = A.take<bf16>(M * H);
+    P.do_ = A.take<bf16>(M * qd);
+    P.dq = A.take<float>(M * qd);
+    P.dk = A.take<bf16>(M * kvd);
+    P.dv = A.take<bf16>(M * kvd);
+    P.delta = A.take<float>((int64_t)B * c.t_heads * L);
+    P.dqkv = A.take<bf16>(M * (qd + 2 * kvd));
+    P.dh = A.take<bf16>(M * H);
+    P.demb = P.dx;   // the LM backward's dx is d(inputs_embeds)
+    kd_attn_bwd_desc ad = lm_attn_desc(m, B, L);
+    P.attn_ws_bytes = attn_bwd_workspace_size(&ad);
+    P.attn_ws = P.attn_ws_bytes ? A.take<char>(P.attn_ws_bytes) : nullptr;
+    P.dfeats = A.take<bf16>(NT * H);
+    P.dz = A.take<bf16>(NT * H);
+    P.dxv = A.take<bf16>(NT * D);
+    P.du = A.take<bf16>(NT * Iv);
+    P.dh2v = A.take<bf16>(NT * D);
+    P.dov = A.take<bf16>(NT * D);
+    P.dqv = A.take<float>((int64_t)NI * c.v_heads * np * hdp);
+    P.dkv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+    P.dvv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+    P.deltav = A.take<float>((int64_t)NI * c.v_heads * np);
+    P.dqkvv = A.take<bf16>(NT * 3 * D);
+    P.dhv = A.take<bf16>(NT * D);
+    kd_attn_bwd_desc vd = vis_attn_desc(m, NI);
+    P.attn_ws_v_bytes = attn_bwd_workspace_size(&vd);
+    P.attn_ws_v = P.attn_ws_v_bytes ? A.take<char>(P.attn_ws_v_bytes) : nullptr;
+    const int64_t Rmax = M > NT ? M : NT;
+    const int Dmax = (int)(H > D ? H : D);
+    P.norm_ws_bytes = norm_bwd_ws((int)Rmax, Dmax);
+    P.norm_ws = A.take<char>(P.norm_ws_bytes);
+    P.splitk_main = A.take<char>(SPLITK_WS);
+    P.splitk_lane = A.take<char>(SPLITK_WS);
+    P.bytes = A.off + 256;
+    return P;
+}
+
+// ----------------------------------------------------------------- backward ----
+int lm_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, const float* cs, const float* sn, int B, int L,
+                const void* dhn, Lane& lane, hipStream_t s, kd_layer_cb cb, void* user) {
+    const kd_model_config& c = m->C.c;
+    const int M = B * L, H = c.t_hidden, TI = c.t_inter, qd = m->C.qd(), kvd = m->C.kvd(), hd = c.t_head_dim;
+    const bool gw = m->train_language != 0;
+    KD_TRY(launch_norm_bwd(1, F.x_lm_last, H, m->W(m->i_norm), dhn, H, nullptr, F.rf, P.dx, H, 0,
+                           gw ? m->G(m->i_norm) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s));
+    for (int i = c.t_layers - 1; i >= 0; --i) {
+        const LmLayerBufs& b = F.ll[i];
+        GemmArgs g0;
+        // MLP: da = dx Wdown ; dgu = swiglu'(gu) da ; dh2 = dgu [Wgate; Wup]
+        KD_TRY(gemm(s, P.splitk_main, M, TI, H, km(P.dx, H), mn(m->W(m->lm(i, LDW)), TI), P.da, TI, g0));
+        hipEvent_t ev = nullptr;
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(M, H, TI, P.dx, H, b.a, TI, m->G(m->lm(i, LDW))));
+            ev = lane.end();
+        }
+        KD_TRY(launch_swiglu_bwd(b.gu, 2 * TI, P.da, TI, P.dgu, 2 * TI, M, TI, s));
+        KD_TRY(gemm(s, P.splitk_main, M, H, 2 * TI, km(P.dgu, 2 * TI), mn(m->W(m->lm(i, LGW)), H), P.dh2, H, g0));
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(M, 2 * TI, H, P.dgu, 2 * TI, b.h2, H, m->G(m->lm(i, LGW))));
+            lane.end();
+        }
+        wait(s, ev);   // dx is updated in place next (the lane read it)
+        KD_TRY(launch_norm_bwd(1, b.x_mid, H, m->W(m->lm(i, LPOSTW)), P.dh2, H, nullptr, b.r2, P.dx, H, 1,
+                               gw ? m->G(m->lm(i, LPOSTW)) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s));
+        // attention: do = dx Wo ; flash backward ; dqkv (RoPE undone) ; dh = dqkv Wqkv
+        KD_TRY(gemm(s, P.splitk_main, M, qd, H, km(P.dx, H), mn(m->W(m->lm(i, LOW)), qd), P.do_, qd, g0));
+        ev = nullptr;
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(M, H, qd, P.dx, H, b.o, qd, m->G(m->lm(i, LOW))));
+            ev = lane.end();
+        }
+        {
+            kd_attn_bwd_desc d = lm_attn_desc(m, B, L);
+            d.q = b.q; d.k = b.k; d.v = b.v; d.o = b.o; d.dO = P.do_; d.lse = b.lse; d.delta = P.delta;
+            d.dq = P.dq; d.dk = P.dk; d.dv = P.dv; d.workspace = P.attn_ws; d.workspace_bytes = P.attn_ws_bytes;
+            KD_TRY(launch_attn_bwd(&d, s));
+        }
+        KD_TRY(launch_qkv_merge(P.dq, P.dk, P.dv, P.dqkv, qd + 2 * kvd, cs, sn, B, L, c.t_heads, c.t_kv_heads, hd, hd, s));
+        KD_TRY(gemm(s, P.splitk_main, M, H, qd + 2 * kvd, km(P.dqkv, qd + 2 * kvd), mn(m->W(m->lm(i, LQW)), H), P.dh, H,
+                    g0));
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(M, qd + 2 * kvd, H, P.dqkv, qd + 2 * kvd, b.h, H, m->G(m->lm(i, LQW))));
+            KD_TRY(lane.colsum(P.dqkv, qd + 2 * kvd, M, qd + 2 * kvd, m->G(m->lm(i, LQB))));
+            lane.end();
+        }
+        wait(s, ev);
+        KD_TRY(launch_norm_bwd(1, b.x, H, m->W(m->lm(i, LINW)), P.dh, H, nullptr, b.r1, P.dx, H, 1,
+                               gw ? m->G(m->lm(i, LINW)) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s));
+        if (cb) cb(user, i);
+    }
+    return KD_OK;
+}
+
+int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, const void* dpost, Lane& lane,
+                    hipStream_t s) {
+    const Cfg& C = m->C;
+    const kd_model_config& c = C.c;
+    const int np = C.np(), D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp(), hd = C.v_hd();
+    const int NT = NI * np;
+    const bool gw = m->train_vision != 0;
+    bf16* dx = P.dxv;
+    if (dpost)
+        KD_TRY(launch_norm_bwd(0, F.x_vis_last, D, m->W(m->i_post_w), dpost, D, F.pm, F.pr, dx, D, 1,
+                               gw ? m->G(m->i_post_w) : nullptr, gw ? m->G(m->i_post_b) : nullptr, 1, P.norm_ws,
+                               P.norm_ws_bytes, NT, D, s));
+    GemmArgs g0;
+    for (int i = c.v_layers - 1; i >= 0; --i) {
+        const VisLayerBufs& b = F.vl[i];
+        KD_TRY(gemm(s, P.splitk_main, NT, Iv, D, km(dx, D), mn(m->W(m->vis(i, VFC2W)), Iv), P.du, Iv, g0));
+        hipEvent_t ev = nullptr;
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(NT, D, Iv, dx, D, b.u, Iv, m->G(m->vis(i, VFC2W))));
+            KD_TRY(lane.colsum(dx, D, NT, D, m->G(m->vis(i, VFC2B))));
+            ev = lane.end();
+        }
+        KD_TRY(launch_act_bwd(b.pre, P.du, P.du, (int64_t)NT * Iv, KD_ACT_GELU_TANH, s));   // dpre in place
+        KD_TRY(gemm(s, P.splitk_main, NT, D, Iv, km(P.du, Iv), mn(m->W(m->vis(i, VFC1W)), D), P.dh2v, D, g0));
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(NT, Iv, D, P.du, Iv, b.h2, D, m->G(m->vis(i, VFC1W))));
+            KD_TRY(lane.colsum(P.du, Iv, NT, Iv, m->G(m->vis(i, VFC1B))));
+            lane.end();
+        }
+        wait(s, ev);
+        KD_TRY(launch_norm_bwd(0, b.x_mid, D, m->W(m->vis(i, VLN2W)), P.dh2v, D, b.m2, b.r2, dx, D, 1,
+                               gw ? m->G(m->vis(i, VLN2W)) : nullptr, gw ? m->G(m->vis(i, VLN2B)) : nullptr, 1, P.norm_ws,
+                               P.norm_ws_bytes, NT, D, s));
+        KD_TRY(gemm(s, P.splitk_main, NT, D, D, km(dx, D), mn(m->W(m->vis(i, VOW)), D), P.dov, D, g0));
+        ev = nullptr;
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(NT, D, D, dx, D, b.o, D, m->G(m->vis(i, VOW))));
+            KD_TRY(lane.colsum(dx, D, NT, D, m->G(m->vis(i, VOB))));
+            ev = lane.end();
+        }
+        {
+            kd_attn_bwd_desc d = vis_attn_desc(m, NI);
+            d.q = b.q; d.k = b.k; d.v = b.v; d.o = b.o; d.dO = P.dov; d.lse = b.lse; d.delta = P.deltav;
+            d.dq = P.dqv; d.dk = P.dkv; d.dv = P.dvv; d.workspace = P.attn_ws_v; d.workspace_bytes = P.attn_ws_v_bytes;
+            KD_TRY(launch_attn_bwd(&d, s));
+        }
+        KD_TRY(launch_qkv_merge(P.dqv, P.dkv, P.dvv, P.dqkvv, 3 * D, nullptr, nullptr, NI, np, c.v_heads, c.v_heads, hd,
+                                hdp, s));
+        KD_TRY(gemm(s, P.splitk_main, NT, D, 3 * D, km(P.dqkvv, 3 * D), mn(m->W(m->vis(i, VQW)), D), P.dhv, D, g0));
+        if (gw) {
+            lane.begin();
+            KD_TRY(lane.wgrad(NT, 3 * D, D, P.dqkvv, 3 * D, b.h, D, m->G(m->vis(i, VQW))));
+            KD_TRY(lane.colsum(P.dqkvv, 3 * D, NT, 3 * D, m->G(m->vis(i, VQB))));
+            lane.end();
+        }
+        wait(s, ev);
+        KD_TRY(launch_norm_bwd(0, b.x, D, m->W(m->vis(i, VLN1W)), P.dhv, D, b.m1, b.r1, dx, D, 1,
+                               gw ? m->G(m->vis(i, VLN1W)) : nullptr, gw ? m->G(m->vis(i, VLN1B)) : nullptr, 1, P.norm_ws,
+                               P.norm_ws_bytes, NT, D, s));
+    }
+    if (gw) {   // patch embedding (im2col GEMM), its bias and the position embedding
+        lane.begin();
+        KD_TRY(lane.wgrad(NT, D, C.kpatch(), dx, D, F.rows, C.kpatch(), m->G(m->i_patch_w)));
+        KD_TRY(lane.colsum(dx, D, NT, D, m->G(m->i_patch_b)));
+        KD_TRY(lane.colsum(dx, (int64_t)np * D, NI, np * D, m->G(m->i_pos)));
+        lane.end();
+    }
+    return KD_OK;
+}
+
+}  // namespace
+}  // namespace kd
+
+// ================================================================== C ABI ====
+extern "C" {
+
+int kd_model_param_count(const kd_model_config* cfg) {
+    if (!kd::cfg_ok(cfg)) {
+        kd::fail(KD_ERR_ARG, "kd_model_param_count: invalid config");
+        return -1;
+    }
+    int64_t tot;
+    return (int)kd::make_specs(kd::Cfg{*cfg}, &tot).size();
+}
+
+int64_t kd_model_param_numel(const kd_model_config* cfg) {
+    if (!kd::cfg_ok(cfg)) {
+        kd::fail(KD_ERR_ARG, "kd_model_param_numel: invalid config");
+        return -1;
+    }
+    int64_t tot;
+    kd::make_specs(kd::Cfg{*cfg}, &tot);
+    return tot;
+}
+
+int kd_model_param_info(const kd_model_config* cfg, int index, char* name, int name_cap, int64_t* offset,
+                        int64_t* numel, int64_t* rows, int64_t* cols) {
+    KD_CHECK_ARG(kd::cfg_ok(cfg), "kd_model_param_info: invalid config");
+    int64_t tot;
+    const auto S = kd::make_specs(kd::Cfg{*cfg}, &tot);
+    KD_CHECK_ARG(index >= 0 && index < (int)S.size(), "kd_model_param_info: index out of range");
+    const auto& s = S[index];
+    if (name && name_cap > 0) {
+        std::strncpy(name, s.name.c_str(), name_cap - 1);
+        name[name_cap - 1] = 0;
+    }
+    if (offset) *offset = s.offset;
+    if (numel) *numel = s.numel;
+    if (rows) *rows = s.rows;
+    if (cols) *cols = s.cols;
+    return KD_OK;
+}
+
+int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad, kd_model** out) {
+    KD_CHECK_ARG(out, "kd_model_create: null out");
+    KD_CHECK_ARG(kd::cfg_ok(cfg), "kd_model_create: invalid config (head dims: text 64|128, vision <= 128)");
+    KD_CHECK_ARG(weights, "kd_model_create: null weights");
+    KD_CHECK_ALIGN(weights, 16, "kd_model_create: weights must be 16-B aligned");
+    kd_model* m = new kd_model();
+    m->C = kd::Cfg{*cfg};
+    m->specs = kd::make_specs(m->C, &m->numel);
+    m->w = (const kd::bf16*)weights;
+    m->g = grad;
+    const int on = grad ? 1 : 0;
+    m->train_vision = m->train_projector = m->train_language = on;
+    const char* e = std::getenv("KD_WGRAD_SPLIT_K");
+    m->lane_split_k = e ? std::atoi(e) : 0;
+    m->i_post_w = m->i_vis0 + cfg->v_layers * kd::VNF;
+    m->i_post_b = m->i_post_w + 1;
+    m->i_p1w = m->i_post_b + 1;
+    m->i_p1b = m->i_p1w + 1;
+    m->i_p2w = m->i_p1b + 1;
+    m->i_p2b = m->i_p2w + 1;
+    m->i_newline = m->i_p2b + 1;
+    m->i_embed = m->i_newline + 1;
+    m->i_lm0 = m->i_embed + 1;
+    m->i_norm = m->i_lm0 + cfg->t_layers * kd::LNF;
+    m->i_head = cfg->t_tie ? m->i_embed : m->i_norm + 1;
+    *out = m;
+    return KD_OK;
+}
+
+void kd_model_destroy(kd_model* m) {
+    if (!m) return;
+    for (auto& e : m->ev_pool) hipEventDestroy(e);
+    delete m;
+}
+
+int kd_model_set_trainable(kd_model* m, int vision, int projector, int language) {
+    KD_CHECK_ARG(m, "kd_model_set_trainable: null model");
+    KD_CHECK_ARG(m->g || !(vision || projector || language), "kd_model_set_trainable: model has no grad buffer");
+    m->train_vision = vision != 0;
+    m->train_projector = projector != 0;
+    m->train_language = language != 0;
+    return KD_OK;
+}
+
+size_t kd_model_forward_workspace_size(const kd_model* m, int B, int L, int tiles, int save) {
+    if (!m || B <= 0 || L <= 0 || tiles <= 0) return 0;
+    return kd::plan_forward(m, B, L, tiles, save, nullptr).bytes;
+}
+
+size_t kd_model_backward_workspace_size(const kd_model* m, int B, int L, int tiles) {
+    if (!m || B <= 0 || L <= 0 || tiles <= 0) return 0;
+    return kd::plan_backward(m, B, L, tiles, nullptr).bytes;
+}
+
+int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pixel_dtype, const int32_t* src,
+                     const float* rope_cos, const float* rope_sin, int B, int L, int tiles, int save,
+                     void* workspace, size_t workspace_bytes, void* hn, void* post_ln, void* logits,
+                     void* const* kv_k, void* const* kv_v, int32_t* err, void* stream) {
+    using namespace kd;
+    KD_CHECK_ARG(m && ids && pixels && src && rope_cos && rope_sin && workspace && hn && err,
+                 "kd_model_forward: null pointer");
+    KD_CHECK_SHAPE(B > 0 && L > 0 && tiles > 0, "kd_model_forward: B, L, tiles must be positive");
+    KD_CHECK_ARG(pixel_dtype == KD_DTYPE_BF16 || pixel_dtype == KD_DTYPE_F32, "kd_model_forward: pixel dtype");
+    const FwdPlan P = plan_forward(m, B, L, tiles, save, workspace);
+    KD_CHECK_ARG(workspace_bytes >= P.bytes, "kd_model_forward: workspace too small");
+    const kd_model_config& c = m->C.c;
+    hipStream_t s = as_stream(stream);
+    const int NI = B * tiles, M = B * L, H = c.t_hidden;
+    KD_TRY(vision_forward(m, P, pixels, pixel_dtype, NI, save, post_ln, s));
+    {   // projector: linear_1 -> gelu -> linear_2 (HF5 llava_onevision :131-150)
+        const int NT = NI * m->C.np(), D = c.v_hidden;
+        GemmArgs g;
+        g.bias = m->W(m->i_p1b);
+        g.act = c.projector_act;
+        g.aux = save ? P.ppre : nullptr;
+        g.ld_aux = H;
+        KD_TRY(gemm(s, P.splitk, NT, H, D, km(P.x_vis_last, D), km(m->W(m->i_p1w), D), P.z, H, g));
+        GemmArgs g2;
+        g2.bias = m->W(m->i_p2b);
+        KD_TRY(gemm(s, P.splitk, NT, H, H, km(P.z, H), km(m->W(m->i_p2w), H), P.feats, H, g2));
+    }
+    // inputs_embeds: token embeddings + the packed image features (masked_scatter)
+    bf16* emb = c.t_layers ? P.ll[0].x : P.x_lm_last;
+    KD_TRY(launch_embed_assemble(ids, src, m->W(m->i_embed), P.feats, m->W(m->i_newline), emb, M, H, c.t_vocab, err, s));
+    KD_TRY(lm_forward(m, P, rope_cos, rope_sin, B, L, save, hn, kv_k, kv_v, s));
+    if (logits) {
+        GemmArgs g;
+        KD_TRY(gemm(s, P.splitk, M, c.t_vocab, H, km(hn, H), km(m->W(m->i_head), H), logits, c.t_vocab, g));
+    }
+    return KD_OK;
+}
+
+int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids, const int32_t* src,
+                      const float* rope_cos, const float* rope_sin, int B, int L, int tiles, const void* dhn,
+                      const void* dpost, void* workspace, size_t workspace_bytes, void* stream, void* wgrad_stream,
+                      kd_layer_cb on_layer_done, void* user) {
+    using namespace kd;
+    KD_CHECK_ARG(m && fwd_workspace && ids && src && rope_cos && rope_sin && dhn && workspace && wgrad_stream,
+                 "kd_model_backward: null pointer");
+    KD_CHECK_ARG(m->g, "kd_model_backward: the model has no grad buffer");
+    KD_CHECK_SHAPE(B > 0 && L > 0 && tiles > 0, "kd_model_backward: B, L, tiles must be positive");
+    const FwdPlan F = plan_forward(m, B, L, tiles, 1, const_cast<void*>(fwd_workspace));
+    const BwdPlan P = plan_backward(m, B, L, tiles, workspace);
+    KD_CHECK_ARG(workspace_bytes >= P.bytes, "kd_model_backward: workspace too small");
+    const kd_model_config& c = m->C.c;
+    hipStream_t s = as_stream(stream);
+    Lane lane{m, s, as_stream(wgrad_stream), P.splitk_lane};
+    // work the caller queued on the lane before this call (the lm_head wgrad into a tied
+    // embedding) precedes the embedding backward below
+    hipEvent_t entry = m->event();
+    hipEventRecord(entry, lane.lane);
+    const int NI = B * tiles, NT = NI * m->C.np(), M = B * L, H = c.t_hidden, D = c.v_hidden;
+    KD_TRY(lm_backward(m, F, P, rope_cos, rope_sin, B, L, dhn, lane, s, on_layer_done, user));
+    wait(s, entry);
+    const bool need_vision = m->train_vision != 0;
+    KD_TRY(launch_embed_bwd(ids, src, P.demb, m->train_language ? m->G(m->i_embed) : nullptr, P.dfeats,
+                            m->train_projector ? m->G(m->i_newline) : nullptr, M, H, s));
+    {   // projector backward
+        GemmArgs g0;
+        KD_TRY(gemm(s, P.splitk_main, NT, H, H, km(P.dfeats, H), mn(m->W(m->i_p2w), H), P.dz, H, g0));
+        if (m->train_projector) {
+            lane.begin();
+            KD_TRY(lane.wgrad(NT, H, H, P.dfeats, H, F.z, H, m->G(m->i_p2w)));
+            KD_TRY(lane.colsum(P.dfeats, H, NT, H, m->G(m->i_p2b)));
+            lane.end();
+        }
+        KD_TRY(launch_act_bwd(F.ppre, P.dz, P.dz, (int64_t)NT * H, c.projector_act, s));   // dpre in place
+        if (m->train_projector) {
+            lane.begin();
+            KD_TRY(lane.wgrad(NT, H, D, P.dz, H, F.x_vis_last, D, m->G(m->i_p1w)));
+            KD_TRY(lane.colsum(P.dz, H, NT, H, m->G(m->i_p1b)));
+            lane.end();
+        }
+        if (need_vision) KD_TRY(gemm(s, P.splitk_main, NT, D, H, km(P.dz, H), mn(m->W(m->i_p1w), D), P.dxv, D, g0));
+    }
+    if (need_vision) KD_TRY(vision_backward(m, F, P, NI, dpost, lane, s));
+    // the caller reads the grads (and reuses these buffers) after this: join the lane
+    hipEvent_t done = m->event();
+    hipEventRecord(done, lane.lane);
+    hipStreamWaitEvent(s, done, 0);
+    KD_LAUNCH_CHECK("kd_model_backward");
+    return KD_OK;
+}
+
+void kd_timer_enable(int on) { kd::g_timer_on = on != 0; }
+
+int kd_timer_count(void) {
+    std::lock_guard<std::mutex> g(kd::g_timer_mu);
+    return (int)kd::g_timer.size();
+}
+
+int kd_timer_read(int i, char* key, int key_cap, double* flops, float* ms) {
+    std::lock_guard<std::mutex> g(kd::g_timer_mu);
+    KD_CHECK_ARG(i >= 0 && i < (int)kd::g_timer.size(), "kd_timer_read: index out of range");
+    auto& r = kd::g_timer[i];
+    if (hipEventSynchronize(r.e1) != hipSuccess) return kd::fail(KD_ERR_LAUNCH, "kd_timer_read: event sync failed");
+    float t = 0.f;
+    hipEventElapsedTime(&t, r.e0, r.e1);
+    if (key && key_cap > 0) {
+        std::strncpy(key, r.key.c_str(), key_cap - 1);
+        key[key_cap - 1] = 0;
+    }
+    if (flops) *flops = r.flops;
+    if (ms) *ms = t;
+    return KD_OK;
+}
+
+void kd_timer_reset(void) {
+    std::lock_guard<std::mutex> g(kd::g_timer_mu);
+    for (auto& r : kd::g_timer) {
+        hipEventDestroy(r.e0);
+        hipEventDestroy(r.e1);
+    }
+    kd::g_timer.clear();
+}
+
+}  // extern "C"

@@ -286,10 +286,8 @@ class _KDBase(_Base):
     # ------------------------------------------------------------- the step ----
     def _teacher_forward(self, batch, need_feats):
         tfwd = self.teacher_model.forward(batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"],
-                                          save=False, want_post_ln=need_feats)
-        t_logits = self.teacher_model.logits(tfwd["hn"])
-        del tfwd["hn"]
-        return t_logits, tfwd.get("post_ln")
+                                          save=False, want_post_ln=need_feats, want_logits=True)
+        return tfwd["logits"], tfwd.get("post_ln")
 
     def _groups(self, B):
         G = self.loss_group_size or B
@@ -322,8 +320,8 @@ class _KDBase(_Base):
             t_logits, t_post = self._teacher_forward(batch, need_feats)
         with torch.cuda.stream(side):
             sfwd = s.forward(batch["depth_input_ids"], batch["depth_pixel_values"], image_sizes, save=train,
-                             want_post_ln=need_feats)
-            s_logits = s.logits(sfwd["hn"])
+                             want_post_ln=need_feats, want_logits=True)
+            s_logits = sfwd.pop("logits")
         main.wait_stream(side)
         Vs = s_logits.shape[1]
         s3 = s_logits.view(B, L, Vs)
@@ -377,11 +375,9 @@ class _KDBase(_Base):
         W = s.lm_head_weight()
         dl = ctx["dlogits"].view(hn.shape[0], -1)
         dhn = ops.gemm(dl, W.t(), alpha_dev=gscale)                          # lm_head dgrad
-        if s.train_language:                                                  # lm_head / tied embed wgrad
-            ev = s.wlane.run(lambda: ops.gemm(dl.t(), hn.t(), out=s.lm_head_grad(), accumulate=True, alpha_dev=gscale),
-                             dl, hn, gscale)
-            if s.cfg.text.tie:
-                s.tied_grad_event = ev
+        if s.train_language:   # lm_head / tied embed wgrad, on the lane ahead of the runtime's backward
+            s.wlane.run(lambda: ops.gemm(dl.t(), hn.t(), out=s.lm_head_grad(), accumulate=True, alpha_dev=gscale),
+                        dl, hn, gscale)
         del dl, ctx["dlogits"]
         dpost = None
         if ctx["dps"] is not None and s.train_vision:

@@ -2,10 +2,10 @@
 
 The reference loads `LlavaOnevisionForConditionalGeneration` from transformers (DT:33-48)
 and calls it as `model(input_ids=, pixel_values=, labels=, image_sizes=)` (DT:228, :238).
-This module is the build's own implementation of that forward and of its autograd
-backward, written as an explicit layer-by-layer forward (saving what the backward needs)
-and a hand-ordered backward; every FLOP runs in libkdstep.so (ops.py).  PyTorch only
-allocates tensors.
+This module is the Python face of the library's model runtime (include/kdstep.h
+kd_model_*: the forward and backward layer loops run in C++, csrc/model.hip, issuing the
+kernels straight onto the caller's streams).  PyTorch allocates the parameters, the
+workspaces and the outputs; every FLOP runs in libkdstep.so.
 
 Parameters live in ONE flat bf16 buffer (plus flat fp32 master / grad / Adam buffers for
 a trainable model) in the transformers-4.45 state_dict order and names
@@ -18,13 +18,14 @@ a trainable model) in the transformers-4.45 state_dict order and names
 """
 from __future__ import annotations
 
-import math
+import ctypes as C
 import os
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
+from . import _native as NV
 from . import anyres
 from . import ops
 
@@ -284,37 +285,23 @@ def rope_tables(seq: int, hd: int, theta: float, device):
             torch.from_numpy(np.sin(f).astype(np.float32)).to(device))
 
 
-class Saved(dict):
-    """Per-layer activations kept for the backward."""
-
-
-# priority of the training step's streams (lower = higher; 0 = default); the teacher
-# prefetch stream stays at 0 (KD_STREAM_PRIORITY=0 turns the distinction off)
+# priority of the training step's streams (lower = higher; 0 = default)
 STREAM_PRIORITY_HIGH = int(os.environ.get("KD_STREAM_PRIORITY", "-1"))
 
 
 class WgradLane:
-    """Weight-gradient work (dW GEMMs, bias column sums) on a side stream.
-
-    A linear layer's dW = dY^T X feeds only the optimizer, so it runs beside the dgrad
-    chain dX = dY W that the next layer waits for; the student's backward GEMMs (hidden
-    896, SigLIP 1152) fill 100-230 tiles of 256x256, fewer than the 256 CUs, so the two
-    streams fill each other's idle CUs.  `run` orders the side stream after everything
-    queued on the current stream, keeps its operands' memory alive for it (record_stream)
-    and returns an event the current stream waits on before it updates an operand in place;
-    `join` makes the current stream wait for all of it (before grads are read)."""
+    """The weight-gradient stream of a trainable model: the runtime's backward issues every
+    dW GEMM and bias column sum on it, beside the dgrad chain on the current stream
+    (csrc/model.hip); `run` puts extra work there (the lm_head wgrad, kd_module), ordered
+    after everything queued on the current stream, keeps its operands alive for it and
+    returns an event; `join` makes the current stream wait for all of it."""
 
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device, priority=STREAM_PRIORITY_HIGH)
-        # split-K default for the lane's GEMMs (0 = the library's cost model, which prices a
-        # GEMM as if it had the GPU to itself; 1 = never split: beside the dgrad chain an
-        # unsplit 76-150-tile dW GEMM leaves the other CUs to it and skips the fp32
-        # partial-plane round trip)
-        self.split_k = int(os.environ.get("KD_WGRAD_SPLIT_K", "0"))
 
     def run(self, fn, *keep):
         self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream), ops.gemm_split_default(self.split_k):
+        with torch.cuda.stream(self.stream):
             fn()
         for t in keep:
             if t is not None:
@@ -327,14 +314,30 @@ class WgradLane:
         torch.cuda.current_stream().wait_stream(self.stream)
 
 
-def _wait(ev):
-    if ev is not None:
-        torch.cuda.current_stream().wait_event(ev)
+def native_config(cfg: LlavaConfig) -> NV.KdModelConfig:
+    V, T = cfg.vision, cfg.text
+    return NV.KdModelConfig(V.hidden, V.inter, V.layers, V.heads, V.patch, V.image, V.eps,
+                            T.hidden, T.inter, T.layers, T.heads, T.kv_heads, T.head_dim, T.vocab, int(T.tie),
+                            T.rope_theta, T.eps, cfg.image_token_id, ops.ACTS[cfg.projector_act])
+
+
+def native_layout(cfg: LlavaConfig) -> list[tuple[str, int, int]]:
+    """(name, offset, numel) of every parameter as the library lays out the flat buffer."""
+    c = native_config(cfg)
+    lib = NV.lib()
+    out = []
+    name = C.create_string_buffer(256)
+    off, n, r, k = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+    for i in range(lib.kd_model_param_count(C.byref(c))):
+        NV.call("kd_model_param_info", C.byref(c), i, name, 256, C.byref(off), C.byref(n), C.byref(r), C.byref(k))
+        out.append((name.value.decode(), off.value, n.value))
+    return out
 
 
 # --------------------------------------------------------------------- model ----
 class LlavaOnevisionModel:
-    """One LLaVA-OneVision instance (teacher or student) on a ParamStore."""
+    """One LLaVA-OneVision instance (teacher or student) on a ParamStore, driven through the
+    library's model runtime (one forward call, one backward call per step)."""
 
     def __init__(self, cfg: LlavaConfig, device, trainable: bool = False, seed: int | None = None,
                  cpu_rng: bool = False):
@@ -345,15 +348,42 @@ class LlavaOnevisionModel:
             self.P.init_(seed, cpu_rng=cpu_rng)
         self._rope = {}
         self._maps = {}
+        self._ws = {}
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         # which regions receive weight gradients (freeze masks, DT:468-523)
-        self.train_vision = self.train_projector = self.train_language = trainable
+        self._train = [trainable] * 3   # vision, projector, language
         self.wlane = WgradLane(self.device) if (trainable and self.device.type == "cuda") else None
-        self.tied_grad_event = None   # lm_head wgrad into the tied embedding grad (kd_module._backward)
+        self._ncfg = native_config(cfg)
+        if NV.lib().kd_model_param_numel(C.byref(self._ncfg)) != self.P.numel:
+            raise RuntimeError("flat parameter layout differs from the library's (kd_model_param_info)")
+        h = C.c_void_p()
+        NV.call("kd_model_create", C.byref(self._ncfg), self.P.flat.data_ptr(),
+                self.P.grad.data_ptr() if trainable else None, C.byref(h))
+        self._h = h
 
-    # -- freeze helpers mirroring DT:468-523 (applied to the student)
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            NV.lib().kd_model_destroy(h)
+            self._h = None
+
+    # -- freeze masks mirroring DT:468-523 (applied to the student), kept in the runtime too
     def set_trainable(self, vision: bool, projector: bool, language: bool):
-        self.train_vision, self.train_projector, self.train_language = vision, projector, language
+        self._train = [bool(vision), bool(projector), bool(language)]
+        NV.call("kd_model_set_trainable", self._h, *map(int, self._train))
+
+    def _flag(i):
+        def get(self):
+            return self._train[i]
+
+        def put(self, v):
+            t = list(self._train)
+            t[i] = bool(v)
+            self.set_trainable(*t)
+        return property(get, put)
+
+    train_vision, train_projector, train_language = _flag(0), _flag(1), _flag(2)
+    del _flag
 
     def _rope_for(self, L):
         if L not in self._rope:
@@ -373,178 +403,14 @@ class LlavaOnevisionModel:
         maps, lens = self._maps[key]
         return ops.image_src_map(input_ids, self.cfg.image_token_id, maps, lens, self.err)
 
-    # ============================================================== vision ====
-    def vision_forward(self, pixels, save: bool):
-        """pixels [NI, 3, 384, 384] -> (x_last [NT, D] pre-post-LN, post_ln [NT, D], saves)."""
-        V, P = self.cfg.vision, self.P
-        NI = pixels.shape[0]
-        NT = NI * V.n_patches
-        vp = "vision_tower.vision_model."
-        rows = ops.patchify(pixels, V.patch, V.kpatch)                           # [NT, Kp]
-        x = ops.gemm(rows, P[vp + "embeddings.patch_embedding.weight"],
-                     bias=P[vp + "embeddings.patch_embedding.bias"],
-                     residual=P[vp + "embeddings.position_embedding.weight"], residual_row_mod=V.n_patches)
-        saved = [rows] if save else None
-        layers = []
-        D = V.hidden
-        for i in range(V.layers):
-            p = f"{vp}encoder.layers.{i}."
-            Wqkv = P.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight", 3 * D, D)
-            bqkv = P.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1, 3 * D).view(-1)
-            h, m1, r1 = ops.norm_fwd(x, P[p + "layer_norm1.weight"], P[p + "layer_norm1.bias"], V.eps, save_stats=save)
-            qkv = ops.gemm(h, Wqkv, bias=bqkv)
-            q, k, v = ops.qkv_split(qkv, NI, V.n_patches, V.heads, V.heads, V.hd, V.hdp)
-            del qkv
-            o, lse = ops.attn_fwd(q, k, v, V.hd, causal=False, want_lse=save)
-            o2 = o.view(NT, D)
-            x_mid = ops.gemm(o2, P[p + "self_attn.out_proj.weight"], bias=P[p + "self_attn.out_proj.bias"], residual=x)
-            h2, m2, r2 = ops.norm_fwd(x_mid, P[p + "layer_norm2.weight"], P[p + "layer_norm2.bias"], V.eps,
-                                      save_stats=save)
-            pre = torch.empty((NT, V.inter), dtype=torch.bfloat16, device=self.device) if save else None
-            u = ops.gemm(h2, P[p + "mlp.fc1.weight"], bias=P[p + "mlp.fc1.bias"], act="gelu_tanh", aux=pre)
-            x_out = ops.gemm(u, P[p + "mlp.fc2.weight"], bias=P[p + "mlp.fc2.bias"], residual=x_mid)
-            if save:
-                layers.append(Saved(x=x, h=h, m1=m1, r1=r1, q=q, k=k, v=v, o=o2, lse=lse, x_mid=x_mid, h2=h2, m2=m2,
-                                    r2=r2, pre=pre, u=u))
-            x = x_out
-        post, pm, pr = ops.norm_fwd(x, P[vp + "post_layernorm.weight"], P[vp + "post_layernorm.bias"], V.eps,
-                                    save_stats=save)
-        sv = None
-        if save:
-            sv = Saved(rows=rows, layers=layers, x_last=x, pm=pm, pr=pr, NI=NI)
-        return x, post, sv
-
-    def vision_backward(self, sv, dx, dpost=None):
-        """dx: grad wrt x_last [NT, D] (bf16, consumed in place); dpost: grad wrt post-LN output."""
-        V, P = self.cfg.vision, self.P
-        vp = "vision_tower.vision_model."
-        D = V.hidden
-        NI = sv["NI"]
-        NT = NI * V.n_patches
-        gw = self.train_vision
-        W = self.wlane
-        if dpost is not None:
-            ops.norm_bwd(sv["x_last"], P[vp + "post_layernorm.weight"], dpost, sv["pm"], sv["pr"], dx=dx,
-                         dx_accum=True,
-                         dweight=P.grad_view(vp + "post_layernorm.weight") if gw else None,
-                         dbias=P.grad_view(vp + "post_layernorm.bias") if gw else None)
-        for i in reversed(range(V.layers)):
-            p = f"{vp}encoder.layers.{i}."
-            s = sv["layers"][i]
-            W2 = P[p + "mlp.fc2.weight"]
-            du = ops.gemm(dx, W2.t())
-            ev = None
-            if gw:
-                ev = W.run(lambda: (ops.gemm(dx.t(), s["u"].t(), out=P.grad_view(p + "mlp.fc2.weight"), accumulate=True),
-                                    ops.colsum(dx, P.grad_view(p + "mlp.fc2.bias"))), dx, s["u"])
-            dpre = ops.act_bwd(s["pre"], du, "gelu_tanh", out=du)
-            dh2 = ops.gemm(dpre, P[p + "mlp.fc1.weight"].t())
-            if gw:
-                W.run(lambda: (ops.gemm(dpre.t(), s["h2"].t(), out=P.grad_view(p + "mlp.fc1.weight"), accumulate=True),
-                               ops.colsum(dpre, P.grad_view(p + "mlp.fc1.bias"))), dpre, s["h2"])
-            del du, dpre
-            _wait(ev)   # dx is updated in place next
-            ops.norm_bwd(s["x_mid"], P[p + "layer_norm2.weight"], dh2, s["m2"], s["r2"], dx=dx, dx_accum=True,
-                         dweight=P.grad_view(p + "layer_norm2.weight") if gw else None,
-                         dbias=P.grad_view(p + "layer_norm2.bias") if gw else None)
-            do = ops.gemm(dx, P[p + "self_attn.out_proj.weight"].t())
-            if gw:
-                ev = W.run(lambda: (ops.gemm(dx.t(), s["o"].t(), out=P.grad_view(p + "self_attn.out_proj.weight"),
-                                             accumulate=True),
-                                    ops.colsum(dx, P.grad_view(p + "self_attn.out_proj.bias"))), dx, s["o"])
-            dq, dk, dv = ops.attn_bwd(s["q"], s["k"], s["v"], s["o"], do, s["lse"], V.hd, causal=False)
-            dqkv = ops.qkv_merge(dq, dk, dv, NI, V.n_patches, V.heads, V.heads, V.hd, V.hdp)
-            del dq, dk, dv, do
-            Wqkv = P.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight", 3 * D, D)
-            dh = ops.gemm(dqkv, Wqkv.t())
-            if gw:
-                W.run(lambda: (ops.gemm(dqkv.t(), s["h"].t(), out=P.grad_span(p + "self_attn.q_proj.weight",
-                                                                               p + "self_attn.v_proj.weight", 3 * D, D),
-                                        accumulate=True),
-                               ops.colsum(dqkv, P.grad_span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1,
-                                                            3 * D).view(-1))), dqkv, s["h"])
-            del dqkv
-            _wait(ev)
-            ops.norm_bwd(s["x"], P[p + "layer_norm1.weight"], dh, s["m1"], s["r1"], dx=dx, dx_accum=True,
-                         dweight=P.grad_view(p + "layer_norm1.weight") if gw else None,
-                         dbias=P.grad_view(p + "layer_norm1.bias") if gw else None)
-            sv["layers"][i] = None   # free activations as we go
-        if gw:
-            W.run(lambda: (ops.gemm(dx.t(), sv["rows"].t(), out=P.grad_view(vp + "embeddings.patch_embedding.weight"),
-                                    accumulate=True),
-                           ops.colsum(dx, P.grad_view(vp + "embeddings.patch_embedding.bias")),
-                           ops.colsum(dx.view(NI, V.n_patches * D),
-                                      P.grad_view(vp + "embeddings.position_embedding.weight").view(-1))),
-                  dx, sv["rows"])
-
-    # =========================================================== projector ====
-    def projector_forward(self, x_last, save: bool):
-        P = self.P
-        pre = torch.empty((x_last.shape[0], self.cfg.text.hidden), dtype=torch.bfloat16,
-                          device=self.device) if save else None
-        z = ops.gemm(x_last, P["multi_modal_projector.linear_1.weight"], bias=P["multi_modal_projector.linear_1.bias"],
-                     act=self.cfg.projector_act, aux=pre)
-        feats = ops.gemm(z, P["multi_modal_projector.linear_2.weight"], bias=P["multi_modal_projector.linear_2.bias"])
-        return feats, (Saved(x_last=x_last, pre=pre, z=z) if save else None)
-
-    def projector_backward(self, s, dfeats, need_dx: bool):
-        P = self.P
-        gw = self.train_projector
-        W = self.wlane
-        dz = ops.gemm(dfeats, P["multi_modal_projector.linear_2.weight"].t())
-        if gw:
-            W.run(lambda: (ops.gemm(dfeats.t(), s["z"].t(), out=P.grad_view("multi_modal_projector.linear_2.weight"),
-                                    accumulate=True),
-                           ops.colsum(dfeats, P.grad_view("multi_modal_projector.linear_2.bias"))), dfeats, s["z"])
-        dpre = ops.act_bwd(s["pre"], dz, self.cfg.projector_act, out=dz)
-        if gw:
-            W.run(lambda: (ops.gemm(dpre.t(), s["x_last"].t(), out=P.grad_view("multi_modal_projector.linear_1.weight"),
-                                    accumulate=True),
-                           ops.colsum(dpre, P.grad_view("multi_modal_projector.linear_1.bias"))), dpre, s["x_last"])
-        if need_dx:
-            return ops.gemm(dpre, P["multi_modal_projector.linear_1.weight"].t())
-        return None
-
-    # ============================================================ language ====
-    def lm_forward(self, embeds, B, L, save: bool, kv_out: list | None = None):
-        T, P = self.cfg.text, self.P
-        M = B * L
-        cos, sin = self._rope_for(L)
-        lp = "language_model.model."
-        qd, kd = T.heads * T.head_dim, T.kv_heads * T.head_dim
-        x = embeds
-        layers = []
-        for i in range(T.layers):
-            p = f"{lp}layers.{i}."
-            Wqkv = P.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight", qd + 2 * kd, T.hidden)
-            bqkv = P.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1, qd + 2 * kd).view(-1)
-            h, _, r1 = ops.norm_fwd(x, P[p + "input_layernorm.weight"], None, T.eps, rms=True, save_stats=save)
-            qkv = ops.gemm(h, Wqkv, bias=bqkv)
-            q, k, v = ops.qkv_split(qkv, B, L, T.heads, T.kv_heads, T.head_dim, T.head_dim, cos, sin)
-            del qkv
-            if kv_out is not None:   # generate(): the prefill's roped keys / values seed the KV cache
-                kv_out.append((k, v))
-            o, lse = ops.attn_fwd(q, k, v, T.head_dim, causal=True, want_lse=save)
-            o2 = o.view(M, qd)
-            x_mid = ops.gemm(o2, P[p + "self_attn.o_proj.weight"], residual=x)
-            h2, _, r2 = ops.norm_fwd(x_mid, P[p + "post_attention_layernorm.weight"], None, T.eps, rms=True,
-                                     save_stats=save)
-            Wgu = P.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight", 2 * T.inter, T.hidden)
-            if T.inter % 128 == 0:   # SwiGLU fused into the gate|up GEMM; gate|up kept only for the backward
-                gu = torch.empty((M, 2 * T.inter), dtype=torch.bfloat16, device=self.device) if save else None
-                a = ops.gemm(h2, Wgu, act="swiglu", aux=gu)
-            else:
-                gu = ops.gemm(h2, Wgu)
-                a = ops.swiglu_fwd(gu, T.inter)
-            x_out = ops.gemm(a, P[p + "mlp.down_proj.weight"], residual=x_mid)
-            if save:
-                layers.append(Saved(x=x, h=h, r1=r1, q=q, k=k, v=v, o=o2, lse=lse, x_mid=x_mid, h2=h2, r2=r2, gu=gu, a=a))
-            else:
-                del gu, a
-            x = x_out
-        hn, _, rf = ops.norm_fwd(x, P[lp + "norm.weight"], None, T.eps, rms=True, save_stats=save)
-        sv = Saved(layers=layers, x_last=x, hn=hn, rf=rf, B=B, L=L) if save else None
-        return hn, sv
+    def _workspace(self, key, nbytes):
+        """One cached workspace per call shape: a save=1 forward's workspace holds the
+        activations its backward reads, so it is only rewritten by the next forward."""
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
 
     def lm_head_weight(self):
         T = self.cfg.text
@@ -557,106 +423,63 @@ class LlavaOnevisionModel:
     def logits(self, hn):
         return ops.gemm(hn, self.lm_head_weight())
 
-    def lm_backward(self, sv, dhn, gscale=None, on_layer_done=None):
-        """dhn: grad wrt the final-norm output [M, H] -> grad wrt inputs_embeds [M, H]."""
-        T, P = self.cfg.text, self.P
-        lp = "language_model.model."
-        B, L = sv["B"], sv["L"]
-        cos, sin = self._rope_for(L)
-        qd, kd = T.heads * T.head_dim, T.kv_heads * T.head_dim
-        gw = self.train_language
-        W = self.wlane
-        dx = ops.norm_bwd(sv["x_last"], P[lp + "norm.weight"], dhn, None, sv["rf"], rms=True,
-                          dweight=P.grad_view(lp + "norm.weight") if gw else None)
-        for i in reversed(range(T.layers)):
-            p = f"{lp}layers.{i}."
-            s = sv["layers"][i]
-            da = ops.gemm(dx, P[p + "mlp.down_proj.weight"].t())
-            ev = None
-            if gw:
-                ev = W.run(lambda: ops.gemm(dx.t(), s["a"].t(), out=P.grad_view(p + "mlp.down_proj.weight"),
-                                            accumulate=True), dx, s["a"])
-            dgu = ops.swiglu_bwd(s["gu"], da, T.inter)
-            del da
-            Wgu = P.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight", 2 * T.inter, T.hidden)
-            dh2 = ops.gemm(dgu, Wgu.t())
-            if gw:
-                W.run(lambda: ops.gemm(dgu.t(), s["h2"].t(), out=P.grad_span(p + "mlp.gate_proj.weight",
-                                                                              p + "mlp.up_proj.weight",
-                                                                              2 * T.inter, T.hidden),
-                                       accumulate=True), dgu, s["h2"])
-            del dgu
-            _wait(ev)   # dx is updated in place next
-            ops.norm_bwd(s["x_mid"], P[p + "post_attention_layernorm.weight"], dh2, None, s["r2"], dx=dx,
-                         dx_accum=True, rms=True,
-                         dweight=P.grad_view(p + "post_attention_layernorm.weight") if gw else None)
-            do = ops.gemm(dx, P[p + "self_attn.o_proj.weight"].t())
-            if gw:
-                ev = W.run(lambda: ops.gemm(dx.t(), s["o"].t(), out=P.grad_view(p + "self_attn.o_proj.weight"),
-                                            accumulate=True), dx, s["o"])
-            dq, dk, dv = ops.attn_bwd(s["q"], s["k"], s["v"], s["o"], do, s["lse"], T.head_dim, causal=True)
-            dqkv = ops.qkv_merge(dq, dk, dv, B, L, T.heads, T.kv_heads, T.head_dim, T.head_dim, cos, sin)
-            del dq, dk, dv, do
-            Wqkv = P.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight", qd + 2 * kd, T.hidden)
-            dh = ops.gemm(dqkv, Wqkv.t())
-            if gw:
-                W.run(lambda: (ops.gemm(dqkv.t(), s["h"].t(), out=P.grad_span(p + "self_attn.q_proj.weight",
-                                                                               p + "self_attn.v_proj.weight",
-                                                                               qd + 2 * kd, T.hidden),
-                                        accumulate=True),
-                               ops.colsum(dqkv, P.grad_span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias", 1,
-                                                            qd + 2 * kd).view(-1))), dqkv, s["h"])
-            del dqkv
-            _wait(ev)
-            ops.norm_bwd(s["x"], P[p + "input_layernorm.weight"], dh, None, s["r1"], dx=dx, dx_accum=True, rms=True,
-                         dweight=P.grad_view(p + "input_layernorm.weight") if gw else None)
-            sv["layers"][i] = None
-            if on_layer_done is not None:
-                on_layer_done(i)
-        return dx
-
     # ========================================================= full model ====
     def forward(self, input_ids, pixel_values, image_sizes, save: bool = False, want_post_ln: bool = False,
-                kv_out: list | None = None):
-        """LlavaOnevisionForConditionalGeneration.forward up to the final norm.
+                kv_out: list | None = None, want_logits: bool = False):
+        """LlavaOnevisionForConditionalGeneration.forward (kd_model_forward).
 
-        input_ids [B, L] int64 (device), pixel_values [B, P, 3, 384, 384], image_sizes
-        [B, 2] (host-readable).  Returns a dict with `hn` (final-norm hidden [B*L, H]),
-        `post_ln` (vision post_layernorm output, the reference's hook, DT:110-121) and the
-        saves for backward."""
+        input_ids [B, L] int64 (device), pixel_values [B, P, 3, 384, 384] (bf16 / fp32),
+        image_sizes [B, 2] (host-readable).  Returns a dict with `hn` (final-norm hidden
+        [B*L, H]), `post_ln` (vision post_layernorm output, the reference's hook, DT:110-121),
+        `logits` [B*L, V] (want_logits) and, with save, the workspace the backward reads.
+        kv_out (a list) receives each layer's roped (k, v) [B, kv_heads, L, head_dim]."""
+        T, V = self.cfg.text, self.cfg.vision
         B, L = input_ids.shape
-        Pn = pixel_values.shape[1]
-        px = pixel_values.reshape(B * Pn, *pixel_values.shape[2:])
-        x_last, post, vsave = self.vision_forward(px, save=save)
-        feats, psave = self.projector_forward(x_last, save=save)
-        src = self._src_map(input_ids, image_sizes.tolist() if hasattr(image_sizes, "tolist") else image_sizes, Pn)
-        emb = ops.embed_assemble(input_ids.reshape(-1), src, self.P["language_model.model.embed_tokens.weight"], feats,
-                                 self.P["image_newline"], self.err)
-        del feats
-        hn, lsave = self.lm_forward(emb, B, L, save=save, kv_out=kv_out)
-        out = dict(hn=hn, src=src, ids=input_ids.reshape(-1))
+        tiles = pixel_values.shape[1]
+        px = pixel_values.reshape(B * tiles, *pixel_values.shape[2:]).contiguous()
+        if px.dtype not in (torch.bfloat16, torch.float32):
+            raise RuntimeError(f"pixel_values: bf16 or fp32, got {px.dtype}")
+        ids = input_ids.contiguous()
+        src = self._src_map(ids, image_sizes.tolist() if hasattr(image_sizes, "tolist") else image_sizes, tiles)
+        cos, sin = self._rope_for(L)
+        lib = NV.lib()
+        nb = lib.kd_model_forward_workspace_size(self._h, B, L, tiles, int(save))
+        ws = self._workspace(("fwd", B, L, tiles, bool(save)), nb)
+        dev = self.device
+        hn = torch.empty((B * L, T.hidden), dtype=torch.bfloat16, device=dev)
+        post = torch.empty((B * tiles * V.n_patches, V.hidden), dtype=torch.bfloat16, device=dev) \
+            if want_post_ln else None
+        logits = torch.empty((B * L, T.vocab), dtype=torch.bfloat16, device=dev) if want_logits else None
+        kvk = kvv = None
+        if kv_out is not None:
+            ks = [torch.empty((B, T.kv_heads, L, T.head_dim), dtype=torch.bfloat16, device=dev) for _ in range(T.layers)]
+            vs = [torch.empty_like(k) for k in ks]
+            kv_out.extend(zip(ks, vs))
+            kvk = (C.c_void_p * T.layers)(*[k.data_ptr() for k in ks])
+            kvv = (C.c_void_p * T.layers)(*[v.data_ptr() for v in vs])
+        NV.call("kd_model_forward", self._h, ids.data_ptr(), px.data_ptr(), ops._DT[px.dtype], src.data_ptr(),
+                cos.data_ptr(), sin.data_ptr(), B, L, tiles, int(save), ws.data_ptr(), ws.numel(), hn.data_ptr(),
+                ops._ptr(post), ops._ptr(logits), kvk, kvv, self.err.data_ptr(), ops._stream())
+        out = dict(hn=hn, src=src, ids=ids, shape=(B, L, tiles))
         if want_post_ln:
             out["post_ln"] = post
+        if want_logits:
+            out["logits"] = logits
         if save:
-            out.update(vsave=vsave, psave=psave, lsave=lsave)
+            out["ws"] = ws
         return out
 
-    def backward(self, fwd, dhn, dpost=None, gscale=None, on_layer_done=None):
-        """Backward from d(final-norm hidden) and d(post-LN hook output) to every trainable grad."""
-        T = self.cfg.text
-        demb = self.lm_backward(fwd["lsave"], dhn, gscale, on_layer_done)
-        _wait(self.tied_grad_event)   # the tied lm_head wgrad accumulates into the embedding grad too
-        self.tied_grad_event = None
-        NT = fwd["vsave"]["x_last"].shape[0] if fwd.get("vsave") else 0
-        dfeats = torch.empty((NT, T.hidden), dtype=torch.bfloat16, device=self.device)
-        ops.embed_bwd(fwd["ids"], fwd["src"], demb,
-                      dtable=self.P.grad_view("language_model.model.embed_tokens.weight") if self.train_language else None,
-                      dfeats=dfeats,
-                      dnewline=self.P.grad_view("image_newline") if self.train_projector else None)
-        del demb
-        need_vision = self.train_vision
-        dx_last = self.projector_backward(fwd["psave"], dfeats, need_dx=need_vision)
-        if need_vision:
-            self.vision_backward(fwd["vsave"], dx_last, dpost)
-        if self.wlane is not None:
-            self.wlane.join()
+    def backward(self, fwd, dhn, dpost=None, on_layer_done=None):
+        """Backward of a save=True forward from d(final-norm hidden) and d(post-LN hook
+        output) into every trainable grad (kd_model_backward).  Weight gradients run on
+        the wgrad lane; the current stream has joined it when this returns."""
+        if "ws" not in fwd:
+            raise RuntimeError("backward needs a forward run with save=True")
+        B, L, tiles = fwd["shape"]
+        cos, sin = self._rope_for(L)
+        nb = NV.lib().kd_model_backward_workspace_size(self._h, B, L, tiles)
+        ws = self._workspace(("bwd", B, L, tiles), nb)
+        cb = NV.LAYER_CB(lambda user, i: on_layer_done(i)) if on_layer_done is not None else NV.LAYER_CB()
+        NV.call("kd_model_backward", self._h, fwd["ws"].data_ptr(), fwd["ids"].data_ptr(), fwd["src"].data_ptr(),
+                cos.data_ptr(), sin.data_ptr(), B, L, tiles, dhn.contiguous().data_ptr(), ops._ptr(dpost),
+                ws.data_ptr(), ws.numel(), ops._stream(), self.wlane.stream.cuda_stream, cb, None)

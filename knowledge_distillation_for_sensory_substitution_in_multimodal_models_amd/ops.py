@@ -16,35 +16,52 @@ _WS: dict = {}
 
 
 class KernelTimer:
-    """Optional HIP-event brackets around GEMM launches (bench.py roofline measurement).
+    """GEMM launch timing for bench.py's roofline pass: the library brackets every kd_gemm
+    launch (ops.gemm and the model runtime's own) with HIP events on its launch stream
+    while enabled (include/kdstep.h kd_timer_*)."""
 
-    Events are recorded on the stream the kernel is launched on (the current stream)."""
+    @property
+    def enabled(self):
+        return getattr(self, "_on", False)
 
-    def __init__(self):
-        self.enabled = False
-        self.records = []   # (kind, flops, start_event, end_event, shape_key)
+    @enabled.setter
+    def enabled(self, on):
+        self._on = bool(on)
+        NV.lib().kd_timer_enable(int(self._on))
 
     def reset(self):
-        self.records = []
+        NV.lib().kd_timer_reset()
+
+    def records(self):
+        """[(key, flops, ms)], key = "<kind>:<M>x<N>x<K>:<out dtype>[:acc]" (synchronises)."""
+        lib = NV.lib()
+        key = C.create_string_buffer(128)
+        fl, ms = C.c_double(), C.c_float()
+        out = []
+        for i in range(lib.kd_timer_count()):
+            NV.call("kd_timer_read", i, key, 128, C.byref(fl), C.byref(ms))
+            out.append((key.value.decode(), fl.value, ms.value))
+        return out
 
     def summary(self, kind):
-        recs = [r for r in self.records if r[0] == kind]
+        recs = [r for r in self.records() if r[0].split(":", 1)[0] == kind]
         if not recs:
             return None
-        torch.cuda.synchronize()
-        ms = [r[2].elapsed_time(r[3]) for r in recs]
+        ms = [r[2] for r in recs]
         flops = sum(r[1] for r in recs)
         return dict(launches=len(recs), total_ms=sum(ms), avg_ms=sum(ms) / len(ms), flops=flops,
                     flops_per_launch=flops / len(recs))
 
+    def kinds(self):
+        return sorted({r[0].split(":", 1)[0] for r in self.records()})
+
     def by_shape(self, top=25):
         """Per (layouts, M, N, K, out dtype) totals, heaviest first (tuning aid)."""
-        torch.cuda.synchronize()
         agg = {}
-        for kind, fl, a, b, key in self.records:
+        for key, fl, ms in self.records():
             t = agg.setdefault(key, [0, 0.0, fl])
             t[0] += 1
-            t[1] += a.elapsed_time(b)
+            t[1] += ms
         rows = sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]
         return [dict(shape=k, launches=n, total_ms=round(ms, 3), avg_us=round(1e3 * ms / n, 2),
                      tflops=round(fl * n / (ms * 1e-3) / 1e12, 1)) for k, (n, ms, fl) in rows]
@@ -240,17 +257,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
         split_k = _SPLIT_DEFAULT[0]
     d, out, M, N, K, la, lb = _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate,
                                          out_dtype, residual_row_mod, variant, split_k)
-    if TIMER.enabled:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        NV.call("kd_gemm", C.byref(d), _stream())
-        e1.record()
-        kind = "gemm_kk_swiglu" if act == "swiglu" else f"gemm_{'kn'[la]}{'kn'[lb]}"
-        TIMER.records.append((kind, 2.0 * M * N * K, e0, e1,
-                              f"{kind}:{M}x{N}x{K}:{'f32' if out.dtype == torch.float32 else 'bf16'}"
-                              f"{':acc' if accumulate else ''}"))
-    else:
-        NV.call("kd_gemm", C.byref(d), _stream())
+    NV.call("kd_gemm", C.byref(d), _stream())
     return out
 
 

@@ -100,8 +100,8 @@ class OracleLlava:
         hd, nq, nkv = T.head_dim, T.heads, T.kv_heads
         inv = 1.0 / (T.rope_theta ** (torch.arange(0, hd, 2, dtype=torch.int64).float() / hd))
         fr = torch.arange(L, dtype=torch.float32)[:, None] * inv[None]
-        cos = torch.cat([fr.cos(), fr.cos()], -1)
-        sin = torch.cat([fr.sin(), fr.sin()], -1)
+        cos = torch.cat([fr.cos(), fr.cos()], -1).to(emb.dtype)   # the activations' dtype (bf16 cpu_baseline leg)
+        sin = torch.cat([fr.sin(), fr.sin()], -1).to(emb.dtype)
         rot = lambda t: torch.cat([-t[..., hd // 2:], t[..., :hd // 2]], -1)
         rms = lambda t, g: g * (t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + T.eps))
         mask = torch.triu(torch.ones(L, L, dtype=torch.bool), 1)

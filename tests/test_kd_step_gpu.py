@@ -5,14 +5,39 @@ Expected values: the reference's own forward()/training_step driving transformer
 same seeded weights (tests/golden/model_*.npz), and the CPU oracle's full gradients
 (oracle/model.py, pinned to the same fixtures on CPU).  The HIP path runs bf16 weights /
 activations with fp32 accumulation; the reference fp32, so:
-  total loss        rel 2e-3
+  every loss term   |d| <= 1e-4 + 1e-3 |ref| (north_star): total, KD term, student CE,
+                    teacher CE, NT-Xent — each against the reference's own value
+  student logits    per-row logsumexp at the north-star tolerance; sampled raw logits
+                    |d| <= 2^-7 |ref| + 0.08 rms(ref) (bf16 logits: a few ulps)
+  grad total norm   |d| <= 1e-3 |ref| + 1.25 |d_bf16|, d_bf16 = the same oracle run in bf16
+                    on the CPU (torch autograd).  A plain bf16 run of the reference's
+                    arithmetic already misses 1e-3 (dt1: +3.4 %, lb: +0.25 %), so the HIP
+                    path is held to that bar, not below it
   per-param grads   cosine(HIP, oracle) >= 0.99 and |norm ratio - 1| <= 5e-2 for every
                     parameter whose grad norm is >= 1e-3 x the largest one
 """
+import math
+
+import numpy as np
 import pytest
 import torch
 
-from model_fixtures import KINDS, batch, frozen, load, oracle_grads
+from model_fixtures import KINDS, batch, frozen, grad_total_norm, load, oracle_grads
+
+ATOL, RTOL = 1e-4, 1e-3   # north_star
+
+
+def _grad(P, name):
+    """The HIP gradient of `name` in the reference's shape (the conv weight's pad columns dropped)."""
+    g = P.grad_view(name)
+    spec = next(s for s in P.specs if s.name == name)
+    if spec.ckpt_shape is not None:
+        g = g[:, :math.prod(spec.ckpt_shape[1:])]
+    return g
+
+
+def _near(got, ref, what):
+    assert abs(got - ref) <= ATOL + RTOL * abs(ref), f"{what}: {got!r} vs reference {ref!r}"
 
 pytestmark = pytest.mark.gpu
 
@@ -38,24 +63,49 @@ def test_training_step_matches_reference(name, dev):
     meta, exp = load(name)
     kind, phase = KINDS[name]
     m = _module(kind, phase)
+    m.keep_logits = True
     b = batch(meta, dev)
     loss = m.training_step(b, 0)
     assert loss.requires_grad and loss.dim() == 0
     loss.backward()
     torch.cuda.synchronize()
-    assert loss.item() == pytest.approx(float(exp["total"]), rel=2e-3)
     assert int(m.student_model.err.item()) == 0
+    # every loss term vs the reference's own forward
+    kd, ce, tce, _ = m.last_terms.tolist()
+    _near(loss.item(), float(exp["total"]), "total")
+    _near(ce, float(exp["student_ce"]), "student CE")
+    if not math.isnan(float(exp["teacher_ce"])):
+        _near(tce, float(exp["teacher_ce"]), "teacher CE")
+    if not math.isnan(float(exp["kd_term"])):
+        _near(kd, float(exp["kd_term"]), "KD term")
+    if not math.isnan(float(exp["ntxent"])):
+        _near(float(m.last_ntxent[1]), float(exp["ntxent"]), "NT-Xent")
+    # student logits
+    s3, _ = m.last_logits
+    lse = torch.logsumexp(s3.double(), -1).reshape(-1).cpu().numpy()
+    ref_lse = exp["s_logit_lse"]
+    assert bool((np.abs(lse - ref_lse) <= ATOL + RTOL * np.abs(ref_lse)).all()), \
+        f"logit lse: max |d| {np.abs(lse - ref_lse).max():.3e}"
+    got_rows = s3[:, exp["logit_rows"].tolist(), ::int(exp["logit_col_stride"])].float().cpu().numpy()
+    ref_rows = exp["s_logit_rows"]
+    bound = 2.0 ** -7 * np.abs(ref_rows) + 0.08 * np.sqrt((ref_rows ** 2).mean())
+    assert bool((np.abs(got_rows - ref_rows) <= bound).all()), f"logits: max |d| {np.abs(got_rows - ref_rows).max():.3e}"
+    m.last_logits = None
     tot, ograds = oracle_grads(name)
     P = m.student_model.P
+    # the gradient's total norm (over the reference's parameters; the conv weight's padded tail excluded)
+    gn = math.sqrt(sum(float(_grad(P, str(n)).double().pow(2).sum()) for n in exp["grad_names"]))
+    ref_gn = float(exp["grad_total_norm"])
+    if abs(gn - ref_gn) > RTOL * ref_gn:
+        _, bgr = oracle_grads(name, torch.bfloat16)
+        d_bf16 = abs(grad_total_norm(bgr) - ref_gn)
+        assert abs(gn - ref_gn) <= RTOL * ref_gn + 1.25 * d_bf16, \
+            f"grad total norm {gn:.6g} vs reference {ref_gn:.6g} (bf16 oracle off by {d_bf16:.4g})"
     names = [str(n) for n in exp["grad_names"]]
     gmax = max(float(g.norm()) for g in ograds.values())
     for n in names:
         ref = ograds[n].double().reshape(-1)
-        got = P.grad_view(n)
-        spec = next(s for s in P.specs if s.name == n)
-        if spec.ckpt_shape is not None:
-            got = got[:, :ref.numel() // got.shape[0]]
-        got = got.double().cpu().reshape(-1)
+        got = _grad(P, n).double().cpu().reshape(-1)
         rn = float(ref.norm())
         if rn < 1e-3 * gmax:
             continue

@@ -192,7 +192,7 @@ def test_colsum_and_group_mean(dev):
     assert torch.allclose(dx.float().view(4, 729, 1152), pm[:, None].expand(4, 729, 1152) / 729, rtol=1e-2, atol=1e-8)
 
 
-@pytest.mark.parametrize("n", [8, 16, 64])   # c1 (2B = 8 tiles), c2 (2B = 16), the kernel's limit
+@pytest.mark.parametrize("n", [8, 16, 32, 64])   # c1 (2B = 8 tiles), c2 (2B = 16), global-memory path, the limit
 def test_ntxent_matches_oracle(n, dev):
     from oracle import kd_losses as O
     ops = _ops()

@@ -1,0 +1,28 @@
+# Round-end style GPU pass (run under gpurun):
+#   STEPS="tests parity bench prof pmc" ROUND=r02 bash tools/gpu_round.sh
+# tests  : pytest -m gpu (every parity test)
+# parity : tools/parity_report.py -> gpurun_out/parity.json (per-term deltas vs the reference)
+# bench  : python bench.py (the driver's default line) -> gpurun_out/bench.log
+# prof   : rocprofv3 --kernel-trace --stats of a serialized bench (its roofline-kernel average
+#          is what bench.py's HIP-event pass measures)
+# pmc    : HBM traffic per kernel (tools/pmc_bench.sh, two --pmc passes)
+# Every step has its own time limit; the first failure ends the script.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+STEPS=${STEPS:-"tests parity bench prof"}
+BENCH_ARGS=${BENCH_ARGS:-""}
+for s in $STEPS; do
+  echo "== $s $(date +%T)"
+  case $s in
+    tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+            tail -2 gpurun_out/pytest_gpu.log ;;
+    parity) timeout -k 10 300 python -u tools/parity_report.py --out gpurun_out/parity.json > gpurun_out/parity.log 2>&1 || { echo "parity failed"; tail -20 gpurun_out/parity.log; exit 1; } ;;
+    bench)  timeout -k 10 900 python -u bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
+            tail -1 gpurun_out/bench.log ;;
+    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-cpu-baseline --no-delta $BENCH_ARGS > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; } ;;
+    pmc)    bash tools/pmc_bench.sh > gpurun_out/pmc_bench.log 2>&1 || { echo "pmc failed"; tail -10 gpurun_out/pmc_bench.log; exit 1; } ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "done $(date +%T)"

@@ -72,6 +72,10 @@ def measure(name, dev):
             g = g[:, :int(np.prod(spec.ckpt_shape[1:]))]
         tot2 += float(g.double().pow(2).sum())
     out["grad_total_norm"] = _d(math.sqrt(tot2), float(exp["grad_total_norm"]))
+    # the yardstick: the same oracle (pinned fp32 restatement) run in bf16 on the CPU
+    from model_fixtures import grad_total_norm, oracle_grads
+    _, bgr = oracle_grads(name, torch.bfloat16)
+    out["grad_total_norm"]["bf16_oracle"] = _d(grad_total_norm(bgr), float(exp["grad_total_norm"]))
     return out
 
 
