@@ -47,7 +47,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 3
+#define KD_ABI_VERSION 4
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -120,7 +120,7 @@ int kd_loss_check(const void* workspace, void* stream);
  * Requirements: 16-B aligned A/B; ld % 8 == 0; K % 8 == 0 for K-major operands,
  * rows % 8 == 0 for MN-major ones.  Any M/N/K otherwise (tails read as zeros). */
 typedef enum { KD_LAYOUT_K_MAJOR = 0, KD_LAYOUT_MN_MAJOR = 1 } kd_layout;
-typedef enum { KD_DTYPE_BF16 = 0, KD_DTYPE_F32 = 1 } kd_dtype;
+typedef enum { KD_DTYPE_BF16 = 0, KD_DTYPE_F32 = 1, KD_DTYPE_FP8_E4M3 = 2 } kd_dtype;
 /* KD_ACT_SWIGLU: Qwen2MLP's act_fn(gate_proj(x)) * up_proj(x) (HF5 qwen2 :35-50) fused into
  * the gate|up GEMM: B = [gate; up] is [N = 2I][K] (I % 128 == 0), C is [M][I] =
  * silu(v[:, :I]) * v[:, I:] with v = alpha * acc rounded to bf16 first (as the unfused
@@ -154,7 +154,15 @@ typedef struct {
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;
+    int32_t ab_dtype;         /* operand dtype: KD_DTYPE_BF16 (0) or KD_DTYPE_FP8_E4M3 (fp8 path) */
+    const float* a_scale;     /* fp8 path: per-row scale of A [M] (A = a_scale[m] * qa[m][k])     */
+    const float* b_scale;     /* fp8 path: per-row scale of B [N] (per output channel)           */
 } kd_gemm_desc;
+/* fp8 path (ab_dtype = KD_DTYPE_FP8_E4M3; the fp8 teacher of BASELINE config c4): A and B are
+ * OCP e4m3 bytes, both K-major, K % 16 == 0, lda / ldb % 16 == 0 (bytes = elements), 16-B
+ * aligned; C = epilogue(alpha * a_scale[m] * b_scale[n] * sum_k qa[m][k] qb[n][k]) with the
+ * epilogue above (bias / aux / act / residual / SWIGLU), bf16 C, no split-K.  MFMA
+ * v_mfma_scale_f32_32x32x64_f8f6f4 (unit block scales), fp32 accumulation. */
 
 /* Bytes of workspace the auto (or forced) split-K plan for `desc` wants; 0 = no split.
  * With split-K the K range is cut into S chunks, each an independent tile grid writing
@@ -252,6 +260,10 @@ int kd_adamw(float* param, void* param_bf16, const float* grad, float* exp_avg, 
 /* out[0] += sum x^2 (gradient norm). */
 int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* fp8 row quantisation (the fp8 GEMM's operands): per row r of x (bf16 [R][K], K % 16 == 0)
+ * scale[r] = amax_r / 448 (1 for an all-zero row) and q[r][k] = e4m3(clamp(x[r][k] * 448 /
+ * amax_r, +-448)), round to nearest even (OCP e4m3fn bytes). */
+int kd_quant_rows_fp8(const void* x, int64_t ldx, int R, int K, void* q, int64_t ldq, float* scale, void* stream);
 
 /* ------------------------------------------------------ depth transform ---- */
 /* Depth image -> 3-channel uint8 image (normalised depth, Prewitt gradient magnitude,
@@ -351,6 +363,17 @@ int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad
 void kd_model_destroy(kd_model* m);
 /* freeze masks (DT:468-523): which regions receive weight gradients */
 int kd_model_set_trainable(kd_model* m, int vision, int projector, int language);
+
+/* fp8 teacher (BASELINE config c4): e4m3 copies of every linear weight the forward's GEMMs
+ * read (all 2-D weights but the patch-embedding conv, the position embedding and
+ * embed_tokens) in a uint8 buffer with the bf16 buffer's element offsets, plus one fp32
+ * scale per weight row (kd_model_fp8_scale_count floats, spec order).  quantize fills both
+ * from the bound bf16 weights (kd_quant_rows_fp8 per weight); set_fp8 binds them (NULL
+ * unbinds) for a model without a grad buffer: its forward then quantises each linear's
+ * input rows per token and runs the fp8 GEMM (kd_gemm fp8 path). */
+int64_t kd_model_fp8_scale_count(const kd_model* m);
+int kd_model_quantize_fp8(const kd_model* m, void* q, float* scales, void* stream);
+int kd_model_set_fp8(kd_model* m, const void* q, const float* scales);
 
 /* Forward.  ids int64 [B, L]; pixels [B*tiles, 3, image, image] (kd_dtype); src int32 [B*L]
  * from kd_image_src_map; rope_cos/rope_sin fp32 [L, head_dim/2] (Qwen2RotaryEmbedding:

@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("KDSTEP_LIB", _PKG / "libkdstep.so"))
 HEADER = _PKG.parent / "include" / "kdstep.h"
 
 KD_OK = 0
-ABI_VERSION = 3
+ABI_VERSION = 4
 STATUS_NAMES = {
     0: "KD_OK", 1: "KD_ERR_SHAPE", 2: "KD_ERR_DTYPE", 3: "KD_ERR_ALIGN", 4: "KD_ERR_ARCH",
     5: "KD_ERR_LABEL_RANGE", 6: "KD_ERR_LAUNCH", 7: "KD_ERR_ARG", 8: "KD_ERR_WORKSPACE",
@@ -46,7 +46,7 @@ class KdLossParams(C.Structure):
 
 # kd_layout / kd_dtype / kd_act
 KD_LAYOUT_K_MAJOR, KD_LAYOUT_MN_MAJOR = 0, 1
-KD_DTYPE_BF16, KD_DTYPE_F32 = 0, 1
+KD_DTYPE_BF16, KD_DTYPE_F32, KD_DTYPE_FP8_E4M3 = 0, 1, 2
 KD_ACT_NONE, KD_ACT_GELU_TANH, KD_ACT_GELU_ERF, KD_ACT_SILU, KD_ACT_SWIGLU = 0, 1, 2, 3, 4
 
 
@@ -65,6 +65,7 @@ class KdGemmDesc(C.Structure):
         ("residual_row_mod", C.c_int32),
         ("variant", C.c_int32),
         ("split_k", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64),
+        ("ab_dtype", C.c_int32), ("a_scale", C.c_void_p), ("b_scale", C.c_void_p),
     ]
 
 
@@ -138,6 +139,7 @@ SIGNATURES = {
     "kd_adamw": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
     "kd_sumsq": (_i32, [_vp, _i64, _vp, _vp]),
     "kd_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
+    "kd_quant_rows_fp8": (_i32, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp]),
     "kd_depth_to_3ch_workspace_size": (_sz, [_i32, _i32, _i32]),
     "kd_depth_to_3ch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp]),
     "kd_image_resize_workspace_size": (_sz, [_i32, _i32, _i32, _i32]),
@@ -155,6 +157,9 @@ SIGNATURES = {
     "kd_model_create": (_i32, [C.POINTER(KdModelConfig), _vp, _vp, C.POINTER(_vp)]),
     "kd_model_destroy": (None, [_vp]),
     "kd_model_set_trainable": (_i32, [_vp, _i32, _i32, _i32]),
+    "kd_model_fp8_scale_count": (_i64, [_vp]),
+    "kd_model_quantize_fp8": (_i32, [_vp, _vp, _vp, _vp]),
+    "kd_model_set_fp8": (_i32, [_vp, _vp, _vp]),
     "kd_model_forward_workspace_size": (_sz, [_vp, _i32, _i32, _i32, _i32]),
     "kd_model_forward": (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _sz, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp]),

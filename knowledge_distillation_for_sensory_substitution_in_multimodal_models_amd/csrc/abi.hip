@@ -108,6 +108,9 @@ int kd_image_src_map(const int64_t* ids, int B, int L, int64_t tok, const int32_
     return kd::launch_image_src_map(ids, B, L, tok, map, ld, len, src, err, s);
 }
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* s) { return kd::launch_cast_f32_bf16(x, y, n, s); }
+int kd_quant_rows_fp8(const void* x, int64_t ldx, int R, int K, void* q, int64_t ldq, float* scale, void* s) {
+    return kd::launch_quant_rows_f8(x, ldx, R, K, q, ldq, scale, s);
+}
 size_t kd_depth_to_3ch_workspace_size(int B, int H, int W) { return kd::depth3_ws(B, H, W); }
 int kd_depth_to_3ch(const void* depth, int dtype, int B, int H, int W, uint8_t* out, void* ws, size_t ws_bytes,
                     void* s) {

@@ -21,6 +21,7 @@
 // 16x16x32 operand access pattern (derivation in DESIGN.md §GEMM).
 #include "common.h"
 
+#include <cstring>
 #include <type_traits>
 
 namespace kd {
@@ -44,6 +45,8 @@ struct GemmP {
     int64_t split_stride;  // split-K: fp32 elements between consecutive partial planes
     int glu;               // SwiGLU epilogue (v8, K-major): I = N/2; B rows [0,I) gate, [I,2I) up; 0 = off
     int tile0;             // first linear tile (grouped order) of this launch: the split tail of a hybrid plan
+    const float* sa;       // fp8 path: per-row scale of A [M] (dequantised A = sa[m] * qa[m, k])
+    const float* sb;       // fp8 path: per-row scale of B [N] (per output channel)
 };
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
@@ -977,6 +980,285 @@ __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
     else epilogue2<256, 256, 2, 4, 128, 64, 8, 4, NTH9, !A_MN && !B_MN>(p, acc, smem, m0, n0, grp, wc, lane, tid);
 }
 
+
+// =============================================================================
+// f8: v8's structure on fp8 (OCP e4m3) operands, for the fp8 teacher (BASELINE config c4):
+//   C = epilogue(alpha * sa[m] * sb[n] * sum_k qa[m,k] qb[n,k])
+// qa / qb e4m3 with a per-row (token) and a per-output-channel fp32 scale, fp32
+// accumulation in the AGPR file. v_mfma_scale_f32_32x32x64_f8f6f4 with unit block scales
+// (e8m0 127 = 2^0) takes a 64-deep K step per instruction at twice the bf16 MFMA rate
+// (MI355X_MICROARCH.md § Matrix cores: the block-scaled e4m3 form, 2x bf16 per clock).
+// A stage is 64 K bytes of 256 rows per operand: the same [256 rows][64 B] image and
+// swizzle as v8's bf16 BK=32 stage, so the DMA offsets, the 4-slot ring (three stages in
+// flight, counted vmcnt, raw barriers) and the WAR/RAW argument of v8 carry over; per step
+// each wave issues 16 MFMAs (4x4 tiles of 32x32 over its 128x128 quadrant), 8 DMAs of
+// stage t+4 and 16 ds_read_b128 of stage t+1's fragments.
+// Fragment (32x32x64, e4m3): lane l holds row (l & 31), k = 32 (l >> 5) + [0, 32) = two
+// 16-B chunks of that row's 64-B stage row; C/D: col = l & 31, row = (reg & 3) +
+// 8 (reg >> 2) + 4 (l >> 5).  Checked against a torch fp32 product of the dequantised
+// operands (tests/test_fp8_gpu.py).
+// =============================================================================
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ uint32_t rec_bytes1(int64_t rows, int64_t ld) {
+    const int64_t b = rows * ld;
+    return b <= 0 ? 0u : (b >= 0x7FFFFFFFll ? 0x7FFFFFFFu : (uint32_t)b);
+}
+
+__device__ __forceinline__ void mfma_f8(f32x16& acc, const i32x8& a, const i32x8& b, int unit_scale) {
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+                 : "+a"(acc) : "v"(a), "v"(b), "v"(unit_scale));
+}
+
+__device__ __forceinline__ i32x8 frag_f8(const char* tile, int r, int h) {
+    const char* rowp = tile + r * 64;
+    const int sw = f4(r);
+    const u32x4 lo = *(const u32x4*)(rowp + (((2 * h) ^ sw) << 4));
+    const u32x4 hi = *(const u32x4*)(rowp + (((2 * h + 1) ^ sw) << 4));
+    i32x8 v;
+    v[0] = (int)lo[0]; v[1] = (int)lo[1]; v[2] = (int)lo[2]; v[3] = (int)lo[3];
+    v[4] = (int)hi[0]; v[5] = (int)hi[1]; v[6] = (int)hi[2]; v[7] = (int)hi[3];
+    return v;
+}
+
+constexpr int F8_RS = 256 * 2 + 16;               // bf16 epilogue image row stride (bytes)
+constexpr int F8_EPI = 256 * F8_RS;               // epilogue image bytes; the tile's row scales follow
+constexpr size_t F8_LDS = (size_t)F8_EPI + 1024;  // > the 128 KiB ring
+
+// pre-activation (and activation ACT) of the 4x4 32x32 accumulator tiles -> bf16 LDS image
+template <int ACT>
+__device__ __forceinline__ void f8_to_lds(const f32x16 (&acc)[4][4], char* smem, const float* sa_l, const float (&sbv)[4],
+                                          const float (&bcol)[4], float alpha, int ra, int cb, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int lc = cb + 32 * j + (lane & 31);
+            const float cs = alpha * sbv[j];
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int lr = ra + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+                const float v = apply_act(acc[i][j][reg] * cs * sa_l[lr] + bcol[j], ACT);
+                *(bf16*)(smem + lr * F8_RS + lc * 2) = (bf16)v;
+            }
+        }
+}
+
+template <int EXP = 0>
+__global__ void __launch_bounds__(NTH8, 1) k_gemm8f8(GemmP p) {
+    constexpr bool glu = EXP & 4;
+    constexpr int SA = 256 * 64, SS = 2 * SA;   // 16 KiB per operand stage, 32 KiB per slot
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    int tm, tn;
+    tile_of((p.M + 255) / 256, glu ? (p.N / 256) : (p.N + 255) / 256, tm, tn, p.tile0);
+    const int m0 = tm * 256, n0 = tn * 256, nb = tn * 128;
+    const int K = p.K;
+    const int nk = (K + 63) / 64, nk_full = K / 64;
+    const char* A8 = (const char*)p.A;
+    const char* B8 = (const char*)p.B;
+    const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A8 + (int64_t)m0 * p.lda, rec_bytes1(min(256, p.M - m0), p.lda));
+    const __amdgpu_buffer_rsrc_t rsB = glu ? make_rsrc(B8, rec_bytes1(p.N, p.ldb))
+                                           : make_rsrc(B8 + (int64_t)n0 * p.ldb, rec_bytes1(min(256, p.N - n0), p.ldb));
+    uint32_t va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {   // [256 rows][64 B]: 16 rows x 64 B per wave-instruction
+        const int row = 16 * (wid * 4 + u) + (lane >> 2);
+        const int gc = (lane & 3) ^ f4(row);
+        va[u] = (uint32_t)((int64_t)row * p.lda + gc * 16);
+        const int wrow = glu ? (row < 128 ? nb + row : p.glu + nb + row - 128) : row;
+        vb[u] = (uint32_t)((int64_t)wrow * p.ldb + gc * 16);
+    }
+    auto dma = [&](int st, int sl, int u, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        const bool isA = u < 4;
+        const int i = wid * 4 + (u & 3);
+        char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
+        uint32_t v = isA ? va[u & 3] : vb[u & 3];
+        int soff = st * 64;
+        if (!FULL) {
+            const int kleft = K - st * 64;   // valid k bytes of this stage (<= 0: past the end)
+            if (kleft < 64) {
+                const int row = 16 * i + (lane >> 2);
+                const int gc = (lane & 3) ^ f4(row);
+                if (gc * 16 >= kleft) v = OOB;
+                if (kleft <= 0) soff = 0;
+            }
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsB, (lds_void_t*)dst, 16, v, soff, 0, 0);
+    };
+    using FullT = std::integral_constant<bool, true>;
+    using PartT = std::integral_constant<bool, false>;
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int unit = 0x7F7F7F7F;   // e8m0 block scale 2^0 in every byte
+    const int ra = wm * 128, cb = wn * 128, lr32 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int st = 0; st < NS8; ++st)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dma(st, st, u, PartT{});
+    wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
+    __builtin_amdgcn_s_barrier();
+    i32x8 xa[4], xb[4], ya[4], yb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        xa[u] = frag_f8(smem, ra + 32 * u + lr32, h);
+        xb[u] = frag_f8(smem + SA, cb + 32 * u + lr32, h);
+    }
+#define KD_F8_SYNC()                                      \
+    {                                                     \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        wait_vm<16>();                                    \
+        __builtin_amdgcn_s_barrier();                     \
+    }
+    KD_F8_SYNC()
+    __builtin_amdgcn_sched_barrier(0);
+#define KD_SB __builtin_amdgcn_sched_barrier(0);
+#define KD_F8_STEP(SL, CA, CB, NA, NB, FT)                                                         \
+    {                                                                                               \
+        const int t_ = t + (SL);                                                                    \
+        const char* na_ = smem + (((SL) + 1) % NS8) * SS;                                           \
+        _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                            \
+            if (u == 15) KD_F8_SYNC()                                                               \
+            KD_SB                                                                                   \
+            mfma_f8(acc[u >> 2][u & 3], CA[u >> 2], CB[u & 3], unit); KD_SB                         \
+            if (u < 8) {                                                                            \
+                dma(t_ + NS8, (SL), u, FT{}); KD_SB                                                 \
+                if (u < 4) NA[u] = frag_f8(na_, ra + 32 * u + lr32, h);                             \
+                else NB[u - 4] = frag_f8(na_ + SA, cb + 32 * (u - 4) + lr32, h);                    \
+                KD_SB                                                                               \
+            }                                                                                       \
+        }                                                                                           \
+    }
+    int t = 0;
+    for (; t + 2 * NS8 <= nk_full; t += NS8) {   // every DMA of these steps lies inside K
+        KD_F8_STEP(0, xa, xb, ya, yb, FullT)
+        KD_F8_STEP(1, ya, yb, xa, xb, FullT)
+        KD_F8_STEP(2, xa, xb, ya, yb, FullT)
+        KD_F8_STEP(3, ya, yb, xa, xb, FullT)
+    }
+    for (; t + NS8 <= nk; t += NS8) {
+        KD_F8_STEP(0, xa, xb, ya, yb, PartT)
+        KD_F8_STEP(1, ya, yb, xa, xb, PartT)
+        KD_F8_STEP(2, xa, xb, ya, yb, PartT)
+        KD_F8_STEP(3, ya, yb, xa, xb, PartT)
+    }
+    const int rem = nk - t;
+    if (rem > 0) KD_F8_STEP(0, xa, xb, ya, yb, PartT)
+    if (rem > 1) KD_F8_STEP(1, ya, yb, xa, xb, PartT)
+    if (rem > 2) KD_F8_STEP(2, xa, xb, ya, yb, PartT)
+#undef KD_F8_STEP
+#undef KD_F8_SYNC
+#undef KD_SB
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    // ---- epilogue: per-row scales of the tile into LDS past the image, per-lane column scales
+    float alpha = p.alpha;
+    if (p.alpha_dev) alpha *= *p.alpha_dev;
+    float* sa_l = (float*)(smem + F8_EPI);
+    if (tid < 256) sa_l[tid] = (m0 + tid < p.M) ? p.sa[m0 + tid] : 0.f;
+    float sbv[4], bcol[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int lc = cb + 32 * j + lr32;
+        const int gcol = glu ? (lc < 128 ? nb + lc : p.glu + nb + lc - 128) : n0 + lc;
+        const bool in = gcol < p.N;
+        sbv[j] = in ? p.sb[gcol] : 0.f;
+        bcol[j] = (p.bias && in) ? (p.bias_f32 ? ((const float*)p.bias)[gcol] : (float)((const bf16*)p.bias)[gcol]) : 0.f;
+    }
+    __syncthreads();
+    if (glu) {
+        f8_to_lds<KD_ACT_NONE>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane);
+        __syncthreads();
+        const int I = p.glu;
+        const bool full = m0 + 256 <= p.M;
+        if (p.aux) {
+#pragma unroll 4
+            for (int idx = tid; idx < 256 * 32; idx += NTH8) {
+                const int lr = idx >> 5, c = idx & 31, row = m0 + lr;
+                if (!full && row >= p.M) continue;
+                const int col = c < 16 ? nb + c * 8 : I + nb + (c - 16) * 8;
+                *(bf16x8*)(p.aux + (int64_t)row * p.ld_aux + col) = *(const bf16x8*)(smem + lr * F8_RS + c * 16);
+            }
+        }
+#pragma unroll 4
+        for (int idx = tid; idx < 256 * 16; idx += NTH8) {
+            const int lr = idx >> 4, c = idx & 15, row = m0 + lr;
+            if (!full && row >= p.M) continue;
+            const bf16x8 g = *(const bf16x8*)(smem + lr * F8_RS + c * 16);
+            const bf16x8 u = *(const bf16x8*)(smem + lr * F8_RS + 256 + c * 16);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float gf = (float)g[e];
+                o[e] = (bf16)(gf / (1.f + __expf(-gf)) * (float)u[e]);
+            }
+            *(bf16x8*)((bf16*)p.C + (int64_t)row * p.ldc + nb + c * 8) = o;
+        }
+        return;
+    }
+    const bool full = m0 + 256 <= p.M && n0 + 256 <= p.N;
+    if (p.aux) {   // pre-activation (bf16) for a backward
+        f8_to_lds<KD_ACT_NONE>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane);
+        __syncthreads();
+        epi_flush<256, 256, NTH8, false, false, false>(p, smem, F8_RS, p.aux, p.ld_aux, m0, n0, tid, full);
+        __syncthreads();
+    }
+    switch (p.act) {
+        case KD_ACT_GELU_TANH: f8_to_lds<KD_ACT_GELU_TANH>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
+        case KD_ACT_GELU_ERF: f8_to_lds<KD_ACT_GELU_ERF>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
+        case KD_ACT_SILU: f8_to_lds<KD_ACT_SILU>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
+        default: f8_to_lds<KD_ACT_NONE>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
+    }
+    __syncthreads();
+    epi_flush_sel<256, 256, NTH8, false>(p, smem, F8_RS, p.C, p.ldc, m0, n0, tid, full, p.resid != nullptr,
+                                        p.accumulate != 0);
+}
+
+// Row quantisation to e4m3 with one fp32 scale per row: scale = amax / 448 (1 for an
+// all-zero row), q = RNE_e4m3(clamp(x * (448 / amax), +-448)) — per-token activations and
+// per-output-channel weights of the fp8 GEMM. One workgroup per row, two passes over the
+// (L1/L2-resident) row.
+__global__ void __launch_bounds__(256) k_quant_rows_f8(const bf16* __restrict__ x, int64_t ldx, int K,
+                                                       uint8_t* __restrict__ q, int64_t ldq, float* __restrict__ scale) {
+    __shared__ float red[4];
+    const int64_t row = blockIdx.x;
+    const bf16* xr = x + row * ldx;
+    float amax = 0.f;
+    for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+        const bf16x8 v = *(const bf16x8*)(xr + k);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf((float)v[e]));
+    }
+    amax = wave_max(amax);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    const float inv = amax > 0.f ? 448.f / amax : 1.f;
+    if (threadIdx.x == 0) scale[row] = amax > 0.f ? amax / 448.f : 1.f;
+    uint8_t* qr = q + row * ldq;
+    for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+        const bf16x8 v = *(const bf16x8*)(xr + k);
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fminf(fmaxf((float)v[e] * inv, -448.f), 448.f);
+        uint32_t w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0u, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w0, true);
+        uint32_t w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0u, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
+        *(u32x2*)(qr + k) = (u32x2){w0, w1};
+    }
+}
+
 // split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
 // (alpha, alpha_dev, bias, aux, act, residual, accumulate), over the split tiles only
 // (linear tiles [tile0, tile0 + gridDim.x) of a BM x BN tiling, grouped order as in the
@@ -1112,6 +1394,61 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
 }  // namespace
 
 
+int launch_gemm_f8(const kd_gemm_desc* d, void* stream_) {
+    KD_CHECK_ARG(d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR, "gemm fp8: K-major operands only");
+    KD_CHECK_ARG(d->a_scale && d->b_scale, "gemm fp8: null a_scale / b_scale");
+    KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16, "gemm fp8: bf16 output");
+    KD_CHECK_ARG(d->split_k <= 1, "gemm fp8: no split-K");
+    KD_CHECK_ALIGN(d->A, 16, "gemm fp8: A must be 16-B aligned");
+    KD_CHECK_ALIGN(d->B, 16, "gemm fp8: B must be 16-B aligned");
+    KD_CHECK_SHAPE(d->K % 16 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0 && d->lda >= d->K && d->ldb >= d->K,
+                   "gemm fp8: K, lda, ldb must be multiples of 16 (lda, ldb >= K)");
+    KD_CHECK_SHAPE((uint64_t)256 * d->lda < 0x7FFFFFFFull && (uint64_t)256 * d->ldb < 0x7FFFFFFFull,
+                   "gemm fp8: leading dimension too large for 31-bit buffer records");
+    const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) &&
+                        (!d->residual || ((d->ldr % 8 == 0) && ((uintptr_t)d->residual % 16 == 0))) &&
+                        (!d->aux || ((d->ld_aux % 8 == 0) && ((uintptr_t)d->aux % 16 == 0)));
+    KD_CHECK_SHAPE(d->N % 8 == 0 && c_ok16, "gemm fp8: N % 8 == 0 and 16-B aligned C / residual / aux rows");
+    KD_CHECK_SHAPE(d->ldc >= (d->act == KD_ACT_SWIGLU ? d->N / 2 : d->N), "gemm fp8: ldc < N (N/2 for swiglu)");
+    KD_CHECK_SHAPE(!d->residual || d->ldr >= d->N, "gemm fp8: ldr < N");
+    KD_CHECK_SHAPE(!d->aux || d->ld_aux >= d->N, "gemm fp8: ld_aux < N");
+    GemmP p;
+    std::memset(&p, 0, sizeof(p));
+    p.A = (const bf16*)d->A; p.B = (const bf16*)d->B; p.C = d->C;
+    p.bias = d->bias; p.resid = (const bf16*)d->residual; p.aux = (bf16*)d->aux; p.alpha_dev = d->alpha_dev;
+    p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc; p.ldr = d->ldr; p.ld_aux = d->ld_aux;
+    p.M = d->M; p.N = d->N; p.K = d->K; p.alpha = d->alpha;
+    p.c_f32 = 0; p.accumulate = d->accumulate; p.bias_f32 = d->bias_dtype == KD_DTYPE_F32;
+    p.act = d->act; p.res_mod = d->residual_row_mod;
+    p.kchunk = d->K; p.sa = d->a_scale; p.sb = d->b_scale;
+    hipStream_t st = as_stream(stream_);
+    if (d->act == KD_ACT_SWIGLU) {
+        KD_CHECK_SHAPE(d->N % 256 == 0, "gemm fp8 swiglu: N = 2I needs I % 128 == 0");
+        KD_CHECK_ARG(!d->bias && !d->residual && !d->accumulate, "gemm fp8 swiglu: no bias / residual / accumulate");
+        p.glu = d->N / 2; p.act = KD_ACT_NONE;
+        hipLaunchKernelGGL((k_gemm8f8<4>), dim3(ceil_div(d->M, 256) * (d->N / 256)), dim3(NTH8), F8_LDS, st, p);
+        KD_LAUNCH_CHECK("k_gemm8f8<swiglu>");
+        return KD_OK;
+    }
+    hipLaunchKernelGGL((k_gemm8f8<0>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256)), dim3(NTH8), F8_LDS, st, p);
+    KD_LAUNCH_CHECK("k_gemm8f8");
+    return KD_OK;
+}
+
+int launch_quant_rows_f8(const void* x, int64_t ldx, int R, int K, void* q, int64_t ldq, float* scale, void* stream) {
+    KD_CHECK_ARG(x && q && scale, "quant_rows_fp8: null pointer");
+    KD_CHECK_SHAPE(R >= 0 && K > 0 && K % 16 == 0 && ldx >= K && ldq >= K && ldx % 8 == 0 && ldq % 8 == 0,
+                   "quant_rows_fp8: K % 16 == 0, ldx / ldq >= K and multiples of 8");
+    KD_CHECK_ALIGN(x, 16, "quant_rows_fp8: x must be 16-B aligned");
+    KD_CHECK_ALIGN(q, 8, "quant_rows_fp8: q must be 8-B aligned");
+    if (R == 0) return KD_OK;
+    hipLaunchKernelGGL(k_quant_rows_f8, dim3(R), dim3(256), 0, as_stream(stream), (const bf16*)x, ldx, K, (uint8_t*)q, ldq,
+                       scale);
+    KD_LAUNCH_CHECK("k_quant_rows_f8");
+    return KD_OK;
+}
+
+
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d != nullptr, "gemm: null descriptor");
     KD_CHECK_ARG(d->A && d->B && d->C, "gemm: null operand");
@@ -1119,6 +1456,8 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->a_layout == KD_LAYOUT_K_MAJOR || d->a_layout == KD_LAYOUT_MN_MAJOR, "gemm: a_layout");
     KD_CHECK_ARG(d->b_layout == KD_LAYOUT_K_MAJOR || d->b_layout == KD_LAYOUT_MN_MAJOR, "gemm: b_layout");
     KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16 || d->c_dtype == KD_DTYPE_F32, "gemm: c_dtype");
+    KD_CHECK_ARG(d->ab_dtype == KD_DTYPE_BF16 || d->ab_dtype == KD_DTYPE_FP8_E4M3, "gemm: ab_dtype");
+    if (d->ab_dtype == KD_DTYPE_FP8_E4M3) return launch_gemm_f8(d, stream_);
     KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_SWIGLU, "gemm: act");
     KD_CHECK_ARG(d->act == KD_ACT_NONE || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
                                           d->c_dtype == KD_DTYPE_BF16),

@@ -49,11 +49,11 @@ int gemm_timed(const kd_gemm_desc* d, void* stream) {
     r.key += ":" + std::to_string(d->M) + "x" + std::to_string(d->N) + "x" + std::to_string(d->K) + ":" +
              (d->c_dtype == KD_DTYPE_F32 ? "f32" : "bf16") + (d->accumulate ? ":acc" : "");
     r.flops = 2.0 * d->M * d->N * d->K;
-    hipEventCreate(&r.e0);
-    hipEventCreate(&r.e1);
-    hipEventRecord(r.e0, as_stream(stream));
+    (void)hipEventCreate(&r.e0);
+    (void)hipEventCreate(&r.e1);
+    (void)hipEventRecord(r.e0, as_stream(stream));
     const int st = launch_gemm(d, stream);
-    hipEventRecord(r.e1, as_stream(stream));
+    (void)hipEventRecord(r.e1, as_stream(stream));
     std::lock_guard<std::mutex> g(g_timer_mu);
     g_timer.push_back(r);
     return st;
@@ -142,6 +142,25 @@ std::vector<Spec> make_specs(const Cfg& C, int64_t* total) {
     return S;
 }
 
+// The fp8 linears: every 2-D weight a GEMM reads as its B operand, i.e. all but the
+// patch-embedding conv (K = 3*14*14, bf16), the position embedding (a residual) and
+// embed_tokens (a gather; the tied student head is never fp8).  Scales follow in spec order.
+std::vector<int64_t> fp8_scale_offsets(const Cfg& C, const std::vector<Spec>& S, int64_t* total) {
+    std::vector<int64_t> off(S.size(), -1);
+    int64_t n = 0;
+    for (size_t i = 0; i < S.size(); ++i) {
+        const std::string& nm = S[i].name;
+        if (S[i].cols == 0 || nm.find("patch_embedding") != std::string::npos ||
+            nm.find("position_embedding") != std::string::npos || nm.find("embed_tokens") != std::string::npos)
+            continue;
+        off[i] = n;
+        n += S[i].rows;
+    }
+    (void)C;
+    *total = n;
+    return off;
+}
+
 bool cfg_ok(const kd_model_config* c) {
     return c && c->v_hidden > 0 && c->v_heads > 0 && c->v_hidden % c->v_heads == 0 && c->v_layers >= 0 &&
            c->v_patch > 0 && c->v_image >= c->v_patch && c->t_hidden > 0 && c->t_heads > 0 &&
@@ -167,6 +186,12 @@ struct kd_model {
     int lane_split_k = 0;     // split-K of the lane's GEMMs (KD_WGRAD_SPLIT_K; 0 = cost model)
     std::vector<hipEvent_t> ev_pool;
     size_t ev_next = 0;
+    // fp8 teacher (BASELINE config c4): e4m3 copies of the linear weights (same element
+    // offsets as `w`) and one fp32 scale per weight row at soff[param]; nullptr = bf16 path
+    const uint8_t* f8q = nullptr;
+    const float* f8s = nullptr;
+    std::vector<int64_t> soff;   // per spec: first scale index (-1: not an fp8 linear)
+    int64_t n_scales = 0;
     // spec indices
     int i_patch_w = 0, i_patch_b = 1, i_pos = 2, i_vis0 = 3, i_post_w, i_post_b, i_p1w, i_p1b, i_p2w, i_p2b, i_newline,
         i_embed, i_lm0, i_norm, i_head;
@@ -179,7 +204,7 @@ struct kd_model {
     hipEvent_t event() {   // reused round-robin: a wait is enqueued long before its event comes round again
         if (ev_pool.empty()) {
             ev_pool.resize(1024);
-            for (auto& e : ev_pool) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+            for (auto& e : ev_pool) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         }
         return ev_pool[ev_next++ % ev_pool.size()];
     }
@@ -260,12 +285,12 @@ struct Lane {
     void* ws;
     void begin() {   // lane waits for everything queued on the main stream so far
         hipEvent_t e = m->event();
-        hipEventRecord(e, main);
-        hipStreamWaitEvent(lane, e, 0);
+        (void)hipEventRecord(e, main);
+        (void)hipStreamWaitEvent(lane, e, 0);
     }
     hipEvent_t end() {
         hipEvent_t e = m->event();
-        hipEventRecord(e, lane);
+        (void)hipEventRecord(e, lane);
         return e;
     }
     // dW[N_out, K_in] (fp32 +=) = dy[M, N_out]^T x[M, K_in]
@@ -281,7 +306,7 @@ struct Lane {
     }
 };
 inline void wait(hipStream_t s, hipEvent_t e) {
-    if (e) hipStreamWaitEvent(s, e, 0);
+    if (e) (void)hipStreamWaitEvent(s, e, 0);
 }
 
 // ------------------------------------------------------ forward buffer plan ----
@@ -304,6 +329,8 @@ struct FwdPlan {
     bf16 *x_lm_last, *qkv_t;
     bf16* x_lm[2];
     float* rf;
+    uint8_t* qa;    // fp8 path: the current linear's activation rows, e4m3 [M][K] ...
+    float* sa;      // ... and their scales [M]
     void* splitk;
     size_t bytes;
 };
@@ -409,12 +436,45 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void*
     }
     P.rf = A.take<float>(M);
     (void)hd;
+    if (m->f8q) {   // the widest linear input of either tower
+        const int64_t R = M > NT ? M : NT;
+        int64_t Kx = D > Iv ? D : Iv;
+        for (int64_t k : {H, qd, TI}) Kx = Kx > k ? Kx : k;
+        P.qa = A.take<uint8_t>(R * Kx);
+        P.sa = A.take<float>(R);
+    } else {
+        P.qa = nullptr;
+        P.sa = nullptr;
+    }
     P.splitk = A.take<char>(SPLITK_WS);
     P.bytes = A.off + 256;
     return P;
 }
 
 // ------------------------------------------------------------------ forward ----
+// One nn.Linear of the forward: the bf16 MFMA GEMM, or on the fp8 path (weights bound by
+// kd_model_set_fp8) the activation rows quantised to e4m3 with a per-row scale and the fp8
+// GEMM against the e4m3 weight rows and their per-channel scales (kdstep.h, fp8 path).
+int lin(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int N, int K, const bf16* x, int64_t ldx, int widx,
+        void* out, int64_t ldo, const GemmArgs& g) {
+    if (!m->f8q || m->soff[widx] < 0)
+        return gemm(s, P.splitk, M, N, K, km(x, ldx), km(m->W(widx), K), out, ldo, g);
+    KD_TRY(launch_quant_rows_f8(x, ldx, M, K, P.qa, K, P.sa, s));
+    kd_gemm_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.M = M; d.N = N; d.K = K;
+    d.a_layout = KD_LAYOUT_K_MAJOR; d.b_layout = KD_LAYOUT_K_MAJOR;
+    d.A = P.qa; d.lda = K; d.B = m->f8q + m->off(widx); d.ldb = K;
+    d.C = out; d.ldc = ldo; d.c_dtype = KD_DTYPE_BF16;
+    d.accumulate = g.accumulate; d.alpha = 1.f;
+    d.bias = g.bias; d.bias_dtype = g.bias_f32 ? KD_DTYPE_F32 : KD_DTYPE_BF16;
+    d.act = g.act; d.residual = g.residual; d.ldr = g.ldr; d.aux = g.aux; d.ld_aux = g.ld_aux;
+    d.residual_row_mod = g.residual_row_mod;
+    d.split_k = 1;
+    d.ab_dtype = KD_DTYPE_FP8_E4M3; d.a_scale = P.sa; d.b_scale = m->f8s + m->soff[widx];
+    return gemm_timed(&d, s);
+}
+
 int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dtype, int NI, int save, void* post,
                    hipStream_t s) {
     const Cfg& C = m->C;
@@ -439,7 +499,7 @@ int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dty
         {
             GemmArgs g;
             g.bias = m->W(m->vis(i, VQB));
-            KD_TRY(gemm(s, P.splitk, NT, 3 * D, D, km(b.h, D), km(m->W(m->vis(i, VQW)), D), P.qkv_v, 3 * D, g));
+            KD_TRY(lin(m, P, s, NT, 3 * D, D, b.h, D, m->vis(i, VQW), P.qkv_v, 3 * D, g));
         }
         KD_TRY(launch_qkv_split(P.qkv_v, 3 * D, b.q, b.k, b.v, nullptr, nullptr, NI, np, c.v_heads, c.v_heads, hd, hdp, s));
         {
@@ -451,7 +511,7 @@ int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dty
             g.bias = m->W(m->vis(i, VOB));
             g.residual = b.x;
             g.ldr = D;
-            KD_TRY(gemm(s, P.splitk, NT, D, D, km(b.o, D), km(m->W(m->vis(i, VOW)), D), b.x_mid, D, g));
+            KD_TRY(lin(m, P, s, NT, D, D, b.o, D, m->vis(i, VOW), b.x_mid, D, g));
         }
         KD_TRY(launch_norm_fwd(0, b.x_mid, D, m->W(m->vis(i, VLN2W)), m->W(m->vis(i, VLN2B)), b.h2, D,
                                save ? b.m2 : nullptr, save ? b.r2 : nullptr, NT, D, c.v_eps, s));
@@ -461,14 +521,14 @@ int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dty
             g.act = KD_ACT_GELU_TANH;
             g.aux = save ? b.pre : nullptr;
             g.ld_aux = Iv;
-            KD_TRY(gemm(s, P.splitk, NT, Iv, D, km(b.h2, D), km(m->W(m->vis(i, VFC1W)), D), b.u, Iv, g));
+            KD_TRY(lin(m, P, s, NT, Iv, D, b.h2, D, m->vis(i, VFC1W), b.u, Iv, g));
         }
         {
             GemmArgs g;
             g.bias = m->W(m->vis(i, VFC2B));
             g.residual = b.x_mid;
             g.ldr = D;
-            KD_TRY(gemm(s, P.splitk, NT, D, Iv, km(b.u, Iv), km(m->W(m->vis(i, VFC2W)), Iv), x_out, D, g));
+            KD_TRY(lin(m, P, s, NT, D, Iv, b.u, Iv, m->vis(i, VFC2W), x_out, D, g));
         }
     }
     if (post)
@@ -490,7 +550,7 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
         {
             GemmArgs g;
             g.bias = m->W(m->lm(i, LQB));
-            KD_TRY(gemm(s, P.splitk, M, qd + 2 * kvd, H, km(b.h, H), km(m->W(m->lm(i, LQW)), H), P.qkv_t, qd + 2 * kvd, g));
+            KD_TRY(lin(m, P, s, M, qd + 2 * kvd, H, b.h, H, m->lm(i, LQW), P.qkv_t, qd + 2 * kvd, g));
         }
         void* k = kv_k ? kv_k[i] : b.k;
         void* v = kv_v ? kv_v[i] : b.v;
@@ -503,7 +563,7 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
             GemmArgs g;
             g.residual = b.x;
             g.ldr = H;
-            KD_TRY(gemm(s, P.splitk, M, H, qd, km(b.o, qd), km(m->W(m->lm(i, LOW)), qd), b.x_mid, H, g));
+            KD_TRY(lin(m, P, s, M, H, qd, b.o, qd, m->lm(i, LOW), b.x_mid, H, g));
         }
         KD_TRY(launch_norm_fwd(1, b.x_mid, H, m->W(m->lm(i, LPOSTW)), nullptr, b.h2, H, nullptr, save ? b.r2 : nullptr, M,
                                H, c.t_eps, s));
@@ -512,17 +572,17 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
             g.act = KD_ACT_SWIGLU;
             g.aux = save ? b.gu : nullptr;
             g.ld_aux = 2 * TI;
-            KD_TRY(gemm(s, P.splitk, M, 2 * TI, H, km(b.h2, H), km(m->W(m->lm(i, LGW)), H), b.a, TI, g));
+            KD_TRY(lin(m, P, s, M, 2 * TI, H, b.h2, H, m->lm(i, LGW), b.a, TI, g));
         } else {
             GemmArgs g;
-            KD_TRY(gemm(s, P.splitk, M, 2 * TI, H, km(b.h2, H), km(m->W(m->lm(i, LGW)), H), b.gu, 2 * TI, g));
+            KD_TRY(lin(m, P, s, M, 2 * TI, H, b.h2, H, m->lm(i, LGW), b.gu, 2 * TI, g));
             KD_TRY(launch_swiglu_fwd(b.gu, 2 * TI, b.a, TI, M, TI, s));
         }
         {
             GemmArgs g;
             g.residual = b.x_mid;
             g.ldr = H;
-            KD_TRY(gemm(s, P.splitk, M, H, TI, km(b.a, TI), km(m->W(m->lm(i, LDW)), TI), x_out, H, g));
+            KD_TRY(lin(m, P, s, M, H, TI, b.a, TI, m->lm(i, LDW), x_out, H, g));
         }
     }
     return launch_norm_fwd(1, P.x_lm_last, H, m->W(m->i_norm), nullptr, hn, H, nullptr, save ? P.rf : nullptr, M, H,
@@ -805,13 +865,14 @@ int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad
     m->i_lm0 = m->i_embed + 1;
     m->i_norm = m->i_lm0 + cfg->t_layers * kd::LNF;
     m->i_head = cfg->t_tie ? m->i_embed : m->i_norm + 1;
+    m->soff = kd::fp8_scale_offsets(m->C, m->specs, &m->n_scales);
     *out = m;
     return KD_OK;
 }
 
 void kd_model_destroy(kd_model* m) {
     if (!m) return;
-    for (auto& e : m->ev_pool) hipEventDestroy(e);
+    for (auto& e : m->ev_pool) (void)hipEventDestroy(e);
     delete m;
 }
 
@@ -821,6 +882,32 @@ int kd_model_set_trainable(kd_model* m, int vision, int projector, int language)
     m->train_vision = vision != 0;
     m->train_projector = projector != 0;
     m->train_language = language != 0;
+    return KD_OK;
+}
+
+int64_t kd_model_fp8_scale_count(const kd_model* m) { return m ? m->n_scales : -1; }
+
+int kd_model_quantize_fp8(const kd_model* m, void* q, float* scales, void* stream) {
+    KD_CHECK_ARG(m && q && scales, "kd_model_quantize_fp8: null pointer");
+    KD_CHECK_ALIGN(q, 16, "kd_model_quantize_fp8: q must be 16-B aligned");
+    for (size_t i = 0; i < m->specs.size(); ++i) {
+        if (m->soff[i] < 0) continue;
+        const kd::Spec& sp = m->specs[i];
+        KD_CHECK_SHAPE(sp.offset % 16 == 0 && sp.cols % 16 == 0, "kd_model_quantize_fp8: " + sp.name +
+                                                                     " is not 16-B aligned / K % 16 != 0");
+        KD_TRY(kd::launch_quant_rows_f8(m->W((int)i), sp.cols, (int)sp.rows, (int)sp.cols, (uint8_t*)q + sp.offset,
+                                        sp.cols, scales + m->soff[i], stream));
+    }
+    return KD_OK;
+}
+
+int kd_model_set_fp8(kd_model* m, const void* q, const float* scales) {
+    KD_CHECK_ARG(m, "kd_model_set_fp8: null model");
+    KD_CHECK_ARG((q == nullptr) == (scales == nullptr), "kd_model_set_fp8: q and scales go together");
+    KD_CHECK_ARG(!q || !m->g, "kd_model_set_fp8: fp8 weights are for a frozen (no-grad) model, e.g. the teacher");
+    KD_CHECK_ALIGN(q, 16, "kd_model_set_fp8: q must be 16-B aligned");
+    m->f8q = (const uint8_t*)q;
+    m->f8s = scales;
     return KD_OK;
 }
 
@@ -856,10 +943,10 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
         g.act = c.projector_act;
         g.aux = save ? P.ppre : nullptr;
         g.ld_aux = H;
-        KD_TRY(gemm(s, P.splitk, NT, H, D, km(P.x_vis_last, D), km(m->W(m->i_p1w), D), P.z, H, g));
+        KD_TRY(lin(m, P, s, NT, H, D, P.x_vis_last, D, m->i_p1w, P.z, H, g));
         GemmArgs g2;
         g2.bias = m->W(m->i_p2b);
-        KD_TRY(gemm(s, P.splitk, NT, H, H, km(P.z, H), km(m->W(m->i_p2w), H), P.feats, H, g2));
+        KD_TRY(lin(m, P, s, NT, H, H, P.z, H, m->i_p2w, P.feats, H, g2));
     }
     // inputs_embeds: token embeddings + the packed image features (masked_scatter)
     bf16* emb = c.t_layers ? P.ll[0].x : P.x_lm_last;
@@ -867,7 +954,7 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
     KD_TRY(lm_forward(m, P, rope_cos, rope_sin, B, L, save, hn, kv_k, kv_v, s));
     if (logits) {
         GemmArgs g;
-        KD_TRY(gemm(s, P.splitk, M, c.t_vocab, H, km(hn, H), km(m->W(m->i_head), H), logits, c.t_vocab, g));
+        KD_TRY(lin(m, P, s, M, c.t_vocab, H, (const bf16*)hn, H, m->i_head, logits, c.t_vocab, g));
     }
     return KD_OK;
 }
@@ -890,7 +977,7 @@ int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids
     // work the caller queued on the lane before this call (the lm_head wgrad into a tied
     // embedding) precedes the embedding backward below
     hipEvent_t entry = m->event();
-    hipEventRecord(entry, lane.lane);
+    (void)hipEventRecord(entry, lane.lane);
     const int NI = B * tiles, NT = NI * m->C.np(), M = B * L, H = c.t_hidden, D = c.v_hidden;
     KD_TRY(lm_backward(m, F, P, rope_cos, rope_sin, B, L, dhn, lane, s, on_layer_done, user));
     wait(s, entry);
@@ -918,8 +1005,8 @@ int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids
     if (need_vision) KD_TRY(vision_backward(m, F, P, NI, dpost, lane, s));
     // the caller reads the grads (and reuses these buffers) after this: join the lane
     hipEvent_t done = m->event();
-    hipEventRecord(done, lane.lane);
-    hipStreamWaitEvent(s, done, 0);
+    (void)hipEventRecord(done, lane.lane);
+    (void)hipStreamWaitEvent(s, done, 0);
     KD_LAUNCH_CHECK("kd_model_backward");
     return KD_OK;
 }
@@ -937,7 +1024,7 @@ int kd_timer_read(int i, char* key, int key_cap, double* flops, float* ms) {
     auto& r = kd::g_timer[i];
     if (hipEventSynchronize(r.e1) != hipSuccess) return kd::fail(KD_ERR_LAUNCH, "kd_timer_read: event sync failed");
     float t = 0.f;
-    hipEventElapsedTime(&t, r.e0, r.e1);
+    (void)hipEventElapsedTime(&t, r.e0, r.e1);
     if (key && key_cap > 0) {
         std::strncpy(key, r.key.c_str(), key_cap - 1);
         key[key_cap - 1] = 0;
@@ -950,8 +1037,8 @@ int kd_timer_read(int i, char* key, int key_cap, double* flops, float* ms) {
 void kd_timer_reset(void) {
     std::lock_guard<std::mutex> g(kd::g_timer_mu);
     for (auto& r : kd::g_timer) {
-        hipEventDestroy(r.e0);
-        hipEventDestroy(r.e1);
+        (void)hipEventDestroy(r.e0);
+        (void)hipEventDestroy(r.e1);
     }
     kd::g_timer.clear();
 }

@@ -190,7 +190,7 @@ class _KDBase(_Base):
 
     def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1,
                  seed_teacher: int = 1, seed_student: int = 2, state_dict=None, loss_group_size: int | None = None,
-                 accumulate_grad_batches: int = 1, **_ignored):
+                 accumulate_grad_batches: int = 1, teacher_fp8: bool = False, **_ignored):
         super().__init__()
         self.phase = phase
         self.learning_rate = learning_rate
@@ -239,6 +239,11 @@ class _KDBase(_Base):
             self._dist.broadcast(self.student_model.P.flat, src=0)
             self.student_model.P.master.copy_(self.student_model.P.flat.float())
             self._gsync = GradSync(self._dist, self.student_model.P.grad)
+        # fp8 (e4m3) teacher weights, quantised once after the broadcast (BASELINE config c4;
+        # the reference loads the teacher fp16, DT:43-48)
+        self.teacher_fp8 = bool(teacher_fp8) and self.teacher_model is not None
+        if self.teacher_fp8:
+            self.teacher_model.enable_fp8()
 
     # ------------------------------------------------------------- freezing ----
     def _trainable_range(self):
@@ -442,6 +447,8 @@ class _KDBase(_Base):
         self.student_model.P.load_state_dict(sd, prefix=self.ckpt_student_prefix)
         if self.teacher_model is not None and any(k.startswith("teacher_model.") for k in sd):
             self.teacher_model.P.load_state_dict(sd, prefix="teacher_model.")
+            if getattr(self.teacher_model, "fp8", False):
+                self.teacher_model.enable_fp8()   # re-quantise the new weights
 
     def _hparams(self):
         return {"model_name_student": self.model_name_student, "model_name_teacher": self.model_name_teacher,

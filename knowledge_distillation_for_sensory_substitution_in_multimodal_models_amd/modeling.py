@@ -360,6 +360,7 @@ class LlavaOnevisionModel:
         NV.call("kd_model_create", C.byref(self._ncfg), self.P.flat.data_ptr(),
                 self.P.grad.data_ptr() if trainable else None, C.byref(h))
         self._h = h
+        self.fp8 = False
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -402,6 +403,28 @@ class LlavaOnevisionModel:
                                                                                       device=self.device))
         maps, lens = self._maps[key]
         return ops.image_src_map(input_ids, self.cfg.image_token_id, maps, lens, self.err)
+
+    # -- fp8 teacher (BASELINE config c4)
+    def enable_fp8(self):
+        """Quantise every linear weight to e4m3 with per-output-channel scales (kd_model_quantize_fp8,
+        on the current stream) and run the forward's linears on the fp8 GEMM from now on
+        (per-token activation scales).  Frozen models only; re-run after the weights change."""
+        if self.P.trainable:
+            raise RuntimeError("fp8 weights are for the frozen teacher (no grad buffer)")
+        lib = NV.lib()
+        n = lib.kd_model_fp8_scale_count(self._h)
+        self._f8q = torch.empty(self.P.numel, dtype=torch.uint8, device=self.device)
+        self._f8s = torch.empty(max(n, 1), dtype=torch.float32, device=self.device)
+        NV.call("kd_model_quantize_fp8", self._h, self._f8q.data_ptr(), self._f8s.data_ptr(), ops._stream())
+        NV.call("kd_model_set_fp8", self._h, self._f8q.data_ptr(), self._f8s.data_ptr())
+        self._ws = {}   # the forward workspace gains the activation-quantisation buffers
+        self.fp8 = True
+
+    def disable_fp8(self):
+        NV.call("kd_model_set_fp8", self._h, None, None)
+        self._f8q = self._f8s = None
+        self._ws = {}
+        self.fp8 = False
 
     def _workspace(self, key, nbytes):
         """One cached workspace per call shape: a save=1 forward's workspace holds the

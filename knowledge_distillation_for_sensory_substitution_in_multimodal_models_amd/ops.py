@@ -261,6 +261,48 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
     return out
 
 
+# ------------------------------------------------------------------ fp8 path ----
+def quant_rows_fp8(x: torch.Tensor, q: torch.Tensor | None = None, scale: torch.Tensor | None = None):
+    """bf16 [R, K] -> (e4m3 bytes uint8 [R, K], fp32 scale [R]): per-row amax / 448 scaling
+    (kd_quant_rows_fp8; the fp8 teacher's activations and weights)."""
+    _require(x, torch.bfloat16, "quant_rows_fp8.x")
+    R, K = x.shape
+    if x.stride(1) != 1:
+        raise RuntimeError("quant_rows_fp8: rows must be contiguous")
+    q = q if q is not None else torch.empty((R, K), dtype=torch.uint8, device=x.device)
+    scale = scale if scale is not None else torch.empty(R, dtype=torch.float32, device=x.device)
+    NV.call("kd_quant_rows_fp8", x.data_ptr(), x.stride(0), R, K, q.data_ptr(), q.stride(0), scale.data_ptr(),
+            _stream())
+    return q, scale
+
+
+def gemm_fp8(qa: torch.Tensor, sa: torch.Tensor, qb: torch.Tensor, sb: torch.Tensor, out: torch.Tensor | None = None,
+             *, bias=None, act=None, residual=None, aux=None, alpha: float = 1.0) -> torch.Tensor:
+    """out[M, N] = epilogue(alpha * sa[m] * sb[n] * qa[M, K] @ qb[N, K]^T), e4m3 operands (uint8
+    bytes, K-major), bf16 out (kd_gemm, ab_dtype = KD_DTYPE_FP8_E4M3)."""
+    M, K = qa.shape
+    N, K2 = qb.shape
+    if K != K2 or qa.dtype != torch.uint8 or qb.dtype != torch.uint8:
+        raise RuntimeError("gemm_fp8: uint8 (e4m3) operands with equal K")
+    if out is None:
+        out = torch.empty((M, N // 2 if act == "swiglu" else N), dtype=torch.bfloat16, device=qa.device)
+    d = NV.KdGemmDesc()
+    d.M, d.N, d.K, d.a_layout, d.b_layout = M, N, K, NV.KD_LAYOUT_K_MAJOR, NV.KD_LAYOUT_K_MAJOR
+    d.A, d.lda, d.B, d.ldb = qa.data_ptr(), qa.stride(0), qb.data_ptr(), qb.stride(0)
+    d.C, d.ldc, d.c_dtype = out.data_ptr(), out.stride(0), NV.KD_DTYPE_BF16
+    d.alpha = float(alpha)
+    if bias is not None:
+        d.bias, d.bias_dtype = bias.data_ptr(), _DT[bias.dtype]
+    d.act = ACTS[act]
+    if residual is not None:
+        d.residual, d.ldr = residual.data_ptr(), residual.stride(0)
+    if aux is not None:
+        d.aux, d.ld_aux = aux.data_ptr(), aux.stride(0)
+    d.ab_dtype, d.a_scale, d.b_scale = NV.KD_DTYPE_FP8_E4M3, sa.data_ptr(), sb.data_ptr()
+    NV.call("kd_gemm", C.byref(d), _stream())
+    return out
+
+
 # ---------------------------------------------------------------- attention ----
 def attn_fwd(q, k, v, hd: int, causal: bool, want_lse: bool = True):
     """q [B,H,S,hdp], k/v [B,HKV,S,hdp] bf16 -> (o [B,S,H,hd] bf16, lse [B,H,S] fp32 | None)."""

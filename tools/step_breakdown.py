@@ -1,5 +1,6 @@
-"""Per-kernel time of one step of a rocprofv3 kernel trace (steps delimited by the patchify
-kernel, which runs twice per step: teacher and student towers).
+"""Per-kernel time of one training step of a rocprofv3 kernel trace: the window between the
+last two AdamW launches (one per optimizer step; the teacher-forward rate pass bench.py
+runs after the timed steps has no AdamW).
     python tools/step_breakdown.py run_results.db [top]"""
 import collections
 import re
@@ -9,8 +10,8 @@ import sys
 c = sqlite3.connect(sys.argv[1])
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 rows = sorted(c.execute("select name, start, end from kernels").fetchall(), key=lambda r: r[1])
-pat = [r[1] for r in rows if "k_patchify" in r[0]]
-a, b = pat[-4], pat[-2]
+opt = [r[1] for r in rows if "k_adamw" in r[0]]
+a, b = opt[-2], opt[-1]
 rr = [r for r in rows if a <= r[1] < b]
 agg = collections.defaultdict(lambda: [0, 0])
 for n, s, e in rr:
