@@ -12,7 +12,8 @@ architectures (no checkpoints are reachable offline).
 
 Configs (BASELINE.json): c1 = logit-based LoCa (T=1) bs 4 per GPU [default];
 c2 = feature-based (NT-Xent + KL) bs 8 per GPU; c3 = double-trouble phase 2 (LoCa, ViT
-frozen) bs 8 per GPU; c4 = double-trouble phase 3 bs 8 per GPU (bf16 teacher).
+frozen) bs 8 per GPU; c4 = double-trouble phase 3 bs 8 per GPU with the fp8 (e4m3) teacher
+(per-channel weight / per-token activation scales, fp8 MFMA GEMMs; --teacher-bf16 for bf16).
 Per-GPU work is fixed as N grows (weak scaling); value = samples of all ranks / max time.
 """
 from __future__ import annotations
@@ -29,13 +30,15 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 PEAK_BF16_TFLOPS = 2500.0      # dense bf16 MFMA peak, MI355X_MICROARCH.md
+PEAK_FP8_TFLOPS = 5000.0       # dense (block-scaled) e4m3 MFMA peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
 CONFIGS = {
     "c1": dict(kind="lb", phase=0, batch=4, desc="logit-based KD (LoCa, T=1), 7B->0.5B, 336x336"),
     "c2": dict(kind="fb", phase=0, batch=8, desc="feature-based KD (NT-Xent + KL), 7B->0.5B, 336x336"),
     "c3": dict(kind="dt", phase=2, batch=8, desc="double-trouble phase 2 (LoCa + CE, ViT frozen)"),
-    "c4": dict(kind="dt", phase=3, batch=8, desc="double-trouble phase 3 (0.8 LoCa + CE)"),
+    "c4": dict(kind="dt", phase=3, batch=8, teacher_fp8=True,
+               desc="double-trouble phase 3 (0.8 LoCa + CE), fp8 (e4m3) teacher"),
 }
 
 # algorithmic FLOPs per sample, L = 1536, 2 tiles
@@ -57,15 +60,15 @@ def step_tflops_per_sample(kind: str, phase: int) -> float:
     return (teacher + s_fwd + s_bwd) / 1e12
 
 
-def build(cfg, dev):
+def build(cfg, dev, teacher_fp8=False):
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
     S, T = "llava-hf/llava-onevision-qwen2-0.5b-ov-hf", "llava-hf/llava-onevision-qwen2-7b-ov-hf"
     if cfg["kind"] == "lb":
-        m = K.LogitBasedKD(S, T)
+        m = K.LogitBasedKD(S, T, teacher_fp8=teacher_fp8)
     elif cfg["kind"] == "fb":
-        m = K.FeatureBasedKD(S, T)
+        m = K.FeatureBasedKD(S, T, teacher_fp8=teacher_fp8)
     else:
-        m = K.OnlineKnowledgeDistillationLLavaOneVision(S, T, phase=cfg["phase"])
+        m = K.OnlineKnowledgeDistillationLLavaOneVision(S, T, phase=cfg["phase"], teacher_fp8=teacher_fp8)
         if cfg["phase"] == 2:
             m.freeze_student_vision_layers()
         if cfg["phase"] == 1:
@@ -228,8 +231,37 @@ def teacher_forward_rate(m, batch, reps=3):
     vit = 2 * 1458 * 395.8e6 + 4 * 2 * 729 ** 2 * 1152 * 26 + 2 * 1458 * 0.677e6
     fl = B * (vit + 2 * 1458 * (1152 * 3584 + 3584 * 3584) + 2 * L * 7070.6e6 + 2 * L * L * 3584 * 28)
     tf = fl / (ms * 1e-3) / 1e12
-    return dict(ms=round(ms, 2), tflop=round(fl / 1e12, 2), tflops=round(tf, 1), frac_of_peak=round(tf / PEAK_BF16_TFLOPS, 4),
-                target_frac=0.40, measured="min of 3 serialized teacher forwards, HIP events on the main stream")
+    out = dict(ms=round(ms, 2), tflop=round(fl / 1e12, 2), tflops=round(tf, 1), frac_of_peak=round(tf / PEAK_BF16_TFLOPS, 4),
+               target_frac=0.40, measured="min of 3 serialized teacher forwards, HIP events on the main stream")
+    if getattr(m.teacher_model, "fp8", False):
+        out.update(dtype="fp8 e4m3 linears (bf16 attention / norms)", frac_of_fp8_peak=round(tf / PEAK_FP8_TFLOPS, 4))
+    return out
+
+
+def fp8_teacher_delta(m, batch):
+    """c4: the same batch through the fp8 teacher and through the bf16 teacher (same weights):
+    teacher-logit rel-L2 / cosine and each loss term (the fp8 teacher's stated tolerance)."""
+    import torch
+    res = {}
+    m.keep_logits = True
+    for name in ("fp8", "bf16"):
+        if name == "bf16":
+            m.teacher_model.disable_fp8()
+        with torch.no_grad():
+            m.forward(batch)
+        torch.cuda.synchronize()
+        res[name] = (m.last_terms.tolist(), m.last_logits[1].float())
+        m.last_logits = None
+    m.keep_logits = False
+    m.teacher_model.enable_fp8()
+    (tf, lf), (tb, lb) = res["fp8"], res["bf16"]
+    rel = float((lf - lb).norm() / lb.norm())
+    cos = float((lf * lb).sum() / (lf.norm() * lb.norm()))
+    del lf, lb, res
+    names = ("kd_term", "student_ce", "teacher_ce", "total")
+    return dict(teacher_logits_rel_l2=round(rel, 5), teacher_logits_cosine=round(cos, 6),
+                terms={n: dict(fp8=a, bf16=b, rel=abs(a - b) / abs(b) if b else None) for n, a, b in zip(names, tf, tb)},
+                tolerance="tests/test_fp8_gpu.py: rel-L2 <= 0.15, cosine >= 0.99, KD term rel <= 0.15")
 
 
 def main():
@@ -246,6 +278,7 @@ def main():
     ap.add_argument("--serial", action="store_true",
                     help="student forward on the main stream (no overlap with the teacher forward)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
+    ap.add_argument("--teacher-bf16", action="store_true", help="c4 with the bf16 teacher instead of fp8")
     a = ap.parse_args()
 
     import torch
@@ -261,7 +294,8 @@ def main():
     B = a.batch or cfg["batch"]
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
-    m, opt = build(cfg, dev)
+    teacher_fp8 = bool(cfg.get("teacher_fp8")) and not a.teacher_bf16
+    m, opt = build(cfg, dev, teacher_fp8=teacher_fp8)
     m.concurrent_student = not a.serial
     # two synthetic batches, alternated, so every step's teacher forward is a fresh one
     batches = [synthetic_batch(B, dev, L=1536, seed=rank * 2 + j) for j in range(2)]
@@ -298,6 +332,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss_v = float(loss.item())
+    # host cost of enqueueing ONE step onto an idle GPU (in the timed loop the HIP queue is
+    # full and every launch waits for a slot, so host_enqueue tracks the GPU time)
+    torch.cuda.synchronize()
+    th = time.perf_counter()
+    step(a.warmup + a.steps + 5)
+    host_idle_ms = (time.perf_counter() - th) * 1e3
+    torch.cuda.synchronize()
     # ---- after the timed region: roofline pass (two steps with the student forward
     # serialized behind the teacher forward, every GEMM bracketed by HIP events on its launch
     # stream, so a kernel's duration is its own and not shared with a concurrent stream)
@@ -315,7 +356,7 @@ def main():
     tf_sample = step_tflops_per_sample(cfg["kind"], cfg["phase"])
     roof = None
     br = {}
-    for kind in ("gemm_kk_swiglu", "gemm_kk", "gemm_kn", "gemm_nn"):
+    for kind in ("gemm_kk_swiglu", "gemm_kk", "gemm_kn", "gemm_nn", "gemm_f8_swiglu", "gemm_f8"):
         s = ops.TIMER.summary(kind)
         if s:
             br[kind] = dict(launches=s["launches"], avg_us=round(s["avg_ms"] * 1e3, 2),
@@ -328,6 +369,7 @@ def main():
     # one launch per call, 28 + 24 calls per step) -- a kernel of its own, so the rocprofv3
     # kernel trace's average for it is directly comparable
     fwd = ops.TIMER.summary("gemm_kk_swiglu")
+    fwd8 = ops.TIMER.summary("gemm_f8_swiglu")
     traffic = None   # PMC HBM bytes per launch of that kernel (tools/pmc_bench.sh -> profiles/)
     for rd in ("r02", "r01"):
         tpath = REPO / "profiles" / rd / "pmc_traffic.json"
@@ -347,6 +389,16 @@ def main():
                     avg_launch_us=round(fwd["avg_ms"] * 1e3, 2),
                     measured="HIP events on the launch stream over 2 serialized steps after the timed region "
                              "(bench.py --serial under rocprofv3 gives the matching kernel trace)")
+    if fwd8:   # c4: the fp8 teacher's fused gate|up GEMM is the dominant kernel
+        ach = fwd8["flops"] / (fwd8["total_ms"] * 1e-3) / 1e12
+        roof = dict(bound="mfma", kernel="k_gemm8f8<4, 0> (fp8 e4m3 fused gate|up GEMM + SwiGLU epilogue of the teacher "
+                                          "MLPs, v_mfma_scale_f32_32x32x64_f8f6f4)",
+                    achieved=round(ach, 1), peak=PEAK_FP8_TFLOPS, unit="TFLOP/s", frac=round(ach / PEAK_FP8_TFLOPS, 4),
+                    traffic=None, flops_per_launch=round(fwd8["flops_per_launch"] / 1e9, 2),
+                    avg_launch_us=round(fwd8["avg_ms"] * 1e3, 2),
+                    measured="HIP events on the launch stream over 2 serialized steps after the timed region",
+                    bf16_student_swiglu=None if not fwd else dict(avg_launch_us=round(fwd["avg_ms"] * 1e3, 2),
+                                                                  tflops=round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 1)))
     tfwd = teacher_forward_rate(m, batches[0]) if m.teacher_model is not None else None
     out = {
         "metric": "KD samples/sec/step (7B->0.5B, 336x336)",
@@ -366,6 +418,7 @@ def main():
                    "parallelism": f"dp{world}"},
         "mfu": round(value * tf_sample / world / PEAK_BF16_TFLOPS, 4),
         "host_enqueue_ms_per_step": round(host_dt * 1e3 / a.steps, 2),
+        "host_enqueue_ms_idle_step": round(host_idle_ms, 2),
         "tflop_per_sample": round(tf_sample, 2),
         "loss": round(loss_v, 5),
         "teacher_fwd": tfwd,
@@ -374,6 +427,10 @@ def main():
         "kd_loss_delta": None,
         "cpu_baseline": None,
     }
+    if teacher_fp8:
+        out["dtype"] = "bf16 (student, loss) + fp8 e4m3 teacher linears"
+        if rank == 0:
+            out["fp8_teacher_delta"] = fp8_teacher_delta(m, batches[0])
     if rank == 0 and not a.no_delta:
         # one more step with its logits kept: the fused loss kernel's terms vs the CPU oracle
         # on the same (bf16) logits

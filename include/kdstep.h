@@ -161,7 +161,7 @@ typedef struct {
 /* fp8 path (ab_dtype = KD_DTYPE_FP8_E4M3; the fp8 teacher of BASELINE config c4): A and B are
  * OCP e4m3 bytes, both K-major, K % 16 == 0, lda / ldb % 16 == 0 (bytes = elements), 16-B
  * aligned; C = epilogue(alpha * a_scale[m] * b_scale[n] * sum_k qa[m][k] qb[n][k]) with the
- * epilogue above (bias / aux / act / residual / SWIGLU), bf16 C, no split-K.  MFMA
+ * epilogue above (bias / act / residual / SWIGLU; aux only with SWIGLU), bf16 C, no split-K.  MFMA
  * v_mfma_scale_f32_32x32x64_f8f6f4 (unit block scales), fp32 accumulation. */
 
 /* Bytes of workspace the auto (or forced) split-K plan for `desc` wants; 0 = no split.
@@ -408,7 +408,8 @@ int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids
 /* GEMM timer (measurement): while enabled, every kd_gemm launch (the ABI entry and the
  * model runtime's) is bracketed by HIP events on its stream.  kd_timer_read synchronises
  * record i's end event and returns its key "<kind>:<M>x<N>x<K>:<f32|bf16>[:acc]", kind =
- * gemm_{k|n}{k|n} (A / B layout) or gemm_kk_swiglu, its FLOPs and milliseconds. */
+ * gemm_{k|n}{k|n} (A / B layout), gemm_kk_swiglu, gemm_f8 / gemm_f8_swiglu (fp8 path), its FLOPs
+ * and milliseconds. */
 void kd_timer_enable(int on);
 int kd_timer_count(void);
 int kd_timer_read(int i, char* key, int key_cap, double* flops, float* ms);

@@ -1045,7 +1045,10 @@ __device__ __forceinline__ void f8_to_lds(const f32x16 (&acc)[4][4], char* smem,
         }
 }
 
-template <int EXP = 0>
+// ACT is a template parameter (one epilogue copy per build): with the activation switch and
+// an aux pass in one kernel the epilogue's register demand made hipcc spill accumulators right
+// after the last (asm, hazard-invisible) MFMA, before its results had landed.
+template <int EXP, int ACT>
 __global__ void __launch_bounds__(NTH8, 1) k_gemm8f8(GemmP p) {
     constexpr bool glu = EXP & 4;
     constexpr int SA = 256 * 64, SS = 2 * SA;   // 16 KiB per operand stage, 32 KiB per slot
@@ -1207,18 +1210,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8f8(GemmP p) {
         return;
     }
     const bool full = m0 + 256 <= p.M && n0 + 256 <= p.N;
-    if (p.aux) {   // pre-activation (bf16) for a backward
-        f8_to_lds<KD_ACT_NONE>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane);
-        __syncthreads();
-        epi_flush<256, 256, NTH8, false, false, false>(p, smem, F8_RS, p.aux, p.ld_aux, m0, n0, tid, full);
-        __syncthreads();
-    }
-    switch (p.act) {
-        case KD_ACT_GELU_TANH: f8_to_lds<KD_ACT_GELU_TANH>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
-        case KD_ACT_GELU_ERF: f8_to_lds<KD_ACT_GELU_ERF>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
-        case KD_ACT_SILU: f8_to_lds<KD_ACT_SILU>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
-        default: f8_to_lds<KD_ACT_NONE>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane); break;
-    }
+    f8_to_lds<ACT>(acc, smem, sa_l, sbv, bcol, alpha, ra, cb, lane);
     __syncthreads();
     epi_flush_sel<256, 256, NTH8, false>(p, smem, F8_RS, p.C, p.ldc, m0, n0, tid, full, p.resid != nullptr,
                                         p.accumulate != 0);
@@ -1426,11 +1418,18 @@ int launch_gemm_f8(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->N % 256 == 0, "gemm fp8 swiglu: N = 2I needs I % 128 == 0");
         KD_CHECK_ARG(!d->bias && !d->residual && !d->accumulate, "gemm fp8 swiglu: no bias / residual / accumulate");
         p.glu = d->N / 2; p.act = KD_ACT_NONE;
-        hipLaunchKernelGGL((k_gemm8f8<4>), dim3(ceil_div(d->M, 256) * (d->N / 256)), dim3(NTH8), F8_LDS, st, p);
+        hipLaunchKernelGGL((k_gemm8f8<4, KD_ACT_NONE>), dim3(ceil_div(d->M, 256) * (d->N / 256)), dim3(NTH8), F8_LDS, st, p);
         KD_LAUNCH_CHECK("k_gemm8f8<swiglu>");
         return KD_OK;
     }
-    hipLaunchKernelGGL((k_gemm8f8<0>), dim3(ceil_div(d->M, 256) * ceil_div(d->N, 256)), dim3(NTH8), F8_LDS, st, p);
+    KD_CHECK_ARG(!d->aux, "gemm fp8: aux (pre-activation) output only with KD_ACT_SWIGLU");
+    const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256));
+    switch (d->act) {
+        case KD_ACT_GELU_TANH: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_GELU_TANH>), grid, dim3(NTH8), F8_LDS, st, p); break;
+        case KD_ACT_GELU_ERF: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_GELU_ERF>), grid, dim3(NTH8), F8_LDS, st, p); break;
+        case KD_ACT_SILU: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_SILU>), grid, dim3(NTH8), F8_LDS, st, p); break;
+        default: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_NONE>), grid, dim3(NTH8), F8_LDS, st, p); break;
+    }
     KD_LAUNCH_CHECK("k_gemm8f8");
     return KD_OK;
 }

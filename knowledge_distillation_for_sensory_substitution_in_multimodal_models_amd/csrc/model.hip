@@ -43,9 +43,9 @@ bool g_timer_on = false;
 int gemm_timed(const kd_gemm_desc* d, void* stream) {
     if (!g_timer_on) return launch_gemm(d, stream);
     TimerRec r;
-    const bool swiglu = d->act == KD_ACT_SWIGLU;
-    r.key = swiglu ? std::string("gemm_kk_swiglu")
-                   : std::string("gemm_") + (d->a_layout ? 'n' : 'k') + (d->b_layout ? 'n' : 'k');
+    const bool swiglu = d->act == KD_ACT_SWIGLU, f8 = d->ab_dtype == KD_DTYPE_FP8_E4M3;
+    r.key = swiglu ? std::string(f8 ? "gemm_f8_swiglu" : "gemm_kk_swiglu")
+                   : (f8 ? std::string("gemm_f8") : std::string("gemm_") + (d->a_layout ? 'n' : 'k') + (d->b_layout ? 'n' : 'k'));
     r.key += ":" + std::to_string(d->M) + "x" + std::to_string(d->N) + "x" + std::to_string(d->K) + ":" +
              (d->c_dtype == KD_DTYPE_F32 ? "f32" : "bf16") + (d->accumulate ? ":acc" : "");
     r.flops = 2.0 * d->M * d->N * d->K;
