@@ -279,8 +279,6 @@ def main():
                     help="student forward on the main stream (no overlap with the teacher forward)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
     ap.add_argument("--teacher-bf16", action="store_true", help="c4 with the bf16 teacher instead of fp8")
-    ap.add_argument("--no-teacher-rate", action="store_true",
-                    help="skip the teacher-forward rate pass (profiling: every launch then belongs to a full step)")
     a = ap.parse_args()
 
     import torch
@@ -401,7 +399,7 @@ def main():
                     measured="HIP events on the launch stream over 2 serialized steps after the timed region",
                     bf16_student_swiglu=None if not fwd else dict(avg_launch_us=round(fwd["avg_ms"] * 1e3, 2),
                                                                   tflops=round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 1)))
-    tfwd = teacher_forward_rate(m, batches[0]) if (m.teacher_model is not None and not a.no_teacher_rate) else None
+    tfwd = teacher_forward_rate(m, batches[0]) if m.teacher_model is not None else None
     out = {
         "metric": "KD samples/sec/step (7B->0.5B, 336x336)",
         "value": round(value, 4),

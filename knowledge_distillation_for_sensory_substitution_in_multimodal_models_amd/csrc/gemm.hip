@@ -28,7 +28,6 @@ namespace kd {
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NTH = 256;
-constexpr uint64_t SPLIT_CNT_BYTES = 64 << 10;   // split-K arrival counters at the end of the workspace
 constexpr int TILE_BYTES = 128 * 64 * 2;  // 16 KiB per operand tile
 constexpr uint32_t OOB = 0x80000000u;     // voffset beyond every num_records -> zeros
 
@@ -48,8 +47,6 @@ struct GemmP {
     int tile0;             // first linear tile (grouped order) of this launch: the split tail of a hybrid plan
     const float* sa;       // fp8 path: per-row scale of A [M] (dequantised A = sa[m] * qa[m, k])
     const float* sb;       // fp8 path: per-row scale of B [N] (per output channel)
-    float* ws;             // split-K: fp32 partial planes (split_stride floats apart) ...
-    int* cnt;              // ... and one arrival counter per tile of the launch (zero at launch)
 };
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
@@ -532,108 +529,6 @@ __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[
     }
 }
 
-
-// =============================================================================
-// Split-K inside the launch. Grid row y of a split launch computes K range [y*kchunk,
-// (y+1)*kchunk) of its tile into fp32 partial plane y (the kernel's own epilogue with
-// every epilogue op off), then takes a ticket on the tile's arrival counter; the block
-// that draws S-1 folds the S planes in plane order (deterministic, the order of the
-// former separate reduce kernel, so results are unchanged) and applies the full epilogue
-// of the descriptor. Hand-off (MI355X_MICROARCH.md correctness boundaries /
-// cdna_hip_programming.md §5 item 2): every wave drains its stores, barrier, one lane
-// releases at agent scope, then the relaxed ticket; the reducer's lane acquires at agent
-// scope before the barrier that precedes its plain loads. The reducer zeroes the counter
-// for the next launch (the launcher also zeroes the counters ahead of each split launch).
-// This replaces a k_splitk_reduce launch per split GEMM and its HBM round trip of the
-// planes (the planes of one tile are re-read while L2 / Infinity-Cache resident).
-// =============================================================================
-template <bool A_MN, bool B_MN>
-__device__ __forceinline__ void split_prologue(GemmP& p) {
-    const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-    p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-    p.A += A_MN ? k0 * p.lda : k0;
-    p.B += B_MN ? k0 * p.ldb : k0;
-    p.C = p.ws + (int64_t)blockIdx.y * p.split_stride;
-    p.ldc = p.N;
-    p.c_f32 = 1; p.accumulate = 0; p.alpha = 1.f; p.alpha_dev = nullptr;
-    p.bias = nullptr; p.aux = nullptr; p.resid = nullptr; p.act = KD_ACT_NONE; p.res_mod = 0;
-}
-
-template <int NTHR>
-__device__ __forceinline__ void splitk_fixup(const GemmP& p, char* smem, int m0, int n0, int BMr, int BNr, int tid) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial-plane stores have left
-    __syncthreads();
-    volatile int* flag = (volatile int*)smem;           // the epilogue is done with LDS
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(p.cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == (int)gridDim.y - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            p.cnt[blockIdx.x] = 0;
-        }
-        *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    const int S = (int)gridDim.y;
-    const int r1 = min(m0 + BMr, p.M), cw = min(BNr, p.N - n0);
-    const int c4 = cw / 4;   // N % 8 == 0 on this path
-    float alpha = p.alpha;
-    if (p.alpha_dev) alpha *= *p.alpha_dev;
-    for (int idx = tid; idx < (r1 - m0) * c4; idx += NTHR) {
-        const int64_t row = m0 + idx / c4;
-        const int col = n0 + (idx % c4) * 4;
-        const float* src = p.ws + row * p.N + col;
-        f32x4 v = *(const f32x4*)src;
-        int s = 1;
-        for (; s + 3 < S; s += 4) {
-            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
-            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
-            const f32x4 c = *(const f32x4*)(src + (int64_t)(s + 2) * p.split_stride);
-            const f32x4 d = *(const f32x4*)(src + (int64_t)(s + 3) * p.split_stride);
-            v += a; v += b; v += c; v += d;
-        }
-        if (s + 1 < S) {
-            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
-            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
-            v += a; v += b;
-            s += 2;
-        }
-        if (s < S) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            float x = v[e] * alpha;
-            if (p.bias) x += p.bias_f32 ? ((const float*)p.bias)[col + e] : (float)((const bf16*)p.bias)[col + e];
-            if (p.aux) p.aux[row * p.ld_aux + col + e] = (bf16)x;
-            v[e] = apply_act(x, p.act);
-        }
-        if (p.resid) {
-            const bf16x4 r = *(const bf16x4*)(p.resid + (p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
-        }
-        if (p.c_f32) {
-            float* dst = (float*)p.C + row * p.ldc + col;
-            if (p.accumulate) v += *(const f32x4*)dst;
-            *(f32x4*)dst = v;
-        } else {
-            bf16* dst = (bf16*)p.C + row * p.ldc + col;
-            bf16x4 o;
-            if (p.accumulate) {
-                const bf16x4 c = *(const bf16x4*)dst;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += (float)c[e];
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-            *(bf16x4*)dst = o;
-        }
-    }
-}
-
 // =============================================================================
 // v3: the tiles above and their 4-stage LDS ring, software-pipelined one stage deeper: the
 // fragments of stage t+1 are read into a second register set WHILE the MFMAs of stage t
@@ -646,7 +541,13 @@ __device__ __forceinline__ void splitk_fixup(const GemmP& p, char* smem, int m0,
 template <int BM, int BN, bool A_MN, bool B_MN, int NS = NST>
 __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     GemmP p = p_;
-    if (gridDim.y > 1) split_prologue<A_MN, B_MN>(p);   // this grid row's K range -> fp32 partial plane
+    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
     constexpr int WM = (BM == 256 && BN == 256) ? 2 : (BM == 256 ? 4 : 2);
     constexpr int WN = 8 / WM;
     constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NT = TN / 16;
@@ -724,7 +625,6 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     epilogue2<BM, BN, WM, WN, TM, TN, MT, NT, NTH2, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-    if (gridDim.y > 1) splitk_fixup<NTH2>(p_, smem, m0, n0, BM, BN, tid);
 }
 
 // =============================================================================
@@ -785,7 +685,13 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
     uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
     if (STAMP) ts0 = __builtin_amdgcn_s_memtime();
-    if (gridDim.y > 1) split_prologue<A_MN, B_MN>(p);   // this grid row's K range -> fp32 partial plane
+    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
     constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -936,7 +842,6 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     __syncthreads();
     if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
     else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-    if (gridDim.y > 1) splitk_fixup<NTH8>(p_, smem, m0, n0, 256, 256, tid);
     if (STAMP) {
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         s_epi = te1 - te0;
@@ -971,7 +876,13 @@ constexpr int NTH9 = 512;
 template <bool A_MN, bool B_MN>
 __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
     GemmP p = p_;
-    if (gridDim.y > 1) split_prologue<A_MN, B_MN>(p);   // this grid row's K range -> fp32 partial plane
+    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
     constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1067,7 +978,6 @@ __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
     __syncthreads();
     if (!A_MN && !B_MN && glu) epilogue_glu<128, 64, 8, 4, NTH9>(p, acc, smem, m0, nb, grp, wc, lane, tid);
     else epilogue2<256, 256, 2, 4, 128, 64, 8, 4, NTH9, !A_MN && !B_MN>(p, acc, smem, m0, n0, grp, wc, lane, tid);
-    if (gridDim.y > 1) splitk_fixup<NTH9>(p_, smem, m0, n0, 256, 256, tid);
 }
 
 
@@ -1341,6 +1251,73 @@ __global__ void __launch_bounds__(256) k_quant_rows_f8(const bf16* __restrict__ 
     }
 }
 
+// split-K fold: C = epilogue(sum_s partial[s]) with the full epilogue of the descriptor
+// (alpha, alpha_dev, bias, aux, act, residual, accumulate), over the split tiles only
+// (linear tiles [tile0, tile0 + gridDim.x) of a BM x BN tiling, grouped order as in the
+// GEMM launch); blockIdx.y takes a BM / gridDim.y row slab of its tile (one 4-column chunk
+// per thread: many blocks, every load of a block in flight at once), the S partial loads
+// of a chunk issued together.
+__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p, int BMr, int BNr) {
+    int tm, tn;
+    tile_grouped(p.tile0 + (int)blockIdx.x, (p.M + BMr - 1) / BMr, (p.N + BNr - 1) / BNr, tm, tn);
+    const int rows_per = BMr / (int)gridDim.y;
+    const int r0 = tm * BMr + (int)blockIdx.y * rows_per;
+    const int r1 = min(r0 + rows_per, p.M);
+    const int c0 = tn * BNr, cw = min(BNr, p.N - c0);
+    const int c4 = cw / 4;   // N % 8 == 0 on this path
+    float alpha = p.alpha;
+    if (p.alpha_dev) alpha *= *p.alpha_dev;
+    for (int idx = threadIdx.x; idx < (r1 - r0) * c4; idx += 256) {
+        const int64_t row = r0 + idx / c4;
+        const int col = c0 + (idx % c4) * 4;
+        const float* src = ws + row * p.N + col;
+        f32x4 v = *(const f32x4*)src;
+        int s = 1;
+        for (; s + 3 < S; s += 4) {
+            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
+            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
+            const f32x4 c = *(const f32x4*)(src + (int64_t)(s + 2) * p.split_stride);
+            const f32x4 d = *(const f32x4*)(src + (int64_t)(s + 3) * p.split_stride);
+            v += a; v += b; v += c; v += d;
+        }
+        if (s + 1 < S) {   // same summation order, both loads in flight
+            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
+            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
+            v += a; v += b;
+            s += 2;
+        }
+        if (s < S) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float x = v[e] * alpha;
+            if (p.bias) x += p.bias_f32 ? ((const float*)p.bias)[col + e] : (float)((const bf16*)p.bias)[col + e];
+            if (p.aux) p.aux[row * p.ld_aux + col + e] = (bf16)x;
+            v[e] = apply_act(x, p.act);
+        }
+        if (p.resid) {
+            const bf16x4 r = *(const bf16x4*)(p.resid + (p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+        }
+        if (p.c_f32) {
+            float* dst = (float*)p.C + row * p.ldc + col;
+            if (p.accumulate) v += *(const f32x4*)dst;
+            *(f32x4*)dst = v;
+        } else {
+            bf16* dst = (bf16*)p.C + row * p.ldc + col;
+            bf16x4 o;
+            if (p.accumulate) {
+                const bf16x4 c = *(const bf16x4*)dst;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)c[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+            *(bf16x4*)dst = o;
+        }
+    }
+}
+
 // Kernel / tile / split-K plan. Cost model in microseconds: waves x (32-deep k-steps per
 // split x per-step tile cost + fixed per-tile prologue/epilogue), plus the fp32
 // partial-plane traffic of a split. Candidates: v3 256x256 / 256x128 / 128x256 (8 waves)
@@ -1539,7 +1516,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,
                                     // 16 v8 256x256 (4 waves, AGPR accumulators), 17-19 v8 diagnostics
     if (force != 1 && big_ok) {
-        const GemmPlan pl = plan_gemm(d, d->workspace && d->workspace_bytes > SPLIT_CNT_BYTES ? d->workspace_bytes - SPLIT_CNT_BYTES : 0);
+        const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
         const int tbm = pl.var == 4 ? 128 : 256, tbn = pl.var == 3 ? 128 : 256;
         const int tiles = ceil_div(d->M, tbm) * ceil_div(d->N, tbn);
         // one launch of the planned kernel over linear tiles [q.tile0, q.tile0 + nt), gy K splits
@@ -1593,26 +1570,25 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             KD_LAUNCH_CHECK("k_gemm (tiles)");
             return KD_OK;
         }
-        KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4 + SPLIT_CNT_BYTES,
+        KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
                      "gemm: split-K workspace too small");
         if (pl.dp_tiles > 0) {   // hybrid: whole waves unsplit with the full epilogue
             p.tile0 = 0;
             launch_tiles(p, pl.dp_tiles, 1);
             KD_LAUNCH_CHECK("k_gemm (whole waves)");
         }
-        // the split tiles: fp32 partial planes + in-launch fold by each tile's last arriver
-        const int nsplit_tiles = tiles - pl.dp_tiles;
-        KD_CHECK_SHAPE(nsplit_tiles * 4 <= (int)SPLIT_CNT_BYTES, "gemm: too many split tiles for the counter block");
-        GemmP pk = p;
-        pk.ws = (float*)d->workspace;
-        pk.cnt = (int*)((char*)d->workspace + d->workspace_bytes - SPLIT_CNT_BYTES);
-        pk.kchunk = pl.kchunk;
-        pk.split_stride = (int64_t)d->M * d->N;
-        pk.tile0 = pl.dp_tiles;
-        if (hipMemsetAsync(pk.cnt, 0, (size_t)nsplit_tiles * 4, st) != hipSuccess)
-            return fail(KD_ERR_LAUNCH, "gemm: counter reset failed");
-        launch_tiles(pk, nsplit_tiles, (unsigned)pl.split);
+        GemmP pk = p;   // the split tiles write plain fp32 partial planes
+        pk.C = d->workspace; pk.ldc = d->N; pk.c_f32 = 1; pk.accumulate = 0; pk.alpha = 1.f;
+        pk.alpha_dev = nullptr; pk.bias = nullptr; pk.aux = nullptr; pk.resid = nullptr; pk.act = KD_ACT_NONE;
+        pk.kchunk = pl.kchunk; pk.split_stride = (int64_t)d->M * d->N; pk.tile0 = pl.dp_tiles;
+        launch_tiles(pk, tiles - pl.dp_tiles, (unsigned)pl.split);
         KD_LAUNCH_CHECK("k_gemm (split tiles)");
+        p.split_stride = (int64_t)d->M * d->N;
+        p.tile0 = pl.dp_tiles;
+        // one float4 column chunk per thread: BM / (1024 / BN) row slabs of 1024 / BN rows per tile
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)(tiles - pl.dp_tiles), (unsigned)(tbm * tbn / 1024)), dim3(256), 0, st,
+                           (const float*)d->workspace, pl.split, p, tbm, tbn);
+        KD_LAUNCH_CHECK("k_splitk_reduce");
         return KD_OK;
     }
     const int tiles = ceil_div(d->M, BM) * ceil_div(d->N, BN);
@@ -1634,7 +1610,7 @@ int gemm_plan_query(const kd_gemm_desc* d, int32_t* var, int32_t* split, int32_t
                         (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0);
     if (d->act == KD_ACT_SWIGLU) { *var = 16; *split = 1; *dp = 0; return KD_OK; }
     if (d->variant == 1 || !big_ok) { *var = 1; *split = 1; *dp = 0; return KD_OK; }
-    const GemmPlan pl = plan_gemm(d, d->workspace && d->workspace_bytes > SPLIT_CNT_BYTES ? d->workspace_bytes - SPLIT_CNT_BYTES : 0);
+    const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
     *var = pl.var; *split = pl.split; *dp = pl.dp_tiles;
     return KD_OK;
 }
@@ -1642,7 +1618,7 @@ int gemm_plan_query(const kd_gemm_desc* d, int32_t* var, int32_t* split, int32_t
 size_t gemm_workspace_size(const kd_gemm_desc* d) {
     if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->variant == 1 || d->act == KD_ACT_SWIGLU) return 0;
     const GemmPlan pl = plan_gemm(d, ~0ull);
-    return pl.split > 1 ? (size_t)pl.split * d->M * d->N * 4 + SPLIT_CNT_BYTES : 0;
+    return pl.split > 1 ? (size_t)pl.split * d->M * d->N * 4 : 0;
 }
 
 }  // namespace kd
