@@ -1,0 +1,65 @@
+"""Host time of each call of a c1 bench step (after warmup), to see where the host waits:
+    python tools/host_phases.py [--config c1] [--steps 4]
+Prints per step: training_step / backward / opt.step / zero_grad host ms, and the GPU time of
+the step (HIP events on the main stream)."""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c1")
+    ap.add_argument("--steps", type=int, default=4)
+    a = ap.parse_args()
+    import torch
+    import bench
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import STREAM_PRIORITY_HIGH
+    dev = torch.device("cuda:0")
+    cfg = bench.CONFIGS[a.config]
+    m, opt = bench.build(cfg, dev, teacher_fp8=bool(cfg.get("teacher_fp8")))
+    batches = [synthetic_batch(cfg["batch"], dev, L=1536, seed=j) for j in range(2)]
+    hp = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
+    hp.wait_stream(torch.cuda.current_stream())
+    torch.cuda.set_stream(hp)
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops as OPS
+    tm = {}
+
+    def wrap(obj, name, key):
+        f = getattr(obj, name)
+
+        def g(*args, **kw):
+            t0 = time.perf_counter()
+            r = f(*args, **kw)
+            tm[key] = tm.get(key, 0.0) + (time.perf_counter() - t0) * 1e3
+            return r
+        setattr(obj, name, g)
+    wrap(m._errors, "check", "errors.check")
+    wrap(OPS, "adamw", "ops.adamw")
+    wrap(m, "_check_errors", "m._check_errors")
+    for i in range(2 + a.steps):
+        tm.clear()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        t = [time.perf_counter()]
+        loss = m.training_step(batches[i % 2], i)
+        t.append(time.perf_counter())
+        loss.backward()
+        t.append(time.perf_counter())
+        opt.step()
+        t.append(time.perf_counter())
+        opt.zero_grad()
+        t.append(time.perf_counter())
+        e1.record()
+        d = [round((t[k + 1] - t[k]) * 1e3, 2) for k in range(4)]
+        print(f"step {i}: host ms training_step {d[0]} backward {d[1]} opt.step {d[2]} zero_grad {d[3]} "
+              f"(total {round((t[-1] - t[0]) * 1e3, 1)}) inner {dict((k, round(v, 2)) for k, v in tm.items())}", flush=True)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
