@@ -276,7 +276,7 @@ def main():
     ap.add_argument("--no-timer", action="store_true", help="skip the serialized roofline pass (per-GEMM HIP events)")
     ap.add_argument("--no-delta", action="store_true", help="skip kd_loss_delta (the CPU oracle on this step's logits)")
     ap.add_argument("--serial", action="store_true",
-                    help="student forward on the main stream (no overlap with the teacher forward)")
+                    help="one stream: student forward and the weight gradients on the main stream (profiling)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
     ap.add_argument("--teacher-bf16", action="store_true", help="c4 with the bf16 teacher instead of fp8")
     a = ap.parse_args()
@@ -297,6 +297,7 @@ def main():
     teacher_fp8 = bool(cfg.get("teacher_fp8")) and not a.teacher_bf16
     m, opt = build(cfg, dev, teacher_fp8=teacher_fp8)
     m.concurrent_student = not a.serial
+    m.student_model.wlane.serial = a.serial   # --serial: one stream for everything (profiling)
     # two synthetic batches, alternated, so every step's teacher forward is a fresh one
     batches = [synthetic_batch(B, dev, L=1536, seed=rank * 2 + j) for j in range(2)]
 
@@ -339,11 +340,13 @@ def main():
     step(a.warmup + a.steps + 5)
     host_idle_ms = (time.perf_counter() - th) * 1e3
     torch.cuda.synchronize()
-    # ---- after the timed region: roofline pass (two steps with the student forward
-    # serialized behind the teacher forward, every GEMM bracketed by HIP events on its launch
-    # stream, so a kernel's duration is its own and not shared with a concurrent stream)
+    # ---- after the timed region: roofline pass (two fully serialized steps: the student
+    # forward behind the teacher forward, the weight gradients on the main stream; every GEMM
+    # bracketed by HIP events on its launch stream, so a kernel's duration is its own and not
+    # shared with a concurrent stream)
     if not a.no_timer:
         m.concurrent_student = False
+        m.student_model.wlane.serial = True   # the backward's weight gradients on the main stream too
         ops.TIMER.reset()
         ops.TIMER.enabled = True
         for i in range(2):
@@ -351,6 +354,7 @@ def main():
         torch.cuda.synchronize()
         ops.TIMER.enabled = False
         m.concurrent_student = not a.serial
+        m.student_model.wlane.serial = a.serial
     samples = world * B * a.steps
     value = samples / dt
     tf_sample = step_tflops_per_sample(cfg["kind"], cfg["phase"])

@@ -358,6 +358,15 @@ int64_t kd_model_param_numel(const kd_model_config* cfg);          /* flat lengt
 int kd_model_param_info(const kd_model_config* cfg, int index, char* name, int name_cap, int64_t* offset,
                         int64_t* numel, int64_t* rows, int64_t* cols);
 
+/* anyres pack plan on the host (transformers' select_best_resolution / unpad_image /
+ * pack_image_features for the 384-px tile grid of the -ov checkpoints, anyres_max_9): for
+ * sample b with image_sizes_host[b] = (H, W) and `tiles` pixel tiles per sample, map_host[b][j]
+ * = the flattened vision-feature row (over B * tiles * 729) of its j-th image token, or -1
+ * (image_newline); len_host[b] = its image-token count; the rest of the row is -2.  The
+ * input of kd_image_src_map. */
+int kd_anyres_batch_map(const int64_t* image_sizes_host, int B, int tiles, int32_t* map_host, int map_ld,
+                        int32_t* len_host);
+
 typedef struct kd_model kd_model;
 int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad, kd_model** out);
 void kd_model_destroy(kd_model* m);

@@ -150,6 +150,7 @@ SIGNATURES = {
     "kd_rope_row": (_i32, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "kd_image_resize_u8": (_i32, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _sz, _vp]),
     "kd_anyres_tiles": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp]),
+    "kd_anyres_batch_map": (_i32, [_vp, _i32, _i32, _vp, _i32, _vp]),
     "kd_model_param_count": (_i32, [C.POINTER(KdModelConfig)]),
     "kd_model_param_numel": (_i64, [C.POINTER(KdModelConfig)]),
     "kd_model_param_info": (_i32, [C.POINTER(KdModelConfig), _i32, C.c_char_p, _i32, C.POINTER(_i64),

@@ -53,6 +53,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
         objs = list(ex.map(_compile, srcs))
     newest = max(o.stat().st_mtime for o in objs)
     if LIB.exists() and LIB.stat().st_mtime > newest:
+        build_c_host(verbose)
         return LIB
     cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(LIB)]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -60,7 +61,27 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     if verbose:
         print(f"built {LIB}")
+    build_c_host(verbose)
     return LIB
+
+
+C_HOST_SRC = REPO / "tools" / "c_host_step.cpp"
+C_HOST_BIN = OUT_DIR / "kd_c_host_step"
+
+
+def build_c_host(verbose: bool = False) -> Path:
+    """The C-ABI host example (tools/c_host_step.cpp: a full KD step with no Python), linked
+    against libkdstep.so next to it (rpath $ORIGIN)."""
+    if C_HOST_BIN.exists() and C_HOST_BIN.stat().st_mtime > max(C_HOST_SRC.stat().st_mtime, LIB.stat().st_mtime):
+        return C_HOST_BIN
+    cmd = [HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", f"-I{REPO / 'include'}", str(C_HOST_SRC),
+           f"-L{OUT_DIR}", "-lkdstep", "-Wl,-rpath,$ORIGIN", "-o", str(C_HOST_BIN)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"c host build failed:\n{r.stderr}")
+    if verbose:
+        print(f"built {C_HOST_BIN}")
+    return C_HOST_BIN
 
 
 if __name__ == "__main__":

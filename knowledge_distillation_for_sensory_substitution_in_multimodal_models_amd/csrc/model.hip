@@ -20,6 +20,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -800,8 +802,88 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
 }  // namespace
 }  // namespace kd
 
+
+// ================================================================ anyres plan ====
+// Host-side pack plan of LLaVA-OneVision's anyres image features (the C restatement of
+// anyres.py, itself transformers' select_best_resolution / get_anyres_image_grid_shape /
+// unpad_image / pack_image_features, HF5 llava_onevision :152-343): for each image token of
+// each sample, the flattened vision feature row it takes ([B*tiles*729] rows; tile 0 = the
+// base image, then the grid tiles) or -1 for image_newline. Pinpoints: 384 x {1..6} squared
+// grid (the checkpoints' image_grid_pinpoints); max 9 patches (anyres_max_9).
+namespace {
+constexpr int AR_PATCH = 384, AR_GRID = 27, AR_TILE = AR_GRID * AR_GRID;
+
+void best_resolution(int oh, int ow, int& bh, int& bw) {
+    double best_eff = 0, best_waste = 1e300;
+    bh = bw = 0;
+    for (int h = 384; h <= 2304; h += 384)
+        for (int w = 384; w <= 2304; w += 384) {
+            const double scale = std::min((double)w / ow, (double)h / oh);
+            const long long dw = (long long)(ow * scale), dh = (long long)(oh * scale);
+            const double eff = (double)std::min(dw * dh, (long long)ow * oh);
+            const double waste = (double)w * h - eff;
+            if (eff > best_eff || (eff == best_eff && waste < best_waste)) {
+                best_eff = eff; best_waste = waste; bh = h; bw = w;
+            }
+        }
+}
+
+// Python's int(round(x, 7)) for the x of unpad_image (x > 0)
+long long round7_int(double x) { return (long long)(std::nearbyint(x * 1e7) / 1e7); }
+
+int pack_map(int oh, int ow, int base, int32_t* out, int cap) {
+    int bh, bw;
+    best_resolution(oh, ow, bh, bw);
+    const int nph = bh / AR_PATCH, npw = bw / AR_PATCH;
+    int n = 0;
+    auto put = [&](int v) { if (n < cap) out[n] = v; ++n; };
+    for (int p = 0; p < AR_TILE; ++p) put(base + p);
+    const int H = nph * AR_GRID, W = npw * AR_GRID;
+    int r0 = 0, r1 = H, c0 = 0, c1 = W;
+    if ((double)ow / oh > (double)W / H) {
+        const long long new_h = round7_int(oh * ((double)W / ow));
+        const int pad = (int)((H - new_h) / 2);
+        r0 = pad; r1 = H - pad;
+    } else {
+        const long long new_w = round7_int(ow * ((double)H / oh));
+        const int pad = (int)((W - new_w) / 2);
+        c0 = pad; c1 = W - pad;
+    }
+    const int ch = r1 - r0, cw = c1 - c0;
+    if (std::sqrt((double)ch * cw / (9.0 * AR_TILE)) > 1.1) return -1;   // anyres_max_9 downsampling: unsupported
+    for (int R = r0; R < r1; ++R) {
+        const int ph = R / AR_GRID, y = R % AR_GRID;
+        for (int Cc = c0; Cc < c1; ++Cc) {
+            const int pw = Cc / AR_GRID, x = Cc % AR_GRID;
+            put(base + (1 + ph * npw + pw) * AR_TILE + y * AR_GRID + x);
+        }
+        put(-1);
+    }
+    return n;
+}
+}  // namespace
 // ================================================================== C ABI ====
 extern "C" {
+
+int kd_anyres_batch_map(const int64_t* image_sizes_host, int B, int tiles, int32_t* map_host, int map_ld,
+                        int32_t* len_host) {
+    KD_CHECK_ARG(image_sizes_host && map_host && len_host, "kd_anyres_batch_map: null pointer");
+    KD_CHECK_SHAPE(B > 0 && tiles > 0 && map_ld > 0, "kd_anyres_batch_map: B, tiles, map_ld must be positive");
+    for (int b = 0; b < B; ++b) {
+        const int oh = (int)image_sizes_host[2 * b], ow = (int)image_sizes_host[2 * b + 1];
+        KD_CHECK_SHAPE(oh > 0 && ow > 0, "kd_anyres_batch_map: image sizes must be positive");
+        int bh, bw;
+        best_resolution(oh, ow, bh, bw);
+        KD_CHECK_SHAPE((bh / 384) * (bw / 384) + 1 <= tiles, "kd_anyres_batch_map: the batch has too few tiles per sample");
+        int32_t* row = map_host + (int64_t)b * map_ld;
+        const int n = pack_map(oh, ow, b * tiles * AR_TILE, row, map_ld);
+        KD_CHECK_SHAPE(n >= 0, "kd_anyres_batch_map: anyres_max_9 downsampling of very large grids is not supported");
+        KD_CHECK_SHAPE(n <= map_ld, "kd_anyres_batch_map: map_ld too small");
+        for (int j = n; j < map_ld; ++j) row[j] = -2;
+        len_host[b] = n;
+    }
+    return KD_OK;
+}
 
 int kd_model_param_count(const kd_model_config* cfg) {
     if (!kd::cfg_ok(cfg)) {

@@ -298,8 +298,15 @@ class WgradLane:
 
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device, priority=STREAM_PRIORITY_HIGH)
+        self.serial = False   # True: the weight gradients run on the current stream (measurement)
+
+    def lane_stream(self):
+        return torch.cuda.current_stream() if self.serial else self.stream
 
     def run(self, fn, *keep):
+        if self.serial:
+            fn()
+            return None
         self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):
             fn()
@@ -311,7 +318,8 @@ class WgradLane:
         return ev
 
     def join(self):
-        torch.cuda.current_stream().wait_stream(self.stream)
+        if not self.serial:
+            torch.cuda.current_stream().wait_stream(self.stream)
 
 
 def native_config(cfg: LlavaConfig) -> NV.KdModelConfig:
@@ -392,15 +400,17 @@ class LlavaOnevisionModel:
         return self._rope[L]
 
     def _src_map(self, input_ids, image_sizes, tiles):
+        """Per-token source rows of inputs_embeds: the anyres pack plan (kd_anyres_batch_map,
+        host, cached per image_sizes) expanded on the device by kd_image_src_map."""
         key = (tuple(tuple(int(v) for v in hw) for hw in image_sizes), tiles)
         if key not in self._maps:
-            maps, lens = anyres.batch_maps(key[0], tiles)
-            w = max(lens)
-            arr = np.full((len(maps), w), -2, dtype=np.int32)
-            for i, m in enumerate(maps):
-                arr[i, :len(m)] = m
-            self._maps[key] = (torch.from_numpy(arr).to(self.device), torch.tensor(lens, dtype=torch.int32,
-                                                                                      device=self.device))
+            B = len(key[0])
+            isz = np.asarray(key[0], dtype=np.int64).reshape(B, 2)
+            ld = max(anyres.num_image_tokens(hw) for hw in key[0])
+            arr = np.empty((B, ld), dtype=np.int32)
+            lens = np.empty(B, dtype=np.int32)
+            NV.call("kd_anyres_batch_map", isz.ctypes.data, B, tiles, arr.ctypes.data, ld, lens.ctypes.data)
+            self._maps[key] = (torch.from_numpy(arr).to(self.device), torch.from_numpy(lens).to(self.device))
         maps, lens = self._maps[key]
         return ops.image_src_map(input_ids, self.cfg.image_token_id, maps, lens, self.err)
 
@@ -505,4 +515,4 @@ class LlavaOnevisionModel:
         cb = NV.LAYER_CB(lambda user, i: on_layer_done(i)) if on_layer_done is not None else NV.LAYER_CB()
         NV.call("kd_model_backward", self._h, fwd["ws"].data_ptr(), fwd["ids"].data_ptr(), fwd["src"].data_ptr(),
                 cos.data_ptr(), sin.data_ptr(), B, L, tiles, dhn.contiguous().data_ptr(), ops._ptr(dpost),
-                ws.data_ptr(), ws.numel(), ops._stream(), self.wlane.stream.cuda_stream, cb, None)
+                ws.data_ptr(), ws.numel(), ops._stream(), self.wlane.lane_stream().cuda_stream, cb, None)

@@ -31,3 +31,36 @@ def test_batch_maps_offsets():
     maps, lens = A.batch_maps([(336, 336), (336, 336)], tiles_per_sample=2)
     assert lens == [1485, 1485]
     assert maps[1][0] == 2 * 729 and maps[0][729] == 729 and maps[0][729 + 27] == -1
+
+
+def test_library_pack_plan_matches_python():
+    """kd_anyres_batch_map (C, for non-Python hosts) == anyres.batch_maps on a sweep of image
+    sizes (aspect ratios from 1:6 to 6:1, odd sizes, the 336^2 bench size)."""
+    import ctypes as C
+    import numpy as np
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import _native as N
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import anyres
+    sizes = [(336, 336), (480, 640), (640, 480), (300, 900), (1000, 500), (530, 730), (1, 1), (384, 2304),
+             (2304, 384), (701, 233), (233, 701), (999, 1001), (1536, 1537), (17, 3000)]
+    rng = np.random.default_rng(0)
+    sizes += [(int(h), int(w)) for h, w in rng.integers(1, 2400, size=(200, 2))]
+    for tiles in (37,):   # up to 6 x 6 + 1 tiles
+        ok = []
+        for hw in sizes:
+            try:
+                maps, lens = anyres.batch_maps([hw], tiles)
+            except (NotImplementedError, ValueError):
+                continue
+            ok.append((hw, maps[0], lens[0]))
+        B = len(ok)
+        ld = max(l for _, _, l in ok)
+        isz = np.array([hw for hw, _, _ in ok], dtype=np.int64)
+        out = np.zeros((B, ld), dtype=np.int32)
+        lens = np.zeros(B, dtype=np.int32)
+        N.call("kd_anyres_batch_map", isz.ctypes.data, B, tiles, out.ctypes.data, ld, lens.ctypes.data)
+        for b, (hw, m, n) in enumerate(ok):
+            base = b * tiles * anyres.TOKENS_PER_TILE   # the C plan numbers rows over the whole batch
+            ref = [(-1 if e == -1 else e + base) for e in m]
+            assert lens[b] == n, hw
+            assert out[b, :n].tolist() == ref, hw
+            assert (out[b, n:] == -2).all()
