@@ -47,7 +47,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 4
+#define KD_ABI_VERSION 5
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -253,10 +253,13 @@ int kd_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx, int
 int kd_ntxent(const float* fs, const float* ft, int n, int D, float tau, float weight, float* loss_out,
               float* dfs, float grad_scale, void* stream);
 /* torch.optim.AdamW step (DT:198-201) on flat fp32 master params with a bf16 working copy;
- * gscale (device, optional) multiplies the gradient first. */
+ * gscale (device, optional) multiplies the gradient first.  skip_words (device, n_skip <= 64
+ * int32, optional): if any is nonzero the step changes nothing — pass the step's error words
+ * (kd_loss_params.err_out, kd_model_forward's err) so that a batch the reference would have
+ * rejected (DT:166) never updates the weights, without a host wait before the update. */
 int kd_adamw(float* param, void* param_bf16, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
              float lr, float beta1, float beta2, float eps, float weight_decay, int step, const float* gscale,
-             void* stream);
+             const int32_t* skip_words, int n_skip, void* stream);
 /* out[0] += sum x^2 (gradient norm). */
 int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);

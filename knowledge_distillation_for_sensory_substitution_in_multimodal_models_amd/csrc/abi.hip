@@ -99,8 +99,8 @@ int kd_ntxent(const float* fs, const float* ft, int n, int D, float tau, float w
     return kd::launch_ntxent(fs, ft, n, D, tau, w, lo, dfs, gs, s);
 }
 int kd_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
-             float wd, int step, const float* gscale, void* s) {
-    return kd::launch_adamw(p, pb, g, m, v, n, lr, b1, b2, eps, wd, step, gscale, s);
+             float wd, int step, const float* gscale, const int32_t* skip, int n_skip, void* s) {
+    return kd::launch_adamw(p, pb, g, m, v, n, lr, b1, b2, eps, wd, step, gscale, skip, n_skip, s);
 }
 int kd_sumsq(const float* x, int64_t n, float* out, void* s) { return kd::launch_sumsq(x, n, out, s); }
 int kd_image_src_map(const int64_t* ids, int B, int L, int64_t tok, const int32_t* map, int ld, const int32_t* len,

@@ -41,7 +41,7 @@ int launch_row_group_mean_bwd(const float* dpool, int G, int P, int D, void* dx,
 int launch_ntxent(const float* fs, const float* ft, int n, int D, float tau, float weight, float* loss_out, float* dfs,
                   float grad_scale, void* stream);
 int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
-                 float eps, float wd, int step, const float* gscale, void* stream);
+                 float eps, float wd, int step, const float* gscale, const int32_t* skip, int n_skip, void* stream);
 int launch_sumsq(const float* x, int64_t n, float* out, void* stream);
 int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, const int* map, int map_ld,
                          const int* map_len, int* src, int* err, void* stream);

@@ -633,7 +633,13 @@ __global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, con
 // p -= lr * (m / (1-b1^t)) / (sqrt(v / (1-b2^t)) + eps).  Master fp32, working copy bf16.
 __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const float* __restrict__ g, float* __restrict__ m,
                         float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                        float bc1, float bc2, const float* __restrict__ gscale) {
+                        float bc1, float bc2, const float* __restrict__ gscale, const int32_t* __restrict__ skip,
+                        int n_skip) {
+    // a step whose batch raised a device error (the sticky error words of the step, see
+    // kd_adamw) leaves every weight and moment untouched
+    int bad = 0;
+    for (int j = 0; j < n_skip; ++j) bad |= skip[j];
+    if (bad) return;
     const float gs = gscale ? *gscale : 1.f;
     auto step = [&](float& pi, float& mi, float& vi, float graw) {
         const float gi = graw * gs;
@@ -933,11 +939,12 @@ int launch_ntxent(const float* fs, const float* ft, int n, int D, float tau, flo
 }
 
 int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
-                 float eps, float wd, int step, const float* gscale, void* stream) {
+                 float eps, float wd, int step, const float* gscale, const int32_t* skip, int n_skip, void* stream) {
     KD_CHECK_ARG(p && pb && g && m && v && step >= 1, "adamw: bad argument");
+    KD_CHECK_ARG(n_skip >= 0 && n_skip <= 64 && (n_skip == 0 || skip), "adamw: bad skip words");
     const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
     hipLaunchKernelGGL(k_adamw, dim3(grid_for(n, 256, 16384)), dim3(256), 0, as_stream(stream), p, (bf16*)pb, g, m, v, n,
-                       lr, b1, b2, eps, wd, bc1, bc2, gscale);
+                       lr, b1, b2, eps, wd, bc1, bc2, gscale, skip, n_skip);
     KD_LAUNCH_CHECK("k_adamw");
     return KD_OK;
 }

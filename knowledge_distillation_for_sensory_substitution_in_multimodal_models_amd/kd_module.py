@@ -88,10 +88,10 @@ class FusedAdamW(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         m = self.module
         g = self.param_groups[0]
-        # a batch the reference would have rejected (label out of range, DT:166) must not
-        # update the weights: the step's loss kernel has long finished by now, so this
-        # host wait costs nothing in steady state
-        m._check_errors(block=True)
+        # a batch the reference would have rejected (label out of range, DT:166) never
+        # updates the weights: the kernel skips on the step's sticky error words (device
+        # side, no host wait); the host raises as soon as it sees them
+        m._check_errors(block=False)
         lo, hi = m._trainable_range()
         if m._gsync is not None:
             m._gsync.finish(lo, hi)
@@ -103,7 +103,8 @@ class FusedAdamW(torch.optim.Optimizer):
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 ops.adamw(P.master[lo:hi], P.flat[lo:hi], P.grad[lo:hi], P.exp_avg[lo:hi], P.exp_avg_sq[lo:hi],
-                          g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count)
+                          g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count,
+                          skip_words=m._errors.words)
                 m._opt_done.record(side)
             m._opt_pending = True
         return loss
@@ -121,36 +122,37 @@ class FusedAdamW(torch.optim.Optimizer):
 
 class _ErrorWatch:
     """Device error words of a step (label range in the KD loss, token ids / image-token
-    count in the embedding assembly), copied asynchronously into pinned host slots and
-    read when their event has completed — no device sync on the step's path.  The
-    reference raises at the offending call (gather, DT:166; embedding / masked_scatter);
-    here the error surfaces at the next optimizer.step() (before any weight update) or
-    the next training_step."""
+    count in the embedding assembly) in one int32 buffer: [0:4] kd_loss_params.err_out,
+    [4] the student's embedding error, [5] the teacher's.  The words are STICKY (never
+    reset on the device until the host has reported them) and kd_adamw reads them as its
+    skip words, so a batch the reference would have rejected (DT:166) leaves the weights
+    untouched, and so does every step queued behind it — the state the reference's
+    RuntimeError leaves.  The host side is asynchronous: after each step's loss the words
+    are copied into a pinned slot and an event is recorded; training_step / optimizer.step
+    raise for any completed slot (no wait), validation_step and check(block=True) wait."""
 
     SLOTS = 4
 
     def __init__(self, dev):
-        self.kd = torch.zeros(4, dtype=torch.int32, device=dev)    # kd_loss_params.err_out
+        self.words = torch.zeros(8, dtype=torch.int32, device=dev)
+        self.kd = self.words[0:4]
         self.host = torch.zeros((self.SLOTS, 6), dtype=torch.int32).pin_memory()
         self.pending = []    # (event, slot, info)
         self.next = 0
 
-    def record(self, student_err, teacher_err, info):
-        """Enqueue the copies on the current stream (after the step's loss), then reset."""
+    def bind(self, student, teacher):
+        """Point the models' embedding error words into the buffer."""
+        student.err = self.words[4:5]
+        if teacher is not None:
+            teacher.err = self.words[5:6]
+
+    def record(self, info):
+        """Enqueue the copy on the current stream (after the step's loss)."""
         if len(self.pending) >= self.SLOTS:
             self.check(block=True, upto=1)
         slot = self.next
         self.next = (self.next + 1) % self.SLOTS
-        h = self.host[slot]
-        h[4:6].zero_()
-        h[0:4].copy_(self.kd, non_blocking=True)
-        h[4:5].copy_(student_err, non_blocking=True)
-        if teacher_err is not None:
-            h[5:6].copy_(teacher_err, non_blocking=True)
-        self.kd.zero_()
-        student_err.zero_()
-        if teacher_err is not None:
-            teacher_err.zero_()
+        self.host[slot].copy_(self.words[0:6], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.pending.append((ev, slot, info))
@@ -160,7 +162,13 @@ class _ErrorWatch:
         for i, (ev, slot, info) in enumerate(self.pending):
             if (block and (upto is None or i < upto)) or ev.query():
                 ev.synchronize()
-                self._raise_if(self.host[slot].tolist(), info)
+                h = self.host[slot].tolist()
+                if any(h):
+                    # reported once: later slots hold the same sticky words
+                    self.pending = []
+                    torch.cuda.synchronize()
+                    self.words.zero_()
+                    self._raise_if(h, info)
             else:
                 keep.append((ev, slot, info))
         self.pending = keep
@@ -222,6 +230,7 @@ class _KDBase(_Base):
         self._opt_pending = False
         self._ctx = None
         self._errors = _ErrorWatch(dev)
+        self._errors.bind(self.student_model, self.teacher_model)
         self.keep_logits = False         # tests: keep the step's logits in last_logits
         self.last_terms = None
         self.last_ntxent = None
@@ -361,8 +370,7 @@ class _KDBase(_Base):
             total = total + ntx[0]
             self.last_ntxent = (ntx[0], ntx_rows[:, 1].mean() if ng > 1 else ntx_rows[0, 1])
         self.last_terms = loss4
-        self._errors.record(s.err, None if self.teacher_model is None else self.teacher_model.err,
-                            dict(L=L, V=Vs))
+        self._errors.record(dict(L=L, V=Vs))
         if train:
             self._ctx = dict(sfwd=sfwd, dlogits=dlogits, dps=dps)
         return total
@@ -418,6 +426,11 @@ class _KDBase(_Base):
 
     def _check_errors(self, block: bool):
         self._errors.check(block=block)
+
+    def check_errors(self):
+        """Wait for every queued step and raise its device-detected error (label range,
+        token ids, image-token count), if any."""
+        self._errors.check(block=True)
 
     # ---------------------------------------------------------- Lightning API ----
     def training_step(self, batch, batch_idx):           # DT:123-131

@@ -463,9 +463,11 @@ def ntxent(fs, ft, tau: float = 0.07, weight: float = 1.0, want_grad: bool = Tru
     return loss, dfs
 
 
-def adamw(p, pb, g, m, v, lr, b1, b2, eps, wd, step, gscale=None):
+def adamw(p, pb, g, m, v, lr, b1, b2, eps, wd, step, gscale=None, skip_words=None):
+    """skip_words: optional int32 device tensor; any nonzero word makes the step a no-op."""
+    ns = 0 if skip_words is None else skip_words.numel()
     NV.call("kd_adamw", p.data_ptr(), pb.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr),
-            float(b1), float(b2), float(eps), float(wd), int(step), _ptr(gscale), _stream())
+            float(b1), float(b2), float(eps), float(wd), int(step), _ptr(gscale), _ptr(skip_words), ns, _stream())
 
 
 def sumsq(x, out):

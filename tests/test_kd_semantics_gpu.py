@@ -5,6 +5,7 @@ data-parallel step equals the single-process step on the union batch, and checkp
 reload through load_from_checkpoint with the reference's keyword arguments."""
 import math
 import os
+import re
 import subprocess
 import sys
 from pathlib import Path
@@ -34,22 +35,69 @@ def _close_grads(a, b, rel=2e-3):
     assert cos >= 0.9999 and abs(nr - 1) <= rel, f"cosine {cos:.6f}, norm ratio {nr:.6f}"
 
 
+def _attempt(f, raised):
+    try:
+        f()
+    except RuntimeError as e:
+        raised.append(str(e))
+
+
 def test_loca_minus100_label_raises_before_the_update(dev):
     """LoCa gathers at every label: -100 (a pad) is out of bounds (DT:166, SURVEY KAT 2).
-    The error surfaces at optimizer.step(), before any weight changes."""
+    AdamW skips on the step's device error words, so the weights never change; the host
+    reports the error once, at the first training_step / optimizer.step after the loss
+    kernel has finished (no host wait on the step's path); training then continues."""
     K = _K()
     meta, _ = load("lb")
     m = K.LogitBasedKD("tiny-student", "tiny-teacher")
     (opt,), _ = m.configure_optimizers()
-    b = batch(meta, dev)
-    b["labels"] = b["labels"].clone()
+    good = batch(meta, dev)
+    b = dict(good)
+    b["labels"] = good["labels"].clone()
     b["labels"][1, 37] = -100
     before = m.student_model.P.flat.clone()
-    loss = m.training_step(b, 0)
-    loss.backward()
-    with pytest.raises(RuntimeError, match=r"index -100 is out of bounds for dimension 2.*batch 1, position 37"):
-        opt.step()
+    master = m.student_model.P.master.clone()
+    raised = []
+    m.training_step(b, 0).backward()
+    _attempt(opt.step, raised)
+    opt.zero_grad()
     torch.cuda.synchronize()
+    assert torch.equal(m.student_model.P.flat, before) and torch.equal(m.student_model.P.master, master)
+    if not raised:   # the loss kernel has finished now: the next call reports it
+        _attempt(lambda: m.training_step(good, 1), raised)
+    assert len(raised) == 1, raised
+    assert re.search(r"index -100 is out of bounds for dimension 2.*batch 1, position 37", raised[0]), raised
+    # reported once; a valid batch trains again
+    m.training_step(good, 2).backward()
+    opt.step()
+    m.check_errors()
+    assert not torch.equal(m.student_model.P.flat, before)
+
+
+@pytest.mark.skipif(not hasattr(torch.cuda, "_sleep"), reason="needs torch.cuda._sleep")
+def test_error_words_are_sticky_for_queued_steps(dev):
+    """A valid step queued behind a rejected one (the host has not seen the error yet)
+    does not update the weights either: the state after the report is the state before
+    the rejected batch, as after the reference's RuntimeError."""
+    K = _K()
+    meta, _ = load("lb")
+    m = K.LogitBasedKD("tiny-student", "tiny-teacher")
+    (opt,), _ = m.configure_optimizers()
+    good = batch(meta, dev)
+    bad = dict(good)
+    bad["labels"] = good["labels"].clone()
+    bad["labels"][0, 5] = -100
+    torch.cuda.synchronize()
+    before = m.student_model.P.flat.clone()
+    torch.cuda._sleep(2_000_000_000)   # hold the stream: both steps are queued before either runs
+    raised = []
+    for i, bt in enumerate((bad, good)):
+        _attempt(lambda: m.training_step(bt, i).backward(), raised)
+        _attempt(opt.step, raised)
+        opt.zero_grad()
+    _attempt(m.check_errors, raised)
+    torch.cuda.synchronize()
+    assert len(raised) == 1 and "index -100" in raised[0], raised
     assert torch.equal(m.student_model.P.flat, before)
 
 
@@ -67,6 +115,7 @@ def test_ce_only_accepts_minus100_and_rejects_out_of_vocab(dev):
     m.training_step(b, 1).backward()
     with pytest.raises(RuntimeError, match="out of bounds"):
         opt.step()
+        m.check_errors()
 
 
 @pytest.mark.parametrize("kind", ["lb", "fb"])

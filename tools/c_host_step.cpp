@@ -237,7 +237,7 @@ int main(int argc, char** argv) {
     float* ss2 = (float*)dalloc(4);
     HIP(hipMemsetAsync(ss2, 0, 4, main_s));
     KD(kd_sumsq(grad, ns, ss2, main_s));
-    KD(kd_adamw(master, sw, grad, m1, m2, ns, 1e-5f, 0.9f, 0.999f, 1e-8f, 1e-2f, 1, nullptr, main_s));
+    KD(kd_adamw(master, sw, grad, m1, m2, ns, 1e-5f, 0.9f, 0.999f, 1e-8f, 1e-2f, 1, nullptr, nullptr, 0, main_s));
     HIP(hipStreamSynchronize(main_s));
 
     float l4[4], g2;

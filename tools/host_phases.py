@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c1")
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--idle", action="store_true", help="synchronize before each step (host cost on an idle GPU)")
     a = ap.parse_args()
     import torch
     import bench
@@ -42,6 +43,8 @@ def main():
     wrap(OPS, "adamw", "ops.adamw")
     wrap(m, "_check_errors", "m._check_errors")
     for i in range(2 + a.steps):
+        if a.idle:
+            torch.cuda.synchronize()
         tm.clear()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
