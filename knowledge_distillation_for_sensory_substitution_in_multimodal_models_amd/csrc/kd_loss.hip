@@ -72,7 +72,7 @@ inline Layout make_layout(int B, int L, int V) {
     lo.lab_last = off; off = align16(off + (size_t)V * 4);
     lo.klo_last = off; off = align16(off + (size_t)V * 4);
     lo.mask = off;     off = align16(off + (size_t)((V + 63) / 64) * 8);
-    lo.ovr = off;      off = align16(off + (size_t)V * 4);
+    lo.ovr = off;      off = align16(off + (size_t)V * 8);   // q [V], then log2 q [V]
     lo.part_kl = off;  off = align16(off + rows * 4);
     lo.total = off;
     return lo;
@@ -310,7 +310,14 @@ __global__ void k_ovr_mask(const int* __restrict__ lab_last, const int* __restri
     // 64 | V, into ovr[0..1], racing with the block that owns them)
     if ((threadIdx.x & 63) == 0 && v < V) mask[v >> 6] = bits;
     // klogits are written second (DT:185) and win over the label columns (DT:184)
-    if (v < V) ovr[v] = kl >= 0 ? stats[kl].ovy : (ll >= 0 ? stats[ll].ovx : 0.f);
+    // {q, log2 q} with log2 q := 0 for q <= 0 (the KL term's 0 * log 0 = 0; a negative
+    // override contributes -q log c only, as in the generic path)
+    if (v < V) {
+        const float q = kl >= 0 ? stats[kl].ovy : (ll >= 0 ? stats[ll].ovx : 0.f);
+        // NaN marks a column without an override (the LoCa fast path's select)
+        ovr[v] = on ? q : __builtin_nanf("");
+        ovr[V + v] = q > 0.f ? __log2f(q) : 0.f;
+    }
 }
 
 template <int VARIANT>
@@ -450,6 +457,170 @@ loss_grad_body(const bf16* __restrict__ T_, int64_t ld_t,
     }
 }
 
+// LoCa fast path: the per-element arithmetic in base-2 log space with per-row constants
+// (the generic body above spends ~35 VALU + 3 exps per element in pass A and ~28 + 3 in
+// pass B, which made the kernel VALU-bound, not HBM-bound):
+//   lq = t*a - cq = log2 p_T,   lps = s*a - cs = log2 p_S,   a = log2(e) / T
+//   log2 c = max(lps, log2 clamp)   (c = clamp(p_S, min=1e-8), DT:162);  unc = lps >= log2 clamp
+//   pass A: term2 += q (log2 q - log2 c),  S += unc ? q : 0      (term = ln 2 * term2)
+//   pass B: g = kd_coef (p_S S - unc q) + cec (p1 - onehot),  p1 = p_S when T = 1
+// Overridden columns (LoCa's `loca[:, :, labels] = X` / klogits, DT:184-185) take q and
+// log2 q from the table (NaN = not overridden); a chunk loads it only when its mask byte
+// is set.  The CE's one-hot (one element per row) is rewritten after pass B by the lane
+// that owns it, with the same arithmetic.
+constexpr float KD_LOG2E = 1.4426950408889634f;
+constexpr float KD_LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ void bf16x8_to_f32(const bf16x8& x, float* f) {
+    const u32x4 u = __builtin_bit_cast(u32x4, x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        f[2 * k] = __uint_as_float(u[k] << 16);
+        f[2 * k + 1] = __uint_as_float(u[k] & 0xffff0000u);
+    }
+}
+
+struct LocaRow {
+    float a, cq, cs, cqk, c1, K, cec, lcl, kd_coef;
+};
+
+// pass B's gradient of one element from kd_coef * q (also the one-hot fix-up: identical
+// arithmetic)
+template <bool T1>
+__device__ __forceinline__ float loca_grad(const LocaRow& R, float qk, float s) {
+    const float lps = fmaf(s, R.a, -R.cs);
+    float g = fmaf(ex2(lps), R.K, lps >= R.lcl ? -qk : 0.f);
+    if (!T1) g = fmaf(ex2(fmaf(s, KD_LOG2E, -R.c1)), R.cec, g);
+    return g;
+}
+
+template <bool T1>
+__global__ void __launch_bounds__(LG_NT)
+k_loss_grad_loca(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
+                 int V, int rows, float invT, float clamp_min, const RowStats* __restrict__ stats,
+                 const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g, float kd_coef,
+                 float ce_coef_num, const float* __restrict__ n_valid, bf16* __restrict__ D_, int64_t ld_d,
+                 float* __restrict__ part_kl) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long smask[];
+    __shared__ float red[LG_NW];
+    const float nv = *n_valid;
+    const float ce_coef = nv > 0.f ? ce_coef_num / nv : 0.f;
+    const int tid = threadIdx.x;
+    const int nwords = (V + 63) / 64;
+    for (int i = tid; i < nwords; i += LG_NT) smask[i] = mask_g[i];
+    __syncthreads();
+    LocaRow R;
+    R.a = invT * KD_LOG2E;
+    R.lcl = log2f(clamp_min);
+    R.kd_coef = kd_coef;
+    const float lk = kd_coef > 0.f ? log2f(kd_coef) : -INFINITY;   // q * kd_coef = 2^(lq + lk)
+    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+        const RowStats st = stats[r];
+        const bf16* srow = S_ + (int64_t)r * ld_s;
+        const bf16* trow = T_ + (int64_t)r * ld_t;
+        R.cq = (st.mt * invT + logf(st.zt)) * KD_LOG2E;
+        R.cs = (st.ms * invT + logf(st.zs)) * KD_LOG2E;
+        // ---- pass A: KD term and S (element pairs in packed fp32: v_pk_fma / v_pk_add)
+        typedef __attribute__((ext_vector_type(2))) float f32x2;
+        const f32x2 a2 = {R.a, R.a}, cq2 = {R.cq, R.cq}, cs2 = {R.cs, R.cs};
+        f32x2 term2 = {0.f, 0.f}, sacc2 = {0.f, 0.f};
+        for (int v0 = tid * 8; v0 < V; v0 += LG_NT * 8 * LG_U) {
+            bf16x8 xtu[LG_U], xsu[LG_U];
+#pragma unroll
+            for (int u = 0; u < LG_U; ++u) {
+                const int v = v0 + u * LG_NT * 8;
+                if (v < V) { xtu[u] = *(const bf16x8*)(trow + v); xsu[u] = *(const bf16x8*)(srow + v); }
+            }
+#pragma unroll
+            for (int u = 0; u < LG_U; ++u) {
+                const int v = v0 + u * LG_NT * 8;
+                if (v >= V) break;
+                float t[8], sv[8], lq[8], q[8], lps[8];
+                bf16x8_to_f32(xtu[u], t);
+                bf16x8_to_f32(xsu[u], sv);
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    const f32x2 lq2 = f32x2{t[j], t[j + 1]} * a2 - cq2;
+                    const f32x2 lp2 = f32x2{sv[j], sv[j + 1]} * a2 - cs2;
+                    lq[j] = lq2.x; lq[j + 1] = lq2.y;
+                    lps[j] = lp2.x; lps[j + 1] = lp2.y;
+                    q[j] = ex2(lq[j]);
+                    q[j + 1] = ex2(lq[j + 1]);
+                }
+                if ((smask[v >> 6] >> (v & 63)) & 0xffu) {   // V % 8 == 0: aligned 16-B table loads
+                    const f32x4 o0 = *(const f32x4*)(ovr + v), o1 = *(const f32x4*)(ovr + v + 4);
+                    const f32x4 l0 = *(const f32x4*)(ovr + V + v), l1 = *(const f32x4*)(ovr + V + v + 4);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float o = j < 4 ? o0[j] : o1[j - 4];
+                        const bool on = o == o;
+                        q[j] = on ? o : q[j];
+                        lq[j] = on ? (j < 4 ? l0[j] : l1[j - 4]) : lq[j];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    const f32x2 q2 = {q[j], q[j + 1]};
+                    const f32x2 lc2 = {fmaxf(lps[j], R.lcl), fmaxf(lps[j + 1], R.lcl)};
+                    term2 = q2 * (f32x2{lq[j], lq[j + 1]} - lc2) + term2;
+                    sacc2 += f32x2{lps[j] >= R.lcl ? q[j] : 0.f, lps[j + 1] >= R.lcl ? q[j + 1] : 0.f};
+                }
+            }
+        }
+        const float term = block_sum<LG_NW>(term2.x + term2.y, red);
+        const float Ssum = block_sum<LG_NW>(sacc2.x + sacc2.y, red);
+        if (tid == 0) part_kl[r] = term * KD_LN2;
+        if (D_ == nullptr) continue;
+        // ---- pass B: dlogits
+        R.cec = st.valid ? ce_coef : 0.f;
+        R.K = kd_coef * Ssum + (T1 ? R.cec : 0.f);
+        R.cqk = R.cq - lk;
+        R.c1 = (st.ms + logf(st.zs1)) * KD_LOG2E;
+        bf16* drow = D_ + (int64_t)r * ld_d;
+        for (int v0 = tid * 8; v0 < V; v0 += LG_NT * 8 * LG_U) {
+            bf16x8 xtu[LG_U], xsu[LG_U];
+#pragma unroll
+            for (int u = 0; u < LG_U; ++u) {
+                const int v = v0 + u * LG_NT * 8;
+                if (v < V) { xsu[u] = *(const bf16x8*)(srow + v); xtu[u] = *(const bf16x8*)(trow + v); }
+            }
+#pragma unroll
+            for (int u = 0; u < LG_U; ++u) {
+                const int v = v0 + u * LG_NT * 8;
+                if (v >= V) break;
+                float t[8], sv[8], qk[8];
+                bf16x8_to_f32(xtu[u], t);
+                bf16x8_to_f32(xsu[u], sv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qk[j] = ex2(fmaf(t[j], R.a, -R.cqk));
+                if ((smask[v >> 6] >> (v & 63)) & 0xffu) {
+                    const f32x4 o0 = *(const f32x4*)(ovr + v), o1 = *(const f32x4*)(ovr + v + 4);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float o = j < 4 ? o0[j] : o1[j - 4];
+                        qk[j] = o == o ? o * kd_coef : qk[j];
+                    }
+                }
+                bf16x8 out;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) out[j] = (bf16)loca_grad<T1>(R, qk[j], sv[j]);
+                *(bf16x8*)(drow + v) = out;
+            }
+        }
+        // the CE one-hot: the lane that wrote labn's chunk rewrites that element (program
+        // order makes its second store land after the first)
+        const int labn = st.lab_next;
+        if (st.valid && ((labn >> 3) & (LG_NT - 1)) == tid) {
+            float qk = ex2(fmaf((float)trow[labn], R.a, -R.cqk));
+            if ((smask[labn >> 6] >> (labn & 63)) & 1ull) qk = ovr[labn] * kd_coef;
+            const float g = loca_grad<T1>(R, qk, (float)srow[labn]);
+            drow[labn] = (bf16)(g - R.cec);
+        }
+    }
+}
+
 __global__ void k_finalize(const RowStats* __restrict__ stats, const float* __restrict__ part_kl,
                            int rows, double kl_scale, float kd_weight, float ce_weight,
                            float out_scale, int out_acc, float* __restrict__ out) {
@@ -578,7 +749,14 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, \
                        V_s, rows, invT, p.clamp_min, stats, ovr, mask, kd_coef,                    \
                        ce_num, nvalid, D_, ld_d, part_kl)
-    switch (variant) {
+    const bool loca_fast = variant == KD_LOSS_LOCA && kd_coef >= 0.f && T_ != nullptr;
+    if (loca_fast && invT == 1.f) {
+        hipLaunchKernelGGL(k_loss_grad_loca<true>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, V_s,
+                           rows, invT, p.clamp_min, stats, ovr, mask, kd_coef, ce_num, nvalid, D_, ld_d, part_kl);
+    } else if (loca_fast) {
+        hipLaunchKernelGGL(k_loss_grad_loca<false>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, V_s,
+                           rows, invT, p.clamp_min, stats, ovr, mask, kd_coef, ce_num, nvalid, D_, ld_d, part_kl);
+    } else switch (variant) {
         case KD_LOSS_NONE: KD_LAUNCH_LG(KD_LOSS_NONE); break;
         case KD_LOSS_LOCA: KD_LAUNCH_LG(KD_LOSS_LOCA); break;
         case KD_LOSS_KL: KD_LAUNCH_LG(KD_LOSS_KL); break;

@@ -101,8 +101,10 @@ class FusedAdamW(torch.optim.Optimizer):
         if hi > lo:
             side = m._opt_stream
             side.wait_stream(torch.cuda.current_stream())
+            if m._bwd_pending:   # the backward runs on its own stream
+                side.wait_event(m._bwd_done)
             with torch.cuda.stream(side):
-                ops.adamw(P.master[lo:hi], P.flat[lo:hi], P.grad[lo:hi], P.exp_avg[lo:hi], P.exp_avg_sq[lo:hi],
+                ops.adamw(P.master[lo:hi], P.flat[lo:hi], P._grad[lo:hi], P.exp_avg[lo:hi], P.exp_avg_sq[lo:hi],
                           g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count,
                           skip_words=m._errors.words)
                 m._opt_done.record(side)
@@ -114,7 +116,7 @@ class FusedAdamW(torch.optim.Optimizer):
         lo, hi = m._trainable_range()
         if m._opt_pending:   # zero behind the AdamW on its stream; the next backward is ordered after it
             with torch.cuda.stream(m._opt_stream):
-                m.student_model.P.grad[lo:hi].zero_()
+                m.student_model.P._grad[lo:hi].zero_()
                 m._opt_done.record(m._opt_stream)
         else:
             m.student_model.P.grad[lo:hi].zero_()
@@ -223,11 +225,22 @@ class _KDBase(_Base):
             self.load_kd_state_dict(state_dict)
         self.config = self.student_model.cfg
         self._anchor = nn.Parameter(torch.zeros((), device=dev))
-        self._opt_stream = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
+        # one stream for all student work (forward, backward dgrad chain, AdamW, zero_grad):
+        # they are a dependency chain anyway, and HIP multiplexes more streams than hardware
+        # queues (GPU_MAX_HW_QUEUES, 4 by default) onto shared queues in enqueue order, which
+        # would put the next step's teacher forward behind this step's backward
         self._stu_stream = torch.cuda.Stream(device=dev, priority=STREAM_PRIORITY_HIGH)
+        self._opt_stream = self._stu_stream
         self.concurrent_student = True   # False: student forward on the main stream (bench.py --serial)
         self._opt_done = torch.cuda.Event()
         self._opt_pending = False
+        # the student backward runs on its own stream, so the next step's teacher forward
+        # (main stream; it reads no student state) overlaps it; whatever reads the student
+        # gradient or rewrites the saved activations waits for _bwd_done
+        self._bwd_stream = self._stu_stream
+        self._bwd_done = torch.cuda.Event()
+        self._bwd_pending = False
+        self.student_model.P.grad_fence = self._grad_fence
         self._ctx = None
         self._errors = _ErrorWatch(dev)
         self._errors.bind(self.student_model, self.teacher_model)
@@ -326,6 +339,8 @@ class _KDBase(_Base):
         # pole, large GEMMs that do not read student weights) is ENQUEUED first.
         side = self._stu_stream if self.concurrent_student else main
         side.wait_stream(main)
+        if self._bwd_pending:     # the saved activations of the last backward are rewritten
+            side.wait_event(self._bwd_done)
         if self._opt_pending:
             side.wait_event(self._opt_done)
             self._opt_pending = False
@@ -375,8 +390,26 @@ class _KDBase(_Base):
             self._ctx = dict(sfwd=sfwd, dlogits=dlogits, dps=dps)
         return total
 
+    def _grad_fence(self):
+        if self._bwd_pending:
+            torch.cuda.current_stream().wait_event(self._bwd_done)
+
     def _backward(self, gscale):
         ctx, self._ctx = self._ctx, None
+        main = torch.cuda.current_stream()
+        bwd = self._bwd_stream if self.concurrent_student else main
+        if bwd is not main:
+            bwd.wait_stream(main)
+            sf = ctx["sfwd"]
+            for t in (gscale, ctx["dlogits"], ctx["dps"], sf["hn"], sf["src"], sf["ids"], sf.get("post_ln")):
+                if t is not None:
+                    t.record_stream(bwd)   # freed on the host before the backward has run
+        with torch.cuda.stream(bwd):
+            self._backward_body(ctx, gscale)
+        self._bwd_done.record(bwd)
+        self._bwd_pending = bwd is not main
+
+    def _backward_body(self, ctx, gscale):
         s = self.student_model
         self._micro += 1
         sync = self._gsync is not None and self._no_sync_depth == 0 and \

@@ -183,9 +183,12 @@ class ParamStore:
         self.numel = (off + 7) // 8 * 8
         self.flat = torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device)
         self.trainable = trainable
+        # called before the flat gradient is handed out: the owner of a backward that runs
+        # on its own stream makes the reader's stream wait for it (kd_module)
+        self.grad_fence = None
         if trainable:
             self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
-            self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+            self._grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
             self.exp_avg = torch.zeros_like(self.master)
             self.exp_avg_sq = torch.zeros_like(self.master)
         self._views = {s.name: self.view(s.name) for s in self.specs}
@@ -194,6 +197,13 @@ class ParamStore:
         first_lm = self.offsets["language_model.model.embed_tokens.weight"][0]
         self.regions = {"vision": (0, first_proj), "projector": (first_proj, first_lm),
                         "language": (first_lm, self.numel)}
+
+    @property
+    def grad(self):
+        """The flat fp32 gradient, complete on the current stream."""
+        if self.grad_fence is not None:
+            self.grad_fence()
+        return self._grad
 
     # -- views
     def view(self, name, buf=None):
