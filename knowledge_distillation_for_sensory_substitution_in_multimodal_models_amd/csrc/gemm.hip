@@ -47,6 +47,10 @@ struct GemmP {
     int tile0;             // first linear tile (grouped order) of this launch: the split tail of a hybrid plan
     const float* sa;       // fp8 path: per-row scale of A [M] (dequantised A = sa[m] * qa[m, k])
     const float* sb;       // fp8 path: per-row scale of B [N] (per output channel)
+    // the launch grid, passed explicitly: a kernel that reads gridDim gets the 256-B block of
+    // hidden kernel arguments, and the HIP runtime's per-stream kernel-argument pool (~1 MB)
+    // then holds ~2000 queued GEMM launches instead of ~5000 before hipLaunchKernel blocks
+    int gx, gy;
 };
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
@@ -153,8 +157,8 @@ __host__ __device__ inline void tile_grouped(int wg, int tiles_m, int tiles_n, i
 
 // Block -> tile map: XCD-aware bijective remap (the blocks dispatched to one XCD, b, b+8,
 // ..., get consecutive ids), offset by the launch's first tile, then the grouped order.
-__device__ __forceinline__ void tile_of(int tiles_m, int tiles_n, int& tm, int& tn, int tile0 = 0) {
-    const int nwg = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ void tile_of(int nwg, int tiles_m, int tiles_n, int& tm, int& tn, int tile0 = 0) {
+    const int b = blockIdx.x;
     const int q8 = nwg / 8, r8 = nwg % 8, x = b % 8;
     const int wg = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + b / 8 + tile0;
     tile_grouped(wg, tiles_m, tiles_n, tm, tn);
@@ -166,7 +170,7 @@ __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
     int tm, tn;
-    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
+    tile_of(p.gx, (p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
 
     f32x4 acc[4][4];
@@ -541,7 +545,7 @@ __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[
 template <int BM, int BN, bool A_MN, bool B_MN, int NS = NST>
 __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     GemmP p = p_;
-    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
         const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
         p.K = (int)min((int64_t)p.K - k0, p.kchunk);
         p.A += A_MN ? k0 * p.lda : k0;
@@ -557,7 +561,7 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     int tm, tn;
-    tile_of((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn, p.tile0);
+    tile_of(p.gx, (p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn, p.tile0);
     const int m0 = tm * BM, n0 = tn * BN;
     __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
     if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
@@ -685,7 +689,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
     uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
     if (STAMP) ts0 = __builtin_amdgcn_s_memtime();
-    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
         const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
         p.K = (int)min((int64_t)p.K - k0, p.kchunk);
         p.A += A_MN ? k0 * p.lda : k0;
@@ -698,7 +702,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: LDS-DMA bases in SGPRs
     const int wm = wid >> 1, wn = wid & 1;
     int tm, tn;
-    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
+    tile_of(p.gx, (p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
     const int m0 = tm * 256, n0 = tn * 256;
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
@@ -846,7 +850,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         s_epi = te1 - te0;
         if (lane == 0) {
-            uint32_t* o = stamps + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wid) * 8;
+            uint32_t* o = stamps + ((int64_t)(blockIdx.y * p.gx + blockIdx.x) * 4 + wid) * 8;
             o[0] = (uint32_t)s_pro; o[1] = 0; o[2] = 0; o[3] = (uint32_t)s_bar;
             o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
         }
@@ -876,7 +880,7 @@ constexpr int NTH9 = 512;
 template <bool A_MN, bool B_MN>
 __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
     GemmP p = p_;
-    if (gridDim.y > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
         const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
         p.K = (int)min((int64_t)p.K - k0, p.kchunk);
         p.A += A_MN ? k0 * p.lda : k0;
@@ -889,7 +893,7 @@ __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wid >> 2, wc = wid & 3;
     int tm, tn;
-    tile_of((p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
+    tile_of(p.gx, (p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
     const int m0 = tm * 256, n0 = tn * 256;
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2;
@@ -1057,7 +1061,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8f8(GemmP p) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid >> 1, wn = wid & 1;
     int tm, tn;
-    tile_of((p.M + 255) / 256, glu ? (p.N / 256) : (p.N + 255) / 256, tm, tn, p.tile0);
+    tile_of(p.gx, (p.M + 255) / 256, glu ? (p.N / 256) : (p.N + 255) / 256, tm, tn, p.tile0);
     const int m0 = tm * 256, n0 = tn * 256, nb = tn * 128;
     const int K = p.K;
     const int nk = (K + 63) / 64, nk_full = K / 64;
@@ -1260,7 +1264,7 @@ __global__ void __launch_bounds__(256) k_quant_rows_f8(const bf16* __restrict__ 
 __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p, int BMr, int BNr) {
     int tm, tn;
     tile_grouped(p.tile0 + (int)blockIdx.x, (p.M + BMr - 1) / BMr, (p.N + BNr - 1) / BNr, tm, tn);
-    const int rows_per = BMr / (int)gridDim.y;
+    const int rows_per = BMr / p.gy;
     const int r0 = tm * BMr + (int)blockIdx.y * rows_per;
     const int r1 = min(r0 + rows_per, p.M);
     const int c0 = tn * BNr, cw = min(BNr, p.N - c0);
@@ -1418,12 +1422,14 @@ int launch_gemm_f8(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->N % 256 == 0, "gemm fp8 swiglu: N = 2I needs I % 128 == 0");
         KD_CHECK_ARG(!d->bias && !d->residual && !d->accumulate, "gemm fp8 swiglu: no bias / residual / accumulate");
         p.glu = d->N / 2; p.act = KD_ACT_NONE;
-        hipLaunchKernelGGL((k_gemm8f8<4, KD_ACT_NONE>), dim3(ceil_div(d->M, 256) * (d->N / 256)), dim3(NTH8), F8_LDS, st, p);
+        p.gx = ceil_div(d->M, 256) * (d->N / 256); p.gy = 1;
+        hipLaunchKernelGGL((k_gemm8f8<4, KD_ACT_NONE>), dim3(p.gx), dim3(NTH8), F8_LDS, st, p);
         KD_LAUNCH_CHECK("k_gemm8f8<swiglu>");
         return KD_OK;
     }
     KD_CHECK_ARG(!d->aux, "gemm fp8: aux (pre-activation) output only with KD_ACT_SWIGLU");
     const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256));
+    p.gx = (int)grid.x; p.gy = 1;
     switch (d->act) {
         case KD_ACT_GELU_TANH: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_GELU_TANH>), grid, dim3(NTH8), F8_LDS, st, p); break;
         case KD_ACT_GELU_ERF: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_GELU_ERF>), grid, dim3(NTH8), F8_LDS, st, p); break;
@@ -1490,6 +1496,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.act = d->act;
     p.res_mod = d->residual_row_mod;
     p.kchunk = d->K; p.split_stride = 0; p.glu = 0; p.tile0 = 0;
+    p.sa = p.sb = nullptr; p.gx = 0; p.gy = 1;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
@@ -1508,6 +1515,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         GemmP pk = p;
         pk.glu = d->N / 2; pk.act = KD_ACT_NONE;
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
+        pk.gx = (int)grid.x; pk.gy = 1;
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
         else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
@@ -1520,8 +1528,10 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         const int tbm = pl.var == 4 ? 128 : 256, tbn = pl.var == 3 ? 128 : 256;
         const int tiles = ceil_div(d->M, tbm) * ceil_div(d->N, tbn);
         // one launch of the planned kernel over linear tiles [q.tile0, q.tile0 + nt), gy K splits
-        auto launch_tiles = [&](const GemmP& q, int nt, unsigned gy) {
+        auto launch_tiles = [&](const GemmP& q0, int nt, unsigned gy) {
             const dim3 grid((unsigned)nt, gy);
+            GemmP q = q0;
+            q.gx = nt; q.gy = (int)gy;
             if (pl.var == 20) {   // v9
                 const size_t lds = gemm2_lds<256, 256>();
                 if (!amn && !bmn) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), lds, st, q);
@@ -1585,6 +1595,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_LAUNCH_CHECK("k_gemm (split tiles)");
         p.split_stride = (int64_t)d->M * d->N;
         p.tile0 = pl.dp_tiles;
+        p.gx = tiles - pl.dp_tiles; p.gy = tbm * tbn / 1024;
         // one float4 column chunk per thread: BM / (1024 / BN) row slabs of 1024 / BN rows per tile
         hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)(tiles - pl.dp_tiles), (unsigned)(tbm * tbn / 1024)), dim3(256), 0, st,
                            (const float*)d->workspace, pl.split, p, tbm, tbn);
@@ -1593,6 +1604,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     }
     const int tiles = ceil_div(d->M, BM) * ceil_div(d->N, BN);
     const size_t smem = 4 * TILE_BYTES;
+    p.gx = tiles; p.gy = 1;
     if (!amn && !bmn) hipLaunchKernelGGL((k_gemm<false, false>), dim3(tiles), dim3(NTH), smem, st, p);
     else if (!amn && bmn) hipLaunchKernelGGL((k_gemm<false, true>), dim3(tiles), dim3(NTH), smem, st, p);
     else if (amn && bmn) hipLaunchKernelGGL((k_gemm<true, true>), dim3(tiles), dim3(NTH), smem, st, p);

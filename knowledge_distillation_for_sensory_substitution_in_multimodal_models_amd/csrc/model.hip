@@ -254,6 +254,12 @@ struct GemmArgs {
     int split_k = 0;
 };
 
+// split-K default of the runtime's GEMMs (KD_GEMM_SPLIT_K: 0 = the cost model, 1 = never split)
+static const int g_split_default = [] {
+    const char* e = std::getenv("KD_GEMM_SPLIT_K");
+    return e ? std::atoi(e) : 0;
+}();
+
 int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int64_t ldc, const GemmArgs& g) {
     kd_gemm_desc d;
     std::memset(&d, 0, sizeof(d));
@@ -269,8 +275,8 @@ int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int6
     d.residual = g.residual; d.ldr = g.ldr;
     d.aux = g.aux; d.ld_aux = g.ld_aux;
     d.residual_row_mod = g.residual_row_mod;
-    d.split_k = g.split_k;
-    if (g.split_k != 1 && ws) { d.workspace = ws; d.workspace_bytes = SPLITK_WS; }
+    d.split_k = g.split_k ? g.split_k : g_split_default;
+    if (d.split_k != 1 && ws) { d.workspace = ws; d.workspace_bytes = SPLITK_WS; }
     return gemm_timed(&d, s);
 }
 

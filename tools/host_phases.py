@@ -40,8 +40,41 @@ def main():
             return r
         setattr(obj, name, g)
     wrap(m._errors, "check", "errors.check")
+    wrap(m._errors, "record", "errors.record")
+    if m.teacher_model is not None:
+        wrap(m.teacher_model, "forward", "teacher.forward")
+    wrap(m.student_model, "forward", "student.forward")
+    wrap(m.student_model, "backward", "student.backward")
+    wrap(m.student_model.wlane, "run", "wlane.run")
+    wrap(OPS, "kd_loss_fwd_bwd", "ops.kd_loss")
+    wrap(OPS, "gemm", "ops.gemm")
     wrap(OPS, "adamw", "ops.adamw")
     wrap(m, "_check_errors", "m._check_errors")
+    # GPU-side markers (elapsed ms from the step's first event): when the main stream reaches
+    # the teacher forward, when the teacher forward and the loss end, when the backward ends
+    marks = {}
+
+    def mark(name, stream=None):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream or torch.cuda.current_stream())
+        marks.setdefault(name, []).append(e)
+
+    tf = m.teacher_model.forward
+
+    def tf_marked(*args, **kw):
+        mark("teacher_start")
+        r = tf(*args, **kw)
+        mark("teacher_end")
+        return r
+    m.teacher_model.forward = tf_marked
+    bw = m._backward
+
+    def bw_marked(g):
+        mark("bwd_enqueued_main")
+        r = bw(g)
+        mark("bwd_end", m._bwd_stream)
+        return r
+    m._backward = bw_marked
     for i in range(2 + a.steps):
         if a.idle:
             torch.cuda.synchronize()
@@ -62,6 +95,10 @@ def main():
         print(f"step {i}: host ms training_step {d[0]} backward {d[1]} opt.step {d[2]} zero_grad {d[3]} "
               f"(total {round((t[-1] - t[0]) * 1e3, 1)}) inner {dict((k, round(v, 2)) for k, v in tm.items())}", flush=True)
     torch.cuda.synchronize()
+    base = marks["teacher_start"][0]
+    for k in range(len(marks["teacher_start"])):
+        row = {n: round(base.elapsed_time(v[k]), 1) for n, v in marks.items() if k < len(v)}
+        print("gpu marks step", k, row)
 
 
 if __name__ == "__main__":
