@@ -48,16 +48,22 @@ def main():
     wrap(m.student_model.wlane, "run", "wlane.run")
     wrap(OPS, "kd_loss_fwd_bwd", "ops.kd_loss")
     wrap(OPS, "gemm", "ops.gemm")
-    wrap(OPS, "adamw", "ops.adamw")
     wrap(m, "_check_errors", "m._check_errors")
     # GPU-side markers (elapsed ms from the step's first event): when the main stream reaches
     # the teacher forward, when the teacher forward and the loss end, when the backward ends
     marks = {}
 
+    hmarks = {}
+    t_host0 = [None]
+
     def mark(name, stream=None):
         e = torch.cuda.Event(enable_timing=True)
         e.record(stream or torch.cuda.current_stream())
         marks.setdefault(name, []).append(e)
+        now = time.perf_counter()
+        if t_host0[0] is None:
+            t_host0[0] = now
+        hmarks.setdefault(name, []).append(round((now - t_host0[0]) * 1e3, 1))
 
     tf = m.teacher_model.forward
 
@@ -75,6 +81,22 @@ def main():
         mark("bwd_end", m._bwd_stream)
         return r
     m._backward = bw_marked
+    sf = m.student_model.forward
+
+    def sf_marked(*args, **kw):
+        mark("student_start")
+        r = sf(*args, **kw)
+        mark("student_end")
+        return r
+    m.student_model.forward = sf_marked
+    ad = OPS.adamw
+
+    def ad_marked(*args, **kw):
+        mark("adamw_start")
+        r = ad(*args, **kw)
+        mark("adamw_end")
+        return r
+    OPS.adamw = ad_marked
     for i in range(2 + a.steps):
         if a.idle:
             torch.cuda.synchronize()
@@ -99,6 +121,7 @@ def main():
     for k in range(len(marks["teacher_start"])):
         row = {n: round(base.elapsed_time(v[k]), 1) for n, v in marks.items() if k < len(v)}
         print("gpu marks step", k, row)
+        print("host marks step", k, {n: v[k] for n, v in hmarks.items() if k < len(v)})
 
 
 if __name__ == "__main__":
