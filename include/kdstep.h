@@ -150,7 +150,9 @@ typedef struct {
     int32_t variant;          /* 0 auto (cost model); forced (tests/tools): 1 128x128 4-wave; 2|5 / 3|6 / 4|7
                                  256x256 / 256x128 / 128x256 8-wave; 16 256x256 4-wave (AGPR accumulators);
                                  17-19 diagnostic builds of 16 (tools/stamp_gemm.py, tools/ablate_gemm.py);
-                                 20 256x256 8-wave ping-pong (two wave groups alternate on each SIMD) */
+                                 20 256x256 8-wave ping-pong (two wave groups alternate on each SIMD);
+                                 21 stream-K on 16 (256 workgroups take equal runs of the tiles' k-steps,
+                                 shared tiles folded from fp32 partial planes; needs workspace) */
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;
@@ -170,8 +172,9 @@ typedef struct {
 size_t kd_gemm_workspace_size(const kd_gemm_desc* desc);
 
 /* The plan kd_gemm would run for `desc` (inspection only; no device work): kernel variant
- * (1 v1, 2/3/4 v3 256x256 / 256x128 / 128x256, 16 v8), K splits, and how many leading
- * tiles (whole waves of 256) run unsplit before the split tail (0 = every tile split). */
+ * (1 v1, 2/3/4 v3 256x256 / 256x128 / 128x256, 16 v8, 21 stream-K v8), K splits (stream-K:
+ * the partial planes its workspace holds), and how many leading tiles (whole waves of 256)
+ * run unsplit before the split tail (0 = every tile split). */
 int kd_gemm_plan(const kd_gemm_desc* desc, int32_t* variant, int32_t* split_k, int32_t* dp_tiles);
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream);

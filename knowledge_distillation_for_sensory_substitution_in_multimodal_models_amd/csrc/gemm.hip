@@ -51,7 +51,17 @@ struct GemmP {
     // hidden kernel arguments, and the HIP runtime's per-stream kernel-argument pool (~1 MB)
     // then holds ~2000 queued GEMM launches instead of ~5000 before hipLaunchKernel blocks
     int gx, gy;
+    // stream-K (v8): the launch's sk_grid workgroups split the tiles' sk_steps-deep K loops
+    // evenly (one workgroup's run may cover the end of one tile and the start of the next);
+    // a tile covered by several workgroups gets fp32 partial planes in sk_ws (plane stride
+    // split_stride, plane = the workgroup's piece index in that tile), folded by
+    // k_splitk_reduce. 0 = off.
+    int sk_steps, sk_grid;
+    float* sk_ws;
 };
+
+// stream-K: the workgroup whose run [floor(tot w / G), floor(tot (w+1) / G)) holds step s
+__host__ __device__ inline int sk_wg_of(int64_t s, int64_t tot, int G) { return (int)(((s + 1) * G - 1) / tot); }
 
 __device__ __forceinline__ uint32_t sw_k(int row) { return (uint32_t)((row >> 1) & 7); }
 __device__ __forceinline__ uint32_t sw_mn(int k) { return (uint32_t)(((k & 3) | (((k >> 3) & 1) << 2)) << 1); }
@@ -681,28 +691,18 @@ __device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, i
 // then carries no pre-activation output); bit 1 drops the in-loop DMA (timing ablation:
 // WRONG results); bit 6 re-reads stage 0 for every stage (same addresses, L2-hot:
 // separates issue cost from memory-system cost; WRONG results).
-template <bool A_MN, bool B_MN, int EXP = 0>
-__global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
+// one 256x256 output tile over p's K range (the whole K, a split-K plane or a stream-K piece)
+template <bool A_MN, bool B_MN, int EXP>
+__device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     constexpr bool STAMP = EXP & 1, NODMA = EXP & 2, HOT = EXP & 64;
-    GemmP p = p_;
     uint32_t* stamps = nullptr;
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
     uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
     if (STAMP) ts0 = __builtin_amdgcn_s_memtime();
-    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += A_MN ? k0 * p.lda : k0;
-        p.B += B_MN ? k0 * p.ldb : k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
     constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: LDS-DMA bases in SGPRs
     const int wm = wid >> 1, wn = wid & 1;
-    int tm, tn;
-    tile_of(p.gx, (p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
     const int m0 = tm * 256, n0 = tn * 256;
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
@@ -855,6 +855,50 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
             o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
         }
     }
+}
+
+template <bool A_MN, bool B_MN, int EXP = 0>
+__global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tiles_m = (p_.M + 255) / 256, tiles_n = (p_.N + 255) / 256;
+    if (p_.sk_steps > 0) {   // stream-K: this workgroup's run of the tiles' k-steps
+        const int nkt = p_.sk_steps, G = p_.sk_grid, w = blockIdx.x;
+        const int64_t tot = (int64_t)tiles_m * tiles_n * nkt;
+        int64_t s0 = tot * w / G;
+        const int64_t s1 = tot * (w + 1) / G;
+        while (s0 < s1) {
+            const int t = (int)(s0 / nkt);
+            const int64_t tb = (int64_t)t * nkt, e = min(s1, tb + nkt);
+            const int wf = sk_wg_of(tb, tot, G), wl = sk_wg_of(tb + nkt - 1, tot, G);
+            GemmP q = p_;
+            const int64_t k0 = (s0 - tb) * BK2;
+            q.K = (int)min((int64_t)p_.K - k0, (e - s0) * BK2);
+            q.A += A_MN ? k0 * q.lda : k0;
+            q.B += B_MN ? k0 * q.ldb : k0;
+            if (wl > wf) {   // a piece of a shared tile: plain fp32 partial plane
+                q.C = p_.sk_ws + (int64_t)(w - wf) * p_.split_stride;
+                q.ldc = p_.N; q.c_f32 = 1; q.accumulate = 0; q.alpha = 1.f; q.alpha_dev = nullptr;
+                q.bias = nullptr; q.aux = nullptr; q.resid = nullptr; q.act = KD_ACT_NONE;
+            }
+            int tm, tn;
+            tile_grouped(t, tiles_m, tiles_n, tm, tn);
+            g8_tile<A_MN, B_MN, EXP>(q, tm, tn, smem);
+            s0 = e;
+            __syncthreads();   // the next piece's DMA refills the LDS the epilogue staged through
+        }
+        return;
+    }
+    GemmP p = p_;
+    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += A_MN ? k0 * p.lda : k0;
+        p.B += B_MN ? k0 * p.ldb : k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    int tm, tn;
+    tile_of(p.gx, tiles_m, tiles_n, tm, tn, p.tile0);
+    g8_tile<A_MN, B_MN, EXP>(p, tm, tn, smem);
 }
 
 // =============================================================================
@@ -1263,7 +1307,14 @@ __global__ void __launch_bounds__(256) k_quant_rows_f8(const bf16* __restrict__ 
 // of a chunk issued together.
 __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p, int BMr, int BNr) {
     int tm, tn;
-    tile_grouped(p.tile0 + (int)blockIdx.x, (p.M + BMr - 1) / BMr, (p.N + BNr - 1) / BNr, tm, tn);
+    const int tiles_m = (p.M + BMr - 1) / BMr, tiles_n = (p.N + BNr - 1) / BNr;
+    tile_grouped(p.tile0 + (int)blockIdx.x, tiles_m, tiles_n, tm, tn);
+    if (p.sk_steps > 0) {   // stream-K: this tile's piece count; a one-piece tile is already final
+        const int64_t tot = (int64_t)tiles_m * tiles_n * p.sk_steps;
+        const int64_t tb = (int64_t)(p.tile0 + (int)blockIdx.x) * p.sk_steps;
+        S = sk_wg_of(tb + p.sk_steps - 1, tot, p.sk_grid) - sk_wg_of(tb, tot, p.sk_grid) + 1;
+        if (S <= 1) return;
+    }
     const int rows_per = BMr / p.gy;
     const int r0 = tm * BMr + (int)blockIdx.y * rows_per;
     const int r1 = min(r0 + rows_per, p.M);
@@ -1334,7 +1385,15 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
 // x S splits), priced by the same constants.
 // var: 2/3/4 v3 tiles, 16 v8, 20 v9; split > 1 with dp_tiles > 0: the first dp_tiles tiles (whole
 // waves of 256) run unsplit with the full epilogue, only the tail tiles are split-K
+// var 21: stream-K on v8 (split = the partial planes its workspace needs)
 struct GemmPlan { int var; int split; int64_t kchunk; int dp_tiles; };
+constexpr int SK_GRID = 256;   // stream-K workgroups: one per CU
+
+// stream-K pieces: at most this many workgroups share one tile (the workspace's planes)
+inline int sk_max_pieces(int64_t tiles, int64_t nk, int G) {
+    const int64_t per = tiles * nk / G;   // >= 1 k-step per workgroup (callers ensure tot >= G)
+    return (int)((nk - 1) / per + 2);
+}
 
 GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t M = d->M, N = d->N;
@@ -1382,6 +1441,25 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
                             ((double)S * tail * tb * 8 + tail * tb * out_e) / 7.458e6;
                 if (th < bt) { bt = th; best = GemmPlan{vcode[v], S, kcs * BK2, (int)dp}; }
             }
+        }
+    }
+    // stream-K on v8 (forced variant 21 only): SK_GRID workgroups take equal runs of the tiles'
+    // k-steps (runs cross tile boundaries); tiles shared by several runs fold fp32 partial
+    // planes. Measured slower than the split-K / hybrid plans on every backward shape of the
+    // step (1152x1152x5832 wgrad 71 vs 39 us, 6144x896x9728 dgrad 155 vs 149 us, down_proj
+    // 1020 vs 710 us): a run accumulates one tile over a contiguous K range, so the ~32
+    // workgroups of an XCD no longer share A / B k-slices in L2 (each tile's panels are
+    // fetched once per piece), and a sub-wave tile count makes every tile a shared one.
+    const int64_t tot = t256 * nk;
+    if (d->variant == 21 && d->split_k <= 0 && tot >= 2 * SK_GRID) {
+        const int64_t per = (tot + SK_GRID - 1) / SK_GRID;
+        const int pieces = sk_max_pieces(t256, nk, SK_GRID);
+        const double segs = 1.0 + (double)((per + nk - 1) / nk);
+        const double t_sk = (double)per * step[3] + segs * fixed[3] +
+                            ((double)(t256 + SK_GRID) * 65536.0 * 8.0 + out_b) / 7.458e6;
+        if ((uint64_t)pieces * M * N * 4 <= ws_cap) {
+            bt = t_sk;
+            best = GemmPlan{21, pieces, d->K, 0};
         }
     }
     return best;
@@ -1467,7 +1545,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->act == KD_ACT_NONE || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
                                           d->c_dtype == KD_DTYPE_BF16),
                  "gemm: an activation epilogue needs K-major operands and a bf16 output");
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 20), "gemm: unknown variant");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 21), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     KD_CHECK_SHAPE(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
@@ -1497,6 +1575,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.res_mod = d->residual_row_mod;
     p.kchunk = d->K; p.split_stride = 0; p.glu = 0; p.tile0 = 0;
     p.sa = p.sb = nullptr; p.gx = 0; p.gy = 1;
+    p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
@@ -1527,6 +1606,26 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
         const int tbm = pl.var == 4 ? 128 : 256, tbn = pl.var == 3 ? 128 : 256;
         const int tiles = ceil_div(d->M, tbm) * ceil_div(d->N, tbn);
+        if (pl.var == 21) {   // stream-K (v8), then the fold of the shared tiles
+            KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
+                         "gemm: stream-K workspace too small");
+            GemmP q = p;
+            q.sk_steps = ceil_div(d->K, BK2); q.sk_grid = SK_GRID; q.sk_ws = (float*)d->workspace;
+            q.split_stride = (int64_t)d->M * d->N;
+            q.gx = SK_GRID; q.gy = 1; q.tile0 = 0;
+            const size_t lds = gemm2_lds<256, 256>();
+            const dim3 grid(SK_GRID);
+            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, 0>), grid, dim3(NTH8), lds, st, q);
+            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, 0>), grid, dim3(NTH8), lds, st, q);
+            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, 0>), grid, dim3(NTH8), lds, st, q);
+            else hipLaunchKernelGGL((k_gemm8<true, false, 0>), grid, dim3(NTH8), lds, st, q);
+            KD_LAUNCH_CHECK("k_gemm8 (stream-K)");
+            q.gx = tiles; q.gy = 256 * 256 / 1024;
+            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)tiles, (unsigned)q.gy), dim3(256), 0, st,
+                               (const float*)d->workspace, 0, q, 256, 256);
+            KD_LAUNCH_CHECK("k_splitk_reduce (stream-K)");
+            return KD_OK;
+        }
         // one launch of the planned kernel over linear tiles [q.tile0, q.tile0 + nt), gy K splits
         auto launch_tiles = [&](const GemmP& q0, int nt, unsigned gy) {
             const dim3 grid((unsigned)nt, gy);

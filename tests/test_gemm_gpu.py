@@ -159,6 +159,48 @@ def test_splitk_all_layouts(split, variant, M, N, K, dev):
     assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(1152, 1152, 5832), (1000, 904, 4296), (6144, 5632, 256)])
+def test_stream_k_all_layouts(M, N, K, dev):
+    """Stream-K (variant 21): 256 workgroups take equal runs of the tiles' k-steps; shared
+    tiles are folded from fp32 partial planes, tiles a single run covers get the epilogue
+    directly (the 528-tile case). Ragged M / N / K tails; every operand layout; fp32 +=."""
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=60)
+    w = _rand(N, K, dev=dev, seed=61, scale=0.05)
+    _check(ops.gemm(a, w, variant=21), a.float() @ w.float().t())
+    wt = _rand(K, N, dev=dev, seed=63, scale=0.05)
+    _check(ops.gemm(a, wt.t(), variant=21), a.float() @ wt.float())
+    if M % 8 == 0:
+        at = _rand(K, M, dev=dev, seed=62)
+        _check(ops.gemm(at.t(), w, variant=21), at.float().t() @ w.float().t())
+        acc = torch.ones(M, N, dtype=torch.float32, device=dev)
+        ops.gemm(at.t(), wt.t(), out=acc, accumulate=True, variant=21)
+        ref = 1 + at.float().t() @ wt.float()
+        assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
+
+
+def test_stream_k_epilogue(dev):
+    """The stream-K fold and the direct tiles apply the whole epilogue: alpha * alpha_dev,
+    bias, aux, act, residual (row mod), bf16 accumulate."""
+    ops = _ops()
+    M, N, K = 1458, 1152, 4304
+    a = _rand(M, K, dev=dev, seed=64)
+    w = _rand(N, K, dev=dev, seed=65, scale=0.02)
+    bias = _rand(N, dev=dev, seed=66)
+    pos = _rand(729, N, dev=dev, seed=67)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    s = torch.tensor([0.5], device=dev)
+    pre = 0.5 * 2.0 * (a.float() @ w.float().t()) + bias.float()
+    out = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=pos, residual_row_mod=729, aux=aux, alpha=2.0,
+                   alpha_dev=s, variant=21)
+    _check(out, torch.nn.functional.gelu(pre, approximate="tanh") + pos.float().repeat(2, 1))
+    _check(aux, pre)
+    o = _rand(M, N, dev=dev, seed=68)
+    ref = o.float() + a.float() @ w.float().t()
+    ops.gemm(a, w, out=o, accumulate=True, variant=21)
+    _check(o, ref)
+
+
 def test_splitk_epilogue(dev):
     """The reduce pass applies the whole epilogue: alpha * alpha_dev, bias, aux, act,
     residual (row mod), bf16 accumulate."""
