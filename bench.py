@@ -1,6 +1,6 @@
 """KD training-step throughput on MI355X (BASELINE.json metric), one JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4] [--no-cpu-baseline] [--cpu-full]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4] [--no-cpu-baseline] [--cpu-extrapolate]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 A step = one `training_step(batch)` + `loss.backward()` + `optimizer.step()` +
@@ -144,9 +144,10 @@ def _oracle_step_time(kind, phase, depth, dtype, batch):
 
 def cpu_baseline(kind: str, phase: int, threads: int, full: bool = False):
     """The oracle (CPU torch restatement of the reference's step, kind `port`) at bs=1,
-    L=1536, full widths, in fp32 and bf16.  Default (bounded, ~1 min): depth 1 and 3 of
-    every tower, each timed twice (min), extrapolated to the full 26/28 + 26/24 layers by
-    the per-layer FLOP share of the depth 1 -> 3 delta.  full=True: one full-depth step."""
+    L=1536, full widths, in fp32 and bf16.  full=True (default, ~1 min on 16 threads): one
+    full-depth step of each.  full=False (--cpu-extrapolate): depth 1 and 3 of every tower,
+    each timed twice (min), extrapolated to the full 26/28 + 26/24 layers by the per-layer
+    FLOP share of the depth 1 -> 3 delta."""
     import torch
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
     torch.set_num_threads(threads)
@@ -272,13 +273,18 @@ def main():
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-full", action="store_true", help="cpu_baseline: one full-depth step instead of depth 1/3")
+    ap.add_argument("--cpu-extrapolate", action="store_true",
+                    help="cpu_baseline: depth-1/3 runs extrapolated by per-layer FLOP share instead of one "
+                         "full-depth step (the default since round 2: 43 s fp32 + 15 s bf16 on 16 threads)")
     ap.add_argument("--no-timer", action="store_true", help="skip the serialized roofline pass (per-GEMM HIP events)")
     ap.add_argument("--no-delta", action="store_true", help="skip kd_loss_delta (the CPU oracle on this step's logits)")
     ap.add_argument("--serial", action="store_true",
                     help="one stream: student forward and the weight gradients on the main stream (profiling)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
     ap.add_argument("--teacher-bf16", action="store_true", help="c4 with the bf16 teacher instead of fp8")
+    ap.add_argument("--no-teacher-rate", action="store_true",
+                    help="skip the teacher-forward rate pass (profiling runs: its launches would enter the "
+                         "roofline kernel's rocprof average)")
     a = ap.parse_args()
 
     import torch
@@ -405,7 +411,7 @@ def main():
                     measured="HIP events on the launch stream over 2 serialized steps after the timed region",
                     bf16_student_swiglu=None if not fwd else dict(avg_launch_us=round(fwd["avg_ms"] * 1e3, 2),
                                                                   tflops=round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 1)))
-    tfwd = teacher_forward_rate(m, batches[0]) if m.teacher_model is not None else None
+    tfwd = teacher_forward_rate(m, batches[0]) if (m.teacher_model is not None and not a.no_teacher_rate) else None
     out = {
         "metric": "KD samples/sec/step (7B->0.5B, 336x336)",
         "value": round(value, 4),
@@ -452,7 +458,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = host_cpu_info()[0]
         try:
-            out["cpu_baseline"] = cpu_baseline(cfg["kind"], cfg["phase"], threads, full=a.cpu_full)
+            out["cpu_baseline"] = cpu_baseline(cfg["kind"], cfg["phase"], threads, full=not a.cpu_extrapolate)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -99,7 +99,9 @@ class FusedAdamW(torch.optim.Optimizer):
         self.step_count += 1
         P = m.student_model.P
         if hi > lo:
-            side = m._opt_stream
+            # the student stream (beside the next teacher forward); the caller's stream when
+            # the module runs serialized (bench.py --serial, measurement)
+            side = m._opt_stream if m.concurrent_student else torch.cuda.current_stream()
             side.wait_stream(torch.cuda.current_stream())
             if m._bwd_pending:   # the backward runs on its own stream
                 side.wait_event(m._bwd_done)
@@ -114,7 +116,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         m = self.module
         lo, hi = m._trainable_range()
-        if m._opt_pending:   # zero behind the AdamW on its stream; the next backward is ordered after it
+        if m._opt_pending and m.concurrent_student:   # zero behind the AdamW on its stream
             with torch.cuda.stream(m._opt_stream):
                 m.student_model.P._grad[lo:hi].zero_()
                 m._opt_done.record(m._opt_stream)

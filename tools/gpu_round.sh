@@ -21,8 +21,8 @@ for s in $STEPS; do
     parity) timeout -k 10 300 python -u tools/parity_report.py --out gpurun_out/parity.json > gpurun_out/parity.log 2>&1 || { echo "parity failed"; tail -20 gpurun_out/parity.log; exit 1; } ;;
     bench)  timeout -k 10 900 python -u bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
             tail -1 gpurun_out/bench.log ;;
-    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-cpu-baseline --no-delta $BENCH_ARGS > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; } ;;
-    step)   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/profstep -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-delta --no-timer $BENCH_ARGS > gpurun_out/profstep.log 2>&1 || { echo "profstep failed"; tail -20 gpurun_out/profstep.log; exit 1; }
+    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-teacher-rate --no-cpu-baseline --no-delta $BENCH_ARGS > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; } ;;
+    step)   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/profstep -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-delta --no-timer --no-teacher-rate $BENCH_ARGS > gpurun_out/profstep.log 2>&1 || { echo "profstep failed"; tail -20 gpurun_out/profstep.log; exit 1; }
             python3 tools/step_breakdown.py $(ls gpurun_out/profstep/*/run_results.db gpurun_out/profstep/run_results.db 2>/dev/null | head -1) 40 > gpurun_out/step_breakdown.txt 2>&1; head -45 gpurun_out/step_breakdown.txt ;;
     pmc)    bash tools/pmc_bench.sh > gpurun_out/pmc_bench.log 2>&1 || { echo "pmc failed"; tail -10 gpurun_out/pmc_bench.log; exit 1; } ;;
     *) echo "unknown step $s"; exit 2 ;;
