@@ -22,6 +22,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace kd {
 namespace {
@@ -98,6 +99,15 @@ __device__ __forceinline__ bf16x4 tr_read_asm(const char* lds, int r, int d) {
     return __builtin_bit_cast(bf16x4, v);
 }
 
+// The same read from a precomputed per-lane LDS byte address plus an immediate offset (the
+// buffer / row part of the address is a compile-time constant in the unrolled tile loop).
+template <int OFF>
+__device__ __forceinline__ bf16x4 tr_read_off(uint32_t addr) {
+    u32x2 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+    return __builtin_bit_cast(bf16x4, v);
+}
+
 // NQ query sub-tiles of 16 rows per wave (workgroup = 4 waves x 16·NQ rows): every K
 // fragment (b128) and V^T fragment (tr_b16) read from LDS feeds NQ MFMAs, so LDS bytes
 // per FLOP drop by NQ (at NQ = 1 the kernel was bound by its LDS reads: one 64-key tile =
@@ -141,18 +151,33 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     const int nkv = CAUSAL ? min((qb + 1) * QBLK / 64, nkv_all) : nkv_all;
     stage_kv<HDP, false>(smem, K, 0, p.S, wid, lane);
     stage_kv<HDP, true>(smem + TILE, V, 0, p.S, wid, lane);
+    // per-lane LDS byte offsets of the fragment reads: the swizzles depend on the lane only,
+    // so the buffer, the key tile kt and the 32-key step ks are immediate offsets of the
+    // ds_read instructions in the tile loop (unrolled by two: even tiles read buffer 0)
+    int koff[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) koff[kk] = li * RB + (((kk * 4 + g) ^ swK<RB>(li)) << 4);
+    uint32_t vaddr[DT];
+    {
+        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+        const int r = 4 * g + (li >> 2);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+            const int dc = d * 16 + 4 * (li & 3);
+            vaddr[d] = sbase + TILE + r * RB + ((((dc >> 3) ^ swV<RB>(r))) << 4) + ((dc & 4) << 1);
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    for (int t = 0; t < nkv; ++t) {
-        const int cur = t & 1;
+    auto tile = [&](const int t, auto buf_c) {
+        constexpr int BUF = decltype(buf_c)::value;
         if (t + 1 < nkv) {
-            char* nb = smem + (cur ^ 1) * 2 * TILE;
+            char* nb = smem + (BUF ^ 1) * 2 * TILE;
             stage_kv<HDP, false>(nb, K, (t + 1) * 64, p.S, wid, lane);
             stage_kv<HDP, true>(nb + TILE, V, (t + 1) * 64, p.S, wid, lane);
         }
-        const char* kt_l = smem + cur * 2 * TILE;
-        const char* vt_l = kt_l + TILE;
+        const char* kt_l = smem + BUF * 2 * TILE;
         // ---- S^T tiles: rows = keys 16kt + 4g + r, col = the lane's query of sub-tile j
         f32x4 sc[NQ][4];
 #pragma unroll
@@ -161,7 +186,7 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
             for (int j = 0; j < NQ; ++j) sc[j][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kk = 0; kk < KS; ++kk) {
-                const bf16x8 kf = k_frag<RB>(kt_l, 16 * kt + li, kk * 4 + g);
+                const bf16x8 kf = *(const bf16x8*)(kt_l + koff[kk] + kt * 16 * RB);
 #pragma unroll
                 for (int j = 0; j < NQ; ++j)
                     sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[j][kk], sc[j][kt], 0, 0, 0);
@@ -170,6 +195,9 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
         // ---- online softmax in the log2 domain. The mask is applied only on tiles that
         // cross the causal diagonal or the sequence end (wave-uniform test); the scale is
         // folded into the exponent's fma; v_exp_f32 directly (exp2f adds range handling).
+        // Lazy rescale: the exponent reference m only moves when the tile's max exceeds it
+        // by more than 8 (P <= 2^8 otherwise, exact in fp32 accumulation and bf16 range), so
+        // the O rescale (8·DT multiplies per sub-tile) runs on a few tiles per row only.
         const int key0 = t * 64 + 4 * g;
         bf16x8 pf[NQ][2];
 #pragma unroll
@@ -191,9 +219,17 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
                 for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sc[j][kt][r]);
             mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
             mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-            const float mn = fmaxf(m[j], mt * p.scale_log2);   // scale > 0: max commutes
-            const float mref = (mn == -INFINITY) ? 0.f : mn;
-            const float alpha = __builtin_amdgcn_exp2f(m[j] - mref);
+            const float mts = mt * p.scale_log2;   // scale > 0: max commutes
+            const bool move = mts > m[j] + 8.f;   // also the first tile with a finite score (m = -inf)
+            if (__ballot(move)) {
+                const float mn = move ? mts : m[j];
+                const float alpha = __builtin_amdgcn_exp2f(m[j] - mn);   // m = -inf: 0 (O, l are 0)
+                l[j] *= alpha;
+#pragma unroll
+                for (int d = 0; d < DT; ++d) o[j][d] *= alpha;
+                m[j] = mn;
+            }
+            const float mref = (m[j] == -INFINITY) ? 0.f : m[j];
             float ls = 0.f;
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
@@ -203,27 +239,21 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
                     sc[j][kt][r] = e;
                     ls += e;
                 }
-            l[j] = l[j] * alpha + ls;
-            m[j] = mn;
-            if (__ballot(alpha != 1.f)) {   // once the running max settles, most tiles skip it
-#pragma unroll
-                for (int d = 0; d < DT; ++d) o[j][d] *= alpha;
-            }
+            l[j] += ls;
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) { pf[j][ks][r] = (bf16)sc[j][2 * ks][r]; pf[j][ks][4 + r] = (bf16)sc[j][2 * ks + 1][r]; }
         }
         // ---- O^T += V^T P^T, two 32-key steps; each V^T fragment feeds the NQ sub-tiles
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int kr = 32 * ks + 4 * g + (li >> 2);
+        auto pv = [&](auto ks_c) {
+            constexpr int KS_ = decltype(ks_c)::value;
+            constexpr int OFF0 = BUF * 2 * TILE + (32 * KS_) * RB, OFF1 = OFF0 + 16 * RB;
             bf16x4 v0[DT], v1[DT];
 #pragma unroll
             for (int d = 0; d < DT; ++d) {
-                const int dc = d * 16 + 4 * (li & 3);
-                v0[d] = tr_read_asm<RB>(vt_l, kr, dc);
-                v1[d] = tr_read_asm<RB>(vt_l, kr + 16, dc);
+                v0[d] = tr_read_off<OFF0>(vaddr[d]);
+                v1[d] = tr_read_off<OFF1>(vaddr[d]);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
@@ -233,12 +263,20 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
                 vf[0] = v0[d][0]; vf[1] = v0[d][1]; vf[2] = v0[d][2]; vf[3] = v0[d][3];
                 vf[4] = v1[d][0]; vf[5] = v1[d][1]; vf[6] = v1[d][2]; vf[7] = v1[d][3];
 #pragma unroll
-                for (int j = 0; j < NQ; ++j) o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[j][ks], o[j][d], 0, 0, 0);
+                for (int j = 0; j < NQ; ++j) o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[j][KS_], o[j][d], 0, 0, 0);
             }
-        }
+        };
+        pv(std::integral_constant<int, 0>{});
+        pv(std::integral_constant<int, 1>{});
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+    };
+    int t = 0;
+    for (; t + 1 < nkv; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        tile(t + 1, std::integral_constant<int, 1>{});
     }
+    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
         float lj = l[j];
