@@ -116,6 +116,11 @@ template <int HDP, bool CAUSAL, int NQ>
 __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
     constexpr int TILE = 64 * RB;
+    // HDP 96 holds hd <= 80 (SigLIP: 72): the QK^T products take two 32-deep MFMA steps and
+    // one 16-deep step (v_mfma_f32_16x16x16_bf16) over dims [64, 80) instead of a third
+    // 32-deep step over zero padding
+    constexpr bool HALF = HDP == 96;
+    constexpr int KSF = HALF ? KS - 1 : KS;
     constexpr int QBLK = 64 * NQ;   // query rows per workgroup
     extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][K TILE | V TILE]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -131,13 +136,16 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     for (int j = 0; j < NQ; ++j) myq[j] = qb * QBLK + wid * 16 * NQ + j * 16 + li;
 
     bf16x8 qf[NQ][KS];
+    bf16x4 qh[NQ];
 #pragma unroll
-    for (int j = 0; j < NQ; ++j)
+    for (int j = 0; j < NQ; ++j) {
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
+        for (int kk = 0; kk < KSF; ++kk) {
             if (myq[j] < p.S) qf[j][kk] = *(const bf16x8*)(Q + (int64_t)myq[j] * HDP + kk * 32 + 8 * g);
             else qf[j][kk] = (bf16x8){};
         }
+        if (HALF) qh[j] = myq[j] < p.S ? *(const bf16x4*)(Q + (int64_t)myq[j] * HDP + KSF * 32 + 4 * g) : (bf16x4){};
+    }
     f32x4 o[NQ][DT];
 #pragma unroll
     for (int j = 0; j < NQ; ++j)
@@ -157,6 +165,8 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     int koff[KS];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) koff[kk] = li * RB + (((kk * 4 + g) ^ swK<RB>(li)) << 4);
+    // the 16-deep step's A fragment: row li, dims 32 KSF + 4g + [0, 4) = 8 B of chunk 4 KSF + g/2
+    const int khoff = li * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(li)) << 4) + (g & 1) * 8;
     uint32_t vaddr[DT];
     {
         const uint32_t sbase = (uint32_t)(uintptr_t)smem;
@@ -185,11 +195,17 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
 #pragma unroll
             for (int j = 0; j < NQ; ++j) sc[j][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
+            for (int kk = 0; kk < KSF; ++kk) {
                 const bf16x8 kf = *(const bf16x8*)(kt_l + koff[kk] + kt * 16 * RB);
 #pragma unroll
                 for (int j = 0; j < NQ; ++j)
                     sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[j][kk], sc[j][kt], 0, 0, 0);
+            }
+            if (HALF) {
+                const bf16x4 kh = *(const bf16x4*)(kt_l + khoff + kt * 16 * RB);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kh, qh[j], sc[j][kt], 0, 0, 0);
             }
         }
         // ---- online softmax in the log2 domain. The mask is applied only on tiles that
