@@ -392,6 +392,8 @@ template <int HDP, bool CAUSAL>
 __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
     constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
     constexpr int TILE = 64 * RB, BUF = 2 * TILE + 512;
+    constexpr bool HALF = HDP == 96;   // hd <= 80: a 16-deep last step (see k_attn_fwd)
+    constexpr int KSF = HALF ? KS - 1 : KS;
     extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][Q TILE | dO TILE | lse2 64 | delta 64]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = lane >> 4, li = lane & 15;
@@ -408,14 +410,19 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
     const int mykey = kb0 + wid * 16 + li;
 
     bf16x8 kf[KS], vf[KS];
+    bf16x4 kh = {}, vh = {};
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
+    for (int kk = 0; kk < KSF; ++kk) {
         if (mykey < p.S) {
             kf[kk] = *(const bf16x8*)(K + (int64_t)mykey * HDP + kk * 32 + 8 * g);
             vf[kk] = *(const bf16x8*)(V + (int64_t)mykey * HDP + kk * 32 + 8 * g);
         } else {
             kf[kk] = (bf16x8){}; vf[kk] = (bf16x8){};
         }
+    }
+    if (HALF && mykey < p.S) {
+        kh = *(const bf16x4*)(K + (int64_t)mykey * HDP + KSF * 32 + 4 * g);
+        vh = *(const bf16x4*)(V + (int64_t)mykey * HDP + KSF * 32 + 4 * g);
     }
     f32x4 dk[DT], dv[DT];
 #pragma unroll
@@ -449,9 +456,15 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
             s[qs] = (f32x4){0.f, 0.f, 0.f, 0.f};
             dp[qs] = s[qs];
 #pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
+            for (int kk = 0; kk < KSF; ++kk) {
                 s[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lQ, 16 * qs + li, kk * 4 + g), kf[kk], s[qs], 0, 0, 0);
                 dp[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lO, 16 * qs + li, kk * 4 + g), vf[kk], dp[qs], 0, 0, 0);
+            }
+            if (HALF) {
+                const int row = 16 * qs + li;
+                const int off = row * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(row)) << 4) + (g & 1) * 8;
+                s[qs] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*(const bf16x4*)(lQ + off), kh, s[qs], 0, 0, 0);
+                dp[qs] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*(const bf16x4*)(lO + off), vh, dp[qs], 0, 0, 0);
             }
         }
         // mask only where the tile crosses the diagonal or an edge (wave-uniform test)
@@ -557,6 +570,8 @@ template <int HDP, bool CAUSAL, int NQ>
 __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
     constexpr int TILE = 64 * RB;
+    constexpr bool HALF = HDP == 96;   // hd <= 80: a 16-deep last step (see k_attn_fwd)
+    constexpr int KSF = HALF ? KS - 1 : KS;
     constexpr int QBLK = 64 * NQ;
     extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][K TILE | V TILE]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -570,6 +585,7 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     int myq[NQ];
     bool qok[NQ];
     bf16x8 qf[NQ][KS], df[NQ][KS];
+    bf16x4 qh[NQ], dh[NQ];
     float lse2[NQ], dl[NQ];
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
@@ -577,10 +593,15 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
         qok[j] = myq[j] < p.S;
         const bf16* dOr = p.dO + (((int64_t)b * p.S + myq[j]) * p.H + h) * p.hd;
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
+        for (int kk = 0; kk < KSF; ++kk) {
             const int d0 = kk * 32 + 8 * g;
             qf[j][kk] = qok[j] ? *(const bf16x8*)(Q + (int64_t)myq[j] * HDP + d0) : (bf16x8){};
             df[j][kk] = (qok[j] && d0 < p.hd) ? *(const bf16x8*)(dOr + d0) : (bf16x8){};
+        }
+        if (HALF) {   // dims 32 KSF + 4g + [0, 4); dO rows hold hd (a multiple of 4) columns
+            const int d0 = KSF * 32 + 4 * g;
+            qh[j] = qok[j] ? *(const bf16x4*)(Q + (int64_t)myq[j] * HDP + d0) : (bf16x4){};
+            dh[j] = (qok[j] && d0 < p.hd) ? *(const bf16x4*)(dOr + d0) : (bf16x4){};
         }
         lse2[j] = qok[j] ? p.lse[((int64_t)b * p.H + h) * p.S + myq[j]] * 1.4426950408889634f : 0.f;
         dl[j] = qok[j] ? p.delta[((int64_t)b * p.H + h) * p.S + myq[j]] : 0.f;
@@ -613,13 +634,23 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 #pragma unroll
             for (int j = 0; j < NQ; ++j) { sc[j][kt] = (f32x4){0.f, 0.f, 0.f, 0.f}; dp[j][kt] = sc[j][kt]; }
 #pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
+            for (int kk = 0; kk < KSF; ++kk) {
                 const bf16x8 kf = k_frag<RB>(lK, 16 * kt + li, kk * 4 + g);
                 const bf16x8 vf = k_frag<RB>(lV, 16 * kt + li, kk * 4 + g);
 #pragma unroll
                 for (int j = 0; j < NQ; ++j) {
                     sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[j][kk], sc[j][kt], 0, 0, 0);
                     dp[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[j][kk], dp[j][kt], 0, 0, 0);
+                }
+            }
+            if (HALF) {
+                const int row = 16 * kt + li;
+                const int off = row * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(row)) << 4) + (g & 1) * 8;
+                const bf16x4 kh = *(const bf16x4*)(lK + off), vh = *(const bf16x4*)(lV + off);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kh, qh[j], sc[j][kt], 0, 0, 0);
+                    dp[j][kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vh, dh[j], dp[j][kt], 0, 0, 0);
                 }
             }
         }
