@@ -93,18 +93,21 @@ class FusedAdamW(torch.optim.Optimizer):
         # side, no host wait); the host raises as soon as it sees them
         m._check_errors(block=False)
         lo, hi = m._trainable_range()
+        # the student stream (beside the next teacher forward); the caller's stream when
+        # the module runs serialized (bench.py --serial, measurement)
+        side = m._opt_stream if m.concurrent_student else torch.cuda.current_stream()
+        side.wait_stream(torch.cuda.current_stream())
+        if m._bwd_pending:   # the backward runs on its own stream
+            side.wait_event(m._bwd_done)
         if m._gsync is not None:
-            m._gsync.finish(lo, hi)
+            # the all-reduce's completion is awaited on the student stream only: the caller's
+            # stream (the next teacher forward) does not queue behind the collective
+            with torch.cuda.stream(side):
+                m._gsync.finish(lo, hi)
         m._micro = 0
         self.step_count += 1
         P = m.student_model.P
         if hi > lo:
-            # the student stream (beside the next teacher forward); the caller's stream when
-            # the module runs serialized (bench.py --serial, measurement)
-            side = m._opt_stream if m.concurrent_student else torch.cuda.current_stream()
-            side.wait_stream(torch.cuda.current_stream())
-            if m._bwd_pending:   # the backward runs on its own stream
-                side.wait_event(m._bwd_done)
             with torch.cuda.stream(side):
                 ops.adamw(P.master[lo:hi], P.flat[lo:hi], P._grad[lo:hi], P.exp_avg[lo:hi], P.exp_avg_sq[lo:hi],
                           g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count,
@@ -395,6 +398,8 @@ class _KDBase(_Base):
     def _grad_fence(self):
         if self._bwd_pending:
             torch.cuda.current_stream().wait_event(self._bwd_done)
+        if self._gsync is not None and self._gsync.works:
+            self._gsync.wait()   # reading .grad after backward sees the reduced gradient (DDP)
 
     def _backward(self, gscale):
         ctx, self._ctx = self._ctx, None

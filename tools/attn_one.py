@@ -1,5 +1,5 @@
 """Run one attention forward shape repeatedly (for rocprofv3 PMC passes).
-    python tools/attn_one.py teacher|student|siglip [iters]"""
+    python tools/attn_one.py teacher|student|siglip [iters] [bwd]"""
 import sys
 from pathlib import Path
 
@@ -17,7 +17,13 @@ g = torch.Generator(device=dev).manual_seed(0)
 q = torch.randn(B, H, S, hdp, device=dev, generator=g).bfloat16()
 k = torch.randn(B, HKV, S, hdp, device=dev, generator=g).bfloat16()
 v = torch.randn(B, HKV, S, hdp, device=dev, generator=g).bfloat16()
+bwd = len(sys.argv) > 3 and sys.argv[3] == "bwd"
+o, lse = ops.attn_fwd(q, k, v, hd, causal)
+do = torch.randn(B, S, H, hd, device=dev, generator=g).bfloat16()
 for _ in range(it):
-    ops.attn_fwd(q, k, v, hd, causal)
+    if bwd:
+        ops.attn_bwd(q, k, v, o, do, lse, hd, causal)
+    else:
+        ops.attn_fwd(q, k, v, hd, causal)
 torch.cuda.synchronize()
 print("done")
