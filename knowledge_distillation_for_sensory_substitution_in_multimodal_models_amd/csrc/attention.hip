@@ -29,6 +29,7 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 constexpr uint32_t OOB = 0x80000000u;
 
 struct AttnP {
@@ -126,8 +127,10 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = lane >> 4, li = lane & 15;
     const int nqb = (p.S + QBLK - 1) / QBLK;
-    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-    const int h = blockIdx.y, b = blockIdx.z, kvh = h / (p.H / p.HKV);
+    // grid (H, B, query blocks): every head's longest causal block is dispatched first, the
+    // shortest fill the tail
+    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
+    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
@@ -395,10 +398,12 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
     constexpr bool HALF = HDP == 96;   // hd <= 80: a 16-deep last step (see k_attn_fwd)
     constexpr int KSF = HALF ? KS - 1 : KS;
     extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][Q TILE | dO TILE | lse2 64 | delta 64]
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // the wave index is wave-uniform (readfirstlane): the edge test below is a scalar branch
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, li = lane & 15;
-    const int kb0 = blockIdx.x * 64;
-    const int h = blockIdx.y, b = blockIdx.z;
+    // grid (H, B, key blocks): key block 0 (the most causal query tiles) of every head first
+    const int kb0 = blockIdx.z * 64;
+    const int h = blockIdx.x, b = blockIdx.y;
     const int grp = p.H / p.HKV, kvh = h / grp;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
@@ -428,18 +433,40 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
 #pragma unroll
     for (int d = 0; d < DT; ++d) { dk[d] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
 
+    // per-lane LDS byte offsets inside one buffer (the swizzles depend on the lane only):
+    // row fragments (rows 16qs + li, + 16 qs RB immediate), the 16-deep step's fragment, and
+    // the transposed reads (rows 32ks + 4g + li/4 (+16): + (32ks + 16) RB immediate)
+    int qoff[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) qoff[kk] = li * RB + (((kk * 4 + g) ^ swK<RB>(li)) << 4);
+    const int qhoff = li * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(li)) << 4) + (g & 1) * 8;
+    int troff[DT];
+    {
+        const int r = 4 * g + (li >> 2);
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+            troff[d] = r * RB + (((2 * d + ((li & 3) >> 1)) ^ swK<RB>(r)) << 4) + (li & 1) * 8;
+    }
+
     const int nqt = (p.S + 63) / 64;
-    const int qt0 = CAUSAL ? (int)blockIdx.x : 0;
+    const int qt0 = CAUSAL ? (int)blockIdx.z : 0;
+    // lse reaches LDS pre-scaled to log2 units (wave 0: a register load issued with the
+    // tile's DMA, written after the tile's compute), delta by LDS-DMA
+    float lse_nx = 0.f;
     auto stage = [&](char* buf, int qt) {
         stage_kv<HDP, false>(buf, Q, qt * 64, p.S, wid, lane);
         stage_rows_dma<HDP>(buf + TILE, dO, ldo, p.hd, qt * 64, p.S, wid, lane);
         if (wid == 0) {
-            stage_vec64((float*)(buf + 2 * TILE), LSE, qt * 64, p.S, lane);
+            lse_nx = qt * 64 + lane < p.S ? LSE[qt * 64 + lane] : 0.f;
             stage_vec64((float*)(buf + 2 * TILE + 256), DEL, qt * 64, p.S, lane);
         }
     };
+    auto put_lse = [&](char* buf) {
+        if (wid == 0) ((float*)(buf + 2 * TILE))[lane] = lse_nx * 1.4426950408889634f;
+    };
     stage(smem, qt0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    put_lse(smem);
     __syncthreads();
     for (int qt = qt0; qt < nqt; ++qt) {
         const int cur = (qt - qt0) & 1;
@@ -457,29 +484,47 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
             dp[qs] = s[qs];
 #pragma unroll
             for (int kk = 0; kk < KSF; ++kk) {
-                s[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lQ, 16 * qs + li, kk * 4 + g), kf[kk], s[qs], 0, 0, 0);
-                dp[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k_frag<RB>(lO, 16 * qs + li, kk * 4 + g), vf[kk], dp[qs], 0, 0, 0);
+                s[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(lQ + qoff[kk] + qs * 16 * RB), kf[kk],
+                                                               s[qs], 0, 0, 0);
+                dp[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(lO + qoff[kk] + qs * 16 * RB), vf[kk],
+                                                                dp[qs], 0, 0, 0);
             }
             if (HALF) {
-                const int row = 16 * qs + li;
-                const int off = row * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(row)) << 4) + (g & 1) * 8;
-                s[qs] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*(const bf16x4*)(lQ + off), kh, s[qs], 0, 0, 0);
-                dp[qs] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*(const bf16x4*)(lO + off), vh, dp[qs], 0, 0, 0);
+                s[qs] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*(const bf16x4*)(lQ + qhoff + qs * 16 * RB), kh, s[qs],
+                                                                 0, 0, 0);
+                dp[qs] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(*(const bf16x4*)(lO + qhoff + qs * 16 * RB), vh, dp[qs],
+                                                                  0, 0, 0);
             }
         }
-        // mask only where the tile crosses the diagonal or an edge (wave-uniform test)
-        const bool edge = q0 + 63 >= p.S || kb0 + wid * 16 + 15 >= p.S || (CAUSAL && kb0 + wid * 16 + 15 > q0);
+        // mask only where the tile crosses the diagonal or an edge (wave-uniform branch):
+        // masked scores become -inf, so P = 0 there (the empty volatile asm keeps the branch:
+        // hipcc would otherwise speculate the compares into every tile)
+        if (q0 + 63 >= p.S || kb0 + wid * 16 + 15 >= p.S || (CAUSAL && kb0 + wid * 16 + 15 > q0)) {
+            asm volatile("" ::: "memory");
 #pragma unroll
-        for (int qs = 0; qs < 4; ++qs)
+            for (int qs = 0; qs < 4; ++qs)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int ql = 16 * qs + 4 * g + r, q = q0 + ql;
-                float pv = __builtin_amdgcn_exp2f(fmaf(s[qs][r], p.scale_log2, -lL[ql] * 1.4426950408889634f));
-                if (edge && (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q))) pv = 0.f;
-                s[qs][r] = pv;
-                dp[qs][r] = pv * (dp[qs][r] - lD[ql]);
+                for (int r = 0; r < 4; ++r) {
+                    const int q = q0 + 16 * qs + 4 * g + r;
+                    if (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q)) s[qs][r] = -INFINITY;
+                }
+        }
+        // P = 2^(s·scale_log2 - lse2), dS = P (dP - delta): packed fp32 pairs (v_pk_fma / add / mul)
+        const f32x2 sl2 = {p.scale_log2, p.scale_log2};
+#pragma unroll
+        for (int qs = 0; qs < 4; ++qs) {
+            const f32x4 l2 = *(const f32x4*)(lL + 16 * qs + 4 * g), dl = *(const f32x4*)(lD + 16 * qs + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+                const f32x2 x = f32x2{s[qs][r], s[qs][r + 1]} * sl2 - f32x2{l2[r], l2[r + 1]};
+                const f32x2 pv = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+                const f32x2 ds = pv * (f32x2{dp[qs][r], dp[qs][r + 1]} - f32x2{dl[r], dl[r + 1]});
+                s[qs][r] = pv[0]; s[qs][r + 1] = pv[1];
+                dp[qs][r] = ds[0]; dp[qs][r + 1] = ds[1];
             }
+        }
         // dV^T += dO^T P ; dK^T += Q^T dS over two 32-query steps
+        const uint32_t bq = (uint32_t)(uintptr_t)lQ;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             bf16x8 pfr, dsf;
@@ -488,15 +533,21 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
                 pfr[r] = (bf16)s[2 * ks][r]; pfr[4 + r] = (bf16)s[2 * ks + 1][r];
                 dsf[r] = (bf16)dp[2 * ks][r]; dsf[4 + r] = (bf16)dp[2 * ks + 1][r];
             }
-            const int qr = 32 * ks + 4 * g + (li >> 2);
             bf16x4 o0[DT], o1[DT], x0[DT], x1[DT];
 #pragma unroll
             for (int d = 0; d < DT; ++d) {
-                const int dc = d * 16 + 4 * (li & 3);
-                o0[d] = tr_read_k_asm<RB>(lO, qr, dc);
-                o1[d] = tr_read_k_asm<RB>(lO, qr + 16, dc);
-                x0[d] = tr_read_k_asm<RB>(lQ, qr, dc);
-                x1[d] = tr_read_k_asm<RB>(lQ, qr + 16, dc);
+                const uint32_t a = bq + troff[d];
+                if (ks == 0) {
+                    o0[d] = tr_read_off<TILE>(a);
+                    o1[d] = tr_read_off<TILE + 16 * RB>(a);
+                    x0[d] = tr_read_off<0>(a);
+                    x1[d] = tr_read_off<16 * RB>(a);
+                } else {
+                    o0[d] = tr_read_off<TILE + 32 * RB>(a);
+                    o1[d] = tr_read_off<TILE + 48 * RB>(a);
+                    x0[d] = tr_read_off<32 * RB>(a);
+                    x1[d] = tr_read_off<48 * RB>(a);
+                }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
@@ -507,6 +558,7 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (qt + 1 < nqt) put_lse(smem + (cur ^ 1) * BUF);
         __syncthreads();
     }
     // lane owns key = mykey, d = 16d + 4g + r
@@ -574,11 +626,14 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     constexpr int KSF = HALF ? KS - 1 : KS;
     constexpr int QBLK = 64 * NQ;
     extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][K TILE | V TILE]
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // wave-uniform wave index (readfirstlane): the per-sub-tile edge test is a scalar branch
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, li = lane & 15;
     const int nqb = (p.S + QBLK - 1) / QBLK;
-    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-    const int h = blockIdx.y, b = blockIdx.z, kvh = h / (p.H / p.HKV);
+    // grid (H, B, query blocks): every head's longest causal block is dispatched first, the
+    // shortest fill the tail
+    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
+    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
@@ -612,6 +667,18 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 #pragma unroll
         for (int d = 0; d < DT; ++d) acc[j][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+    // per-lane LDS byte offsets inside one buffer (see k_attn_bwd_dkdv)
+    int koff[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) koff[kk] = li * RB + (((kk * 4 + g) ^ swK<RB>(li)) << 4);
+    const int khoff = li * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(li)) << 4) + (g & 1) * 8;
+    int troff[DT];
+    {
+        const int r = 4 * g + (li >> 2);
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+            troff[d] = r * RB + (((2 * d + ((li & 3) >> 1)) ^ swK<RB>(r)) << 4) + (li & 1) * 8;
+    }
     const int nkv_all = (p.S + 63) / 64;
     const int nkv = CAUSAL ? min((qb + 1) * QBLK / 64, nkv_all) : nkv_all;
     stage_kv<HDP, false>(smem, K, 0, p.S, wid, lane);
@@ -635,8 +702,8 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
             for (int j = 0; j < NQ; ++j) { sc[j][kt] = (f32x4){0.f, 0.f, 0.f, 0.f}; dp[j][kt] = sc[j][kt]; }
 #pragma unroll
             for (int kk = 0; kk < KSF; ++kk) {
-                const bf16x8 kf = k_frag<RB>(lK, 16 * kt + li, kk * 4 + g);
-                const bf16x8 vf = k_frag<RB>(lV, 16 * kt + li, kk * 4 + g);
+                const bf16x8 kf = *(const bf16x8*)(lK + koff[kk] + kt * 16 * RB);
+                const bf16x8 vf = *(const bf16x8*)(lV + koff[kk] + kt * 16 * RB);
 #pragma unroll
                 for (int j = 0; j < NQ; ++j) {
                     sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[j][kk], sc[j][kt], 0, 0, 0);
@@ -644,9 +711,8 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
                 }
             }
             if (HALF) {
-                const int row = 16 * kt + li;
-                const int off = row * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(row)) << 4) + (g & 1) * 8;
-                const bf16x4 kh = *(const bf16x4*)(lK + off), vh = *(const bf16x4*)(lV + off);
+                const bf16x4 kh = *(const bf16x4*)(lK + khoff + kt * 16 * RB);
+                const bf16x4 vh = *(const bf16x4*)(lV + khoff + kt * 16 * RB);
 #pragma unroll
                 for (int j = 0; j < NQ; ++j) {
                     sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kh, qh[j], sc[j][kt], 0, 0, 0);
@@ -658,15 +724,26 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
             const int qlo = qb * QBLK + wid * 16 * NQ + j * 16;   // first query of this sub-tile
-            const bool edge = qlo + 15 >= p.S || t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qlo);
+            // masked scores -> -inf (P = 0) only on tiles crossing the diagonal or an edge
+            if (qlo + 15 >= p.S || t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qlo)) {
+                asm volatile("" ::: "memory");   // keep the branch (no speculated compares)
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int key = t * 64 + 16 * kt + 4 * g + r;
+                        if (!qok[j] || key >= p.S || (CAUSAL && key > myq[j])) sc[j][kt][r] = -INFINITY;
+                    }
+            }
+            const f32x2 sl2 = {p.scale_log2, p.scale_log2}, ls2 = {lse2[j], lse2[j]}, dl2 = {dl[j], dl[j]};
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = t * 64 + 16 * kt + 4 * g + r;
-                    float pv = __builtin_amdgcn_exp2f(fmaf(sc[j][kt][r], p.scale_log2, -lse2[j]));
-                    if (edge && (!qok[j] || key >= p.S || (CAUSAL && key > myq[j]))) pv = 0.f;
-                    dp[j][kt][r] = pv * (dp[j][kt][r] - dl[j]);
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2 x = f32x2{sc[j][kt][r], sc[j][kt][r + 1]} * sl2 - ls2;
+                    const f32x2 pv = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+                    const f32x2 ds = pv * (f32x2{dp[j][kt][r], dp[j][kt][r + 1]} - dl2);
+                    dp[j][kt][r] = ds[0]; dp[j][kt][r + 1] = ds[1];
                 }
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
@@ -675,13 +752,12 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
         }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const int kr = 32 * ks + 4 * g + (li >> 2);
             bf16x4 k0[DT], k1[DT];
 #pragma unroll
             for (int d = 0; d < DT; ++d) {
-                const int dc = d * 16 + 4 * (li & 3);
-                k0[d] = tr_read_k_asm<RB>(lK, kr, dc);
-                k1[d] = tr_read_k_asm<RB>(lK, kr + 16, dc);
+                const uint32_t a = (uint32_t)(uintptr_t)lK + troff[d];
+                if (ks == 0) { k0[d] = tr_read_off<0>(a); k1[d] = tr_read_off<16 * RB>(a); }
+                else { k0[d] = tr_read_off<32 * RB>(a); k1[d] = tr_read_off<48 * RB>(a); }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
@@ -735,7 +811,7 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
             d->B, d->H, d->HKV, d->S, d->hd, (float)(1.4426950408889634 / std::sqrt((double)d->hd))};
     // NQ query sub-tiles per wave (KD_ATTN_FWD_NQ=1 restores one, for A/B)
     static const int nq = [] { const char* e = std::getenv("KD_ATTN_FWD_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
-    dim3 grid((d->S + 64 * nq - 1) / (64 * nq), d->H, d->B);
+    dim3 grid(d->H, d->B, (d->S + 64 * nq - 1) / (64 * nq));
     hipStream_t st = as_stream(stream_);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem = 2 * 2 * 64 * rb;
@@ -781,9 +857,9 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, d->lse, d->delta,
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
                (float)(sc * 1.4426950408889634)};
-    dim3 grid((d->S + 63) / 64, d->H, d->B);
+    dim3 grid(d->H, d->B, (d->S + 63) / 64);
     static const int nq_dq = [] { const char* e = std::getenv("KD_ATTN_DQ_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
-    dim3 grid_q((d->S + 64 * nq_dq - 1) / (64 * nq_dq), d->H, d->B);
+    dim3 grid_q(d->H, d->B, (d->S + 64 * nq_dq - 1) / (64 * nq_dq));
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem_kv = 2 * (2 * 64 * rb + 512);
     const size_t smem_q = 2 * 2 * 64 * rb;
