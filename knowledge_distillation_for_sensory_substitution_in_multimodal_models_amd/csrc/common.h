@@ -43,6 +43,12 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
+// SiLU / sigmoid with v_exp_f32 + v_rcp_f32 instead of an IEEE fp32 division (~10 instructions
+// each). Every SiLU of the build (GEMM epilogues, k_swiglu_fwd / bwd, the decode GEMV) uses these
+// forms, so the fused and unfused paths stay bit-identical.
+__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float silu_fast(float x) { return x * sigmoid_fast(x); }
+
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 

@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(NT) k_gemv(const bf16* __restrict__ x, const b
     if (lane == 0) {
         float v = a0;
         if constexpr (EPI == 1 || EPI == 2) v += (float)extra[n];
-        if constexpr (EPI == 3) v = a0 / (1.f + __expf(-a0)) * a1;
+        if constexpr (EPI == 3) v = silu_fast(a0) * a1;
         y[n] = (bf16)v;
     }
 }
@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(NT) k_gemv_rows(const bf16* __restrict__ x, co
     if (threadIdx.x == 0) {
         float v = a0;
         if constexpr (EPI == 1 || EPI == 2) v += (float)extra[n];
-        if constexpr (EPI == 3) v = a0 / (1.f + __expf(-a0)) * a1;
+        if constexpr (EPI == 3) v = silu_fast(a0) * a1;
         y[n] = (bf16)v;
     }
 }

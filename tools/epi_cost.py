@@ -1,0 +1,63 @@
+"""Epilogue cost of the step's small forward GEMMs: each shape timed with the epilogue it has
+in the step (bias / GELU-tanh / aux / residual) and plain, back to back (sustained clock).
+    python tools/epi_cost.py [iters] [variant ...]"""
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops  # noqa: E402
+
+it = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+variants = [int(v) for v in sys.argv[2:]] or [0]
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+# (name, M, N, K, bias, act, aux, residual)
+SHAPES = [
+    ("siglip qkv", 5832, 3456, 1152, True, None, False, False),
+    ("siglip o", 5832, 1152, 1152, True, None, False, True),
+    ("siglip fc1", 5832, 4304, 1152, True, "gelu_tanh", False, False),
+    ("siglip fc1+aux", 5832, 4304, 1152, True, "gelu_tanh", True, False),
+    ("siglip fc2", 5832, 1152, 4304, True, None, False, True),
+    ("qwen 0.5b qkv", 6144, 1152, 896, True, None, False, False),
+    ("qwen 0.5b o", 6144, 896, 896, False, None, False, True),
+    ("qwen 0.5b down", 6144, 896, 4864, False, None, False, True),
+    ("qwen 0.5b gate|up", 6144, 9728, 896, False, None, False, False),
+    ("qwen 7b qkv", 6144, 4608, 3584, True, None, False, False),
+    ("qwen 7b o", 6144, 3584, 3584, False, None, False, True),
+    ("qwen 7b down", 6144, 3584, 18944, False, None, False, True),
+    ("qwen 7b gate|up", 6144, 37888, 3584, False, None, False, False),
+]
+import os
+if os.environ.get("EPI_SHAPES"):
+    SHAPES = [s_ for s_ in SHAPES if any(k in s_[0] for k in os.environ["EPI_SHAPES"].split(","))]
+
+
+def timed(f):
+    for _ in range(10):
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / it * 1e3
+
+
+for name, M, N, K, bias, act, aux, res in SHAPES:
+    A = (torch.randn(M, K, device=dev, generator=g) * 0.5).bfloat16()
+    W = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, device=dev, generator=g).bfloat16() if bias else None
+    R = torch.randn(M, N, device=dev, generator=g).bfloat16() if res else None
+    X = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if aux else None
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    for v in variants:
+        plan = ops.gemm_plan(A, W, out, bias=b, act=act, residual=R, aux=X, variant=v)
+        t_full = timed(lambda: ops.gemm(A, W, out, bias=b, act=act, residual=R, aux=X, variant=v))
+        t_plain = timed(lambda: ops.gemm(A, W, out, variant=v))
+        tf = 2 * M * N * K / 1e6
+        print(f"{name:16s} {M}x{N}x{K} var {v:2d} plan {plan}: full {t_full:7.1f} us ({tf / t_full:6.1f} TF/s)  "
+              f"plain {t_plain:7.1f} us ({tf / t_plain:6.1f})  epilogue extra {t_full - t_plain:6.1f} us", flush=True)
