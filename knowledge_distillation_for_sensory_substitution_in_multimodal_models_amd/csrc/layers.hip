@@ -657,8 +657,11 @@ __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const floa
     const int64_t n4 = vec ? n >> 2 : 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-        f32x4 pv = ((const f32x4*)p)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
-        const f32x4 gv = ((const f32x4*)g)[i];
+        // every byte is touched once: non-temporal loads / stores (4.79 -> 4.65 ms for 894 M
+        // parameters, tools/bench_adamw.py)
+        f32x4 pv = __builtin_nontemporal_load((const f32x4*)p + i), mv = __builtin_nontemporal_load((const f32x4*)m + i);
+        f32x4 vv = __builtin_nontemporal_load((const f32x4*)v + i);
+        const f32x4 gv = __builtin_nontemporal_load((const f32x4*)g + i);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             float pe = pv[e], me = mv[e], ve = vv[e];
@@ -667,10 +670,11 @@ __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const floa
             mv[e] = me;
             vv[e] = ve;
         }
-        ((f32x4*)m)[i] = mv;
-        ((f32x4*)v)[i] = vv;
-        ((f32x4*)p)[i] = pv;
-        ((bf16x4*)pb)[i] = bf16x4{(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
+        const bf16x4 pbv = bf16x4{(bf16)pv[0], (bf16)pv[1], (bf16)pv[2], (bf16)pv[3]};
+        __builtin_nontemporal_store(mv, (f32x4*)m + i);
+        __builtin_nontemporal_store(vv, (f32x4*)v + i);
+        __builtin_nontemporal_store(pv, (f32x4*)p + i);
+        __builtin_nontemporal_store(pbv, (bf16x4*)pb + i);
     }
     for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         float pi = p[i], mi = m[i], vi = v[i];

@@ -28,6 +28,7 @@ SHAPES = [
     ("qwen 7b o", 6144, 3584, 3584, False, None, False, True),
     ("qwen 7b down", 6144, 3584, 18944, False, None, False, True),
     ("qwen 7b gate|up", 6144, 37888, 3584, False, None, False, False),
+    ("qwen 7b swiglu", 6144, 37888, 3584, False, "swiglu", False, False),
 ]
 import os
 if os.environ.get("EPI_SHAPES"):
@@ -47,17 +48,31 @@ def timed(f):
     return e0.elapsed_time(e1) / it * 1e3
 
 
+WGRAD = [("wgrad 0.5b gate|up", 9728, 896, 6144), ("wgrad siglip fc1", 4304, 1152, 5832),
+         ("wgrad siglip fc2", 1152, 4304, 5832), ("wgrad 0.5b down", 896, 4864, 6144), ("wgrad 0.5b lm_head", 151936, 896, 6144)]
+if os.environ.get("EPI_SHAPES"):
+    WGRAD = [w for w in WGRAD if any(k in w[0] for k in os.environ["EPI_SHAPES"].split(","))]
+for name, M, N, K in WGRAD:   # dW[M, N] += dY^T X (both operands MN-major), fp32 accumulate
+    dY = (torch.randn(K, M, device=dev, generator=g) * 0.1).bfloat16()
+    X = torch.randn(K, N, device=dev, generator=g).bfloat16()
+    acc = torch.zeros(M, N, device=dev)
+    for v in variants:
+        plan = ops.gemm_plan(dY.t(), X.t(), acc, accumulate=True, out_dtype=torch.float32, variant=v)
+        t = timed(lambda: ops.gemm(dY.t(), X.t(), acc, accumulate=True, out_dtype=torch.float32, variant=v))
+        print(f"{name:16s} {M}x{N}x{K} var {v:2d} plan {plan}: {t:7.1f} us ({2 * M * N * K / 1e6 / t:6.1f} TF/s)", flush=True)
+
 for name, M, N, K, bias, act, aux, res in SHAPES:
     A = (torch.randn(M, K, device=dev, generator=g) * 0.5).bfloat16()
     W = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).bfloat16()
     b = torch.randn(N, device=dev, generator=g).bfloat16() if bias else None
     R = torch.randn(M, N, device=dev, generator=g).bfloat16() if res else None
     X = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if aux else None
-    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(M, N // 2 if act == "swiglu" else N, device=dev, dtype=torch.bfloat16)
+    out_plain = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     for v in variants:
         plan = ops.gemm_plan(A, W, out, bias=b, act=act, residual=R, aux=X, variant=v)
         t_full = timed(lambda: ops.gemm(A, W, out, bias=b, act=act, residual=R, aux=X, variant=v))
-        t_plain = timed(lambda: ops.gemm(A, W, out, variant=v))
+        t_plain = timed(lambda: ops.gemm(A, W, out_plain, variant=v))
         tf = 2 * M * N * K / 1e6
         print(f"{name:16s} {M}x{N}x{K} var {v:2d} plan {plan}: full {t_full:7.1f} us ({tf / t_full:6.1f} TF/s)  "
               f"plain {t_plain:7.1f} us ({tf / t_plain:6.1f})  epilogue extra {t_full - t_plain:6.1f} us", flush=True)
