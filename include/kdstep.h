@@ -126,8 +126,16 @@ typedef enum { KD_DTYPE_BF16 = 0, KD_DTYPE_F32 = 1, KD_DTYPE_FP8_E4M3 = 2 } kd_d
  * silu(v[:, :I]) * v[:, I:] with v = alpha * acc rounded to bf16 first (as the unfused
  * GEMM output), aux (optional) receives v [M][2I] for the backward.  K-major operands,
  * bf16 C, no bias / residual / accumulate / split-K. */
+/* Backward activations, fused into the DGRAD GEMM that produces the activation's output
+ * gradient (any operand layouts; bf16 C; no bias / residual / accumulate; never split-K; aux =
+ * the forward pre-activation, READ):
+ * KD_ACT_DGELU_TANH: C[m][n] = v * gelu_tanh'(aux[m][n])      (SigLIP MLP: fc2 dgrad -> dfc1-out)
+ * KD_ACT_DSWIGLU   : aux = [gate | up] [M][2N] (ld_aux >= 2N), C is [M][2N] (ldc >= 2N):
+ *   C[m][n] = v * up * silu'(gate), C[m][N + n] = v * silu(gate)  (Qwen2 MLP: down dgrad -> dgate|dup)
+ * with v = alpha * acc rounded to bf16 first, so C equals the unfused GEMM followed by the
+ * activation-backward kernel bit for bit. */
 typedef enum { KD_ACT_NONE = 0, KD_ACT_GELU_TANH = 1, KD_ACT_GELU_ERF = 2, KD_ACT_SILU = 3,
-               KD_ACT_SWIGLU = 4 } kd_act;
+               KD_ACT_SWIGLU = 4, KD_ACT_DGELU_TANH = 5, KD_ACT_DSWIGLU = 6 } kd_act;
 
 typedef struct {
     int32_t M, N, K;

@@ -48,6 +48,7 @@ class KdLossParams(C.Structure):
 KD_LAYOUT_K_MAJOR, KD_LAYOUT_MN_MAJOR = 0, 1
 KD_DTYPE_BF16, KD_DTYPE_F32, KD_DTYPE_FP8_E4M3 = 0, 1, 2
 KD_ACT_NONE, KD_ACT_GELU_TANH, KD_ACT_GELU_ERF, KD_ACT_SILU, KD_ACT_SWIGLU = 0, 1, 2, 3, 4
+KD_ACT_DGELU_TANH, KD_ACT_DSWIGLU = 5, 6
 
 
 class KdGemmDesc(C.Structure):

@@ -48,6 +48,22 @@ typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 // forms, so the fused and unfused paths stay bit-identical.
 __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float silu_fast(float x) { return x * sigmoid_fast(x); }
+// SwiGLU backward of one element: d = dL/dh, h = silu(g) * u -> (dL/dg, dL/du); shared by
+// k_swiglu_bwd and the fused dgrad epilogue (KD_ACT_DSWIGLU), so both agree bit for bit
+__device__ __forceinline__ void swiglu_grad(float d, float g, float u, float& dg, float& du) {
+    const float sg = sigmoid_fast(g);
+    du = d * (g * sg);
+    dg = d * u * sg * (1.f + g * (1.f - sg));
+}
+// gelu_pytorch_tanh'(x): gelu = x * s, s = sigmoid(2u) = (1 + tanh u) / 2, u = k0 (x + k1 x^3):
+// gelu' = s + 2 x s (1 - s) u', u' = k0 (1 + 3 k1 x^2); s by one v_exp_f32 + v_rcp_f32
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+    constexpr float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    constexpr float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f, c1 = c0 * 0.044715f;
+    const float x2 = x * x;
+    const float sg = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * fmaf(c1, x2, c0)));
+    return sg + 2.f * x * sg * (1.f - sg) * k0 * fmaf(3.f * k1, x2, 1.f);
+}
 
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }

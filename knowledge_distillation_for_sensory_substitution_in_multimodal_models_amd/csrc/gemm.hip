@@ -463,6 +463,43 @@ __device__ __forceinline__ void epi_flush_sel(const GemmP& p, const char* smem, 
     else epi_flush<ROWS, BN, NTHR, F32, true, true>(p, smem, rs, dst, ld, m0, n0, tid, full);
 }
 
+// Backward-activation flush (KD_ACT_DGELU_TANH / KD_ACT_DSWIGLU): the staged bf16 tile is the
+// activation's output gradient v (exactly the unfused GEMM output); multiply by act'(aux)
+// with the same per-element functions as k_act_bwd / k_swiglu_bwd.
+template <int ROWS, int BN, int NTHR>
+__device__ __forceinline__ void epi_flush_dact(const GemmP& p, const char* smem, int rs, int m0, int n0, int tid, bool full) {
+    constexpr int CPR = BN / 8;
+    const bool glu = p.act == KD_ACT_DSWIGLU;
+#pragma unroll 4
+    for (int idx = tid; idx < ROWS * CPR; idx += NTHR) {
+        const int lr = idx / CPR, c = idx % CPR;
+        const int row = m0 + lr, col = n0 + c * 8;
+        if (!full && (row >= p.M || col >= p.N)) continue;
+        const bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
+        const bf16* ar = p.aux + (int64_t)row * p.ld_aux;
+        bf16* cr = (bf16*)p.C + (int64_t)row * p.ldc;
+        if (glu) {
+            const bf16x8 g8 = *(const bf16x8*)(ar + col), u8 = *(const bf16x8*)(ar + p.N + col);
+            bf16x8 og, ou;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float dg, du;
+                swiglu_grad((float)v[e], (float)g8[e], (float)u8[e], dg, du);
+                og[e] = (bf16)dg;
+                ou[e] = (bf16)du;
+            }
+            *(bf16x8*)(cr + col) = og;
+            *(bf16x8*)(cr + p.N + col) = ou;
+        } else {
+            const bf16x8 x8 = *(const bf16x8*)(ar + col);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)v[e] * gelu_tanh_grad((float)x8[e]));
+            *(bf16x8*)(cr + col) = o;
+        }
+    }
+}
+
 // HAS_ACT: the activation epilogue is instantiated for the forward (K-major x K-major) kernels
 // only; the launcher rejects an activation with MN-major operands or an fp32 output.
 template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2, bool HAS_ACT = true>
@@ -482,6 +519,12 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
         }
     }
     constexpr int RS16 = BN * 2 + 16, RS32 = BN * 4 + 16;
+    if (p.act == KD_ACT_DGELU_TANH || p.act == KD_ACT_DSWIGLU) {   // aux is READ (the forward pre-activation)
+        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        __syncthreads();
+        epi_flush_dact<BM, BN, NTHR>(p, smem, RS16, m0, n0, tid, full);
+        return;
+    }
     if (p.aux) {   // pre-activation (bf16) for the backward
         epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
@@ -1547,10 +1590,19 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16 || d->c_dtype == KD_DTYPE_F32, "gemm: c_dtype");
     KD_CHECK_ARG(d->ab_dtype == KD_DTYPE_BF16 || d->ab_dtype == KD_DTYPE_FP8_E4M3, "gemm: ab_dtype");
     if (d->ab_dtype == KD_DTYPE_FP8_E4M3) return launch_gemm_f8(d, stream_);
-    KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_SWIGLU, "gemm: act");
-    KD_CHECK_ARG(d->act == KD_ACT_NONE || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
-                                          d->c_dtype == KD_DTYPE_BF16),
+    KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_DSWIGLU, "gemm: act");
+    const bool dact = d->act == KD_ACT_DGELU_TANH || d->act == KD_ACT_DSWIGLU;
+    KD_CHECK_ARG(d->act == KD_ACT_NONE || dact || (d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR &&
+                                                   d->c_dtype == KD_DTYPE_BF16),
                  "gemm: an activation epilogue needs K-major operands and a bf16 output");
+    if (dact) {
+        const int64_t w = d->act == KD_ACT_DSWIGLU ? 2 * (int64_t)d->N : d->N;
+        KD_CHECK_ARG(d->aux && d->c_dtype == KD_DTYPE_BF16 && !d->bias && !d->residual && !d->accumulate && d->split_k <= 1 &&
+                     d->variant != 1 && d->variant != 21,
+                     "gemm backward activation: aux (forward pre-activation), bf16 C, no bias / residual / accumulate / split-K");
+        KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldc >= w && d->ld_aux >= w && d->ldc % 8 == 0 && d->ld_aux % 8 == 0 &&
+                       (uintptr_t)d->aux % 16 == 0, "gemm backward activation: ldc / ld_aux >= N (2N for dswiglu), 16-B rows");
+    }
     KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 21), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
@@ -1590,6 +1642,13 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                         ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
                         (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
                         (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
+    KD_CHECK_ARG(!dact || big_ok, "gemm backward activation: needs the tiled kernels (M, N >= 128, M*N >= 2^20)");
+    kd_gemm_desc d1;
+    if (dact && d->split_k != 1) {   // the fused backward activation is never split-K
+        d1 = *d;
+        d1.split_k = 1;
+        d = &d1;
+    }
     if (d->act == KD_ACT_SWIGLU) {   // fused gate|up GEMM + silu(gate) * up, on v8
         KD_CHECK_SHAPE(d->N % 256 == 0 && d->M >= 1, "gemm swiglu: N = 2I needs I % 128 == 0");
         KD_CHECK_ARG(!d->bias && !d->residual && !d->accumulate && d->split_k <= 1,

@@ -372,12 +372,7 @@ __global__ void k_swiglu_bwd(const bf16* __restrict__ gu, int64_t ldg, const bf1
         load8(gu + m * ldg + I + c, u);
         load8(dh + m * ldh + c, d);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float sg = sigmoid_fast(g[j]);
-            const float silu = g[j] * sg;
-            ou[j] = d[j] * silu;
-            og[j] = d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg));
-        }
+        for (int j = 0; j < 8; ++j) swiglu_grad(d[j], g[j], u[j], og[j], ou[j]);
         store8(dgu + m * ldd + c, og);
         store8(dgu + m * ldd + I + c, ou);
     }
@@ -395,13 +390,7 @@ __global__ void k_act_bwd(const bf16* __restrict__ pre, const bf16* __restrict__
         for (int j = 0; j < 8; ++j) {
             float dv;
             if (act == KD_ACT_GELU_TANH) {
-                // gelu = x * s, s = sigmoid(2u) = (1 + tanh u) / 2: gelu' = s + 2 x s (1 - s) u',
-                // u' = k0 (1 + 3 k1 x^2); s by one v_exp_f32 + v_rcp_f32 (as the GEMM epilogue)
-                const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-                constexpr float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f, c1 = c0 * 0.044715f;
-                const float x2 = x[j] * x[j];
-                const float sg = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x[j] * fmaf(c1, x2, c0)));
-                dv = sg + 2.f * x[j] * sg * (1.f - sg) * k0 * fmaf(3.f * k1, x2, 1.f);
+                dv = gelu_tanh_grad(x[j]);
             } else if (act == KD_ACT_GELU_ERF) {
                 const float cdf = 0.5f * (1.f + erff(x[j] * 0.7071067811865476f));
                 const float pdf = 0.3989422804014327f * __expf(-0.5f * x[j] * x[j]);

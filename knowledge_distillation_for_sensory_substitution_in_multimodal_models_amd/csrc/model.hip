@@ -280,6 +280,16 @@ int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int6
     return gemm_timed(&d, s);
 }
 
+// the dgrad GEMMs feeding an activation backward run it in their epilogue (KD_ACT_DGELU_TANH /
+// KD_ACT_DSWIGLU) where the tiled GEMM kernels take the shape; KD_FUSE_DACT=0 turns it off (A/B)
+static const bool g_fuse_dact = [] {
+    const char* e = std::getenv("KD_FUSE_DACT");
+    return !(e && e[0] == '0');
+}();
+static bool fused_dact_ok(int64_t M, int64_t N) {
+    return g_fuse_dact && M >= 128 && N >= 128 && N % 8 == 0 && M * N >= (int64_t)1 << 20;
+}
+
 #define KD_TRY(x)                    \
     do {                             \
         const int st__ = (x);        \
@@ -683,15 +693,22 @@ int lm_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, const float* cs
     for (int i = c.t_layers - 1; i >= 0; --i) {
         const LmLayerBufs& b = F.ll[i];
         GemmArgs g0;
-        // MLP: da = dx Wdown ; dgu = swiglu'(gu) da ; dh2 = dgu [Wgate; Wup]
-        KD_TRY(gemm(s, P.splitk_main, M, TI, H, km(P.dx, H), mn(m->W(m->lm(i, LDW)), TI), P.da, TI, g0));
+        // MLP: dgu = swiglu'(gu) (dx Wdown) -- one GEMM with the KD_ACT_DSWIGLU epilogue where the
+        // tiled kernels run it, else the GEMM + k_swiglu_bwd (same bits) ; dh2 = dgu [Wgate; Wup]
+        if (fused_dact_ok(M, TI)) {
+            GemmArgs gs;
+            gs.act = KD_ACT_DSWIGLU; gs.aux = b.gu; gs.ld_aux = 2 * TI; gs.split_k = 1;
+            KD_TRY(gemm(s, P.splitk_main, M, TI, H, km(P.dx, H), mn(m->W(m->lm(i, LDW)), TI), P.dgu, 2 * TI, gs));
+        } else {
+            KD_TRY(gemm(s, P.splitk_main, M, TI, H, km(P.dx, H), mn(m->W(m->lm(i, LDW)), TI), P.da, TI, g0));
+        }
         hipEvent_t ev = nullptr;
         if (gw) {
             lane.begin();
             KD_TRY(lane.wgrad(M, H, TI, P.dx, H, b.a, TI, m->G(m->lm(i, LDW))));
             ev = lane.end();
         }
-        KD_TRY(launch_swiglu_bwd(b.gu, 2 * TI, P.da, TI, P.dgu, 2 * TI, M, TI, s));
+        if (!fused_dact_ok(M, TI)) KD_TRY(launch_swiglu_bwd(b.gu, 2 * TI, P.da, TI, P.dgu, 2 * TI, M, TI, s));
         KD_TRY(gemm(s, P.splitk_main, M, H, 2 * TI, km(P.dgu, 2 * TI), mn(m->W(m->lm(i, LGW)), H), P.dh2, H, g0));
         if (gw) {
             lane.begin();
@@ -747,7 +764,14 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
     GemmArgs g0;
     for (int i = c.v_layers - 1; i >= 0; --i) {
         const VisLayerBufs& b = F.vl[i];
-        KD_TRY(gemm(s, P.splitk_main, NT, Iv, D, km(dx, D), mn(m->W(m->vis(i, VFC2W)), Iv), P.du, Iv, g0));
+        const bool fuse_gelu = fused_dact_ok(NT, Iv);
+        if (fuse_gelu) {   // du = gelu'(pre) (dx Wfc2) in one GEMM (KD_ACT_DGELU_TANH epilogue)
+            GemmArgs gd;
+            gd.act = KD_ACT_DGELU_TANH; gd.aux = b.pre; gd.ld_aux = Iv; gd.split_k = 1;
+            KD_TRY(gemm(s, P.splitk_main, NT, Iv, D, km(dx, D), mn(m->W(m->vis(i, VFC2W)), Iv), P.du, Iv, gd));
+        } else {
+            KD_TRY(gemm(s, P.splitk_main, NT, Iv, D, km(dx, D), mn(m->W(m->vis(i, VFC2W)), Iv), P.du, Iv, g0));
+        }
         hipEvent_t ev = nullptr;
         if (gw) {
             lane.begin();
@@ -755,7 +779,7 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
             KD_TRY(lane.colsum(dx, D, NT, D, m->G(m->vis(i, VFC2B))));
             ev = lane.end();
         }
-        KD_TRY(launch_act_bwd(b.pre, P.du, P.du, (int64_t)NT * Iv, KD_ACT_GELU_TANH, s));   // dpre in place
+        if (!fuse_gelu) KD_TRY(launch_act_bwd(b.pre, P.du, P.du, (int64_t)NT * Iv, KD_ACT_GELU_TANH, s));   // dpre in place
         KD_TRY(gemm(s, P.splitk_main, NT, D, Iv, km(P.du, Iv), mn(m->W(m->vis(i, VFC1W)), D), P.dh2v, D, g0));
         if (gw) {
             lane.begin();

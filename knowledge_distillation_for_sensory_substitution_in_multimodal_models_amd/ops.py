@@ -161,7 +161,8 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
 
 # --------------------------------------------------------------------- GEMM ----
 ACTS = {None: NV.KD_ACT_NONE, "none": NV.KD_ACT_NONE, "gelu_tanh": NV.KD_ACT_GELU_TANH,
-        "gelu_erf": NV.KD_ACT_GELU_ERF, "silu": NV.KD_ACT_SILU, "swiglu": NV.KD_ACT_SWIGLU}
+        "gelu_erf": NV.KD_ACT_GELU_ERF, "silu": NV.KD_ACT_SILU, "swiglu": NV.KD_ACT_SWIGLU,
+        "dgelu_tanh": NV.KD_ACT_DGELU_TANH, "dswiglu": NV.KD_ACT_DSWIGLU}
 _DT = {torch.bfloat16: NV.KD_DTYPE_BF16, torch.float32: NV.KD_DTYPE_F32}
 
 
@@ -187,7 +188,8 @@ def _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate
     pa, lda, la = _operand(a, "gemm.a")
     pb, ldb, lb = _operand(b, "gemm.b")
     if out is None:
-        out = torch.empty((M, N // 2 if act == "swiglu" else N), dtype=out_dtype, device=a.device)
+        out = torch.empty((M, N // 2 if act == "swiglu" else (2 * N if act == "dswiglu" else N)), dtype=out_dtype,
+                          device=a.device)
     if out.stride(1) != 1:
         raise RuntimeError("gemm: out must have a contiguous last dim")
     d = NV.KdGemmDesc()

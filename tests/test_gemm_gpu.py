@@ -301,3 +301,26 @@ def test_v9_bitexact_vs_v8(M, N, K, dev):
         o9 = ops.gemm(a, w, act="swiglu", aux=g9, variant=20)
         o8 = ops.gemm(a, w, act="swiglu", aux=g8, variant=16)
         assert torch.equal(o9, o8) and torch.equal(g9, g8)
+
+
+@pytest.mark.parametrize("variant", [0, 5, 6, 7, 16])
+@pytest.mark.parametrize("M, N, K", [(1100, 1040, 392), (6144 // 2, 4864, 896), (5832 // 4, 4304, 1152)])
+def test_fused_backward_activation(variant, M, N, K, dev):
+    """KD_ACT_DGELU_TANH / KD_ACT_DSWIGLU: the dgrad GEMM with the activation backward in its
+    epilogue equals the unfused GEMM (no split) followed by k_act_bwd / k_swiglu_bwd bit for
+    bit (the SigLIP fc2 dgrad and the Qwen2 down-proj dgrad of the student backward)."""
+    ops = _ops()
+    dy = _rand(M, K, dev=dev, seed=41)
+    w = _rand(K, N, dev=dev, seed=42, scale=K ** -0.5)
+    v = ops.gemm(dy, w.t(), variant=variant, split_k=1)
+    pre = _rand(M, N, dev=dev, seed=43)
+    out = ops.gemm(dy, w.t(), act="dgelu_tanh", aux=pre, variant=variant)
+    assert torch.equal(out, ops.act_bwd(pre, v, "gelu_tanh"))
+    gu = _rand(M, 2 * N, dev=dev, seed=44)
+    out2 = ops.gemm(dy, w.t(), act="dswiglu", aux=gu, variant=variant)
+    assert out2.shape == (M, 2 * N)
+    assert torch.equal(out2, ops.swiglu_bwd(gu, v, N))
+    # and against torch autograd of the activations (fp32 math on the same bf16 operands)
+    x = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(x, approximate="tanh").backward(v.float())
+    _check(out, x.grad)
