@@ -328,9 +328,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    c0 = time.thread_time()
     for i in range(a.steps):
         loss = step(a.warmup + i)
     host_dt = time.perf_counter() - t0   # host enqueue time of the K steps
+    host_cpu = time.thread_time() - c0   # CPU time of the enqueueing thread (not the time it sat blocked)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -431,6 +433,7 @@ def main():
         "mfu": round(value * tf_sample / world / PEAK_BF16_TFLOPS, 4),
         "host_enqueue_ms_per_step": round(host_dt * 1e3 / a.steps, 2),
         "host_enqueue_ms_idle_step": round(host_idle_ms, 2),
+        "host_cpu_ms_per_step": round(host_cpu * 1e3 / a.steps, 2),
         "tflop_per_sample": round(tf_sample, 2),
         "loss": round(loss_v, 5),
         "teacher_fwd": tfwd,

@@ -58,6 +58,7 @@ struct GemmP {
     // k_splitk_reduce. 0 = off.
     int sk_steps, sk_grid;
     float* sk_ws;
+    int gm;                // tile rows per group of the grouped tile order (0: GM_GROUP)
 };
 
 // stream-K: the workgroup whose run [floor(tot w / G), floor(tot (w+1) / G)) holds step s
@@ -161,8 +162,8 @@ __device__ __forceinline__ float apply_act(float x, int act) {
 // Linear tile id -> (tm, tn) in grouped order, GM tile-rows at a time, so the ~32
 // co-resident blocks of an XCD share GM A-panels and 32/GM B-panels in its L2.
 constexpr int GM_GROUP = 8;
-__host__ __device__ inline void tile_grouped(int wg, int tiles_m, int tiles_n, int& tm, int& tn) {
-    constexpr int GM = GM_GROUP;
+__host__ __device__ inline void tile_grouped(int wg, int tiles_m, int tiles_n, int& tm, int& tn, int gm_ = 0) {
+    const int GM = gm_ > 0 ? gm_ : GM_GROUP;
     const int group = wg / (GM * tiles_n);
     const int first_m = group * GM;
     const int gm = min(tiles_m - first_m, GM);
@@ -171,13 +172,32 @@ __host__ __device__ inline void tile_grouped(int wg, int tiles_m, int tiles_n, i
     tn = idx / gm;
 }
 
+// Tile rows per group for a GEMM of tiles_m x tiles_n tiles (one value per GEMM call: every
+// launch of a hybrid / split plan must walk the same order). Each XCD runs a contiguous chunk
+// of nwg/8 linear tiles, ~32 at a time: prefer a group height g that divides tiles_m and the
+// chunk (every XCD's chunk is whole columns of one group: no XCD straddles two groups), with
+// the fewest distinct A + B k-slices among 32 co-resident tiles, g + 32/g (g = 6, 5, 7, 4, 8).
+// Measured on the 6144 x 37888 x 3584 gate|up GEMM (24 x 148 tiles, chunks of 444): g = 6
+// 1260-1276 us, g = 3 1279-1285, g = 4 1315-1338, g = 8 1341-1358, g = 12 1331, g = 24 1362-1388.
+inline int pick_gm(int tiles_m, int tiles_n) {
+    static const int env = [] { const char* e = std::getenv("KD_GEMM_GM"); return e ? std::atoi(e) : 0; }();
+    if (env > 0) return env;
+    const int64_t nwg = (int64_t)tiles_m * tiles_n;
+    if (nwg % 8 == 0) {
+        const int64_t chunk = nwg / 8;
+        for (int g : {6, 5, 7, 4, 8})
+            if (tiles_m % g == 0 && chunk % g == 0) return g;
+    }
+    return GM_GROUP;
+}
+
 // Block -> tile map: XCD-aware bijective remap (the blocks dispatched to one XCD, b, b+8,
 // ..., get consecutive ids), offset by the launch's first tile, then the grouped order.
-__device__ __forceinline__ void tile_of(int nwg, int tiles_m, int tiles_n, int& tm, int& tn, int tile0 = 0) {
+__device__ __forceinline__ void tile_of(int nwg, int tiles_m, int tiles_n, int& tm, int& tn, int tile0 = 0, int gm = 0) {
     const int b = blockIdx.x;
     const int q8 = nwg / 8, r8 = nwg % 8, x = b % 8;
     const int wg = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + b / 8 + tile0;
-    tile_grouped(wg, tiles_m, tiles_n, tm, tn);
+    tile_grouped(wg, tiles_m, tiles_n, tm, tn, gm);
 }
 
 template <bool A_MN, bool B_MN>
@@ -620,7 +640,7 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     int tm, tn;
-    tile_of(p.gx, (p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn, p.tile0);
+    tile_of(p.gx, (p.M + BM - 1) / BM, (p.N + BN - 1) / BN, tm, tn, p.tile0, p.gm);
     const int m0 = tm * BM, n0 = tn * BN;
     __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 0), rsB = make_rsrc(p.B, 0);
     if (!A_MN) rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(BM, p.M - m0), p.lda));
@@ -930,7 +950,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
                 q.bias = nullptr; q.aux = nullptr; q.resid = nullptr; q.act = KD_ACT_NONE;
             }
             int tm, tn;
-            tile_grouped(t, tiles_m, tiles_n, tm, tn);
+            tile_grouped(t, tiles_m, tiles_n, tm, tn, p_.gm);
             g8_tile<A_MN, B_MN, EXP>(q, tm, tn, smem);
             s0 = e;
             __syncthreads();   // the next piece's DMA refills the LDS the epilogue staged through
@@ -946,7 +966,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
         p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
     }
     int tm, tn;
-    tile_of(p.gx, tiles_m, tiles_n, tm, tn, p.tile0);
+    tile_of(p.gx, tiles_m, tiles_n, tm, tn, p.tile0, p.gm);
     g8_tile<A_MN, B_MN, EXP>(p, tm, tn, smem);
 }
 
@@ -986,7 +1006,7 @@ __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wid >> 2, wc = wid & 3;
     int tm, tn;
-    tile_of(p.gx, (p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0);
+    tile_of(p.gx, (p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0, p.gm);
     const int m0 = tm * 256, n0 = tn * 256;
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2;
@@ -1154,7 +1174,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8f8(GemmP p) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid >> 1, wn = wid & 1;
     int tm, tn;
-    tile_of(p.gx, (p.M + 255) / 256, glu ? (p.N / 256) : (p.N + 255) / 256, tm, tn, p.tile0);
+    tile_of(p.gx, (p.M + 255) / 256, glu ? (p.N / 256) : (p.N + 255) / 256, tm, tn, p.tile0, p.gm);
     const int m0 = tm * 256, n0 = tn * 256, nb = tn * 128;
     const int K = p.K;
     const int nk = (K + 63) / 64, nk_full = K / 64;
@@ -1357,7 +1377,7 @@ __global__ void __launch_bounds__(256) k_quant_rows_f8(const bf16* __restrict__ 
 __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p, int BMr, int BNr) {
     int tm, tn;
     const int tiles_m = (p.M + BMr - 1) / BMr, tiles_n = (p.N + BNr - 1) / BNr;
-    tile_grouped(p.tile0 + (int)blockIdx.x, tiles_m, tiles_n, tm, tn);
+    tile_grouped(p.tile0 + (int)blockIdx.x, tiles_m, tiles_n, tm, tn, p.gm);
     if (p.sk_steps > 0) {   // stream-K: this tile's piece count; a one-piece tile is already final
         const int64_t tot = (int64_t)tiles_m * tiles_n * p.sk_steps;
         const int64_t tb = (int64_t)(p.tile0 + (int)blockIdx.x) * p.sk_steps;
@@ -1550,6 +1570,7 @@ int launch_gemm_f8(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_ARG(!d->bias && !d->residual && !d->accumulate, "gemm fp8 swiglu: no bias / residual / accumulate");
         p.glu = d->N / 2; p.act = KD_ACT_NONE;
         p.gx = ceil_div(d->M, 256) * (d->N / 256); p.gy = 1;
+        p.gm = pick_gm(ceil_div(d->M, 256), d->N / 256);
         hipLaunchKernelGGL((k_gemm8f8<4, KD_ACT_NONE>), dim3(p.gx), dim3(NTH8), F8_LDS, st, p);
         KD_LAUNCH_CHECK("k_gemm8f8<swiglu>");
         return KD_OK;
@@ -1557,6 +1578,7 @@ int launch_gemm_f8(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(!d->aux, "gemm fp8: aux (pre-activation) output only with KD_ACT_SWIGLU");
     const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256));
     p.gx = (int)grid.x; p.gy = 1;
+    p.gm = pick_gm(ceil_div(d->M, 256), ceil_div(d->N, 256));
     switch (d->act) {
         case KD_ACT_GELU_TANH: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_GELU_TANH>), grid, dim3(NTH8), F8_LDS, st, p); break;
         case KD_ACT_GELU_ERF: hipLaunchKernelGGL((k_gemm8f8<0, KD_ACT_GELU_ERF>), grid, dim3(NTH8), F8_LDS, st, p); break;
@@ -1634,6 +1656,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.kchunk = d->K; p.split_stride = 0; p.glu = 0; p.tile0 = 0;
     p.sa = p.sb = nullptr; p.gx = 0; p.gy = 1;
     p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr;
+    p.gm = 0;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
@@ -1658,6 +1681,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_ARG(!d->aux || (d->ld_aux % 8 == 0 && (uintptr_t)d->aux % 16 == 0), "gemm swiglu: aux alignment");
         GemmP pk = p;
         pk.glu = d->N / 2; pk.act = KD_ACT_NONE;
+        pk.gm = pick_gm(ceil_div(d->M, 256), d->N / 256);
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
         pk.gx = (int)grid.x; pk.gy = 1;
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
@@ -1671,6 +1695,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
         const int tbm = pl.var == 4 ? 128 : 256, tbn = pl.var == 3 ? 128 : 256;
         const int tiles = ceil_div(d->M, tbm) * ceil_div(d->N, tbn);
+        p.gm = pick_gm(ceil_div(d->M, tbm), ceil_div(d->N, tbn));
         if (pl.var == 21) {   // stream-K (v8), then the fold of the shared tiles
             KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
                          "gemm: stream-K workspace too small");
