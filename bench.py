@@ -370,7 +370,7 @@ def main():
     tf_sample = step_tflops_per_sample(cfg["kind"], cfg["phase"])
     roof = None
     br = {}
-    for kind in ("gemm_kk_swiglu", "gemm_kk", "gemm_kn", "gemm_nn", "gemm_f8_swiglu", "gemm_f8"):
+    for kind in ("gemm_kk_swiglu", "gemm_kk", "gemm_kn", "gemm_kn_dact", "gemm_nn", "gemm_f8_swiglu", "gemm_f8"):
         s = ops.TIMER.summary(kind)
         if s:
             br[kind] = dict(launches=s["launches"], avg_us=round(s["avg_ms"] * 1e3, 2),

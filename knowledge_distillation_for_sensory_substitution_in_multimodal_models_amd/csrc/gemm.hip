@@ -178,7 +178,8 @@ __host__ __device__ inline void tile_grouped(int wg, int tiles_m, int tiles_n, i
 // chunk (every XCD's chunk is whole columns of one group: no XCD straddles two groups), with
 // the fewest distinct A + B k-slices among 32 co-resident tiles, g + 32/g (g = 6, 5, 7, 4, 8).
 // Measured on the 6144 x 37888 x 3584 gate|up GEMM (24 x 148 tiles, chunks of 444): g = 6
-// 1260-1276 us, g = 3 1279-1285, g = 4 1315-1338, g = 8 1341-1358, g = 12 1331, g = 24 1362-1388.
+// 1260-1276 us, g = 3 1279-1285, g = 4 1315-1338, g = 8 1341-1358, g = 12 1331, g = 24 1362-1388
+// (profiles/r02/gemm_group_height.txt).
 inline int pick_gm(int tiles_m, int tiles_n) {
     static const int env = [] { const char* e = std::getenv("KD_GEMM_GM"); return e ? std::atoi(e) : 0; }();
     if (env > 0) return env;
@@ -188,7 +189,7 @@ inline int pick_gm(int tiles_m, int tiles_n) {
         for (int g : {6, 5, 7, 4, 8})
             if (tiles_m % g == 0 && chunk % g == 0) return g;
     }
-    return GM_GROUP;
+    return 4;   // no clean split: 4 measured ahead of 8 (SigLIP fc2 81 vs 87 us, lm_head wgrad 1668 vs 1715 us)
 }
 
 // Block -> tile map: XCD-aware bijective remap (the blocks dispatched to one XCD, b, b+8,

@@ -46,8 +46,13 @@ int gemm_timed(const kd_gemm_desc* d, void* stream) {
     if (!g_timer_on) return launch_gemm(d, stream);
     TimerRec r;
     const bool swiglu = d->act == KD_ACT_SWIGLU, f8 = d->ab_dtype == KD_DTYPE_FP8_E4M3;
+    // kinds: gemm_<A layout><B layout> (k = K-major, n = MN-major); the fused epilogues with extra
+    // elementwise work of their own are kinds of their own (_swiglu forward; _dact: the dgrad
+    // with the activation backward, KD_ACT_DGELU_TANH / KD_ACT_DSWIGLU)
+    const bool dact = d->act == KD_ACT_DGELU_TANH || d->act == KD_ACT_DSWIGLU;
     r.key = swiglu ? std::string(f8 ? "gemm_f8_swiglu" : "gemm_kk_swiglu")
-                   : (f8 ? std::string("gemm_f8") : std::string("gemm_") + (d->a_layout ? 'n' : 'k') + (d->b_layout ? 'n' : 'k'));
+                   : (f8 ? std::string("gemm_f8") : std::string("gemm_") + (d->a_layout ? 'n' : 'k') + (d->b_layout ? 'n' : 'k') +
+                                                        (dact ? "_dact" : ""));
     r.key += ":" + std::to_string(d->M) + "x" + std::to_string(d->N) + "x" + std::to_string(d->K) + ":" +
              (d->c_dtype == KD_DTYPE_F32 ? "f32" : "bf16") + (d->accumulate ? ":acc" : "");
     r.flops = 2.0 * d->M * d->N * d->K;

@@ -1,6 +1,7 @@
 # Round-end style GPU pass (run under gpurun):
 #   STEPS="tests parity bench prof pmc" ROUND=r02 bash tools/gpu_round.sh
-# tests  : pytest -m gpu (every parity test)
+# tests  : pytest -m gpu (every parity test); gemm: only the GEMM / fp8 GEMM tests
+# c2, c4 : bench.py --config c2 / c4 (the other single-GPU BASELINE configs) -> gpurun_out/bench_c*.log
 # parity : tools/parity_report.py -> gpurun_out/parity.json (per-term deltas vs the reference)
 # bench  : python bench.py (the driver's default line) -> gpurun_out/bench.log
 # prof   : rocprofv3 --kernel-trace --stats of a serialized bench (its roofline-kernel average
@@ -21,6 +22,10 @@ for s in $STEPS; do
     parity) timeout -k 10 300 python -u tools/parity_report.py --out gpurun_out/parity.json > gpurun_out/parity.log 2>&1 || { echo "parity failed"; tail -20 gpurun_out/parity.log; exit 1; } ;;
     bench)  timeout -k 10 900 python -u bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
             tail -1 gpurun_out/bench.log ;;
+    c2|c4)  timeout -k 10 600 python -u bench.py --config $s --no-cpu-baseline > gpurun_out/bench_$s.log 2>&1 || { echo "bench $s failed"; tail -30 gpurun_out/bench_$s.log; exit 1; }
+            tail -1 gpurun_out/bench_$s.log | cut -c1-240 ;;
+    gemm)   timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_fp8_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gemm.log 2>&1 || { echo "gemm tests failed"; tail -30 gpurun_out/pytest_gemm.log; exit 1; }
+            tail -1 gpurun_out/pytest_gemm.log ;;
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-teacher-rate --no-cpu-baseline --no-delta $BENCH_ARGS > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; } ;;
     step)   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/profstep -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-delta --no-timer --no-teacher-rate $BENCH_ARGS > gpurun_out/profstep.log 2>&1 || { echo "profstep failed"; tail -20 gpurun_out/profstep.log; exit 1; }
             python3 tools/step_breakdown.py $(ls gpurun_out/profstep/*/run_results.db gpurun_out/profstep/run_results.db 2>/dev/null | head -1) 40 > gpurun_out/step_breakdown.txt 2>&1; head -45 gpurun_out/step_breakdown.txt ;;
