@@ -273,6 +273,9 @@ int kd_adamw(float* param, void* param_bf16, const float* grad, float* exp_avg, 
              const int32_t* skip_words, int n_skip, void* stream);
 /* out[0] += sum x^2 (gradient norm). */
 int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
+/* bytes zero bytes at ptr, stream-ordered (optimizer.zero_grad() on the flat gradient:
+ * torch.optim.Optimizer.zero_grad(set_to_none=False) that Lightning calls after each step). */
+int kd_zero(void* ptr, uint64_t bytes, void* stream);
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 /* fp8 row quantisation (the fp8 GEMM's operands): per row r of x (bf16 [R][K], K % 16 == 0)
  * scale[r] = amax_r / 448 (1 for an all-zero row) and q[r][k] = e4m3(clamp(x[r][k] * 448 /

@@ -103,6 +103,13 @@ int kd_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, 
     return kd::launch_adamw(p, pb, g, m, v, n, lr, b1, b2, eps, wd, step, gscale, skip, n_skip, s);
 }
 int kd_sumsq(const float* x, int64_t n, float* out, void* s) { return kd::launch_sumsq(x, n, out, s); }
+int kd_zero(void* ptr, uint64_t bytes, void* s) {
+    KD_CHECK_ARG(ptr || bytes == 0, "zero: null pointer");
+    if (bytes == 0) return KD_OK;
+    const hipError_t e = hipMemsetAsync(ptr, 0, bytes, kd::as_stream(s));
+    if (e != hipSuccess) return kd::fail(KD_ERR_LAUNCH, std::string("kd_zero: ") + hipGetErrorString(e));
+    return KD_OK;
+}
 int kd_image_src_map(const int64_t* ids, int B, int L, int64_t tok, const int32_t* map, int ld, const int32_t* len,
                      int32_t* src, int32_t* err, void* s) {
     return kd::launch_image_src_map(ids, B, L, tok, map, ld, len, src, err, s);

@@ -121,10 +121,10 @@ class FusedAdamW(torch.optim.Optimizer):
         lo, hi = m._trainable_range()
         if m._opt_pending and m.concurrent_student:   # zero behind the AdamW on its stream
             with torch.cuda.stream(m._opt_stream):
-                m.student_model.P._grad[lo:hi].zero_()
+                ops.zero_(m.student_model.P._grad[lo:hi])
                 m._opt_done.record(m._opt_stream)
         else:
-            m.student_model.P.grad[lo:hi].zero_()
+            ops.zero_(m.student_model.P.grad[lo:hi])
 
 
 class _ErrorWatch:

@@ -472,6 +472,14 @@ def adamw(p, pb, g, m, v, lr, b1, b2, eps, wd, step, gscale=None, skip_words=Non
             float(b1), float(b2), float(eps), float(wd), int(step), _ptr(gscale), _ptr(skip_words), ns, _stream())
 
 
+def zero_(x: torch.Tensor) -> torch.Tensor:
+    """x[...] = 0 on the current stream through the library (kd_zero; x contiguous)."""
+    if not x.is_contiguous():
+        raise RuntimeError("zero_: needs a contiguous tensor")
+    NV.call("kd_zero", x.data_ptr(), x.numel() * x.element_size(), _stream())
+    return x
+
+
 def sumsq(x, out):
     NV.call("kd_sumsq", x.data_ptr(), x.numel(), out.data_ptr(), _stream())
     return out
