@@ -1,6 +1,8 @@
-"""Epilogue cost of the step's small forward GEMMs: each shape timed with the epilogue it has
-in the step (bias / GELU-tanh / aux / residual) and plain, back to back (sustained clock).
+"""Epilogue cost of the step's forward GEMMs: each shape timed with the epilogue it has in the
+step (bias / GELU-tanh / aux / residual / SwiGLU) and plain, back to back (sustained clock),
+plus the fp32-accumulate weight-gradient shapes. EPI_SHAPES=a,b filters by name substring.
     python tools/epi_cost.py [iters] [variant ...]"""
+import os
 import sys
 from pathlib import Path
 
@@ -30,7 +32,6 @@ SHAPES = [
     ("qwen 7b gate|up", 6144, 37888, 3584, False, None, False, False),
     ("qwen 7b swiglu", 6144, 37888, 3584, False, "swiglu", False, False),
 ]
-import os
 if os.environ.get("EPI_SHAPES"):
     SHAPES = [s_ for s_ in SHAPES if any(k in s_[0] for k in os.environ["EPI_SHAPES"].split(","))]
 
