@@ -382,9 +382,13 @@ class LlavaOnevisionModel:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is None or not h.value:
+            return
+        try:
             NV.lib().kd_model_destroy(h)
-            self._h = None
+        except Exception:   # interpreter shutdown: the module's globals are already torn down
+            return
+        self._h = None
 
     # -- freeze masks mirroring DT:468-523 (applied to the student), kept in the runtime too
     def set_trainable(self, vision: bool, projector: bool, language: bool):
