@@ -47,7 +47,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 5
+#define KD_ABI_VERSION 6
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -87,11 +87,20 @@ typedef struct {
                                [1] first offending label, [2] its row + row_base,
                                [3] claim flag                                          */
     int32_t row_base;       /* added to the row reported in err_out[2]                   */
+    float* dscale;          /* optional device float: dlogits are stored relative to a scale
+                               c (dlogits = d(total)/d(logits) * grad_scale / c) and the
+                               consumer multiplies c back in fp32 (e.g. kd_gemm alpha_dev).
+                               c = the CE coefficient ce_weight * grad_scale / n_valid (else
+                               the KD coefficient) is written here, so the CE one-hot
+                               element, the same value in every row, is ~ -1 (exact in
+                               bf16) instead of a bf16-rounded -1/n_valid (a systematic
+                               bias of the whole gradient).  NULL: c = 1.               */
+    int32_t dscale_given;   /* 1: read c from *dscale (an earlier call's; loss groups)    */
 } kd_loss_params;
 
 /* loss_out (device float[4]): [0] KD term (mean, incl. T^2, unweighted)
  *                             [1] student CE   [2] teacher CE   [3] total
- * dlogits: d(total)/d(student_logits) * grad_scale, bf16 [B*L, ld_d] (may be NULL).
+ * dlogits: d(total)/d(student_logits) * grad_scale (/ *dscale), bf16 [B*L, ld_d] (may be NULL).
  * labels: int64 [B, L] (row-major).  LoCa requires every label in [0, V_s): a label
  * outside raises KD_ERR_LABEL_RANGE from kd_loss_check() (the reference raises
  * RuntimeError from gather, DT:166) and is recorded in params.err_out (read
@@ -271,6 +280,9 @@ int kd_ntxent(const float* fs, const float* ft, int n, int D, float tau, float w
 int kd_adamw(float* param, void* param_bf16, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
              float lr, float beta1, float beta2, float eps, float weight_decay, int step, const float* gscale,
              const int32_t* skip_words, int n_skip, void* stream);
+/* out[i] = a[i] * b[i], i < n (device scalars: e.g. the upstream gradient times the
+ * dlogits scale of kd_loss_params.dscale, for kd_gemm's alpha_dev). */
+int kd_scalar_mul(const float* a, const float* b, float* out, int n, void* stream);
 /* out[0] += sum x^2 (gradient norm). */
 int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
 /* bytes zero bytes at ptr, stream-ordered (optimizer.zero_grad() on the flat gradient:

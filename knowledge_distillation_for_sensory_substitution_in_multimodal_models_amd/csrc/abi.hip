@@ -103,6 +103,9 @@ int kd_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, 
     return kd::launch_adamw(p, pb, g, m, v, n, lr, b1, b2, eps, wd, step, gscale, skip, n_skip, s);
 }
 int kd_sumsq(const float* x, int64_t n, float* out, void* s) { return kd::launch_sumsq(x, n, out, s); }
+int kd_scalar_mul(const float* a, const float* b, float* out, int n, void* s) {
+    return kd::launch_scalar_mul(a, b, out, n, s);
+}
 int kd_zero(void* ptr, uint64_t bytes, void* s) {
     KD_CHECK_ARG(ptr || bytes == 0, "zero: null pointer");
     if (bytes == 0) return KD_OK;

@@ -53,7 +53,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
         objs = list(ex.map(_compile, srcs))
     newest = max(o.stat().st_mtime for o in objs)
     if LIB.exists() and LIB.stat().st_mtime > newest:
-        build_c_host(verbose)
+        _try_c_host(verbose)
         return LIB
     cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(LIB)]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -61,8 +61,19 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     if verbose:
         print(f"built {LIB}")
-    build_c_host(verbose)
+    _try_c_host(verbose)
     return LIB
+
+
+def _try_c_host(verbose: bool) -> None:
+    """The C-host example is not part of the library: build it when its source is shipped,
+    and only warn when it does not compile."""
+    if not C_HOST_SRC.exists():
+        return
+    try:
+        build_c_host(verbose)
+    except RuntimeError as e:   # pragma: no cover - an example build failure is not fatal
+        print(f"warning: {e}", file=sys.stderr)
 
 
 C_HOST_SRC = REPO / "tools" / "c_host_step.cpp"

@@ -500,13 +500,12 @@ template <bool T1>
 __global__ void __launch_bounds__(LG_NT)
 k_loss_grad_loca(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
                  int V, int rows, float invT, float clamp_min, const RowStats* __restrict__ stats,
-                 const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g, float kd_coef,
-                 float ce_coef_num, const float* __restrict__ n_valid, bf16* __restrict__ D_, int64_t ld_d,
+                 const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g,
+                 const float* __restrict__ coefs, bf16* __restrict__ D_, int64_t ld_d,
                  float* __restrict__ part_kl) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smask[];
     __shared__ float red[LG_NW];
-    const float nv = *n_valid;
-    const float ce_coef = nv > 0.f ? ce_coef_num / nv : 0.f;
+    const float ce_coef = coefs[1], kd_coef = coefs[2];   // both / the stored dlogits scale
     const int tid = threadIdx.x;
     const int nwords = (V + 63) / 64;
     for (int i = tid; i < nwords; i += LG_NT) smask[i] = mask_g[i];
@@ -646,8 +645,21 @@ __global__ void k_finalize(const RowStats* __restrict__ stats, const float* __re
     }
 }
 
-// count of valid shifted labels, computed on device into a float (for the CE mean)
-__global__ void k_count_valid(const int64_t* __restrict__ labels, int B, int L, int V, float* out) {
+// count of valid shifted labels (the CE mean's denominator lives on the device: no host
+// sync) and the gradient coefficients coefs = {n_valid, ce_coef / c, kd_coef / c}, where c
+// is the scale the dlogits are stored relative to (dlogits = dz / c):
+//   dscale == NULL       c = 1
+//   dscale, !given       c = ce_coef (= ce_weight * grad_scale / n_valid) if > 0, else kd_coef
+//                        if > 0, else 1; written to *dscale
+//   dscale, given        c = *dscale (an earlier call's: loss groups share one scale)
+// Why: every row's one-hot element of the CE gradient is ce_coef * (p - 1) ~ -ce_coef, the
+// SAME value in every row; rounded to bf16 it carries the same relative error (up to 2^-9)
+// in every row, a systematic bias of the whole student gradient (+0.13 % of its norm on the
+// tiny fixtures).  Stored relative to c it is ~ -1, exact in bf16; the consumer multiplies
+// c back in fp32 (the dgrad / wgrad GEMMs' alpha_dev).
+__global__ void k_count_valid(const int64_t* __restrict__ labels, int B, int L, int V, float ce_num,
+                              float kd_coef, float* __restrict__ dscale, int given, float* __restrict__ coefs) {
+    float* out = coefs;
     __shared__ float red[NW];
     float c = 0.f;
     for (int r = threadIdx.x; r < B * L; r += NT) {
@@ -658,7 +670,20 @@ __global__ void k_count_valid(const int64_t* __restrict__ labels, int B, int L, 
         }
     }
     c = block_sum<NW>(c, red);
-    if (threadIdx.x == 0) *out = c;
+    if (threadIdx.x == 0) {
+        *out = c;
+        const float cec = c > 0.f ? ce_num / c : 0.f;
+        float sc = 1.f;
+        if (dscale != nullptr) {
+            if (given) sc = *dscale;
+            else {
+                sc = cec > 0.f ? cec : (kd_coef > 0.f ? kd_coef : 1.f);
+                *dscale = sc;
+            }
+        }
+        coefs[1] = cec / sc;
+        coefs[2] = kd_coef / sc;
+    }
 }
 
 template <int VARIANT>
@@ -666,14 +691,11 @@ __global__ void __launch_bounds__(LG_NT)
 k_loss_grad(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
             int V, int rows, float invT, float clamp_min, const RowStats* __restrict__ stats,
             const float* __restrict__ ovr,
-            const unsigned long long* __restrict__ mask_g, float kd_coef, float ce_coef_num,
-            const float* __restrict__ n_valid, bf16* __restrict__ D_, int64_t ld_d,
-            float* __restrict__ part_kl) {
+            const unsigned long long* __restrict__ mask_g, const float* __restrict__ coefs,
+            bf16* __restrict__ D_, int64_t ld_d, float* __restrict__ part_kl) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smask[];
     __shared__ float red[LG_NW];
-    // the CE mean's denominator lives on the device (no host sync)
-    const float nv = *n_valid;
-    const float ce_coef = nv > 0.f ? ce_coef_num / nv : 0.f;
+    const float ce_coef = coefs[1], kd_coef = coefs[2];
     loss_grad_body<VARIANT>(T_, ld_t, S_, ld_s, V, rows, invT, clamp_min, stats, ovr,
                             mask_g, kd_coef, ce_coef, D_, ld_d, part_kl, smask, red);
 }
@@ -711,7 +733,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     float* ovr = (float*)(w + lo.ovr);
     float* part_kl = (float*)(w + lo.part_kl);
     int* err = (int*)(w + lo.err);
-    float* nvalid = (float*)(w + lo.err + 4);
+    float* coefs = (float*)(w + lo.err + 4);   // {n_valid, ce coef, kd coef} (k_count_valid)
     const int rows = B * L;
     const float invT = 1.f / p.temperature;
     const bf16* T_ = (const bf16*)(variant == KD_LOSS_NONE ? nullptr : teacher);
@@ -733,12 +755,13 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
         hipLaunchKernelGGL(k_ovr_mask, dim3(nb), dim3(256), 0, stream, lab_last, klo_last, stats, V_s, mask, ovr);
         KD_LAUNCH_CHECK("k_ovr_mask");
     }
-    hipLaunchKernelGGL(k_count_valid, dim3(1), dim3(NT), 0, stream, labels, B, L, V_s, nvalid);
-    KD_LAUNCH_CHECK("k_count_valid");
     const double N = (double)rows * (double)V_s;
     const float T = p.temperature;
     const float kd_coef = (float)((double)p.kd_weight * T / N * p.grad_scale);
     const float ce_num = p.ce_weight * p.grad_scale;
+    hipLaunchKernelGGL(k_count_valid, dim3(1), dim3(NT), 0, stream, labels, B, L, V_s, ce_num,
+                       variant == KD_LOSS_NONE ? 0.f : kd_coef, p.dscale, p.dscale_given ? 1 : 0, coefs);
+    KD_LAUNCH_CHECK("k_count_valid");
     const size_t smem = variant == KD_LOSS_LOCA ? (size_t)((V_s + 63) / 64) * 8 : 0;
     if (smem > 150 * 1024) return fail(KD_ERR_SHAPE, "kd_loss: vocab too large for LDS mask");
     bf16* D_ = (bf16*)dlogits;
@@ -747,15 +770,14 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     const int lg_grid = rows < LG_ROWS ? rows : LG_ROWS;
 #define KD_LAUNCH_LG(VAR)                                                                          \
     hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, \
-                       V_s, rows, invT, p.clamp_min, stats, ovr, mask, kd_coef,                    \
-                       ce_num, nvalid, D_, ld_d, part_kl)
+                       V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl)
     const bool loca_fast = variant == KD_LOSS_LOCA && kd_coef >= 0.f && T_ != nullptr;
     if (loca_fast && invT == 1.f) {
         hipLaunchKernelGGL(k_loss_grad_loca<true>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, V_s,
-                           rows, invT, p.clamp_min, stats, ovr, mask, kd_coef, ce_num, nvalid, D_, ld_d, part_kl);
+                           rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl);
     } else if (loca_fast) {
         hipLaunchKernelGGL(k_loss_grad_loca<false>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, V_s,
-                           rows, invT, p.clamp_min, stats, ovr, mask, kd_coef, ce_num, nvalid, D_, ld_d, part_kl);
+                           rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl);
     } else switch (variant) {
         case KD_LOSS_NONE: KD_LAUNCH_LG(KD_LOSS_NONE); break;
         case KD_LOSS_LOCA: KD_LAUNCH_LG(KD_LOSS_LOCA); break;

@@ -43,6 +43,7 @@ int launch_ntxent(const float* fs, const float* ft, int n, int D, float tau, flo
 int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                  float eps, float wd, int step, const float* gscale, const int32_t* skip, int n_skip, void* stream);
 int launch_sumsq(const float* x, int64_t n, float* out, void* stream);
+int launch_scalar_mul(const float* a, const float* b, float* out, int n, void* stream);
 int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, const int* map, int map_ld,
                          const int* map_len, int* src, int* err, void* stream);
 int launch_quant_rows_f8(const void* x, int64_t ldx, int R, int K, void* q, int64_t ldq, float* scale, void* stream);

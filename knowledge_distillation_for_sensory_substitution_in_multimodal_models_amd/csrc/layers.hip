@@ -683,6 +683,11 @@ __global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restric
     if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
+__global__ void k_scalar_mul(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ out, int n) {
+    const int i = threadIdx.x;
+    if (i < n) out[i] = a[i] * b[i];
+}
+
 __global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16* __restrict__ y, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = (bf16)x[i];
 }
@@ -958,6 +963,15 @@ int launch_sumsq(const float* x, int64_t n, float* out, void* stream) {
     KD_CHECK_ARG(x && out, "sumsq: null pointer");
     hipLaunchKernelGGL(k_sumsq, dim3(grid_for(n, 256, 2048)), dim3(256), 0, as_stream(stream), x, n, out);
     KD_LAUNCH_CHECK("k_sumsq");
+    return KD_OK;
+}
+
+int launch_scalar_mul(const float* a, const float* b, float* out, int n, void* stream) {
+    KD_CHECK_ARG(a && b && out, "scalar_mul: null pointer");
+    KD_CHECK_SHAPE(n >= 0 && n <= 1024, "scalar_mul: n must be in [0, 1024]");
+    if (n == 0) return KD_OK;
+    hipLaunchKernelGGL(k_scalar_mul, dim3(1), dim3(n), 0, as_stream(stream), a, b, out, n);
+    KD_LAUNCH_CHECK("k_scalar_mul");
     return KD_OK;
 }
 

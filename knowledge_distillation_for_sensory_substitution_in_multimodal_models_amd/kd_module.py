@@ -109,9 +109,15 @@ class FusedAdamW(torch.optim.Optimizer):
         P = m.student_model.P
         if hi > lo:
             with torch.cuda.stream(side):
+                # the error words as of this step's loss (a snapshot taken on the main stream
+                # right after it): the live words may already carry the NEXT step's teacher
+                # error (its forward runs on the main stream beside this AdamW), which must not
+                # cancel this valid step's update
+                skip = m._errors.snapshot if m._errors.snapshot is not None else m._errors.words
                 ops.adamw(P.master[lo:hi], P.flat[lo:hi], P._grad[lo:hi], P.exp_avg[lo:hi], P.exp_avg_sq[lo:hi],
                           g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count,
-                          skip_words=m._errors.words)
+                          skip_words=skip)
+                skip.record_stream(side)   # allocated on the main stream
                 m._opt_done.record(side)
             m._opt_pending = True
         return loss
@@ -143,6 +149,7 @@ class _ErrorWatch:
     def __init__(self, dev):
         self.words = torch.zeros(8, dtype=torch.int32, device=dev)
         self.kd = self.words[0:4]
+        self.snapshot = None  # the words as of the last step's loss (kd_adamw's skip words)
         self.host = torch.zeros((self.SLOTS, 6), dtype=torch.int32).pin_memory()
         self.pending = []    # (event, slot, info)
         self.next = 0
@@ -159,6 +166,9 @@ class _ErrorWatch:
             self.check(block=True, upto=1)
         slot = self.next
         self.next = (self.next + 1) % self.SLOTS
+        # device snapshot for this step's AdamW (ordered after this step's loss and teacher
+        # forward, before the next step's teacher forward: all on this stream)
+        self.snapshot = self.words.clone()
         self.host[slot].copy_(self.words[0:6], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -175,6 +185,8 @@ class _ErrorWatch:
                     self.pending = []
                     torch.cuda.synchronize()
                     self.words.zero_()
+                    if self.snapshot is not None:
+                        self.snapshot.zero_()
                     self._raise_if(h, info)
             else:
                 keep.append((ev, slot, info))
@@ -205,7 +217,7 @@ class _KDBase(_Base):
 
     def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1,
                  seed_teacher: int = 1, seed_student: int = 2, state_dict=None, loss_group_size: int | None = None,
-                 accumulate_grad_batches: int = 1, teacher_fp8: bool = False, **_ignored):
+                 accumulate_grad_batches: int | None = None, teacher_fp8: bool = False, **_ignored):
         super().__init__()
         self.phase = phase
         self.learning_rate = learning_rate
@@ -216,8 +228,9 @@ class _KDBase(_Base):
         # batch_size=1 x accumulate_grad_batches semantics (DT1T:70, :155).
         self.loss_group_size = loss_group_size
         # micro-batches per optimizer step (Lightning's accumulate_grad_batches): only the last
-        # backward of a step all-reduces (DP); see also no_sync()
-        self.accumulate_grad_batches = int(accumulate_grad_batches)
+        # backward of a step all-reduces (DP); see also no_sync().  None: the attached
+        # Trainer's value (the reference sets it there, DT1T:70, :155), else 1
+        self.accumulate_grad_batches = None if accumulate_grad_batches is None else int(accumulate_grad_batches)
         dev = _device()
         small = model_name_student.startswith("tiny")
         self.student_model = LlavaOnevisionModel(MODEL_CONFIGS[model_name_student], dev, trainable=True,
@@ -253,6 +266,7 @@ class _KDBase(_Base):
         self.last_terms = None
         self.last_ntxent = None
         self.last_logits = None
+        self.last_post = None            # (student, teacher) post-LN hook outputs when keep_logits
         self._micro = 0                  # backward passes since the last optimizer step
         self._no_sync_depth = 0
         # data parallel
@@ -362,15 +376,20 @@ class _KDBase(_Base):
         t3 = None if t_logits is None else t_logits.view(B, L, -1)
         loss4 = torch.empty(4, dtype=torch.float32, device=s_logits.device)
         dlogits = torch.empty((B, L, Vs), dtype=torch.bfloat16, device=s_logits.device) if train else None
+        # dlogits are stored relative to the CE coefficient (kd_loss_params.dscale): the one-hot
+        # element of every row is then ~ -1, exact in bf16, instead of the same bf16-rounded
+        # -1/n_valid in every row, a systematic +0.13 % on the whole gradient (tools/grad_bias_study.py)
+        dscale = torch.empty(1, dtype=torch.float32, device=s_logits.device) if train else None
         for g in range(ng):   # loss groups: mean over groups of each group's loss
             sl = slice(g * G, (g + 1) * G)
             ops.kd_loss_fwd_bwd(s3[sl], None if t3 is None else t3[sl], labels[sl], variant,
                                 temperature=T, alpha=0.8, kd_weight=kd_w, ce_weight=ce_w, grad_scale=1.0 / ng,
                                 want_grad=train, loss_out=loss4, out_scale=1.0 / ng, accumulate=g > 0,
                                 dlogits_out=None if dlogits is None else dlogits[sl], err_out=self._errors.kd,
-                                row_base=g * G * L)
+                                row_base=g * G * L, dscale=dscale, dscale_given=g > 0)
         if self.keep_logits:
             self.last_logits = (s3, t3)
+            self.last_post = (sfwd.get("post_ln"), t_post)
         del s_logits, t_logits, s3, t3
         total = loss4[3]
         dps = None
@@ -392,7 +411,7 @@ class _KDBase(_Base):
         self.last_terms = loss4
         self._errors.record(dict(L=L, V=Vs))
         if train:
-            self._ctx = dict(sfwd=sfwd, dlogits=dlogits, dps=dps)
+            self._ctx = dict(sfwd=sfwd, dlogits=dlogits, dscale=dscale, dps=dps)
         return total
 
     def _grad_fence(self):
@@ -408,7 +427,8 @@ class _KDBase(_Base):
         if bwd is not main:
             bwd.wait_stream(main)
             sf = ctx["sfwd"]
-            for t in (gscale, ctx["dlogits"], ctx["dps"], sf["hn"], sf["src"], sf["ids"], sf.get("post_ln")):
+            for t in (gscale, ctx["dlogits"], ctx["dscale"], ctx["dps"], sf["hn"], sf["src"], sf["ids"],
+                      sf.get("post_ln")):
                 if t is not None:
                     t.record_stream(bwd)   # freed on the host before the backward has run
         with torch.cuda.stream(bwd):
@@ -420,17 +440,18 @@ class _KDBase(_Base):
         s = self.student_model
         self._micro += 1
         sync = self._gsync is not None and self._no_sync_depth == 0 and \
-            self._micro % max(1, self.accumulate_grad_batches) == 0
+            self._micro % self._accumulate() == 0
         if self._gsync is not None:
             self._gsync.begin(sync)
         sf = ctx["sfwd"]
         hn = sf["hn"]
         W = s.lm_head_weight()
         dl = ctx["dlogits"].view(hn.shape[0], -1)
-        dhn = ops.gemm(dl, W.t(), alpha_dev=gscale)                          # lm_head dgrad
+        dscale = ops.scalar_mul(gscale, ctx["dscale"])                      # upstream x the dlogits scale
+        dhn = ops.gemm(dl, W.t(), alpha_dev=dscale)                          # lm_head dgrad
         if s.train_language:   # lm_head / tied embed wgrad, on the lane ahead of the runtime's backward
-            s.wlane.run(lambda: ops.gemm(dl.t(), hn.t(), out=s.lm_head_grad(), accumulate=True, alpha_dev=gscale),
-                        dl, hn, gscale)
+            s.wlane.run(lambda: ops.gemm(dl.t(), hn.t(), out=s.lm_head_grad(), accumulate=True, alpha_dev=dscale),
+                        dl, hn, dscale)
         del dl, ctx["dlogits"]
         dpost = None
         if ctx["dps"] is not None and s.train_vision:
@@ -438,6 +459,17 @@ class _KDBase(_Base):
         s.backward(sf, dhn, dpost, on_layer_done=self._on_layer_done if sync else None)
         if self._gsync is not None:
             self._gsync.end(*self._trainable_range())
+
+    def _accumulate(self) -> int:
+        """Micro-batches per optimizer step: the constructor's value, else the attached
+        Lightning Trainer's accumulate_grad_batches, else 1."""
+        if self.accumulate_grad_batches is not None:
+            return max(1, self.accumulate_grad_batches)
+        try:
+            tr = self.trainer   # LightningModule.trainer raises when no Trainer is attached
+        except Exception:
+            tr = None
+        return max(1, int(getattr(tr, "accumulate_grad_batches", 1) or 1)) if tr is not None else 1
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -504,11 +536,26 @@ class _KDBase(_Base):
                 self.teacher_model.enable_fp8()   # re-quantise the new weights
 
     def _hparams(self):
+        # everything that changes the objective or the update is saved, so load_from_checkpoint
+        # resumes the same run (loss grouping changes the loss: test_loss_group_size_*)
         return {"model_name_student": self.model_name_student, "model_name_teacher": self.model_name_teacher,
-                "learning_rate": self.learning_rate, "phase": self.phase}
+                "learning_rate": self.learning_rate, "phase": self.phase, **self._run_hparams()}
+
+    def _run_hparams(self):
+        return {"loss_group_size": self.loss_group_size, "accumulate_grad_batches": self.accumulate_grad_batches,
+                "teacher_fp8": bool(getattr(self, "teacher_fp8", False))}
+
+    def on_train_epoch_end(self):
+        """A batch rejected among the last steps of an epoch is reported here (the reference
+        raises inside its training_step, DT:166), not silently dropped."""
+        self.check_errors()
+
+    def on_train_end(self):
+        self.check_errors()
 
     def save_checkpoint(self, path, epoch: int = 0, global_step: int = 0):
         """Lightning-style .ckpt: {'state_dict': {student_model.*, teacher_model.*}, ...}."""
+        self.check_errors()   # never write weights past an unreported rejected batch
         sd = {k: v.detach().cpu() for k, v in self.kd_state_dict().items()}
         torch.save({"state_dict": sd, "epoch": epoch, "global_step": global_step,
                     "pytorch-lightning_version": "2.4.0", "hyper_parameters": self._hparams()}, path)
@@ -595,7 +642,7 @@ class LlavaOnevisionModule(_KDBase):
         self.model = self.student_model
 
     def _hparams(self):
-        return {"model_name": self.model_name, "learning_rate": self.learning_rate}
+        return {"model_name": self.model_name, "learning_rate": self.learning_rate, **self._run_hparams()}
 
     def _loss_spec(self):
         return "none", 1.0, 0.0, 1.0, None

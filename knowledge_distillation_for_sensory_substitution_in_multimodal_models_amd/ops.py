@@ -108,7 +108,8 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
                     clamp_min: float = 1e-8, teacher_ce: bool = True, want_grad: bool = True,
                     check: bool = False, loss_out: torch.Tensor | None = None, out_scale: float = 1.0,
                     accumulate: bool = False, dlogits_out: torch.Tensor | None = None,
-                    err_out: torch.Tensor | None = None, row_base: int = 0):
+                    err_out: torch.Tensor | None = None, row_base: int = 0,
+                    dscale: torch.Tensor | None = None, dscale_given: bool = False):
     """Fused KD-loss forward + backward (include/kdstep.h kd_loss_fwd_bwd).
 
     student_logits [B, L, V_s] bf16 (last dim contiguous), teacher_logits [B, L, V_t] bf16,
@@ -118,7 +119,10 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
     Loss groups: loss_out / out_scale / accumulate let consecutive calls on
     sub-batches average their terms on the device; dlogits_out receives the gradient rows
     of this call.  err_out (device int32[4], caller-zeroed) collects label-range errors
-    without a host sync (kd_loss_params.err_out).
+    without a host sync (kd_loss_params.err_out).  dscale (device fp32 [1]): the dlogits are
+    stored relative to the scale written there (or read from there, dscale_given), which
+    the consumer multiplies back in fp32 (kd_loss_params.dscale: the CE one-hot element
+    stays exact in bf16).
     """
     B, L, V_s = student_logits.shape
     _require(student_logits, torch.bfloat16, "student_logits")
@@ -146,11 +150,14 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
         dl = None
     if err_out is not None:
         _require(err_out, torch.int32, "err_out")
+    if dscale is not None:
+        _require(dscale, torch.float32, "dscale")
     nbytes = NV.lib().kd_loss_workspace_size(B, L, V_s)
     ws = _workspace("kd_loss", nbytes, dev)
     prm = NV.KdLossParams(v, float(temperature), float(alpha), float(kd_weight), float(ce_weight),
                          float(grad_scale), float(clamp_min), 1 if teacher_ce else 0, float(out_scale),
-                         1 if accumulate else 0, _ptr(err_out), int(row_base))
+                         1 if accumulate else 0, _ptr(err_out), int(row_base), _ptr(dscale),
+                         1 if dscale_given else 0)
     NV.call("kd_loss_fwd_bwd", _ptr(teacher_logits), ld_t, V_t, _ptr(student_logits),
            student_logits.stride(1), V_s, _ptr(labels), B, L, prm, _ptr(loss), _ptr(dl),
            V_s, _ptr(ws), ws.numel(), _stream())
@@ -482,6 +489,17 @@ def zero_(x: torch.Tensor) -> torch.Tensor:
 
 def sumsq(x, out):
     NV.call("kd_sumsq", x.data_ptr(), x.numel(), out.data_ptr(), _stream())
+    return out
+
+
+def scalar_mul(a, b, out=None):
+    """out = a * b elementwise on device fp32 scalars (kd_scalar_mul)."""
+    _require(a, torch.float32, "a")
+    _require(b, torch.float32, "b")
+    if a.numel() != b.numel():
+        raise RuntimeError("scalar_mul: size mismatch")
+    out = out if out is not None else torch.empty_like(a)
+    NV.call("kd_scalar_mul", a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), _stream())
     return out
 
 

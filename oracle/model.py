@@ -146,7 +146,7 @@ def kd_step_losses(kind: str, teacher: OracleLlava | None, student: OracleLlava,
     s_logits, s_post = student(batch["depth_input_ids"], batch["depth_pixel_values"], batch["image_sizes"])
     labels = batch["labels"]
     if kind == "bd":
-        return KL.bd_total(s_logits, labels), dict(ce=KL.causal_lm_ce(s_logits, labels))
+        return KL.bd_total(s_logits, labels), dict(ce=KL.causal_lm_ce(s_logits, labels), s_logits=s_logits)
     with torch.no_grad():
         t_logits, t_post = teacher(batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"])
     sf = KL.pooled_features(s_post)

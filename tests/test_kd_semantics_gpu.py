@@ -106,6 +106,51 @@ def test_error_words_are_sticky_for_queued_steps(dev):
     assert torch.equal(m.student_model.P.flat, before)
 
 
+@pytest.mark.skipif(not hasattr(torch.cuda, "_sleep"), reason="needs torch.cuda._sleep")
+def test_next_steps_teacher_error_does_not_cancel_this_update(dev):
+    """Step t is valid; step t+1's RGB ids carry one image token too few (the teacher's
+    masked_scatter size mismatch).  Step t+1's teacher forward runs on the main stream
+    beside step t's AdamW (held back here on the student stream), so its error word is
+    set before AdamW t runs: AdamW t must still apply (it reads the words as of its own
+    loss), AdamW t+1 must not, and the error is reported once."""
+    K = _K()
+    meta, _ = load("lb")
+    good = batch(meta, dev)
+    bad = dict(good)
+    bad["rgb_input_ids"] = good["rgb_input_ids"].clone()
+    img = (bad["rgb_input_ids"][0] == 151646).nonzero()[0, 0]
+    bad["rgb_input_ids"][0, img] = 100
+    # the expected state: one valid step, fully synchronised
+    r = K.LogitBasedKD("tiny-student", "tiny-teacher")
+    (ropt,), _ = r.configure_optimizers()
+    w0 = r.student_model.P.master.clone()
+    r.training_step(good, 0).backward()
+    ropt.step()
+    r.check_errors()
+    torch.cuda.synchronize()
+    ref_upd = (r.student_model.P.master - w0).double()
+    m = K.LogitBasedKD("tiny-student", "tiny-teacher")
+    (opt,), _ = m.configure_optimizers()
+    assert torch.equal(m.student_model.P.master, w0)
+    m.training_step(good, 0).backward()
+    with torch.cuda.stream(m._stu_stream):
+        torch.cuda._sleep(1_000_000_000)     # AdamW t queues behind this
+    raised = []
+    _attempt(opt.step, raised)
+    opt.zero_grad()
+    _attempt(lambda: m.training_step(bad, 1).backward(), raised)
+    if not raised:
+        _attempt(opt.step, raised)
+    if not raised:
+        _attempt(m.check_errors, raised)
+    torch.cuda.synchronize()
+    assert len(raised) == 1 and "image-token count" in raised[0], raised
+    upd = (m.student_model.P.master - w0).double()
+    assert float(upd.abs().max()) > 0, "step t's valid update was skipped"
+    cos = float((upd @ ref_upd) / (upd.norm() * ref_upd.norm()))
+    assert cos >= 0.999 and abs(float(upd.norm() / ref_upd.norm()) - 1) <= 1e-3, cos
+
+
 def test_ce_only_accepts_minus100_and_rejects_out_of_vocab(dev):
     K = _K()
     meta, _ = load("bd")
@@ -172,6 +217,12 @@ def test_checkpoint_reload_with_reference_keywords(dev, tmp_path):
     rb = K.LlavaOnevisionModule.load_from_checkpoint(str(pb), model_name="tiny-student", processor=None,
                                                      torch_dtype=torch.float16)
     assert torch.equal(rb.student_model.P.flat, bd.student_model.P.flat)
+    # the knobs that change the objective / the update survive a reload without keywords
+    lb = K.LogitBasedKD("tiny-student", "tiny-teacher", loss_group_size=1, accumulate_grad_batches=4)
+    pl = tmp_path / "lb.ckpt"
+    lb.save_checkpoint(str(pl))
+    rl = K.LogitBasedKD.load_from_checkpoint(str(pl))
+    assert rl.loss_group_size == 1 and rl.accumulate_grad_batches == 4 and rl.teacher_fp8 is False
 
 
 _DP_CHILD = r'''

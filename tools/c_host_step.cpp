@@ -195,6 +195,9 @@ int main(int argc, char** argv) {
     lp.variant = KD_LOSS_LOCA; lp.temperature = 1.f; lp.alpha = 0.8f; lp.kd_weight = 1.f; lp.ce_weight = 1.f;
     lp.grad_scale = 1.f; lp.clamp_min = 1e-8f; lp.teacher_ce = 1; lp.out_scale = 1.f; lp.out_accumulate = 0;
     lp.err_out = err + 2; lp.row_base = 0;
+    // dlogits relative to the CE coefficient (kd_loss_params.dscale), multiplied back by the GEMMs
+    float* dscale = (float*)dalloc(4);
+    lp.dscale = dscale; lp.dscale_given = 0;
     KD(kd_loss_fwd_bwd(t_logits, Vt, Vt, s_logits, Vs, Vs, labels, B, L, lp, loss4, dlogits, Vs, lws, lwsb, main_s));
 
     // ---- lm_head (tied to embed_tokens in the 0.5B): dgrad dhn = dlogits W, wgrad on the lane
@@ -215,7 +218,7 @@ int main(int argc, char** argv) {
     kd_gemm_desc g{};
     g.M = M; g.N = H; g.K = Vs; g.a_layout = KD_LAYOUT_K_MAJOR; g.b_layout = KD_LAYOUT_MN_MAJOR;
     g.A = dlogits; g.lda = Vs; g.B = (char*)sw + emb_off * 2; g.ldb = H; g.C = dhn; g.ldc = H;
-    g.c_dtype = KD_DTYPE_BF16; g.alpha = 1.f; g.workspace = wsm; g.workspace_bytes = splitk;
+    g.c_dtype = KD_DTYPE_BF16; g.alpha = 1.f; g.alpha_dev = dscale; g.workspace = wsm; g.workspace_bytes = splitk;
     KD(kd_gemm(&g, main_s));
     hipEvent_t ev;
     HIP(hipEventCreate(&ev));
@@ -224,7 +227,8 @@ int main(int argc, char** argv) {
     kd_gemm_desc w{};
     w.M = Vs; w.N = H; w.K = M; w.a_layout = KD_LAYOUT_MN_MAJOR; w.b_layout = KD_LAYOUT_MN_MAJOR;
     w.A = dlogits; w.lda = Vs; w.B = hn_s; w.ldb = H; w.C = grad + emb_off; w.ldc = H;
-    w.c_dtype = KD_DTYPE_F32; w.accumulate = 1; w.alpha = 1.f; w.workspace = wsl; w.workspace_bytes = splitk;
+    w.c_dtype = KD_DTYPE_F32; w.accumulate = 1; w.alpha = 1.f; w.alpha_dev = dscale; w.workspace = wsl;
+    w.workspace_bytes = splitk;
     KD(kd_gemm(&w, lane_s));
 
     // ---- student backward (every trainable grad, +=), weight gradients on the lane

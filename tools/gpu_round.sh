@@ -19,7 +19,7 @@ for s in $STEPS; do
   case $s in
     tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
             tail -2 gpurun_out/pytest_gpu.log ;;
-    parity) timeout -k 10 300 python -u tools/parity_report.py --out gpurun_out/parity.json > gpurun_out/parity.log 2>&1 || { echo "parity failed"; tail -20 gpurun_out/parity.log; exit 1; } ;;
+    parity) timeout -k 10 600 python -u tools/parity_report.py --out gpurun_out/parity.json $PARITY_KINDS > gpurun_out/parity.log 2>&1 || { echo "parity failed"; tail -20 gpurun_out/parity.log; exit 1; } ;;
     bench)  timeout -k 10 900 python -u bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
             tail -1 gpurun_out/bench.log ;;
     c2|c4)  timeout -k 10 600 python -u bench.py --config $s --no-cpu-baseline > gpurun_out/bench_$s.log 2>&1 || { echo "bench $s failed"; tail -30 gpurun_out/bench_$s.log; exit 1; }
