@@ -254,7 +254,7 @@ def fp8_teacher_delta(m, batch):
         res[name] = (m.last_terms.tolist(), m.last_logits[1].float())
         m.last_logits = None
     m.keep_logits = False
-    m.teacher_model.enable_fp8()
+    m.teacher_model.enable_fp8(m.teacher_fp8)
     (tf, lf), (tb, lb) = res["fp8"], res["bf16"]
     rel = float((lf - lb).norm() / lb.norm())
     cos = float((lf * lb).sum() / (lf.norm() * lb.norm()))

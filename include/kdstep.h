@@ -176,6 +176,8 @@ typedef struct {
     int32_t ab_dtype;         /* operand dtype: KD_DTYPE_BF16 (0) or KD_DTYPE_FP8_E4M3 (fp8 path) */
     const float* a_scale;     /* fp8 path: per-row scale of A [M] (A = a_scale[m] * qa[m][k])     */
     const float* b_scale;     /* fp8 path: per-row scale of B [N] (per output channel)           */
+    int32_t residual_dtype;   /* kd_dtype of residual: KD_DTYPE_BF16 (0) or KD_DTYPE_F32 (an fp32
+                                 residual stream; then C must be fp32 and act NONE; bf16 path only) */
 } kd_gemm_desc;
 /* fp8 path (ab_dtype = KD_DTYPE_FP8_E4M3; the fp8 teacher of BASELINE config c4): A and B are
  * OCP e4m3 bytes, both K-major, K % 16 == 0, lda / ldb % 16 == 0 (bytes = elements), 16-B
@@ -225,15 +227,16 @@ int kd_attn_bwd(const kd_attn_bwd_desc* desc, void* stream);
 /* ------------------------------------------------------------ layer ops ---- */
 /* LayerNorm (rms = 0; nn.LayerNorm, SigLIP, HF5 siglip :325-357, :567) or RMSNorm
  * (rms = 1; Qwen2RMSNorm, HF5 qwen2 :35-55) over rows of D (D % 8 == 0, D <= 4096).
+ * x: kd_dtype x_dtype (bf16, or fp32 for an fp32 residual stream); y bf16.
  * mean/rstd fp32 [R] saved for backward (mean unused for RMS, may be NULL). */
 int kd_norm_fwd(int rms, const void* x, int64_t ldx, const void* weight, const void* bias, void* y, int64_t ldy,
-                float* mean, float* rstd, int R, int D, float eps, void* stream);
+                float* mean, float* rstd, int R, int D, float eps, int x_dtype, void* stream);
 /* dx (bf16, or += when dx_accum) and fp32 dweight/dbias (+= when accum_w); D <= 2048. */
 size_t kd_norm_bwd_workspace_size(int R, int D);
 int kd_norm_bwd(int rms, const void* x, int64_t ldx, const void* weight, const void* dy, int64_t lddy,
                 const float* mean, const float* rstd, void* dx, int64_t lddx, int dx_accum,
                 float* dweight, float* dbias, int accum_w, void* workspace, size_t workspace_bytes,
-                int R, int D, void* stream);
+                int R, int D, int x_dtype, void* stream);
 /* q/k/v split of a fused projection output qkv [B*S, (nq+2nkv)*hd] into padded head-major
  * q/k/v (+ RoPE rotate_half with fp32 cos/sin tables [S, hd/2] when non-NULL; HF5 qwen2
  * apply_rotary_pos_emb) and its transpose for the backward (dq fp32). */
@@ -389,10 +392,13 @@ int kd_model_param_info(const kd_model_config* cfg, int index, char* name, int n
 
 /* anyres pack plan on the host (transformers' select_best_resolution / unpad_image /
  * pack_image_features for the 384-px tile grid of the -ov checkpoints, anyres_max_9): for
- * sample b with image_sizes_host[b] = (H, W) and `tiles` pixel tiles per sample, map_host[b][j]
- * = the flattened vision-feature row (over B * tiles * 729) of its j-th image token, or -1
- * (image_newline); len_host[b] = its image-token count; the rest of the row is -2.  The
- * input of kd_image_src_map. */
+ * sample b with image_sizes_host[b] = (H, W), map_host[b][j] = the flattened vision-feature
+ * row of its j-th image token, or -1 (image_newline); len_host[b] = its image-token count;
+ * the rest of the row is -2.  The input of kd_image_src_map.  Tile layout of the feature
+ * rows: tiles > 0 = `tiles` tiles per sample (sample b from tile b * tiles); tiles == 0 =
+ * compact: each sample's REAL tiles only (1 + the grid: 2 for 336x336, 5 for 480x640),
+ * sample b from the sum of the earlier samples' counts — what the reference's model runs
+ * through the vision tower (HF5 llava_onevision: pixel_values unpadded per image_sizes). */
 int kd_anyres_batch_map(const int64_t* image_sizes_host, int B, int tiles, int32_t* map_host, int map_ld,
                         int32_t* len_host);
 
@@ -401,6 +407,14 @@ int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad
 void kd_model_destroy(kd_model* m);
 /* freeze masks (DT:468-523): which regions receive weight gradients */
 int kd_model_set_trainable(kd_model* m, int vision, int projector, int language);
+
+/* fp32 residual streams: vision / language != 0 keeps that tower's hidden state x (the
+ * stream every layer adds into: SigLIP encoder, Qwen2 decoder) in fp32 — the residual adds
+ * in the o_proj / fc2 / down_proj GEMM epilogues in fp32, the norms read fp32 — instead of
+ * rounding it to bf16 after every add (the reference's own precision: fp32 in LB / FB, the
+ * residual adds of fp16 autocast in DT, which run in fp32).  Default off; not with fp8
+ * weights.  Changes the forward / backward workspace sizes. */
+int kd_model_set_residual_f32(kd_model* m, int vision, int language);
 
 /* fp8 teacher (BASELINE config c4): e4m3 copies of every linear weight the forward's GEMMs
  * read (all 2-D weights but the patch-embedding conv, the position embedding and
@@ -412,20 +426,35 @@ int kd_model_set_trainable(kd_model* m, int vision, int projector, int language)
 int64_t kd_model_fp8_scale_count(const kd_model* m);
 int kd_model_quantize_fp8(const kd_model* m, void* q, float* scales, void* stream);
 int kd_model_set_fp8(kd_model* m, const void* q, const float* scales);
+/* Which linear families run on the fp8 path once fp8 weights are bound (default all); the
+ * others keep the bf16 GEMM on the same weights.  e4m3 costs ~3.7 % rel-L2 per GEMM output
+ * whatever the scaling (3 mantissa bits), and on the random-init teacher these
+ * errors add in quadrature along the ~220 GEMMs of the forward, so a policy trades accuracy
+ * for fp8 MFMA throughput family by family (tools/fp8_depth_study.py --families). */
+typedef enum {
+    KD_FP8_VISION = 1,      /* SigLIP q|k|v, out_proj, fc1, fc2                           */
+    KD_FP8_PROJECTOR = 2,   /* multi_modal_projector linear_1 / linear_2                  */
+    KD_FP8_LM_ATTN = 4,     /* Qwen2 q|k|v, o_proj                                        */
+    KD_FP8_LM_MLP = 8,      /* Qwen2 gate|up, down_proj                                   */
+    KD_FP8_LM_HEAD = 16,    /* lm_head                                                    */
+    KD_FP8_ALL = 31
+} kd_fp8_family;
+int kd_model_set_fp8_families(kd_model* m, int families);
 
-/* Forward.  ids int64 [B, L]; pixels [B*tiles, 3, image, image] (kd_dtype); src int32 [B*L]
+/* Forward.  ids int64 [B, L]; pixels [n_tiles, 3, image, image] (kd_dtype: the batch's
+ * vision tiles, e.g. the compact real tiles of kd_anyres_batch_map(tiles = 0)); src int32 [B*L]
  * from kd_image_src_map; rope_cos/rope_sin fp32 [L, head_dim/2] (Qwen2RotaryEmbedding:
  * inv_freq = 1 / theta^(2i/hd) in fp32, angle = pos * inv_freq).  save = 1 keeps every
  * activation the backward reads in `workspace` (the saved-activation handle: pass the
  * same pointer to kd_model_backward and leave it untouched until then).
  * Outputs: hn bf16 [B*L, t_hidden] (final-norm hidden state); post_ln (optional) bf16
- * [B*tiles*np, v_hidden] (the vision post_layernorm output the reference hooks, DT:100-121);
+ * [n_tiles*np, v_hidden] (the vision post_layernorm output the reference hooks, DT:100-121);
  * logits (optional) bf16 [B*L, vocab] (lm_head); kv_k / kv_v (optional, host arrays of
  * t_layers device pointers) receive each layer's roped keys / values [B, kv_heads, L,
  * head_dim] (generate()'s prefill).  err: kd_embed_assemble's error word. */
-size_t kd_model_forward_workspace_size(const kd_model* m, int B, int L, int tiles, int save);
+size_t kd_model_forward_workspace_size(const kd_model* m, int B, int L, int n_tiles, int save);
 int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pixel_dtype, const int32_t* src,
-                     const float* rope_cos, const float* rope_sin, int B, int L, int tiles, int save,
+                     const float* rope_cos, const float* rope_sin, int B, int L, int n_tiles, int save,
                      void* workspace, size_t workspace_bytes, void* hn, void* post_ln, void* logits,
                      void* const* kv_k, void* const* kv_v, int32_t* err, void* stream);
 
@@ -437,9 +466,9 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
  * on_layer_done (optional) is called after each Qwen2 layer's backward is enqueued,
  * top-down (bucketed data-parallel all-reduce). */
 typedef void (*kd_layer_cb)(void* user, int layer);
-size_t kd_model_backward_workspace_size(const kd_model* m, int B, int L, int tiles);
+size_t kd_model_backward_workspace_size(const kd_model* m, int B, int L, int n_tiles);
 int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids, const int32_t* src,
-                      const float* rope_cos, const float* rope_sin, int B, int L, int tiles,
+                      const float* rope_cos, const float* rope_sin, int B, int L, int n_tiles,
                       const void* dhn, const void* dpost, void* workspace, size_t workspace_bytes,
                       void* stream, void* wgrad_stream, kd_layer_cb on_layer_done, void* user);
 

@@ -46,6 +46,9 @@ class KdLossParams(C.Structure):
     ]
 
 
+# kd_fp8_family
+KD_FP8_VISION, KD_FP8_PROJECTOR, KD_FP8_LM_ATTN, KD_FP8_LM_MLP, KD_FP8_LM_HEAD, KD_FP8_ALL = 1, 2, 4, 8, 16, 31
+
 # kd_layout / kd_dtype / kd_act
 KD_LAYOUT_K_MAJOR, KD_LAYOUT_MN_MAJOR = 0, 1
 KD_DTYPE_BF16, KD_DTYPE_F32, KD_DTYPE_FP8_E4M3 = 0, 1, 2
@@ -69,6 +72,7 @@ class KdGemmDesc(C.Structure):
         ("variant", C.c_int32),
         ("split_k", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64),
         ("ab_dtype", C.c_int32), ("a_scale", C.c_void_p), ("b_scale", C.c_void_p),
+        ("residual_dtype", C.c_int32),
     ]
 
 
@@ -122,10 +126,10 @@ SIGNATURES = {
     "kd_attn_bwd_workspace_size": (C.c_size_t, [C.POINTER(KdAttnBwdDesc)]),
     "kd_gemm_workspace_size": (C.c_size_t, [C.POINTER(KdGemmDesc)]),
     "kd_gemm_plan": (_i32, [C.POINTER(KdGemmDesc), C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
-    "kd_norm_fwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _f32, _vp]),
+    "kd_norm_fwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _f32, _i32, _vp]),
     "kd_norm_bwd_workspace_size": (_sz, [_i32, _i32]),
     "kd_norm_bwd": (_i32, [_i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _sz,
-                           _i32, _i32, _vp]),
+                           _i32, _i32, _i32, _vp]),
     "kd_qkv_split": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "kd_qkv_merge": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "kd_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _i32, _i32, _vp]),
@@ -163,9 +167,11 @@ SIGNATURES = {
     "kd_model_create": (_i32, [C.POINTER(KdModelConfig), _vp, _vp, C.POINTER(_vp)]),
     "kd_model_destroy": (None, [_vp]),
     "kd_model_set_trainable": (_i32, [_vp, _i32, _i32, _i32]),
+    "kd_model_set_residual_f32": (_i32, [_vp, _i32, _i32]),
     "kd_model_fp8_scale_count": (_i64, [_vp]),
     "kd_model_quantize_fp8": (_i32, [_vp, _vp, _vp, _vp]),
     "kd_model_set_fp8": (_i32, [_vp, _vp, _vp]),
+    "kd_model_set_fp8_families": (_i32, [_vp, _i32]),
     "kd_model_forward_workspace_size": (_sz, [_vp, _i32, _i32, _i32, _i32]),
     "kd_model_forward": (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _sz, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp]),

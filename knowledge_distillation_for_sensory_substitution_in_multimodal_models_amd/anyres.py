@@ -81,17 +81,21 @@ def num_image_tokens(image_size, pinpoints=DEFAULT_PINPOINTS) -> int:
 def batch_maps(image_sizes, tiles_per_sample: int):
     """Per-sample feature-row maps for a batch whose pixel_values are [B, P, 3, 384, 384].
 
-    Feature rows are numbered over the flattened [B*P*729] vision output; a sample's tiles
-    beyond num_tiles(image_size) are padding (HF drops them: pix_val[:num_patch]).
-    Returns (rows: list[list[int]], lengths: list[int]).
+    tiles_per_sample = P: feature rows are numbered over the flattened [B*P*729] vision
+    output (a sample's tiles beyond num_tiles(image_size) are padding).  tiles_per_sample = 0:
+    compact numbering over the REAL tiles only (sample b's rows follow sample b-1's
+    num_tiles), what the reference's model runs through the vision tower (HF drops the
+    padding tiles: pix_val[:num_patch]).  Returns (rows: list[list[int]], lengths: list[int]).
     """
     maps, lens = [], []
+    base_tile = 0
     for b, hw in enumerate(image_sizes):
         m = pack_map(tuple(int(v) for v in hw))
         nt = num_tiles(hw)
-        if nt > tiles_per_sample:
+        if tiles_per_sample and nt > tiles_per_sample:
             raise ValueError(f"sample {b}: image {tuple(hw)} needs {nt} tiles, batch has {tiles_per_sample}")
-        base = b * tiles_per_sample * TOKENS_PER_TILE
+        base = (b * tiles_per_sample if tiles_per_sample else base_tile) * TOKENS_PER_TILE
+        base_tile += nt
         maps.append([-1 if e == -1 else base + e[0] * TOKENS_PER_TILE + e[1] for e in m])
         lens.append(len(m))
     return maps, lens

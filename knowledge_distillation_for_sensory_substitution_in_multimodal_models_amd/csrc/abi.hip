@@ -49,14 +49,17 @@ int kd_attn_fwd(const kd_attn_desc* d, void* s) { return kd::launch_attn_fwd(d, 
 int kd_attn_bwd(const kd_attn_bwd_desc* d, void* s) { return kd::launch_attn_bwd(d, s); }
 size_t kd_attn_bwd_workspace_size(const kd_attn_bwd_desc* d) { return kd::attn_bwd_workspace_size(d); }
 int kd_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy, float* mean,
-                float* rstd, int R, int D, float eps, void* s) {
-    return kd::launch_norm_fwd(rms, x, ldx, w, b, y, ldy, mean, rstd, R, D, eps, s);
+                float* rstd, int R, int D, float eps, int x_dtype, void* s) {
+    KD_CHECK_ARG(x_dtype == KD_DTYPE_BF16 || x_dtype == KD_DTYPE_F32, "kd_norm_fwd: x_dtype");
+    return kd::launch_norm_fwd(rms, x, ldx, w, b, y, ldy, mean, rstd, R, D, eps, s, x_dtype == KD_DTYPE_F32);
 }
 size_t kd_norm_bwd_workspace_size(int R, int D) { return kd::norm_bwd_ws(R, D); }
 int kd_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
                 const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w, void* ws,
-                size_t wsb, int R, int D, void* s) {
-    return kd::launch_norm_bwd(rms, x, ldx, w, dy, lddy, mean, rstd, dx, lddx, dx_accum, dw, db, accum_w, ws, wsb, R, D, s);
+                size_t wsb, int R, int D, int x_dtype, void* s) {
+    KD_CHECK_ARG(x_dtype == KD_DTYPE_BF16 || x_dtype == KD_DTYPE_F32, "kd_norm_bwd: x_dtype");
+    return kd::launch_norm_bwd(rms, x, ldx, w, dy, lddy, mean, rstd, dx, lddx, dx_accum, dw, db, accum_w, ws, wsb, R, D, s,
+                               x_dtype == KD_DTYPE_F32);
 }
 int kd_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, const float* c, const float* sn, int B, int S,
                  int nq, int nkv, int hd, int hdp, void* s) {

@@ -41,6 +41,7 @@ struct GemmP {
     int M, N, K;
     float alpha;
     int c_f32, accumulate, bias_f32, act, res_mod;
+    int res_f32;           // residual is fp32 (the fp32 residual stream; C is then fp32 too)
     int64_t kchunk;        // split-K: K elements per split (gridDim.y splits)
     int64_t split_stride;  // split-K: fp32 elements between consecutive partial planes
     int glu;               // SwiGLU epilogue (v8, K-major): I = N/2; B rows [0,I) gate, [I,2I) up; 0 = off
@@ -268,7 +269,10 @@ __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
                 float v = acc[i][j][r] * alpha + bcol;
                 if (p.aux) p.aux[(int64_t)row * p.ld_aux + col] = (bf16)v;
                 v = apply_act(v, p.act);
-                if (p.resid) v += (float)p.resid[(int64_t)(p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col];
+                if (p.resid) {
+                    const int64_t ro = (int64_t)(p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col;
+                    v += p.res_f32 ? ((const float*)p.resid)[ro] : (float)p.resid[ro];
+                }
                 const int64_t o = (int64_t)row * p.ldc + col;
                 if (p.c_f32) {
                     float* c = (float*)p.C;
@@ -444,9 +448,13 @@ __device__ __forceinline__ void epi_flush(const GemmP& p, const char* smem, int 
             f32x4 v = *(const f32x4*)(smem + lr * rs + c * 16);
             float* o = (float*)dst_ + (int64_t)row * ld + col;
             if (RES) {
-                const bf16x4 rv = *(const bf16x4*)(p.resid + (int64_t)rr * p.ldr + col);
+                if (p.res_f32) {
+                    v += *(const f32x4*)((const float*)p.resid + (int64_t)rr * p.ldr + col);
+                } else {
+                    const bf16x4 rv = *(const bf16x4*)(p.resid + (int64_t)rr * p.ldr + col);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+                    for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+                }
             }
             if (ACC) v += *(const f32x4*)o;
             *(f32x4*)o = v;
@@ -761,6 +769,25 @@ __device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& a, const bf1
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// The last MFMA of every k-step, with the wait states its result needs before ANY read of the
+// accumulators in the SAME asm statement, taken when `last` (the tile's final k-step) is set.
+// asm MFMAs are invisible to the compiler's hazard recognizer: a register-allocator copy of an
+// accumulator placed at the k-loop exit (a merge of the remainder branches) read AGPRs before
+// the MFMA writing them had finished (81,336 wrong elements in the persistent-v8 experiment,
+// DESIGN §5).  With the drain inside this statement nothing can be scheduled between the final
+// MFMA and its wait states; earlier MFMAs retire in order before it.  32 wait states >= the
+// 16-pass XDL result latency (MI355X ISA: VALU read of an XDL result).  The branch is inside
+// the asm (scalar, uniform): no new basic block for the allocator to put copies in.
+__device__ __forceinline__ void mfma_agpr_last(f32x4& acc, const bf16x8& a, const bf16x8& b, int last) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"
+                 "s_cmp_eq_u32 %3, 0\n\t"
+                 "s_cbranch_scc1 .Lkd_mfma_nodrain%=\n\t"
+                 "s_nop 15\n\t"
+                 "s_nop 15\n"
+                 ".Lkd_mfma_nodrain%=:"
+                 : "+a"(acc) : "v"(a), "v"(b), "s"(__builtin_amdgcn_readfirstlane(last)) : "scc");
+}
+
 // per-lane byte offset of this wave's DMA instruction i (0..15 of an operand stage)
 template <bool MN>
 __device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, int rows_total) {
@@ -905,7 +932,9 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
             if (u < 4) NB[2 * u + 1] = frag2<256, B_MN>(na_ + SA, cb + (2 * u + 1) * 16, lane);               \
             if (u == 7) KD_G8_SYNC()                                                                          \
             KD_SB                                                                                             \
-            mfma_agpr(acc[u][7], CA[u], CB[7]); KD_SB                                                         \
+            if (u == 7) mfma_agpr_last(acc[u][7], CA[u], CB[7], t_ + 1 == nk);                                \
+            else mfma_agpr(acc[u][7], CA[u], CB[7]);                                                          \
+            KD_SB                                                                                             \
         }                                                                                                     \
     }
     int t = 0;
@@ -1106,7 +1135,10 @@ __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) mfma_agpr(acc[i][j], fa[i], fb[j]);
+            for (int j = 0; j < 4; ++j) {
+                if (i == 7 && j == 3) mfma_agpr_last(acc[i][j], fa[i], fb[j], t + 1 == nk);
+                else mfma_agpr(acc[i][j], fa[i], fb[j]);
+            }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -1148,6 +1180,18 @@ __device__ __forceinline__ uint32_t rec_bytes1(int64_t rows, int64_t ld) {
 __device__ __forceinline__ void mfma_f8(f32x16& acc, const i32x8& a, const i32x8& b, int unit_scale) {
     asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
                  : "+a"(acc) : "v"(a), "v"(b), "v"(unit_scale));
+}
+
+// the k-step's last fp8 MFMA with the result wait states in the same asm statement when
+// `last` (see mfma_agpr_last)
+__device__ __forceinline__ void mfma_f8_last(f32x16& acc, const i32x8& a, const i32x8& b, int unit_scale, int last) {
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]\n\t"
+                 "s_cmp_eq_u32 %4, 0\n\t"
+                 "s_cbranch_scc1 .Lkd_mfma8_nodrain%=\n\t"
+                 "s_nop 15\n\t"
+                 "s_nop 15\n"
+                 ".Lkd_mfma8_nodrain%=:"
+                 : "+a"(acc) : "v"(a), "v"(b), "v"(unit_scale), "s"(__builtin_amdgcn_readfirstlane(last)) : "scc");
 }
 
 __device__ __forceinline__ i32x8 frag_f8(const char* tile, int r, int h) {
@@ -1271,7 +1315,9 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8f8(GemmP p) {
         _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                            \
             if (u == 15) KD_F8_SYNC()                                                               \
             KD_SB                                                                                   \
-            mfma_f8(acc[u >> 2][u & 3], CA[u >> 2], CB[u & 3], unit); KD_SB                         \
+            if (u == 15) mfma_f8_last(acc[3][3], CA[3], CB[3], unit, t_ + 1 == nk);                 \
+            else mfma_f8(acc[u >> 2][u & 3], CA[u >> 2], CB[u & 3], unit);                          \
+            KD_SB                                                                                   \
             if (u < 8) {                                                                            \
                 dma(t_ + NS8, (SL), u, FT{}); KD_SB                                                 \
                 if (u < 4) NA[u] = frag_f8(na_, ra + 32 * u + lr32, h);                             \
@@ -1454,9 +1500,14 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
             v[e] = apply_act(x, p.act);
         }
         if (p.resid) {
-            const bf16x4 r = *(const bf16x4*)(p.resid + (p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col);
+            const int64_t ro = (p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col;
+            if (p.res_f32) {
+                v += *(const f32x4*)((const float*)p.resid + ro);
+            } else {
+                const bf16x4 r = *(const bf16x4*)(p.resid + ro);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+                for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+            }
         }
         if (p.c_f32) {
             float* dst = (float*)p.C + row * p.ldc + col;
@@ -1516,7 +1567,8 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     // forced: variants 2/5 v3 256x256, 3/6 256x128, 4/7 128x256, 16+ v8; 0 = model's choice
     const int fv = d->variant == 20 ? 4 : (d->variant >= 16 ? 3 : (d->variant >= 5 ? d->variant - 5 : (d->variant >= 2 ? d->variant - 2 : -1)));
     const double out_e = (double)((d->c_dtype == KD_DTYPE_F32 ? 4 : 2) * (d->accumulate ? 2 : 1) +
-                                  (d->residual ? 2 : 0) + (d->aux ? 2 : 0));   // epilogue bytes per element
+                                  (d->residual ? (d->residual_dtype == KD_DTYPE_F32 ? 4 : 2) : 0) +
+                                  (d->aux ? 2 : 0));   // epilogue bytes per element
     const double out_b = (double)M * N * out_e;
     const int tbm[5] = {256, 256, 128, 256, 256}, tbn[5] = {256, 128, 256, 256, 256};
     GemmPlan best{fv >= 0 ? vcode[fv] : 2, 1, d->K, 0};
@@ -1577,6 +1629,7 @@ int launch_gemm_f8(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->a_scale && d->b_scale, "gemm fp8: null a_scale / b_scale");
     KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16, "gemm fp8: bf16 output");
     KD_CHECK_ARG(d->split_k <= 1, "gemm fp8: no split-K");
+    KD_CHECK_ARG(!d->residual || d->residual_dtype == KD_DTYPE_BF16, "gemm fp8: bf16 residual only");
     KD_CHECK_ALIGN(d->A, 16, "gemm fp8: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm fp8: B must be 16-B aligned");
     KD_CHECK_SHAPE(d->K % 16 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0 && d->lda >= d->K && d->ldb >= d->K,
@@ -1677,6 +1730,9 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     }
     KD_CHECK_SHAPE(d->ldc >= (d->act == KD_ACT_SWIGLU ? d->N / 2 : d->N), "gemm: ldc < N (N/2 for swiglu)");
     KD_CHECK_SHAPE(!d->residual || d->ldr >= d->N, "gemm: ldr < N");
+    KD_CHECK_ARG(!d->residual || d->residual_dtype == KD_DTYPE_BF16 ||
+                 (d->residual_dtype == KD_DTYPE_F32 && d->c_dtype == KD_DTYPE_F32 && d->act == KD_ACT_NONE),
+                 "gemm: an fp32 residual needs an fp32 C and no activation epilogue");
     KD_CHECK_SHAPE(!d->aux || d->ld_aux >= d->N, "gemm: ld_aux < N");
     KD_CHECK_SHAPE((uint64_t)256 * d->lda * 2 < 0x7FFFFFFFull && (uint64_t)256 * d->ldb * 2 < 0x7FFFFFFFull,
                    "gemm: leading dimension too large for 31-bit buffer records");
@@ -1688,6 +1744,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.c_f32 = d->c_dtype == KD_DTYPE_F32; p.accumulate = d->accumulate; p.bias_f32 = d->bias_dtype == KD_DTYPE_F32;
     p.act = d->act;
     p.res_mod = d->residual_row_mod;
+    p.res_f32 = d->residual && d->residual_dtype == KD_DTYPE_F32;
     p.kchunk = d->K; p.split_stride = 0; p.glu = 0; p.tile0 = 0;
     p.sa = p.sb = nullptr; p.gx = 0; p.gy = 1;
     p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr;

@@ -17,11 +17,11 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream);
 int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream);
 size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d);
 int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy,
-                    float* mean, float* rstd, int R, int D, float eps, void* stream);
+                    float* mean, float* rstd, int R, int D, float eps, void* stream, int x_f32 = 0);
 size_t norm_bwd_ws(int R, int D);
 int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
                     const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w,
-                    void* ws, size_t ws_bytes, int R, int D, void* stream);
+                    void* ws, size_t ws_bytes, int R, int D, void* stream, int x_f32 = 0);
 int launch_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, const float* cos_t, const float* sin_t,
                      int B, int S, int nq, int nkv, int hd, int hdp, void* stream);
 int launch_qkv_merge(const float* dq, const void* dk, const void* dv, void* dqkv, int64_t ld, const float* cos_t,
@@ -32,7 +32,7 @@ int launch_swiglu_bwd(const void* gu, int64_t ldg, const void* dh, int64_t ldh, 
 int launch_act_bwd(const void* pre, const void* dy, void* dx, int64_t n, int act, void* stream);
 int launch_patchify(const void* px, int px_dtype, void* out, int NI, int img, int ps, int Kp, void* stream);
 int launch_embed_assemble(const int64_t* ids, const int* src, const void* table, const void* feats, const void* newline,
-                          void* out, int M, int H, int vocab, int* err, void* stream);
+                          void* out, int M, int H, int vocab, int* err, void* stream, int out_f32 = 0);
 int launch_embed_bwd(const int64_t* ids, const int* src, const void* dout, float* dtable, void* dfeats, float* dnewline,
                      int M, int H, void* stream);
 int launch_colsum(const void* dy, int64_t ld, int M, int N, float* out, int accumulate, void* stream);

@@ -30,6 +30,11 @@ __device__ __forceinline__ void load8(const bf16* p, float* f) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
 }
+__device__ __forceinline__ void load8(const float* p, float* f) {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { f[j] = a[j]; f[4 + j] = b[j]; }
+}
 __device__ __forceinline__ void store8(bf16* p, const float* f) {
     bf16x8 v;
 #pragma unroll
@@ -38,15 +43,15 @@ __device__ __forceinline__ void store8(bf16* p, const float* f) {
 }
 
 // -------------------------------------------------------------- LayerNorm ----
-// one wave per row, D % 8 == 0, D <= 64 * 8 * 8
-template <bool RMS>
-__global__ void __launch_bounds__(NT) k_norm_fwd(const bf16* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
+// one wave per row, D % 8 == 0, D <= 64 * 8 * 8; x bf16 or fp32 (XT: the fp32 residual stream)
+template <bool RMS, typename XT>
+__global__ void __launch_bounds__(NT) k_norm_fwd(const XT* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
                                                  const bf16* __restrict__ bias, bf16* __restrict__ y, int64_t ldy,
                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                  int R, int D, float eps) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= R) return;
-    const bf16* xr = x + (int64_t)row * ldx;
+    const XT* xr = x + (int64_t)row * ldx;
     float f[8][8];
     const int nch = D / 8;
     float s = 0.f, ss = 0.f;
@@ -110,8 +115,20 @@ __global__ void __launch_bounds__(NT) k_norm_fwd(const bf16* __restrict__ x, int
 // row i+1 are in flight while row i is reduced and written (one row at a time, with the
 // dx re-load after the reduction, the kernel ran at ~1.5 TB/s).
 constexpr int NW_NORM = NT / 64;   // waves per k_norm_bwd workgroup
-template <bool RMS, int IT>
-__global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
+// x chunk of 8 elements as loaded: bf16x8, or two f32x4 for the fp32 residual stream
+template <typename XT> struct XChunk {
+    bf16x8 v;
+    __device__ __forceinline__ void load(const bf16* p) { v = *(const bf16x8*)p; }
+    __device__ __forceinline__ float get(int j) const { return (float)v[j]; }
+};
+template <> struct XChunk<float> {
+    f32x4 a, b;
+    __device__ __forceinline__ void load(const float* p) { a = *(const f32x4*)p; b = *(const f32x4*)(p + 4); }
+    __device__ __forceinline__ float get(int j) const { return j < 4 ? a[j] : b[j - 4]; }
+};
+
+template <bool RMS, int IT, typename XT>
+__global__ void __launch_bounds__(NT) k_norm_bwd(const XT* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
                                                  const bf16* __restrict__ dy, int64_t lddy,
                                                  const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                  bf16* __restrict__ dx, int64_t lddx, int dx_accum,
@@ -130,19 +147,19 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
     }
     const int r_begin = blockIdx.x * rows_per_block;
     const int r_end = min(R, r_begin + rows_per_block);
-    struct Row { bf16x8 x[IT], g[IT], p[IT]; float mean, rstd; };
+    struct Row { XChunk<XT> x[IT]; bf16x8 g[IT], p[IT]; float mean, rstd; };
     // every load is unconditional (row and chunk clamped into range, dx read even when not
     // accumulated): with a data-dependent number of loads in flight hipcc can only wait
     // vmcnt(0), which drains the next row's loads and undoes the pipeline
     auto load = [&](Row& t, int row_) {
         const int row = min(row_, R - 1);
-        const bf16* xr = x + (int64_t)row * ldx;
+        const XT* xr = x + (int64_t)row * ldx;
         const bf16* gr = dy + (int64_t)row * lddy;
         const bf16* pr = dx + (int64_t)row * lddx;
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int c = min(lane + it * 64, nch - 1);
-            t.x[it] = *(const bf16x8*)(xr + c * 8);
+            t.x[it].load(xr + c * 8);
             t.g[it] = *(const bf16x8*)(gr + c * 8);
             t.p[it] = *(const bf16x8*)(pr + c * 8);
         }
@@ -157,7 +174,7 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
             if (lane + it * 64 >= nch) continue;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float xv = (float)t.x[it][j], dv = (float)t.g[it][j];
+                const float xv = t.x[it].get(j), dv = (float)t.g[it][j];
                 const float xh = (xv - mean) * rstd;
                 const float g = dv * wr[it][j];
                 a1 += g;
@@ -176,7 +193,7 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const bf16* __restrict__ x, int
                 float o[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float xh = ((float)t.x[it][j] - mean) * rstd;
+                    const float xh = (t.x[it].get(j) - mean) * rstd;
                     o[j] = rstd * ((float)t.g[it][j] * wr[it][j] - (RMS ? 0.f : a1) - xh * a2);
                     if (dx_accum) o[j] += (float)t.p[it][j];
                 }
@@ -429,8 +446,9 @@ __global__ void k_patchify(const T* __restrict__ px, bf16* __restrict__ out, int
 
 // --------------------------------------------------------- embed assemble ----
 // src[t] >= 0 : image feature row src[t]; -1 : image newline; -2 : token embedding of ids[t]
+template <typename OT>   // bf16, or fp32 (the first value of an fp32 residual stream: exact)
 __global__ void k_embed_assemble(const int64_t* __restrict__ ids, const int* __restrict__ src, const bf16* __restrict__ table,
-                                 const bf16* __restrict__ feats, const bf16* __restrict__ newline, bf16* __restrict__ out,
+                                 const bf16* __restrict__ feats, const bf16* __restrict__ newline, OT* __restrict__ out,
                                  int M, int H, int vocab, int* __restrict__ err) {
     const int t = blockIdx.x;
     if (t >= M) return;
@@ -443,7 +461,15 @@ __global__ void k_embed_assemble(const int64_t* __restrict__ ids, const int* __r
         if (id < 0 || id >= vocab) { if (threadIdx.x == 0) atomicOr(err, 1); return; }
         from = table + id * H;
     }
-    for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8) *(bf16x8*)(out + (int64_t)t * H + c) = *(const bf16x8*)(from + c);
+    for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8) {
+        const bf16x8 v = *(const bf16x8*)(from + c);
+        if constexpr (sizeof(OT) == 4) {
+            *(f32x4*)(out + (int64_t)t * H + c) = (f32x4){(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+            *(f32x4*)(out + (int64_t)t * H + c + 4) = (f32x4){(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+        } else {
+            *(bf16x8*)(out + (int64_t)t * H + c) = v;
+        }
+    }
 }
 
 __global__ void k_embed_bwd(const int64_t* __restrict__ ids, const int* __restrict__ src, const bf16* __restrict__ dout,
@@ -738,14 +764,22 @@ inline int grid_for(int64_t work, int per_block = 256, int cap = 8192) {
 
 // ------------------------------------------------------------------ launchers ----
 int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy,
-                    float* mean, float* rstd, int R, int D, float eps, void* stream) {
+                    float* mean, float* rstd, int R, int D, float eps, void* stream, int x_f32) {
     KD_CHECK_ARG(x && w && y && (rms || b), "norm_fwd: null pointer");
     KD_CHECK_SHAPE(D % 8 == 0 && D <= 4096 && ldx % 8 == 0 && ldy % 8 == 0, "norm_fwd: D must be a multiple of 8, <= 4096");
     const dim3 grid((R + 3) / 4);
-    if (rms) hipLaunchKernelGGL(k_norm_fwd<true>, grid, dim3(NT), 0, as_stream(stream), (const bf16*)x, ldx, (const bf16*)w,
-                                nullptr, (bf16*)y, ldy, mean, rstd, R, D, eps);
-    else hipLaunchKernelGGL(k_norm_fwd<false>, grid, dim3(NT), 0, as_stream(stream), (const bf16*)x, ldx, (const bf16*)w,
-                            (const bf16*)b, (bf16*)y, ldy, mean, rstd, R, D, eps);
+    hipStream_t st = as_stream(stream);
+    if (x_f32) {
+        if (rms) hipLaunchKernelGGL((k_norm_fwd<true, float>), grid, dim3(NT), 0, st, (const float*)x, ldx, (const bf16*)w,
+                                    nullptr, (bf16*)y, ldy, mean, rstd, R, D, eps);
+        else hipLaunchKernelGGL((k_norm_fwd<false, float>), grid, dim3(NT), 0, st, (const float*)x, ldx, (const bf16*)w,
+                                (const bf16*)b, (bf16*)y, ldy, mean, rstd, R, D, eps);
+    } else {
+        if (rms) hipLaunchKernelGGL((k_norm_fwd<true, bf16>), grid, dim3(NT), 0, st, (const bf16*)x, ldx, (const bf16*)w,
+                                    nullptr, (bf16*)y, ldy, mean, rstd, R, D, eps);
+        else hipLaunchKernelGGL((k_norm_fwd<false, bf16>), grid, dim3(NT), 0, st, (const bf16*)x, ldx, (const bf16*)w,
+                                (const bf16*)b, (bf16*)y, ldy, mean, rstd, R, D, eps);
+    }
     KD_LAUNCH_CHECK("k_norm_fwd");
     return KD_OK;
 }
@@ -762,7 +796,7 @@ size_t norm_bwd_ws(int R, int D) {
 
 int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
                     const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w,
-                    void* ws, size_t ws_bytes, int R, int D, void* stream) {
+                    void* ws, size_t ws_bytes, int R, int D, void* stream, int x_f32) {
     KD_CHECK_ARG(x && w && dy && rstd && dx && (rms || mean), "norm_bwd: null pointer");
     KD_CHECK_SHAPE(D % 8 == 0 && D <= 2048, "norm_bwd: D must be a multiple of 8, <= 2048");
     const int nb = norm_bwd_blocks(R);
@@ -772,10 +806,17 @@ int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const vo
     float* dbp = dwp + (size_t)nb * D;
     hipStream_t st = as_stream(stream);
     const size_t smem = (size_t)NW_NORM * 2 * D * 4;
-#define KD_NB(RMSV, ITV)                                                                                        \
-    hipLaunchKernelGGL((k_norm_bwd<RMSV, ITV>), dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx, (const bf16*)w,    \
-                       (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum, dw ? dwp : nullptr,              \
-                       (RMSV || !db) ? nullptr : dbp, R, D, rows_per)
+#define KD_NB(RMSV, ITV)                                                                                          \
+    do {                                                                                                           \
+        if (x_f32)                                                                                                 \
+            hipLaunchKernelGGL((k_norm_bwd<RMSV, ITV, float>), dim3(nb), dim3(NT), smem, st, (const float*)x, ldx,   \
+                               (const bf16*)w, (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum,          \
+                               dw ? dwp : nullptr, (RMSV || !db) ? nullptr : dbp, R, D, rows_per);                 \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_norm_bwd<RMSV, ITV, bf16>), dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx,     \
+                               (const bf16*)w, (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum,          \
+                               dw ? dwp : nullptr, (RMSV || !db) ? nullptr : dbp, R, D, rows_per);                 \
+    } while (0)
     const int it = (D + 511) / 512;
     if (rms) {
         if (it == 1) KD_NB(true, 1); else if (it == 2) KD_NB(true, 2); else if (it == 3) KD_NB(true, 3); else KD_NB(true, 4);
@@ -876,11 +917,15 @@ int launch_patchify(const void* px, int px_dtype, void* out, int NI, int img, in
 }
 
 int launch_embed_assemble(const int64_t* ids, const int* src, const void* table, const void* feats, const void* newline,
-                          void* out, int M, int H, int vocab, int* err, void* stream) {
+                          void* out, int M, int H, int vocab, int* err, void* stream, int out_f32) {
     KD_CHECK_ARG(ids && src && table && out && err, "embed_assemble: null pointer");
     KD_CHECK_SHAPE(H % 8 == 0, "embed_assemble: H % 8");
-    hipLaunchKernelGGL(k_embed_assemble, dim3(M), dim3(128), 0, as_stream(stream), ids, src, (const bf16*)table,
-                       (const bf16*)feats, (const bf16*)newline, (bf16*)out, M, H, vocab, err);
+    if (out_f32)
+        hipLaunchKernelGGL(k_embed_assemble<float>, dim3(M), dim3(128), 0, as_stream(stream), ids, src, (const bf16*)table,
+                           (const bf16*)feats, (const bf16*)newline, (float*)out, M, H, vocab, err);
+    else
+        hipLaunchKernelGGL(k_embed_assemble<bf16>, dim3(M), dim3(128), 0, as_stream(stream), ids, src, (const bf16*)table,
+                           (const bf16*)feats, (const bf16*)newline, (bf16*)out, M, H, vocab, err);
     KD_LAUNCH_CHECK("k_embed_assemble");
     return KD_OK;
 }

@@ -191,6 +191,10 @@ struct kd_model {
     float* g = nullptr;
     int train_vision = 0, train_projector = 0, train_language = 0;
     int lane_split_k = 0;     // split-K of the lane's GEMMs (KD_WGRAD_SPLIT_K; 0 = cost model)
+    // fp32 residual streams (kd_model_set_residual_f32): the SigLIP / Qwen2 hidden state x that
+    // every layer adds into is kept in fp32 (GEMM epilogues add the residual in fp32 and write
+    // fp32; the norms read fp32) instead of being rounded to bf16 after every add
+    int rf32_v = 0, rf32_t = 0;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_next = 0;
     // fp8 teacher (BASELINE config c4): e4m3 copies of the linear weights (same element
@@ -198,6 +202,8 @@ struct kd_model {
     const uint8_t* f8q = nullptr;
     const float* f8s = nullptr;
     std::vector<int64_t> soff;   // per spec: first scale index (-1: not an fp8 linear)
+    std::vector<int> fam;        // per spec: its kd_fp8_family bit (0: not an fp8 linear)
+    int f8_families = KD_FP8_ALL;   // which families run on the fp8 path (kd_model_set_fp8_families)
     int64_t n_scales = 0;
     // spec indices
     int i_patch_w = 0, i_patch_b = 1, i_pos = 2, i_vis0 = 3, i_post_w, i_post_b, i_p1w, i_p1b, i_p2w, i_p2b, i_newline,
@@ -257,6 +263,7 @@ struct GemmArgs {
     int c_f32 = 0;
     int bias_f32 = 0;
     int split_k = 0;
+    int res_f32 = 0;   // fp32 residual (then c_f32 too)
 };
 
 // split-K default of the runtime's GEMMs (KD_GEMM_SPLIT_K: 0 = the cost model, 1 = never split)
@@ -278,6 +285,7 @@ int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int6
     d.bias = g.bias; d.bias_dtype = g.bias_f32 ? KD_DTYPE_F32 : KD_DTYPE_BF16;
     d.act = g.act;
     d.residual = g.residual; d.ldr = g.ldr;
+    d.residual_dtype = g.res_f32 ? KD_DTYPE_F32 : KD_DTYPE_BF16;
     d.aux = g.aux; d.ld_aux = g.ld_aux;
     d.residual_row_mod = g.residual_row_mod;
     d.split_k = g.split_k ? g.split_k : g_split_default;
@@ -333,24 +341,30 @@ inline void wait(hipStream_t s, hipEvent_t e) {
 }
 
 // ------------------------------------------------------ forward buffer plan ----
+// the residual-stream tensors (x, x_mid, x_*_last) are bf16 or fp32 (kd_model::rf32_v / rf32_t)
 struct VisLayerBufs {
-    bf16 *x, *h, *q, *k, *v, *o, *x_mid, *h2, *pre, *u;
+    void *x, *x_mid;
+    bf16 *h, *q, *k, *v, *o, *h2, *pre, *u;
     float *m1, *r1, *lse, *m2, *r2;
 };
 struct LmLayerBufs {
-    bf16 *x, *h, *q, *k, *v, *o, *x_mid, *h2, *gu, *a;
+    void *x, *x_mid;
+    bf16 *h, *q, *k, *v, *o, *h2, *gu, *a;
     float *r1, *lse, *r2;
 };
 struct FwdPlan {
     bf16* rows;
     std::vector<VisLayerBufs> vl;
-    bf16 *x_vis_last, *qkv_v;     // x_vis_last = vl.back() output (saved) / ping-pong
-    bf16* x_vis[2];               // save = 0 ping-pong
+    void* x_vis_last;             // vl.back() output (saved) / ping-pong
+    bf16* x_vis_bf;               // x_vis_last as bf16 (the projector's GEMM operand; == x_vis_last if bf16)
+    bf16* qkv_v;
+    void* x_vis[2];               // save = 0 ping-pong
     float *pm, *pr;
     bf16 *ppre, *z, *feats;
     std::vector<LmLayerBufs> ll;
-    bf16 *x_lm_last, *qkv_t;
-    bf16* x_lm[2];
+    void* x_lm_last;
+    bf16* qkv_t;
+    void* x_lm[2];
     float* rf;
     uint8_t* qa;    // fp8 path: the current linear's activation rows, e4m3 [M][K] ...
     float* sa;      // ... and their scales [M]
@@ -358,28 +372,30 @@ struct FwdPlan {
     size_t bytes;
 };
 
-FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void* base) {
+// n_tiles: the vision tiles of the whole batch (the pixel rows; samples may have different counts)
+FwdPlan plan_forward(const kd_model* m, int B, int L, int n_tiles, int save, void* base) {
     const Cfg& C = m->C;
     const kd_model_config& c = C.c;
     Arena A(base);
     FwdPlan P;
-    const int NI = B * tiles, np = C.np();
+    const int NI = n_tiles, np = C.np();
     const int64_t NT = (int64_t)NI * np, D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp();
     const int64_t M = (int64_t)B * L, H = c.t_hidden, TI = c.t_inter, qd = C.qd(), kvd = C.kvd(), hd = c.t_head_dim;
     P.rows = A.take<bf16>(NT * C.kpatch());
+    const int64_t ev = m->rf32_v ? 4 : 2, et = m->rf32_t ? 4 : 2;   // residual-stream element bytes
     // vision
     P.vl.resize(c.v_layers);
     P.qkv_v = A.take<bf16>(NT * 3 * D);
     if (save) {
         for (int i = 0; i < c.v_layers; ++i) {
             VisLayerBufs& b = P.vl[i];
-            b.x = A.take<bf16>(NT * D);
+            b.x = A.take<char>(NT * D * ev);
             b.h = A.take<bf16>(NT * D);
             b.q = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
             b.k = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
             b.v = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
             b.o = A.take<bf16>(NT * D);
-            b.x_mid = A.take<bf16>(NT * D);
+            b.x_mid = A.take<char>(NT * D * ev);
             b.h2 = A.take<bf16>(NT * D);
             b.pre = A.take<bf16>(NT * Iv);
             b.u = A.take<bf16>(NT * Iv);
@@ -389,18 +405,18 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void*
             b.m2 = A.take<float>(NT);
             b.r2 = A.take<float>(NT);
         }
-        P.x_vis_last = A.take<bf16>(NT * D);
+        P.x_vis_last = A.take<char>(NT * D * ev);
         P.x_vis[0] = P.x_vis[1] = nullptr;
     } else {
         VisLayerBufs b{};
-        P.x_vis[0] = A.take<bf16>(NT * D);
-        P.x_vis[1] = A.take<bf16>(NT * D);
+        P.x_vis[0] = A.take<char>(NT * D * ev);
+        P.x_vis[1] = A.take<char>(NT * D * ev);
         b.h = A.take<bf16>(NT * D);
         b.q = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
         b.k = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
         b.v = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
         b.o = A.take<bf16>(NT * D);
-        b.x_mid = A.take<bf16>(NT * D);
+        b.x_mid = A.take<char>(NT * D * ev);
         b.h2 = A.take<bf16>(NT * D);
         b.u = A.take<bf16>(NT * Iv);
         for (int i = 0; i < c.v_layers; ++i) {
@@ -409,6 +425,7 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void*
         }
         P.x_vis_last = P.x_vis[c.v_layers & 1];
     }
+    P.x_vis_bf = m->rf32_v ? A.take<bf16>(NT * D) : (bf16*)P.x_vis_last;
     P.pm = A.take<float>(NT);
     P.pr = A.take<float>(NT);
     // projector
@@ -422,13 +439,13 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void*
     if (save) {
         for (int i = 0; i < c.t_layers; ++i) {
             LmLayerBufs& b = P.ll[i];
-            b.x = A.take<bf16>(M * H);
+            b.x = A.take<char>(M * H * et);
             b.h = A.take<bf16>(M * H);
             b.q = A.take<bf16>(M * qd);
             b.k = A.take<bf16>(M * kvd);
             b.v = A.take<bf16>(M * kvd);
             b.o = A.take<bf16>(M * qd);
-            b.x_mid = A.take<bf16>(M * H);
+            b.x_mid = A.take<char>(M * H * et);
             b.h2 = A.take<bf16>(M * H);
             b.gu = A.take<bf16>(M * 2 * TI);
             b.a = A.take<bf16>(M * TI);
@@ -436,18 +453,18 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void*
             b.lse = A.take<float>((int64_t)B * c.t_heads * L);
             b.r2 = A.take<float>(M);
         }
-        P.x_lm_last = A.take<bf16>(M * H);
+        P.x_lm_last = A.take<char>(M * H * et);
         P.x_lm[0] = P.x_lm[1] = nullptr;
     } else {
         LmLayerBufs b{};
-        P.x_lm[0] = A.take<bf16>(M * H);
-        P.x_lm[1] = A.take<bf16>(M * H);
+        P.x_lm[0] = A.take<char>(M * H * et);
+        P.x_lm[1] = A.take<char>(M * H * et);
         b.h = A.take<bf16>(M * H);
         b.q = A.take<bf16>(M * qd);
         b.k = A.take<bf16>(M * kvd);
         b.v = A.take<bf16>(M * kvd);
         b.o = A.take<bf16>(M * qd);
-        b.x_mid = A.take<bf16>(M * H);
+        b.x_mid = A.take<char>(M * H * et);
         b.h2 = A.take<bf16>(M * H);
         b.gu = fused_swiglu ? nullptr : A.take<bf16>(M * 2 * TI);
         b.a = A.take<bf16>(M * TI);
@@ -480,7 +497,7 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int tiles, int save, void*
 // GEMM against the e4m3 weight rows and their per-channel scales (kdstep.h, fp8 path).
 int lin(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int N, int K, const bf16* x, int64_t ldx, int widx,
         void* out, int64_t ldo, const GemmArgs& g) {
-    if (!m->f8q || m->soff[widx] < 0)
+    if (!m->f8q || m->soff[widx] < 0 || !(m->fam[widx] & m->f8_families))
         return gemm(s, P.splitk, M, N, K, km(x, ldx), km(m->W(widx), K), out, ldo, g);
     KD_TRY(launch_quant_rows_f8(x, ldx, M, K, P.qa, K, P.sa, s));
     kd_gemm_desc d;
@@ -505,20 +522,22 @@ int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dty
     const int np = C.np(), D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp(), hd = C.v_hd();
     const int NT = NI * np;
     KD_TRY(launch_patchify(pixels, px_dtype, P.rows, NI, c.v_image, c.v_patch, C.kpatch(), s));
-    bf16* x0 = c.v_layers ? P.vl[0].x : P.x_vis_last;
+    void* x0 = c.v_layers ? P.vl[0].x : P.x_vis_last;
+    const int f32 = m->rf32_v;
     {
         GemmArgs g;
         g.bias = m->W(m->i_patch_b);
         g.residual = m->W(m->i_pos);
         g.ldr = D;
         g.residual_row_mod = np;
+        g.c_f32 = f32;
         KD_TRY(gemm(s, P.splitk, NT, D, C.kpatch(), km(P.rows, C.kpatch()), km(m->W(m->i_patch_w), C.kpatch()), x0, D, g));
     }
     for (int i = 0; i < c.v_layers; ++i) {
         const VisLayerBufs& b = P.vl[i];
-        bf16* x_out = (i + 1 < c.v_layers) ? P.vl[i + 1].x : P.x_vis_last;
+        void* x_out = (i + 1 < c.v_layers) ? P.vl[i + 1].x : P.x_vis_last;
         KD_TRY(launch_norm_fwd(0, b.x, D, m->W(m->vis(i, VLN1W)), m->W(m->vis(i, VLN1B)), b.h, D, save ? b.m1 : nullptr,
-                               save ? b.r1 : nullptr, NT, D, c.v_eps, s));
+                               save ? b.r1 : nullptr, NT, D, c.v_eps, s, f32));
         {
             GemmArgs g;
             g.bias = m->W(m->vis(i, VQB));
@@ -534,10 +553,11 @@ int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dty
             g.bias = m->W(m->vis(i, VOB));
             g.residual = b.x;
             g.ldr = D;
+            g.res_f32 = g.c_f32 = f32;
             KD_TRY(lin(m, P, s, NT, D, D, b.o, D, m->vis(i, VOW), b.x_mid, D, g));
         }
         KD_TRY(launch_norm_fwd(0, b.x_mid, D, m->W(m->vis(i, VLN2W)), m->W(m->vis(i, VLN2B)), b.h2, D,
-                               save ? b.m2 : nullptr, save ? b.r2 : nullptr, NT, D, c.v_eps, s));
+                               save ? b.m2 : nullptr, save ? b.r2 : nullptr, NT, D, c.v_eps, s, f32));
         {
             GemmArgs g;
             g.bias = m->W(m->vis(i, VFC1B));
@@ -551,12 +571,15 @@ int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dty
             g.bias = m->W(m->vis(i, VFC2B));
             g.residual = b.x_mid;
             g.ldr = D;
+            g.res_f32 = g.c_f32 = f32;
             KD_TRY(lin(m, P, s, NT, D, Iv, b.u, Iv, m->vis(i, VFC2W), x_out, D, g));
         }
     }
     if (post)
         KD_TRY(launch_norm_fwd(0, P.x_vis_last, D, m->W(m->i_post_w), m->W(m->i_post_b), post, D, save ? P.pm : nullptr,
-                               save ? P.pr : nullptr, NT, D, c.v_eps, s));
+                               save ? P.pr : nullptr, NT, D, c.v_eps, s, f32));
+    if (f32)   // the projector's GEMM operand (hidden_states[-1], HF5 llava_onevision :131-150)
+        KD_TRY(launch_cast_f32_bf16((const float*)P.x_vis_last, P.x_vis_bf, NT * (int64_t)D, s));
     return KD_OK;
 }
 
@@ -565,11 +588,12 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
     const kd_model_config& c = m->C.c;
     const int M = B * L, H = c.t_hidden, TI = c.t_inter, qd = m->C.qd(), kvd = m->C.kvd(), hd = c.t_head_dim;
     const bool fused = TI % 128 == 0;
+    const int f32 = m->rf32_t;
     for (int i = 0; i < c.t_layers; ++i) {
         const LmLayerBufs& b = P.ll[i];
-        bf16* x_out = (i + 1 < c.t_layers) ? P.ll[i + 1].x : P.x_lm_last;
+        void* x_out = (i + 1 < c.t_layers) ? P.ll[i + 1].x : P.x_lm_last;
         KD_TRY(launch_norm_fwd(1, b.x, H, m->W(m->lm(i, LINW)), nullptr, b.h, H, nullptr, save ? b.r1 : nullptr, M, H,
-                               c.t_eps, s));
+                               c.t_eps, s, f32));
         {
             GemmArgs g;
             g.bias = m->W(m->lm(i, LQB));
@@ -586,10 +610,11 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
             GemmArgs g;
             g.residual = b.x;
             g.ldr = H;
+            g.res_f32 = g.c_f32 = f32;
             KD_TRY(lin(m, P, s, M, H, qd, b.o, qd, m->lm(i, LOW), b.x_mid, H, g));
         }
         KD_TRY(launch_norm_fwd(1, b.x_mid, H, m->W(m->lm(i, LPOSTW)), nullptr, b.h2, H, nullptr, save ? b.r2 : nullptr, M,
-                               H, c.t_eps, s));
+                               H, c.t_eps, s, f32));
         if (fused) {   // SwiGLU in the gate|up GEMM's epilogue; gate|up kept only for the backward
             GemmArgs g;
             g.act = KD_ACT_SWIGLU;
@@ -605,11 +630,12 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
             GemmArgs g;
             g.residual = b.x_mid;
             g.ldr = H;
+            g.res_f32 = g.c_f32 = f32;
             KD_TRY(lin(m, P, s, M, H, TI, b.a, TI, m->lm(i, LDW), x_out, H, g));
         }
     }
     return launch_norm_fwd(1, P.x_lm_last, H, m->W(m->i_norm), nullptr, hn, H, nullptr, save ? P.rf : nullptr, M, H,
-                           c.t_eps, s);
+                           c.t_eps, s, f32);
 }
 
 // ---------------------------------------------------------- backward plan ----
@@ -639,12 +665,12 @@ kd_attn_bwd_desc vis_attn_desc(const kd_model* m, int NI) {
     return d;
 }
 
-BwdPlan plan_backward(const kd_model* m, int B, int L, int tiles, void* base) {
+BwdPlan plan_backward(const kd_model* m, int B, int L, int n_tiles, void* base) {
     const Cfg& C = m->C;
     const kd_model_config& c = C.c;
     Arena A(base);
     BwdPlan P;
-    const int NI = B * tiles, np = C.np();
+    const int NI = n_tiles, np = C.np();
     const int64_t NT = (int64_t)NI * np, D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp();
     const int64_t M = (int64_t)B * L, H = c.t_hidden, TI = c.t_inter, qd = C.qd(), kvd = C.kvd();
     P.dx = A.take<bf16>(M * H);
@@ -693,8 +719,9 @@ int lm_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, const float* cs
     const kd_model_config& c = m->C.c;
     const int M = B * L, H = c.t_hidden, TI = c.t_inter, qd = m->C.qd(), kvd = m->C.kvd(), hd = c.t_head_dim;
     const bool gw = m->train_language != 0;
+    const int f32 = m->rf32_t;
     KD_TRY(launch_norm_bwd(1, F.x_lm_last, H, m->W(m->i_norm), dhn, H, nullptr, F.rf, P.dx, H, 0,
-                           gw ? m->G(m->i_norm) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s));
+                           gw ? m->G(m->i_norm) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s, f32));
     for (int i = c.t_layers - 1; i >= 0; --i) {
         const LmLayerBufs& b = F.ll[i];
         GemmArgs g0;
@@ -722,7 +749,8 @@ int lm_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, const float* cs
         }
         wait(s, ev);   // dx is updated in place next (the lane read it)
         KD_TRY(launch_norm_bwd(1, b.x_mid, H, m->W(m->lm(i, LPOSTW)), P.dh2, H, nullptr, b.r2, P.dx, H, 1,
-                               gw ? m->G(m->lm(i, LPOSTW)) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s));
+                               gw ? m->G(m->lm(i, LPOSTW)) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s,
+                               f32));
         // attention: do = dx Wo ; flash backward ; dqkv (RoPE undone) ; dh = dqkv Wqkv
         KD_TRY(gemm(s, P.splitk_main, M, qd, H, km(P.dx, H), mn(m->W(m->lm(i, LOW)), qd), P.do_, qd, g0));
         ev = nullptr;
@@ -748,7 +776,8 @@ int lm_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, const float* cs
         }
         wait(s, ev);
         KD_TRY(launch_norm_bwd(1, b.x, H, m->W(m->lm(i, LINW)), P.dh, H, nullptr, b.r1, P.dx, H, 1,
-                               gw ? m->G(m->lm(i, LINW)) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s));
+                               gw ? m->G(m->lm(i, LINW)) : nullptr, nullptr, 1, P.norm_ws, P.norm_ws_bytes, M, H, s,
+                               f32));
         if (cb) cb(user, i);
     }
     return KD_OK;
@@ -762,10 +791,11 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
     const int NT = NI * np;
     const bool gw = m->train_vision != 0;
     bf16* dx = P.dxv;
+    const int f32 = m->rf32_v;
     if (dpost)
         KD_TRY(launch_norm_bwd(0, F.x_vis_last, D, m->W(m->i_post_w), dpost, D, F.pm, F.pr, dx, D, 1,
                                gw ? m->G(m->i_post_w) : nullptr, gw ? m->G(m->i_post_b) : nullptr, 1, P.norm_ws,
-                               P.norm_ws_bytes, NT, D, s));
+                               P.norm_ws_bytes, NT, D, s, f32));
     GemmArgs g0;
     for (int i = c.v_layers - 1; i >= 0; --i) {
         const VisLayerBufs& b = F.vl[i];
@@ -795,7 +825,7 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
         wait(s, ev);
         KD_TRY(launch_norm_bwd(0, b.x_mid, D, m->W(m->vis(i, VLN2W)), P.dh2v, D, b.m2, b.r2, dx, D, 1,
                                gw ? m->G(m->vis(i, VLN2W)) : nullptr, gw ? m->G(m->vis(i, VLN2B)) : nullptr, 1, P.norm_ws,
-                               P.norm_ws_bytes, NT, D, s));
+                               P.norm_ws_bytes, NT, D, s, f32));
         KD_TRY(gemm(s, P.splitk_main, NT, D, D, km(dx, D), mn(m->W(m->vis(i, VOW)), D), P.dov, D, g0));
         ev = nullptr;
         if (gw) {
@@ -822,7 +852,7 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
         wait(s, ev);
         KD_TRY(launch_norm_bwd(0, b.x, D, m->W(m->vis(i, VLN1W)), P.dhv, D, b.m1, b.r1, dx, D, 1,
                                gw ? m->G(m->vis(i, VLN1W)) : nullptr, gw ? m->G(m->vis(i, VLN1B)) : nullptr, 1, P.norm_ws,
-                               P.norm_ws_bytes, NT, D, s));
+                               P.norm_ws_bytes, NT, D, s, f32));
     }
     if (gw) {   // patch embedding (im2col GEMM), its bias and the position embedding
         lane.begin();
@@ -903,15 +933,18 @@ extern "C" {
 int kd_anyres_batch_map(const int64_t* image_sizes_host, int B, int tiles, int32_t* map_host, int map_ld,
                         int32_t* len_host) {
     KD_CHECK_ARG(image_sizes_host && map_host && len_host, "kd_anyres_batch_map: null pointer");
-    KD_CHECK_SHAPE(B > 0 && tiles > 0 && map_ld > 0, "kd_anyres_batch_map: B, tiles, map_ld must be positive");
+    KD_CHECK_SHAPE(B > 0 && tiles >= 0 && map_ld > 0, "kd_anyres_batch_map: B, map_ld must be positive, tiles >= 0");
+    int base_tile = 0;   // compact layout (tiles == 0): sample b's tiles follow sample b-1's real ones
     for (int b = 0; b < B; ++b) {
         const int oh = (int)image_sizes_host[2 * b], ow = (int)image_sizes_host[2 * b + 1];
         KD_CHECK_SHAPE(oh > 0 && ow > 0, "kd_anyres_batch_map: image sizes must be positive");
         int bh, bw;
         best_resolution(oh, ow, bh, bw);
-        KD_CHECK_SHAPE((bh / 384) * (bw / 384) + 1 <= tiles, "kd_anyres_batch_map: the batch has too few tiles per sample");
+        const int own = (bh / 384) * (bw / 384) + 1;   // the image's real tiles (base + grid)
+        KD_CHECK_SHAPE(tiles == 0 || own <= tiles, "kd_anyres_batch_map: the batch has too few tiles per sample");
         int32_t* row = map_host + (int64_t)b * map_ld;
-        const int n = pack_map(oh, ow, b * tiles * AR_TILE, row, map_ld);
+        const int n = pack_map(oh, ow, (tiles ? b * tiles : base_tile) * AR_TILE, row, map_ld);
+        base_tile += own;
         KD_CHECK_SHAPE(n >= 0, "kd_anyres_batch_map: anyres_max_9 downsampling of very large grids is not supported");
         KD_CHECK_SHAPE(n <= map_ld, "kd_anyres_batch_map: map_ld too small");
         for (int j = n; j < map_ld; ++j) row[j] = -2;
@@ -983,6 +1016,16 @@ int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad
     m->i_norm = m->i_lm0 + cfg->t_layers * kd::LNF;
     m->i_head = cfg->t_tie ? m->i_embed : m->i_norm + 1;
     m->soff = kd::fp8_scale_offsets(m->C, m->specs, &m->n_scales);
+    m->fam.assign(m->specs.size(), 0);
+    for (size_t i = 0; i < m->specs.size(); ++i) {
+        if (m->soff[i] < 0) continue;
+        const std::string& nm = m->specs[i].name;
+        m->fam[i] = nm.rfind("vision_tower", 0) == 0 ? KD_FP8_VISION
+                  : nm.rfind("multi_modal_projector", 0) == 0 ? KD_FP8_PROJECTOR
+                  : nm.find("self_attn") != std::string::npos ? KD_FP8_LM_ATTN
+                  : nm.find(".mlp.") != std::string::npos ? KD_FP8_LM_MLP
+                  : KD_FP8_LM_HEAD;
+    }
     *out = m;
     return KD_OK;
 }
@@ -1002,6 +1045,14 @@ int kd_model_set_trainable(kd_model* m, int vision, int projector, int language)
     return KD_OK;
 }
 
+int kd_model_set_residual_f32(kd_model* m, int vision, int language) {
+    KD_CHECK_ARG(m, "kd_model_set_residual_f32: null model");
+    KD_CHECK_ARG(!m->f8q || !(vision || language), "kd_model_set_residual_f32: not with fp8 weights bound");
+    m->rf32_v = vision != 0;
+    m->rf32_t = language != 0;
+    return KD_OK;
+}
+
 int64_t kd_model_fp8_scale_count(const kd_model* m) { return m ? m->n_scales : -1; }
 
 int kd_model_quantize_fp8(const kd_model* m, void* q, float* scales, void* stream) {
@@ -1018,40 +1069,48 @@ int kd_model_quantize_fp8(const kd_model* m, void* q, float* scales, void* strea
     return KD_OK;
 }
 
+int kd_model_set_fp8_families(kd_model* m, int families) {
+    KD_CHECK_ARG(m, "kd_model_set_fp8_families: null model");
+    KD_CHECK_ARG((families & ~KD_FP8_ALL) == 0, "kd_model_set_fp8_families: unknown family bits");
+    m->f8_families = families;
+    return KD_OK;
+}
+
 int kd_model_set_fp8(kd_model* m, const void* q, const float* scales) {
     KD_CHECK_ARG(m, "kd_model_set_fp8: null model");
     KD_CHECK_ARG((q == nullptr) == (scales == nullptr), "kd_model_set_fp8: q and scales go together");
     KD_CHECK_ARG(!q || !m->g, "kd_model_set_fp8: fp8 weights are for a frozen (no-grad) model, e.g. the teacher");
     KD_CHECK_ALIGN(q, 16, "kd_model_set_fp8: q must be 16-B aligned");
+    KD_CHECK_ARG(!q || !(m->rf32_v || m->rf32_t), "kd_model_set_fp8: the fp8 path keeps bf16 residual streams");
     m->f8q = (const uint8_t*)q;
     m->f8s = scales;
     return KD_OK;
 }
 
-size_t kd_model_forward_workspace_size(const kd_model* m, int B, int L, int tiles, int save) {
-    if (!m || B <= 0 || L <= 0 || tiles <= 0) return 0;
-    return kd::plan_forward(m, B, L, tiles, save, nullptr).bytes;
+size_t kd_model_forward_workspace_size(const kd_model* m, int B, int L, int n_tiles, int save) {
+    if (!m || B <= 0 || L <= 0 || n_tiles <= 0) return 0;
+    return kd::plan_forward(m, B, L, n_tiles, save, nullptr).bytes;
 }
 
-size_t kd_model_backward_workspace_size(const kd_model* m, int B, int L, int tiles) {
-    if (!m || B <= 0 || L <= 0 || tiles <= 0) return 0;
-    return kd::plan_backward(m, B, L, tiles, nullptr).bytes;
+size_t kd_model_backward_workspace_size(const kd_model* m, int B, int L, int n_tiles) {
+    if (!m || B <= 0 || L <= 0 || n_tiles <= 0) return 0;
+    return kd::plan_backward(m, B, L, n_tiles, nullptr).bytes;
 }
 
 int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pixel_dtype, const int32_t* src,
-                     const float* rope_cos, const float* rope_sin, int B, int L, int tiles, int save,
+                     const float* rope_cos, const float* rope_sin, int B, int L, int n_tiles, int save,
                      void* workspace, size_t workspace_bytes, void* hn, void* post_ln, void* logits,
                      void* const* kv_k, void* const* kv_v, int32_t* err, void* stream) {
     using namespace kd;
     KD_CHECK_ARG(m && ids && pixels && src && rope_cos && rope_sin && workspace && hn && err,
                  "kd_model_forward: null pointer");
-    KD_CHECK_SHAPE(B > 0 && L > 0 && tiles > 0, "kd_model_forward: B, L, tiles must be positive");
+    KD_CHECK_SHAPE(B > 0 && L > 0 && n_tiles > 0, "kd_model_forward: B, L, n_tiles must be positive");
     KD_CHECK_ARG(pixel_dtype == KD_DTYPE_BF16 || pixel_dtype == KD_DTYPE_F32, "kd_model_forward: pixel dtype");
-    const FwdPlan P = plan_forward(m, B, L, tiles, save, workspace);
+    const FwdPlan P = plan_forward(m, B, L, n_tiles, save, workspace);
     KD_CHECK_ARG(workspace_bytes >= P.bytes, "kd_model_forward: workspace too small");
     const kd_model_config& c = m->C.c;
     hipStream_t s = as_stream(stream);
-    const int NI = B * tiles, M = B * L, H = c.t_hidden;
+    const int NI = n_tiles, M = B * L, H = c.t_hidden;
     KD_TRY(vision_forward(m, P, pixels, pixel_dtype, NI, save, post_ln, s));
     {   // projector: linear_1 -> gelu -> linear_2 (HF5 llava_onevision :131-150)
         const int NT = NI * m->C.np(), D = c.v_hidden;
@@ -1060,14 +1119,15 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
         g.act = c.projector_act;
         g.aux = save ? P.ppre : nullptr;
         g.ld_aux = H;
-        KD_TRY(lin(m, P, s, NT, H, D, P.x_vis_last, D, m->i_p1w, P.z, H, g));
+        KD_TRY(lin(m, P, s, NT, H, D, P.x_vis_bf, D, m->i_p1w, P.z, H, g));
         GemmArgs g2;
         g2.bias = m->W(m->i_p2b);
         KD_TRY(lin(m, P, s, NT, H, H, P.z, H, m->i_p2w, P.feats, H, g2));
     }
     // inputs_embeds: token embeddings + the packed image features (masked_scatter)
-    bf16* emb = c.t_layers ? P.ll[0].x : P.x_lm_last;
-    KD_TRY(launch_embed_assemble(ids, src, m->W(m->i_embed), P.feats, m->W(m->i_newline), emb, M, H, c.t_vocab, err, s));
+    void* emb = c.t_layers ? P.ll[0].x : P.x_lm_last;
+    KD_TRY(launch_embed_assemble(ids, src, m->W(m->i_embed), P.feats, m->W(m->i_newline), emb, M, H, c.t_vocab, err, s,
+                                 m->rf32_t));
     KD_TRY(lm_forward(m, P, rope_cos, rope_sin, B, L, save, hn, kv_k, kv_v, s));
     if (logits) {
         GemmArgs g;
@@ -1077,16 +1137,16 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
 }
 
 int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids, const int32_t* src,
-                      const float* rope_cos, const float* rope_sin, int B, int L, int tiles, const void* dhn,
+                      const float* rope_cos, const float* rope_sin, int B, int L, int n_tiles, const void* dhn,
                       const void* dpost, void* workspace, size_t workspace_bytes, void* stream, void* wgrad_stream,
                       kd_layer_cb on_layer_done, void* user) {
     using namespace kd;
     KD_CHECK_ARG(m && fwd_workspace && ids && src && rope_cos && rope_sin && dhn && workspace && wgrad_stream,
                  "kd_model_backward: null pointer");
     KD_CHECK_ARG(m->g, "kd_model_backward: the model has no grad buffer");
-    KD_CHECK_SHAPE(B > 0 && L > 0 && tiles > 0, "kd_model_backward: B, L, tiles must be positive");
-    const FwdPlan F = plan_forward(m, B, L, tiles, 1, const_cast<void*>(fwd_workspace));
-    const BwdPlan P = plan_backward(m, B, L, tiles, workspace);
+    KD_CHECK_SHAPE(B > 0 && L > 0 && n_tiles > 0, "kd_model_backward: B, L, n_tiles must be positive");
+    const FwdPlan F = plan_forward(m, B, L, n_tiles, 1, const_cast<void*>(fwd_workspace));
+    const BwdPlan P = plan_backward(m, B, L, n_tiles, workspace);
     KD_CHECK_ARG(workspace_bytes >= P.bytes, "kd_model_backward: workspace too small");
     const kd_model_config& c = m->C.c;
     hipStream_t s = as_stream(stream);
@@ -1095,7 +1155,7 @@ int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids
     // embedding) precedes the embedding backward below
     hipEvent_t entry = m->event();
     (void)hipEventRecord(entry, lane.lane);
-    const int NI = B * tiles, NT = NI * m->C.np(), M = B * L, H = c.t_hidden, D = c.v_hidden;
+    const int NI = n_tiles, NT = NI * m->C.np(), M = B * L, H = c.t_hidden, D = c.v_hidden;
     KD_TRY(lm_backward(m, F, P, rope_cos, rope_sin, B, L, dhn, lane, s, on_layer_done, user));
     wait(s, entry);
     const bool need_vision = m->train_vision != 0;
@@ -1113,7 +1173,7 @@ int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids
         KD_TRY(launch_act_bwd(F.ppre, P.dz, P.dz, (int64_t)NT * H, c.projector_act, s));   // dpre in place
         if (m->train_projector) {
             lane.begin();
-            KD_TRY(lane.wgrad(NT, H, D, P.dz, H, F.x_vis_last, D, m->G(m->i_p1w)));
+            KD_TRY(lane.wgrad(NT, H, D, P.dz, H, F.x_vis_bf, D, m->G(m->i_p1w)));
             KD_TRY(lane.colsum(P.dz, H, NT, H, m->G(m->i_p1b)));
             lane.end();
         }

@@ -217,7 +217,7 @@ class _KDBase(_Base):
 
     def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1,
                  seed_teacher: int = 1, seed_student: int = 2, state_dict=None, loss_group_size: int | None = None,
-                 accumulate_grad_batches: int | None = None, teacher_fp8: bool = False, **_ignored):
+                 accumulate_grad_batches: int | None = None, teacher_fp8: bool | str = False, **_ignored):
         super().__init__()
         self.phase = phase
         self.learning_rate = learning_rate
@@ -282,9 +282,12 @@ class _KDBase(_Base):
             self._gsync = GradSync(self._dist, self.student_model.P.grad)
         # fp8 (e4m3) teacher weights, quantised once after the broadcast (BASELINE config c4;
         # the reference loads the teacher fp16, DT:43-48)
-        self.teacher_fp8 = bool(teacher_fp8) and self.teacher_model is not None
+        # teacher_fp8: False, True (= "all") or a modeling.FP8_FAMILIES policy name ("lm", "lm_mlp", ...)
+        if teacher_fp8 is True:
+            teacher_fp8 = "all"
+        self.teacher_fp8 = teacher_fp8 if (teacher_fp8 and self.teacher_model is not None) else False
         if self.teacher_fp8:
-            self.teacher_model.enable_fp8()
+            self.teacher_model.enable_fp8(self.teacher_fp8)
 
     # ------------------------------------------------------------- freezing ----
     def _trainable_range(self):
@@ -395,14 +398,16 @@ class _KDBase(_Base):
         dps = None
         if need_feats:
             NP = s.cfg.vision.n_patches
-            NI = sfwd["post_ln"].shape[0] // NP
+            NI = sfwd["post_ln"].shape[0] // NP                      # the batch's real tiles (KAT 7: 2B at 336x336)
             ps = ops.row_group_mean(sfwd["post_ln"], NI, NP)        # DT:243-244
             pt = ops.row_group_mean(t_post, NI, NP)
-            rpg = NI // B * G                                        # pooled tile rows per group
+            cum = [0]
+            for n in sfwd["tile_counts"]:                            # pooled tile rows of each sample
+                cum.append(cum[-1] + n)
             ntx_rows = torch.empty((ng, 2), dtype=torch.float32, device=ps.device)
             dps = torch.empty_like(ps) if train else None
             for g in range(ng):                                      # DT:393-416 per group
-                r = slice(g * rpg, (g + 1) * rpg)
+                r = slice(cum[g * G], cum[(g + 1) * G])
                 ops.ntxent(ps[r], pt[r], tau=0.07, weight=ctr_w / ng, want_grad=train, loss_out=ntx_rows[g],
                            dfs_out=None if dps is None else dps[r])
             ntx = ntx_rows.sum(0) if ng > 1 else ntx_rows[0]
@@ -533,7 +538,7 @@ class _KDBase(_Base):
         if self.teacher_model is not None and any(k.startswith("teacher_model.") for k in sd):
             self.teacher_model.P.load_state_dict(sd, prefix="teacher_model.")
             if getattr(self.teacher_model, "fp8", False):
-                self.teacher_model.enable_fp8()   # re-quantise the new weights
+                self.teacher_model.enable_fp8(self.teacher_model.fp8_families)   # re-quantise the new weights
 
     def _hparams(self):
         # everything that changes the objective or the update is saved, so load_from_checkpoint
@@ -543,7 +548,7 @@ class _KDBase(_Base):
 
     def _run_hparams(self):
         return {"loss_group_size": self.loss_group_size, "accumulate_grad_batches": self.accumulate_grad_batches,
-                "teacher_fp8": bool(getattr(self, "teacher_fp8", False))}
+                "teacher_fp8": getattr(self, "teacher_fp8", False)}
 
     def on_train_epoch_end(self):
         """A batch rejected among the last steps of an epoch is reported here (the reference
@@ -570,13 +575,20 @@ class _KDBase(_Base):
         hp = dict(ck.get("hyper_parameters", {}))
         sig = inspect.signature(cls.__init__)
         args = {}
+        var_kw = False
         for name, prm in list(sig.parameters.items())[1:]:
+            if prm.kind == prm.VAR_KEYWORD:
+                var_kw = True
             if prm.kind in (prm.VAR_KEYWORD, prm.VAR_POSITIONAL):
                 continue
             if name in kw:
                 args[name] = kw.pop(name)
             elif name in hp:
                 args[name] = hp[name]
+        if var_kw:   # saved knobs the subclass forwards to _KDBase through **kw (loss_group_size, ...)
+            for name, v in hp.items():
+                if name not in args and name not in kw:
+                    args[name] = v
         kw.pop("torch_dtype", None)   # the build's weights are bf16 in HBM whatever the caller's dtype
         return cls(**args, state_dict=ck["state_dict"], **kw)
 

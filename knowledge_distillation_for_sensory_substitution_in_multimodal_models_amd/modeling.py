@@ -353,6 +353,16 @@ def native_layout(cfg: LlavaConfig) -> list[tuple[str, int, int]]:
 
 
 # --------------------------------------------------------------------- model ----
+# fp8 (e4m3) teacher policies: which linear families run on the fp8 GEMM (kd_fp8_family bits)
+FP8_FAMILIES = {
+    "all": NV.KD_FP8_ALL,
+    "lm": NV.KD_FP8_LM_ATTN | NV.KD_FP8_LM_MLP | NV.KD_FP8_LM_HEAD,
+    "lm_body": NV.KD_FP8_LM_ATTN | NV.KD_FP8_LM_MLP,
+    "lm_mlp": NV.KD_FP8_LM_MLP,
+    "none": 0,
+}
+
+
 class LlavaOnevisionModel:
     """One LLaVA-OneVision instance (teacher or student) on a ParamStore, driven through the
     library's model runtime (one forward call, one backward call per step)."""
@@ -379,6 +389,18 @@ class LlavaOnevisionModel:
                 self.P.grad.data_ptr() if trainable else None, C.byref(h))
         self._h = h
         self.fp8 = False
+        # the trainable model (the student) keeps both residual streams in fp32, as the
+        # reference's fp32 / autocast step does: with a bf16 stream the rounding after every
+        # residual add moved the tiny fixtures' gradient norm by +0.12 % (tools/grad_bias_study.py)
+        self.residual_f32 = (False, False)
+        if trainable:
+            self.set_residual_f32(True, True)
+
+    def set_residual_f32(self, vision: bool, language: bool):
+        """fp32 residual streams of the SigLIP / Qwen2 towers (kd_model_set_residual_f32)."""
+        NV.call("kd_model_set_residual_f32", self._h, int(vision), int(language))
+        self.residual_f32 = (bool(vision), bool(language))
+        self._ws = {}   # the workspaces' stream buffers change size
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -413,9 +435,10 @@ class LlavaOnevisionModel:
             self._rope[L] = rope_tables(L, self.cfg.text.head_dim, self.cfg.text.rope_theta, self.device)
         return self._rope[L]
 
-    def _src_map(self, input_ids, image_sizes, tiles):
+    def _src_map(self, input_ids, image_sizes, tiles=0):
         """Per-token source rows of inputs_embeds: the anyres pack plan (kd_anyres_batch_map,
-        host, cached per image_sizes) expanded on the device by kd_image_src_map."""
+        host, cached per image_sizes; tiles = 0: feature rows over the compact real tiles)
+        expanded on the device by kd_image_src_map."""
         key = (tuple(tuple(int(v) for v in hw) for hw in image_sizes), tiles)
         if key not in self._maps:
             B = len(key[0])
@@ -429,12 +452,16 @@ class LlavaOnevisionModel:
         return ops.image_src_map(input_ids, self.cfg.image_token_id, maps, lens, self.err)
 
     # -- fp8 teacher (BASELINE config c4)
-    def enable_fp8(self):
+    def enable_fp8(self, families="all"):
         """Quantise every linear weight to e4m3 with per-output-channel scales (kd_model_quantize_fp8,
-        on the current stream) and run the forward's linears on the fp8 GEMM from now on
-        (per-token activation scales).  Frozen models only; re-run after the weights change."""
+        on the current stream) and run the forward's linears of `families` (FP8_FAMILIES name or
+        kd_fp8_family bits) on the fp8 GEMM from now on (per-token activation scales); the other
+        linears keep the bf16 GEMM.  Frozen models only; re-run after the weights change."""
         if self.P.trainable:
             raise RuntimeError("fp8 weights are for the frozen teacher (no grad buffer)")
+        fam = FP8_FAMILIES[families] if isinstance(families, str) else int(families)
+        NV.call("kd_model_set_fp8_families", self._h, fam)
+        self.fp8_families = fam
         lib = NV.lib()
         n = lib.kd_model_fp8_scale_count(self._h)
         self._f8q = torch.empty(self.P.numel, dtype=torch.uint8, device=self.device)
@@ -478,23 +505,36 @@ class LlavaOnevisionModel:
         input_ids [B, L] int64 (device), pixel_values [B, P, 3, 384, 384] (bf16 / fp32),
         image_sizes [B, 2] (host-readable).  Returns a dict with `hn` (final-norm hidden
         [B*L, H]), `post_ln` (vision post_layernorm output, the reference's hook, DT:110-121),
-        `logits` [B*L, V] (want_logits) and, with save, the workspace the backward reads.
+        `logits` [B*L, V] (want_logits), `tile_counts` (each sample's real vision tiles, the
+        post_ln row groups) and, with save, the workspace the backward reads.
         kv_out (a list) receives each layer's roped (k, v) [B, kv_heads, L, head_dim]."""
         T, V = self.cfg.text, self.cfg.vision
         B, L = input_ids.shape
-        tiles = pixel_values.shape[1]
-        px = pixel_values.reshape(B * tiles, *pixel_values.shape[2:]).contiguous()
+        P = pixel_values.shape[1]
+        sizes = image_sizes.tolist() if hasattr(image_sizes, "tolist") else image_sizes
+        # the vision tower runs each image's REAL tiles only (base + anyres grid; HF drops the
+        # zero tiles _pad_for_batching added: pix_val[:num_patch]), so a mixed batch
+        # (336x336: 2 tiles, 480x640: 5) hooks exactly the reference's tile features
+        counts = [anyres.num_tiles(tuple(int(v) for v in hw)) for hw in sizes]
+        if any(n > P for n in counts):
+            raise RuntimeError(f"pixel_values has {P} tiles per sample; image_sizes need {max(counts)}")
+        px = pixel_values.reshape(B * P, *pixel_values.shape[2:])
+        if any(n != P for n in counts):
+            idx = torch.tensor([b * P + t for b in range(B) for t in range(counts[b])], device=px.device)
+            px = px.index_select(0, idx)
+        px = px.contiguous()
+        tiles = int(sum(counts))   # vision tiles of the batch
         if px.dtype not in (torch.bfloat16, torch.float32):
             raise RuntimeError(f"pixel_values: bf16 or fp32, got {px.dtype}")
         ids = input_ids.contiguous()
-        src = self._src_map(ids, image_sizes.tolist() if hasattr(image_sizes, "tolist") else image_sizes, tiles)
+        src = self._src_map(ids, sizes, 0)
         cos, sin = self._rope_for(L)
         lib = NV.lib()
         nb = lib.kd_model_forward_workspace_size(self._h, B, L, tiles, int(save))
         ws = self._workspace(("fwd", B, L, tiles, bool(save)), nb)
         dev = self.device
         hn = torch.empty((B * L, T.hidden), dtype=torch.bfloat16, device=dev)
-        post = torch.empty((B * tiles * V.n_patches, V.hidden), dtype=torch.bfloat16, device=dev) \
+        post = torch.empty((tiles * V.n_patches, V.hidden), dtype=torch.bfloat16, device=dev) \
             if want_post_ln else None
         logits = torch.empty((B * L, T.vocab), dtype=torch.bfloat16, device=dev) if want_logits else None
         kvk = kvv = None
@@ -507,7 +547,7 @@ class LlavaOnevisionModel:
         NV.call("kd_model_forward", self._h, ids.data_ptr(), px.data_ptr(), ops._DT[px.dtype], src.data_ptr(),
                 cos.data_ptr(), sin.data_ptr(), B, L, tiles, int(save), ws.data_ptr(), ws.numel(), hn.data_ptr(),
                 ops._ptr(post), ops._ptr(logits), kvk, kvv, self.err.data_ptr(), ops._stream())
-        out = dict(hn=hn, src=src, ids=ids, shape=(B, L, tiles))
+        out = dict(hn=hn, src=src, ids=ids, shape=(B, L, tiles), tile_counts=counts)
         if want_post_ln:
             out["post_ln"] = post
         if want_logits:

@@ -213,9 +213,11 @@ def _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate
         ws = _workspace(("gemm_splitk", _stream()), GEMM_SPLITK_WS, a.device)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     if residual is not None:
-        _require(residual, torch.bfloat16, "gemm.residual")
+        if residual.dtype not in _DT or not residual.is_cuda:
+            raise RuntimeError("gemm.residual: expected a bf16 or fp32 device tensor")
         d.residual, d.ldr = residual.data_ptr(), residual.stride(0)
         d.residual_row_mod = int(residual_row_mod)
+        d.residual_dtype = _DT[residual.dtype]
     if aux is not None:
         _require(aux, torch.bfloat16, "gemm.aux")
         d.aux, d.ld_aux = aux.data_ptr(), aux.stride(0)
@@ -352,13 +354,16 @@ def attn_bwd(q, k, v, o, do, lse, hd: int, causal: bool):
 
 # -------------------------------------------------------------------- norms ----
 def norm_fwd(x, weight, bias=None, eps: float = 1e-6, rms: bool = False, out=None, save_stats: bool = True):
-    """LayerNorm (rms=False) / RMSNorm (rms=True) over the last dim of a 2-D bf16 tensor."""
+    """LayerNorm (rms=False) / RMSNorm (rms=True) over the last dim of a 2-D bf16 or fp32
+    (residual stream) tensor; bf16 output."""
     R, D = x.shape
+    if x.dtype not in _DT:
+        raise RuntimeError("norm_fwd: x must be bf16 or fp32")
     y = out if out is not None else torch.empty((R, D), dtype=torch.bfloat16, device=x.device)
     mean = torch.empty(R, dtype=torch.float32, device=x.device) if (save_stats and not rms) else None
     rstd = torch.empty(R, dtype=torch.float32, device=x.device) if save_stats else None
     NV.call("kd_norm_fwd", int(rms), x.data_ptr(), x.stride(0), weight.data_ptr(), _ptr(bias), y.data_ptr(),
-            y.stride(0), _ptr(mean), _ptr(rstd), R, D, float(eps), _stream())
+            y.stride(0), _ptr(mean), _ptr(rstd), R, D, float(eps), _DT[x.dtype], _stream())
     return y, mean, rstd
 
 
@@ -371,7 +376,7 @@ def norm_bwd(x, weight, dy, mean, rstd, dx=None, dx_accum: bool = False, dweight
     ws = _workspace("norm_bwd", nb, x.device)
     NV.call("kd_norm_bwd", int(rms), x.data_ptr(), x.stride(0), weight.data_ptr(), dy.data_ptr(), dy.stride(0),
             _ptr(mean), rstd.data_ptr(), dx.data_ptr(), dx.stride(0), int(dx_accum), _ptr(dweight), _ptr(dbias),
-            int(accum_w), ws.data_ptr(), ws.numel(), R, D, _stream())
+            int(accum_w), ws.data_ptr(), ws.numel(), R, D, _DT[x.dtype], _stream())
     return dx
 
 

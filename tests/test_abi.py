@@ -116,9 +116,9 @@ def test_model_handle_workspace_queries_and_errors():
     N.call("kd_model_create", C.byref(cfg), 4096, 8192, C.byref(h))   # fake (aligned) device pointers
     try:
         f1 = lib.kd_model_forward_workspace_size(h, 1, 1536, 2, 1)
-        f4 = lib.kd_model_forward_workspace_size(h, 4, 1536, 2, 1)
-        f4n = lib.kd_model_forward_workspace_size(h, 4, 1536, 2, 0)
-        b4 = lib.kd_model_backward_workspace_size(h, 4, 1536, 2)
+        f4 = lib.kd_model_forward_workspace_size(h, 4, 1536, 8, 1)    # n_tiles = the batch's 4 x 2 tiles
+        f4n = lib.kd_model_forward_workspace_size(h, 4, 1536, 8, 0)
+        b4 = lib.kd_model_backward_workspace_size(h, 4, 1536, 8)
         assert f4 > f1 > 0 and f4 > 4 * f4n // 2 and b4 > 0
         # ~saved activations of the 0.5B student at bs 4: 24 LM layers x ~250 MB + 26 ViT layers
         assert 8e9 < f4 < 2e10, f4

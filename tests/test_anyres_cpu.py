@@ -64,3 +64,23 @@ def test_library_pack_plan_matches_python():
             assert lens[b] == n, hw
             assert out[b, :n].tolist() == ref, hw
             assert (out[b, n:] == -2).all()
+
+
+def test_compact_tile_layout_c_equals_python():
+    """tiles = 0: the feature rows of each sample follow the previous samples' REAL tiles (the
+    vision tower runs only those, as HF's pix_val[:num_patch]); a mixed SUNRGBD-style batch
+    [336x336 (2 tiles, 1485 tokens), 480x640 (5 tiles, 2929 tokens), 336x336]."""
+    import numpy as np
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import _native as N
+    sizes = [(336, 336), (480, 640), (336, 336)]
+    maps, lens = A.batch_maps(sizes, 0)
+    assert lens == [1485, 2929, 1485]
+    assert maps[1][0] == 2 * 729 and maps[2][0] == (2 + 5) * 729
+    assert max(v for v in maps[2] if v >= 0) < (2 + 5 + 2) * 729
+    isz = np.array(sizes, dtype=np.int64)
+    ld = max(lens)
+    out = np.zeros((3, ld), dtype=np.int32)
+    ln = np.zeros(3, dtype=np.int32)
+    N.call("kd_anyres_batch_map", isz.ctypes.data, 3, 0, out.ctypes.data, ld, ln.ctypes.data)
+    for b in range(3):
+        assert ln[b] == lens[b] and out[b, :lens[b]].tolist() == maps[b] and (out[b, lens[b]:] == -2).all()

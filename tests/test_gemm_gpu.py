@@ -93,6 +93,28 @@ def test_epilogue_bias_act_residual_aux_accumulate(dev):
     assert (out - 0.5 * (a.float() @ w.float().t())).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("variant,split_k", [(1, 1), (5, 1), (6, 1), (7, 1), (16, 1), (20, 1), (16, 3), (0, 0)])
+def test_fp32_residual_stream(variant, split_k, dev):
+    """C (fp32) = A B^T + bias + residual (fp32): the fp32 residual stream's epilogue (o_proj /
+    fc2 / down_proj with kd_model_set_residual_f32) in every kernel and through the split-K
+    reduce; the residual is added in fp32, not rounded to bf16."""
+    ops = _ops()
+    M, N, K = 600, 1152, 2304
+    a = _rand(M, K, dev=dev, seed=21)
+    w = _rand(N, K, dev=dev, seed=22, scale=0.05)
+    bias = _rand(N, dev=dev, seed=23)
+    g = torch.Generator(device=dev).manual_seed(24)
+    res = torch.randn(M, N, generator=g, device=dev) * 3 + 1e-3   # fp32 values off the bf16 grid
+    out = ops.gemm(a, w, bias=bias, residual=res, out_dtype=torch.float32, variant=variant, split_k=split_k)
+    ref = a.float() @ w.float().t() + bias.float() + res
+    err = (out - ref).abs()
+    assert float(err.max()) <= 2e-4 * float(ref.abs().max()), float(err.max())
+    # bf16 rounding of the residual alone would be off by up to |res| * 2^-9
+    assert float((out - (a.float() @ w.float().t() + bias.float() + res.bfloat16().float())).abs().max()) > 1e-3
+    with pytest.raises(RuntimeError, match="fp32 residual"):
+        ops.gemm(a, w, residual=res)   # bf16 C with an fp32 residual is rejected
+
+
 VARIANTS = [1, 5, 6, 7, 16, 20]   # 128x128 v1; v3 256x256 / 256x128 / 128x256 (8 waves); v8 256x256 (4 waves, AGPR acc);
 #                                  v9 256x256 (8 waves, ping-pong)
 

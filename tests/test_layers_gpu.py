@@ -54,6 +54,33 @@ def test_norm_fwd_bwd(rms, R, D, dev):
         _close(db, bf.grad, 1e-3)
 
 
+@pytest.mark.parametrize("rms,R,D", [(False, 5832, 1152), (True, 6144, 896), (True, 33, 64)])
+def test_norm_fp32_input(rms, R, D, dev):
+    """Norms over an fp32 residual stream (kd_norm_fwd / kd_norm_bwd x_dtype = fp32): the
+    statistics and x-hat from the fp32 values, equal to the same ops on the fp32 tensor."""
+    ops = _ops()
+    g = torch.Generator(device=dev).manual_seed(31)
+    x = torch.randn(R, D, generator=g, device=dev) * 2 + 0.5
+    w = _r(D, seed=2, dev=dev)
+    b = None if rms else _r(D, seed=3, dev=dev)
+    y, mean, rstd = ops.norm_fwd(x, w, b, eps=1e-6, rms=rms)
+    xf = x.clone().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    bf = None if rms else b.float().requires_grad_(True)
+    ref = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * wf if rms
+           else F.layer_norm(xf, (D,), wf, bf, eps=1e-6))
+    _close(y, ref)
+    ref_rstd = torch.rsqrt((x.pow(2).mean(-1) if rms else x.var(-1, unbiased=False)) + 1e-6)
+    assert float(((rstd - ref_rstd) / ref_rstd).abs().max()) < 1e-5
+    dy = _r(R, D, seed=4, dev=dev)
+    ref.backward(dy.float())
+    dw = torch.zeros(D, device=dev)
+    db = None if rms else torch.zeros(D, device=dev)
+    dx = ops.norm_bwd(x, w, dy, mean, rstd, dweight=dw, dbias=db, rms=rms)
+    _close(dx, xf.grad, 2e-2)
+    _close(dw, wf.grad, 1e-3)
+
+
 def _rope_tables(S, hd, theta=1e6):
     inv = 1.0 / (theta ** (torch.arange(0, hd, 2, dtype=torch.float32) / hd))
     f = torch.arange(S, dtype=torch.float32)[:, None] * inv[None]

@@ -136,6 +136,7 @@ int main(int argc, char** argv) {
     kd_model *teacher = nullptr, *student = nullptr;
     KD(kd_model_create(&tc, tw, nullptr, &teacher));
     KD(kd_model_create(&sc, sw, grad, &student));
+    KD(kd_model_set_residual_f32(student, 1, 1));   // fp32 residual streams, as the drop-in module's student
 
     // ---- batch
     const int64_t* rgb_ids = upload<int64_t>(slurp(dir + "/rgb_ids.bin"));
@@ -173,17 +174,17 @@ int main(int argc, char** argv) {
 
     // ---- teacher forward (no_grad, DT:228) and student forward with saved activations (DT:238)
     const int M = B * L, Vt = tc.t_vocab, Vs = sc.t_vocab, H = sc.t_hidden;
-    const size_t twsb = kd_model_forward_workspace_size(teacher, B, L, tiles, 0);
-    const size_t swsb = kd_model_forward_workspace_size(student, B, L, tiles, 1);
+    const size_t twsb = kd_model_forward_workspace_size(teacher, B, L, B * tiles, 0);
+    const size_t swsb = kd_model_forward_workspace_size(student, B, L, B * tiles, 1);
     void* tws = dalloc(twsb);
     void* sws = dalloc(swsb);
     void* hn_t = dalloc((size_t)M * tc.t_hidden * 2);
     void* hn_s = dalloc((size_t)M * H * 2);
     void* t_logits = dalloc((size_t)M * Vt * 2);
     void* s_logits = dalloc((size_t)M * Vs * 2);
-    KD(kd_model_forward(teacher, rgb_ids, rgb_px, KD_DTYPE_BF16, src_t, cos_t, sin_t, B, L, tiles, 0, tws, twsb, hn_t,
+    KD(kd_model_forward(teacher, rgb_ids, rgb_px, KD_DTYPE_BF16, src_t, cos_t, sin_t, B, L, B * tiles, 0, tws, twsb, hn_t,
                         nullptr, t_logits, nullptr, nullptr, err, main_s));
-    KD(kd_model_forward(student, depth_ids, depth_px, KD_DTYPE_BF16, src_s, cos_s, sin_s, B, L, tiles, 1, sws, swsb,
+    KD(kd_model_forward(student, depth_ids, depth_px, KD_DTYPE_BF16, src_s, cos_s, sin_s, B, L, B * tiles, 1, sws, swsb,
                         hn_s, nullptr, s_logits, nullptr, nullptr, err + 1, main_s));
 
     // ---- fused LoCa (T = 1, LB:164-165) + student CE, forward and d/dlogits
@@ -232,9 +233,9 @@ int main(int argc, char** argv) {
     KD(kd_gemm(&w, lane_s));
 
     // ---- student backward (every trainable grad, +=), weight gradients on the lane
-    const size_t bwsb = kd_model_backward_workspace_size(student, B, L, tiles);
+    const size_t bwsb = kd_model_backward_workspace_size(student, B, L, B * tiles);
     void* bws = dalloc(bwsb);
-    KD(kd_model_backward(student, sws, depth_ids, src_s, cos_s, sin_s, B, L, tiles, dhn, nullptr, bws, bwsb, main_s,
+    KD(kd_model_backward(student, sws, depth_ids, src_s, cos_s, sin_s, B, L, B * tiles, dhn, nullptr, bws, bwsb, main_s,
                          lane_s, nullptr, nullptr));
 
     // ---- gradient norm, AdamW (torch.optim.AdamW defaults of configure_optimizers, DT:198-201)
