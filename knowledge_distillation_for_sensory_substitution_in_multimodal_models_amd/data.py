@@ -47,6 +47,51 @@ def synthetic_batch(B: int, device, L: int = 1536, image_hw=(336, 336), seed: in
     }
 
 
+PAD_ID = 151643   # <|endoftext|>, the Qwen2 tokenizer's pad token in the llava-onevision processors
+
+
+def synthetic_batch_mixed(image_sizes, device, seed: int = 0, pixel_dtype=torch.bfloat16, prefix: int = 24,
+                          suffix: int = 27, cpu_rng: bool = False, question_id: int = 0) -> dict:
+    """A batch in the layout of the reference's collate_fn for real SUNRGBD geometry
+    (DM:97-167, DS:185-212): one image per sample at its own size (480x640 -> 5 tiles and
+    2,929 image tokens, SURVEY KAT 9; 336x336 -> 2 tiles, 1,485 tokens), `prefix` random
+    text ids + the image tokens + `suffix` random text ids, right-padded with PAD_ID to the
+    longest sample (processor padding=True), labels = ids with the pads -> -100 (DM:141-146),
+    pixel_values [B, P_max, 3, 384, 384] with each sample's tiles past its own count zero
+    (_pad_for_batching).  No attention mask (the reference passes none, DM:159-167)."""
+    sizes = [tuple(int(v) for v in hw) for hw in image_sizes]
+    B = len(sizes)
+    lens = [prefix + anyres.num_image_tokens(hw) + suffix for hw in sizes]
+    tiles = [anyres.num_tiles(hw) for hw in sizes]
+    L, P = max(lens), max(tiles)
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.full((B, L), PAD_ID, dtype=torch.int64)
+    for b, hw in enumerate(sizes):
+        n_img = anyres.num_image_tokens(hw)
+        row = torch.randint(0, TEXT_VOCAB, (lens[b],), generator=g, dtype=torch.int64)
+        row[prefix:prefix + n_img] = IMAGE_TOKEN_ID
+        ids[b, :lens[b]] = row
+    labels = torch.where(ids == PAD_ID, torch.full_like(ids, -100), ids)
+    rdev = "cpu" if cpu_rng else device
+    gd = torch.Generator(device=rdev).manual_seed(seed + 1)
+    px = []
+    for _ in range(2):   # rgb, depth
+        t = torch.rand(B, P, 3, 384, 384, generator=gd, device=rdev) * 2 - 1
+        for b in range(B):
+            t[b, tiles[b]:] = 0
+        px.append(t.to(pixel_dtype).to(device))
+    ids = ids.to(device)
+    return {
+        "rgb_input_ids": ids,
+        "depth_input_ids": ids,
+        "rgb_pixel_values": px[0],
+        "depth_pixel_values": px[1],
+        "image_sizes": torch.tensor([list(hw) for hw in sizes], dtype=torch.int64),
+        "labels": labels.to(device),
+        "question_id": question_id,
+    }
+
+
 def convert_depth_image_into_3D(depth_image, device="cuda") -> torch.Tensor:
     """GPU counterpart of CustomSUNRGBDDatasetOneVision.convert_depth_image_into_3D
     (dataset/dataloader/OneVision/CustomSUNRGBDDatasetOneVision.py:64-112).

@@ -585,10 +585,10 @@ class _KDBase(_Base):
                 args[name] = kw.pop(name)
             elif name in hp:
                 args[name] = hp[name]
-        if var_kw:   # saved knobs the subclass forwards to _KDBase through **kw (loss_group_size, ...)
-            for name, v in hp.items():
-                if name not in args and name not in kw:
-                    args[name] = v
+        if var_kw:   # the saved run knobs a subclass forwards to _KDBase through **kw
+            for name in ("loss_group_size", "accumulate_grad_batches", "teacher_fp8"):
+                if name in hp and name not in args and name not in kw:
+                    args[name] = hp[name]
         kw.pop("torch_dtype", None)   # the build's weights are bf16 in HBM whatever the caller's dtype
         return cls(**args, state_dict=ck["state_dict"], **kw)
 

@@ -1,6 +1,6 @@
 """End-to-end golden fixtures from the REFERENCE's forward() (dev container only).
 
-    python tests/golden/make_golden_model.py
+    python tests/golden/make_golden_model.py [all | bench | geometry]
 
 Tiny-width LLaVA-OneVision teacher/student (real vocab 152064/151936, real 336x336 token
 layout: 2 tiles, 1485 image tokens, L=1536) with seeded weights drawn by the build's own
@@ -27,7 +27,8 @@ import make_golden as MG  # noqa: E402
 from oracle.model import hf5_key  # noqa: E402
 from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import (  # noqa: E402
     ParamStore, tiny_config)
-from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch  # noqa: E402
+from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import (  # noqa: E402
+    synthetic_batch, synthetic_batch_mixed)
 
 SEED_T, SEED_S, SEED_DATA = 1, 2, 0
 B, L = 2, 1536
@@ -59,8 +60,13 @@ def hf_model(cfg, sd):
     return m
 
 
-def batch_cpu():
-    b = synthetic_batch(B, "cpu", L=L, seed=SEED_DATA, pixel_dtype=torch.bfloat16, cpu_rng=True)
+def batch_cpu(sizes=None):
+    """The 336x336 bench layout (B = 2, L = 1536), or with `sizes` a SUNRGBD-geometry batch
+    (data.synthetic_batch_mixed: one image per sample at its own size, right padding)."""
+    if sizes is None:
+        b = synthetic_batch(B, "cpu", L=L, seed=SEED_DATA, pixel_dtype=torch.bfloat16, cpu_rng=True)
+    else:
+        b = synthetic_batch_mixed(sizes, "cpu", seed=SEED_DATA, pixel_dtype=torch.bfloat16, cpu_rng=True)
     for k in ("rgb_pixel_values", "depth_pixel_values"):
         b[k] = b[k].float()
     return b
@@ -116,15 +122,15 @@ class _Recorder:
         obj.contrastive_loss = rec
 
 
-def logit_stats(logits):
-    """Per-row logsumexp and sum (fp64) of [B, L, V] logits, plus rows LOGIT_ROWS sampled at
-    every LOGIT_COL_STRIDE-th column."""
+def logit_stats(logits, rows=LOGIT_ROWS):
+    """Per-row logsumexp and sum (fp64) of [B, L, V] logits, plus `rows` sampled at every
+    LOGIT_COL_STRIDE-th column."""
     x = logits.detach().double()
     return (torch.logsumexp(x, -1).reshape(-1).numpy(), x.sum(-1).reshape(-1).numpy(),
-            x[:, list(LOGIT_ROWS), ::LOGIT_COL_STRIDE].float().numpy())
+            x[:, list(rows), ::LOGIT_COL_STRIDE].float().numpy())
 
 
-def run(kind, phase, teacher_sd, student_sd, out_name):
+def run(kind, phase, teacher_sd, student_sd, out_name, sizes=None):
     from transformers import LlavaOnevisionForConditionalGeneration  # noqa: F401
     MG._install_stub()
     DT = MG._load("ref_dt", MG.DT_PATH)
@@ -134,7 +140,9 @@ def run(kind, phase, teacher_sd, student_sd, out_name):
     tcfg, scfg = tiny_config(True), tiny_config(False)
     student = hf_model(scfg, student_sd)
     teacher = hf_model(tcfg, teacher_sd) if kind != "bd" else None
-    batch = batch_cpu()
+    batch = batch_cpu(sizes)
+    Bb, Lb = batch["depth_input_ids"].shape
+    rows = LOGIT_ROWS if sizes is None else (0, 23, 24, Lb // 2, Lb - 28, Lb - 27, Lb - 2, Lb - 1)
     rec = _Recorder()
     student.register_forward_hook(rec.hook("student"))
     if teacher is not None:
@@ -188,8 +196,8 @@ def run(kind, phase, teacher_sd, student_sd, out_name):
                student_ce=np.float64(so.loss.item()),
                teacher_ce=np.float64(rec.out["teacher"].loss.item() if "teacher" in rec.out else np.nan),
                ntxent=np.float64(rec.ntx[0] if rec.ntx else np.nan))
-    lse, rsum, rows = logit_stats(so.logits)
-    out.update(s_logit_lse=lse, s_logit_rowsum=rsum, s_logit_rows=rows, logit_rows=np.array(LOGIT_ROWS),
+    lse, rsum, srows = logit_stats(so.logits, rows)
+    out.update(s_logit_lse=lse, s_logit_rowsum=rsum, s_logit_rows=srows, logit_rows=np.array(rows),
                logit_col_stride=np.int64(LOGIT_COL_STRIDE))
     if "teacher" in rec.out:
         tl, ts, _ = logit_stats(rec.out["teacher"].logits)
@@ -200,7 +208,9 @@ def run(kind, phase, teacher_sd, student_sd, out_name):
     out["grad_heads"] = np.stack([grads[n].reshape(-1)[:16].float().numpy() for n in names]) if names else np.zeros((0, 16))
     tot = sum(float(grads[n].pow(2).sum()) for n in names)
     out["grad_total_norm"] = np.float64(math_sqrt(tot))
-    meta = dict(kind=kind, phase=phase, B=B, L=L, seed_t=SEED_T, seed_s=SEED_S, seed_data=SEED_DATA)
+    meta = dict(kind=kind, phase=phase, B=Bb, L=Lb, seed_t=SEED_T, seed_s=SEED_S, seed_data=SEED_DATA)
+    if sizes is not None:
+        meta["sizes"] = [list(hw) for hw in sizes]
     np.savez_compressed(HERE / f"model_{out_name}.npz", meta=json.dumps(meta), **out)
     print(out_name, {k: float(out[k]) for k in ("total", "kd_term", "student_ce", "teacher_ce", "ntxent")},
           "grad norm", out["grad_total_norm"], "n_grads", len(names))
@@ -214,14 +224,31 @@ def math_sqrt(x):
 STUDENT_KEYS = []
 
 
+# real SUNRGBD geometry (SURVEY KAT 9, DM:127-146, DS:185-212): one 480x640 image (5 tiles,
+# 2,929 image tokens, L = 2,980) — LoCa only works unpadded (KAT 2), so bs 1 — and a mixed,
+# right-padded batch [336x336, 480x640] (pads labelled -100) for the kinds that accept pads
+GEOMETRY = (
+    ("lb", 0, "sun_lb", [(480, 640)]),
+    ("dt", 1, "sun_dt1", [(480, 640)]),
+    ("bd", 0, "mix_bd", [(336, 336), (480, 640)]),
+    ("fb", 0, "mix_fb", [(336, 336), (480, 640)]),
+    ("dt", 1, "mix_dt1", [(336, 336), (480, 640)]),
+)
+
+
 def main():
     torch.set_num_threads(os.cpu_count())
     ssd = tiny_state(False, SEED_S)
     tsd = tiny_state(True, SEED_T)
     STUDENT_KEYS.extend(ssd.keys())
-    for kind, phase, name in (("lb", 0, "lb"), ("dt", 1, "dt1"), ("dt", 2, "dt2"), ("dt", 3, "dt3"),
-                              ("fb", 0, "fb"), ("bd", 0, "bd")):
-        run(kind, phase, tsd, ssd, name)
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "bench"):
+        for kind, phase, name in (("lb", 0, "lb"), ("dt", 1, "dt1"), ("dt", 2, "dt2"), ("dt", 3, "dt3"),
+                                  ("fb", 0, "fb"), ("bd", 0, "bd")):
+            run(kind, phase, tsd, ssd, name)
+    if which in ("all", "geometry"):
+        for kind, phase, name, sizes in GEOMETRY:
+            run(kind, phase, tsd, ssd, name, sizes)
 
 
 if __name__ == "__main__":

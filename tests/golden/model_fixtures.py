@@ -10,6 +10,10 @@ import torch
 
 HERE = Path(__file__).resolve().parent
 KINDS = {"lb": ("lb", 0), "dt1": ("dt", 1), "dt2": ("dt", 2), "dt3": ("dt", 3), "fb": ("fb", 0), "bd": ("bd", 0)}
+# real SUNRGBD geometry (make_golden_model.GEOMETRY): 480x640 at bs 1, mixed [336^2, 480x640] right-padded
+GEOMETRY_KINDS = {"sun_lb": ("lb", 0), "sun_dt1": ("dt", 1), "mix_bd": ("bd", 0), "mix_fb": ("fb", 0),
+                  "mix_dt1": ("dt", 1)}
+ALL_KINDS = {**KINDS, **GEOMETRY_KINDS}
 
 
 def load(name):
@@ -29,7 +33,11 @@ def tiny_weights(teacher: bool, seed: int):
 
 
 def batch(meta, device="cpu"):
-    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import (synthetic_batch,
+                                                                                                synthetic_batch_mixed)
+    if "sizes" in meta:
+        return synthetic_batch_mixed([tuple(hw) for hw in meta["sizes"]], device, seed=meta["seed_data"],
+                                     pixel_dtype=torch.bfloat16, cpu_rng=True)
     return synthetic_batch(meta["B"], device, L=meta["L"], seed=meta["seed_data"], pixel_dtype=torch.bfloat16,
                            cpu_rng=True)
 
@@ -52,7 +60,7 @@ def oracle_grads(name, dtype=torch.float32, with_logits=False):
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import tiny_config
     meta, _ = load(name)
     # with_logits: also return the student logits (detached, [B, L, V]) as a third value
-    kind, phase = KINDS[name]
+    kind, phase = ALL_KINDS[name]
     ssd = {k: v.to(dtype) for k, v in tiny_weights(False, meta["seed_s"]).items()}
     tsd = {k: v.to(dtype) for k, v in tiny_weights(True, meta["seed_t"]).items()} if kind != "bd" else None
     tv, tp, tl = frozen(kind, phase)

@@ -1,30 +1,41 @@
-"""End-to-end KD training_step on the HIP path vs the reference (tiny models, real vocab,
-real 336x336 token layout).
+"""End-to-end KD training_step on the HIP path vs the reference (tiny models, real vocab).
 
-Expected values: the reference's own forward()/training_step driving transformers with the
-same seeded weights (tests/golden/model_*.npz), and the CPU oracle's full gradients
-(oracle/model.py, pinned to the same fixtures on CPU).  The HIP path runs bf16 weights /
-activations with fp32 accumulation; the reference fp32, so:
+Fixtures (tests/golden/model_*.npz): the reference's own forward()/training_step driving
+transformers with the same seeded weights — the 336x336 bench layout (2 tiles, 1,485 image
+tokens, L = 1,536, bs 2) for every module kind, and real SUNRGBD geometry (SURVEY KAT 9):
+480x640 (5 tiles, 2,929 image tokens, L = 2,980) at bs 1 for LoCa / DT phase 1, and a mixed,
+right-padded [336x336, 480x640] batch (-100 labels on the pads, NT-Xent over the 7 real
+tiles) for BD / FB / DT phase 1.  The HIP path stores bf16 with fp32 accumulation and fp32
+residual streams; the reference runs fp32, so:
   every loss term   |d| <= 1e-4 + 1e-3 |ref| (north_star): total, KD term, student CE,
                     teacher CE, NT-Xent — each against the reference's own value
-  student logits    per-row logsumexp at the north-star tolerance; sampled raw logits
-                    |d| <= 2^-7 |ref| + 0.08 rms(ref) (bf16 logits: a few ulps)
-  grad total norm   |d| <= 1e-3 |ref| + 1.25 |d_bf16|, d_bf16 = the same oracle run in bf16
-                    on the CPU (torch autograd).  A plain bf16 run of the reference's
-                    arithmetic already misses 1e-3 (dt1: +3.4 %, lb: +0.25 %), so the HIP
-                    path is held to that bar, not below it
-  per-param grads   cosine(HIP, oracle) >= 0.99 and |norm ratio - 1| <= 5e-2 for every
-                    parameter whose grad norm is >= 1e-3 x the largest one
+  student logits    per-row logsumexp at the north-star tolerance; on the sampled raw
+                    logits the fraction within the north-star tolerance is at least the bf16
+                    floor's (the same oracle run in bf16, tests/golden/bf16_floor.json) and
+                    the largest |d| at most 1.5x the floor's: raw logits of ~0.2 have a bf16
+                    half-ulp of ~5e-4 > 1e-4 + 1e-3 |ref|
+  grad total norm   |d| <= 1e-3 |ref| (north_star) for the kinds in GRAD_NORTH_STAR; the
+                    others (ViT training through NT-Xent of near-identical pooled tile
+                    features, dt1 / fb / mix_*: ill-conditioned on random weights)
+                    |d| <= 1e-3 |ref| + |d_bf16|, the bf16 floor's own miss
+  per-param grads   336x336 kinds: cosine(HIP, fp32 oracle) >= 0.99 and norm within 5 % for
+                    every parameter whose grad norm is >= 1e-3 x the largest; SUNRGBD kinds:
+                    norm within 5 % of the reference's recorded per-parameter norms
 """
+import json
 import math
+from pathlib import Path
 
 import numpy as np
 import pytest
 import torch
 
-from model_fixtures import KINDS, batch, frozen, grad_total_norm, load, oracle_grads
+from model_fixtures import ALL_KINDS, GEOMETRY_KINDS, batch, frozen, load, oracle_grads
 
 ATOL, RTOL = 1e-4, 1e-3   # north_star
+FLOOR = json.loads((Path(__file__).resolve().parent / "golden" / "bf16_floor.json").read_text())
+# kinds whose gradient total norm meets the north-star 1e-3 (profiles/r03/parity.json)
+GRAD_NORTH_STAR = {"lb", "dt2", "dt3", "bd", "sun_lb"}
 
 
 def _grad(P, name):
@@ -58,10 +69,10 @@ def _module(kind, phase):
     return K.LlavaOnevisionModule("tiny-student")
 
 
-@pytest.mark.parametrize("name", list(KINDS))
+@pytest.mark.parametrize("name", list(ALL_KINDS))
 def test_training_step_matches_reference(name, dev):
     meta, exp = load(name)
-    kind, phase = KINDS[name]
+    kind, phase = ALL_KINDS[name]
     m = _module(kind, phase)
     m.keep_logits = True
     b = batch(meta, dev)
@@ -88,30 +99,39 @@ def test_training_step_matches_reference(name, dev):
         f"logit lse: max |d| {np.abs(lse - ref_lse).max():.3e}"
     got_rows = s3[:, exp["logit_rows"].tolist(), ::int(exp["logit_col_stride"])].float().cpu().numpy()
     ref_rows = exp["s_logit_rows"]
-    bound = 2.0 ** -7 * np.abs(ref_rows) + 0.08 * np.sqrt((ref_rows ** 2).mean())
-    assert bool((np.abs(got_rows - ref_rows) <= bound).all()), f"logits: max |d| {np.abs(got_rows - ref_rows).max():.3e}"
+    err = np.abs(got_rows - ref_rows)
+    frac = float((err <= ATOL + RTOL * np.abs(ref_rows)).mean())
+    fl = FLOOR[name]
+    assert frac >= fl["logit_frac_within_north_star"] - 0.01, (frac, fl)
+    assert float(err.max()) <= 1.5 * fl["logit_max_abs"], (float(err.max()), fl)
     m.last_logits = None
-    tot, ograds = oracle_grads(name)
     P = m.student_model.P
     # the gradient's total norm (over the reference's parameters; the conv weight's padded tail excluded)
-    gn = math.sqrt(sum(float(_grad(P, str(n)).double().pow(2).sum()) for n in exp["grad_names"]))
-    ref_gn = float(exp["grad_total_norm"])
-    if abs(gn - ref_gn) > RTOL * ref_gn:
-        _, bgr = oracle_grads(name, torch.bfloat16)
-        d_bf16 = abs(grad_total_norm(bgr) - ref_gn)
-        assert abs(gn - ref_gn) <= RTOL * ref_gn + 1.25 * d_bf16, \
-            f"grad total norm {gn:.6g} vs reference {ref_gn:.6g} (bf16 oracle off by {d_bf16:.4g})"
     names = [str(n) for n in exp["grad_names"]]
-    gmax = max(float(g.norm()) for g in ograds.values())
-    for n in names:
-        ref = ograds[n].double().reshape(-1)
-        got = _grad(P, n).double().cpu().reshape(-1)
-        rn = float(ref.norm())
-        if rn < 1e-3 * gmax:
-            continue
-        cos = float((got @ ref) / (got.norm() * ref.norm() + 1e-30))
-        assert cos >= 0.99, f"{n}: cosine {cos:.4f}"
-        assert abs(float(got.norm()) / rn - 1) <= 5e-2, f"{n}: norm {float(got.norm()):.4g} vs {rn:.4g}"
+    gn = math.sqrt(sum(float(_grad(P, n).double().pow(2).sum()) for n in names))
+    ref_gn = float(exp["grad_total_norm"])
+    d_bf16 = abs(fl["grad_total_norm"] - ref_gn)
+    bound = RTOL * ref_gn + (0.0 if name in GRAD_NORTH_STAR else d_bf16)
+    assert abs(gn - ref_gn) <= bound, f"grad total norm {gn:.6g} vs reference {ref_gn:.6g} (bf16 floor off by {d_bf16:.4g})"
+    if name in GEOMETRY_KINDS:
+        gmax = float(np.max(exp["grad_norms"]))
+        for n, rn in zip(names, exp["grad_norms"]):
+            if rn < 1e-3 * gmax:
+                continue
+            got = float(_grad(P, n).double().norm())
+            assert abs(got / float(rn) - 1) <= 5e-2, f"{n}: norm {got:.4g} vs {float(rn):.4g}"
+    else:
+        _, ograds = oracle_grads(name)
+        gmax = max(float(g.norm()) for g in ograds.values())
+        for n in names:
+            ref = ograds[n].double().reshape(-1)
+            got = _grad(P, n).double().cpu().reshape(-1)
+            rn = float(ref.norm())
+            if rn < 1e-3 * gmax:
+                continue
+            cos = float((got @ ref) / (got.norm() * ref.norm() + 1e-30))
+            assert cos >= 0.99, f"{n}: cosine {cos:.4f}"
+            assert abs(float(got.norm()) / rn - 1) <= 5e-2, f"{n}: norm {float(got.norm()):.4g} vs {rn:.4g}"
     # frozen regions received no gradient
     tv, tp, tl = frozen(kind, phase)
     lo_l = P.regions["language"][0]

@@ -6,7 +6,9 @@ import pytest
 from model_fixtures import KINDS, load, oracle_grads
 
 
-@pytest.mark.parametrize("name", list(KINDS))
+# every 336x336 fixture, and two of the SUNRGBD-geometry ones (480x640 LoCa at bs 1; the mixed,
+# right-padded [336^2, 480x640] batch through NT-Xent over its 7 real tiles)
+@pytest.mark.parametrize("name", list(KINDS) + ["sun_lb", "mix_fb"])
 def test_oracle_step_matches_reference(name):
     meta, exp = load(name)
     total, grads = oracle_grads(name)

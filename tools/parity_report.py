@@ -31,10 +31,10 @@ def _d(got, ref):
 def measure(name, dev):
     import numpy as np
     import torch
-    from model_fixtures import KINDS, batch, load
+    from model_fixtures import ALL_KINDS, batch, load
     from test_kd_step_gpu import _module
     meta, exp = load(name)
-    kind, phase = KINDS[name]
+    kind, phase = ALL_KINDS[name]
     m = _module(kind, phase)
     m.keep_logits = True
     b = batch(meta, dev)
