@@ -292,6 +292,8 @@ int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
  * torch.optim.Optimizer.zero_grad(set_to_none=False) that Lightning calls after each step). */
 int kd_zero(void* ptr, uint64_t bytes, void* stream);
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* y (fp32) = x (bf16), n elements (the bf16 gradient all-reduce buckets, dp.GradSync). */
+int kd_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);
 /* fp8 row quantisation (the fp8 GEMM's operands): per row r of x (bf16 [R][K], K % 16 == 0)
  * scale[r] = amax_r / 448 (1 for an all-zero row) and q[r][k] = e4m3(clamp(x[r][k] * 448 /
  * amax_r, +-448)), round to nearest even (OCP e4m3fn bytes). */

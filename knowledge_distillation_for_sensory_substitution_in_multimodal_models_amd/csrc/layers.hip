@@ -718,6 +718,10 @@ __global__ void k_cast_f32_bf16(const float* __restrict__ x, bf16* __restrict__ 
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = (bf16)x[i];
 }
 
+__global__ void k_cast_bf16_f32(const bf16* __restrict__ x, float* __restrict__ y, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = (float)x[i];
+}
+
 // src[b*L + l] for inputs_embeds assembly: the j-th image token of sample b takes
 // map[b*map_ld + j] (a packed feature row, or -1 for image_newline); text tokens -2.
 // Counts that differ from map_len[b] flag err (HF raises "Image features and image tokens
@@ -1017,6 +1021,13 @@ int launch_scalar_mul(const float* a, const float* b, float* out, int n, void* s
     if (n == 0) return KD_OK;
     hipLaunchKernelGGL(k_scalar_mul, dim3(1), dim3(n), 0, as_stream(stream), a, b, out, n);
     KD_LAUNCH_CHECK("k_scalar_mul");
+    return KD_OK;
+}
+
+int launch_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream) {
+    KD_CHECK_ARG(x && y, "cast: null pointer");
+    hipLaunchKernelGGL(k_cast_bf16_f32, dim3(grid_for(n, 256, 16384)), dim3(256), 0, as_stream(stream), (const bf16*)x, y, n);
+    KD_LAUNCH_CHECK("k_cast_bf16_f32");
     return KD_OK;
 }
 

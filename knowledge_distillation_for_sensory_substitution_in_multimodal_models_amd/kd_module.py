@@ -217,7 +217,8 @@ class _KDBase(_Base):
 
     def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1,
                  seed_teacher: int = 1, seed_student: int = 2, state_dict=None, loss_group_size: int | None = None,
-                 accumulate_grad_batches: int | None = None, teacher_fp8: bool | str = False, **_ignored):
+                 accumulate_grad_batches: int | None = None, teacher_fp8: bool | str = False,
+                 grad_comm_dtype=None, **_ignored):
         super().__init__()
         self.phase = phase
         self.learning_rate = learning_rate
@@ -279,7 +280,8 @@ class _KDBase(_Base):
                 self._dist.broadcast(self.teacher_model.P.flat, src=0)
             self._dist.broadcast(self.student_model.P.flat, src=0)
             self.student_model.P.master.copy_(self.student_model.P.flat.float())
-            self._gsync = GradSync(self._dist, self.student_model.P.grad)
+            # grad_comm_dtype=torch.bfloat16: bf16 all-reduce buckets (half the xGMI bytes; dp.py)
+            self._gsync = GradSync(self._dist, self.student_model.P.grad, comm_dtype=grad_comm_dtype)
         # fp8 (e4m3) teacher weights, quantised once after the broadcast (BASELINE config c4;
         # the reference loads the teacher fp16, DT:43-48)
         # teacher_fp8: False, True (= "all") or a modeling.FP8_FAMILIES policy name ("lm", "lm_mlp", ...)

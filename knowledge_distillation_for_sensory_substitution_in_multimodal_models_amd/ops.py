@@ -513,6 +513,11 @@ def cast_f32_bf16(x, y):
     return y
 
 
+def cast_bf16_f32(x, y):
+    NV.call("kd_cast_bf16_f32", x.data_ptr(), y.data_ptr(), x.numel(), _stream())
+    return y
+
+
 def image_src_map(ids, image_token: int, maps, map_len, err):
     """ids [B, L] int64 -> src int32 [B*L] (see include/kdstep.h kd_image_src_map)."""
     B, L = ids.shape

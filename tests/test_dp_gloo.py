@@ -37,7 +37,7 @@ def _layout(train_vision, train_language):
     return cfg, offsets, numel, lo, hi
 
 
-def _worker(rank, world, port, q, train_vision, train_language, k_micro, early_step):
+def _worker(rank, world, port, q, train_vision, train_language, k_micro, early_step, comm_bf16=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.dp import GradSync
@@ -45,7 +45,7 @@ def _worker(rank, world, port, q, train_vision, train_language, k_micro, early_s
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg, offsets, numel, lo, hi = _layout(train_vision, train_language)
     grad = torch.zeros(numel)
-    gs = GradSync(dist, grad, bucket_bytes=64 << 10)
+    gs = GradSync(dist, grad, bucket_bytes=64 << 10, comm_dtype=torch.bfloat16 if comm_bf16 else None)
     g = torch.Generator().manual_seed(100 + rank)
     local = torch.zeros(numel)
     n_back = k_micro - 1 if early_step else k_micro
@@ -74,14 +74,16 @@ def _worker(rank, world, port, q, train_vision, train_language, k_micro, early_s
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("train_vision,train_language,k_micro,early_step",
-                         [(True, True, 1, False), (False, True, 3, False), (True, False, 2, False),
-                          (True, True, 3, True)])
-def test_accumulated_grads_reduced_once_at_the_boundary(train_vision, train_language, k_micro, early_step):
+@pytest.mark.parametrize("train_vision,train_language,k_micro,early_step,comm_bf16",
+                         [(True, True, 1, False, False), (False, True, 3, False, False), (True, False, 2, False, False),
+                          (True, True, 3, True, False), (True, True, 2, False, True)])
+def test_accumulated_grads_reduced_once_at_the_boundary(train_vision, train_language, k_micro, early_step, comm_bf16):
+    """comm_bf16: bf16 buckets (GradSync comm_dtype): the mean within bf16 rounding."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (hash((train_vision, train_language, k_micro, early_step)) % 1000)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, train_vision, train_language, k_micro, early_step))
+    port = 29500 + (hash((train_vision, train_language, k_micro, early_step, comm_bf16)) % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, train_vision, train_language, k_micro, early_step,
+                                               comm_bf16))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -94,5 +96,11 @@ def test_accumulated_grads_reduced_once_at_the_boundary(train_vision, train_lang
     mean = (res[0][0] + res[1][0]) / 2
     for r in (0, 1):
         local, after, _ = res[r]
-        assert torch.allclose(after[lo:hi], mean[lo:hi], atol=1e-6)
+        if comm_bf16:   # each rank's sum rounded to bf16, then the bf16 sum: ~3 half-ulps of the result
+            err = (after[lo:hi] - mean[lo:hi]).abs()
+            scale = res[0][0][lo:hi].abs() + res[1][0][lo:hi].abs()
+            assert bool((err <= 2.0 ** -8 * scale + 1e-30).all()), float((err / (scale + 1e-30)).max())
+            assert torch.equal(res[0][1][lo:hi], res[1][1][lo:hi])   # replicas agree exactly
+        else:
+            assert torch.allclose(after[lo:hi], mean[lo:hi], atol=1e-6)
         assert float(after[:lo].abs().sum()) == 0.0 and float(after[hi:].abs().sum()) == 0.0

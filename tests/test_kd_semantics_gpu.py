@@ -309,7 +309,7 @@ def close(a, b):   # atomics in the embedding / bias gradients: not bit-exact ru
 
 ref = run(K.LogitBasedKD("tiny-student", "tiny-teacher"))
 dist.init_process_group("nccl", device_id=dev)
-m = K.LogitBasedKD("tiny-student", "tiny-teacher")
+m = K.LogitBasedKD("tiny-student", "tiny-teacher", grad_comm_dtype={comm})
 assert m._gsync is not None and m._gsync.avg_in_collective
 m._gsync.bucket_bytes = 1 << 16          # several buckets, launched during the backward
 got = run(m)
@@ -321,13 +321,16 @@ print("rccl ok")
 '''
 
 
-def test_rccl_world1_steps_equal_local(tmp_path):
+@pytest.mark.parametrize("comm", ["None", "torch.bfloat16"])
+def test_rccl_world1_steps_equal_local(comm, tmp_path):
     """The DP path on RCCL (backend "nccl": async bucketed AVG all-reduces launched on the
     student stream during the backward, awaited on the student stream before AdamW) on a
     one-rank group: three full steps give the same weight update and gradients as the module
-    without a process group (the mean over one rank is the identity)."""
+    without a process group (the mean over one rank is the identity) — with fp32 buckets, and
+    with bf16 buckets (grad_comm_dtype: the gradient rounded to bf16 on the way, the update
+    within the same cosine / 2e-3 norm tolerance)."""
     script = tmp_path / "child.py"
-    script.write_text(_RCCL_CHILD.format(repo=str(REPO), golden=str(REPO / "tests" / "golden")))
+    script.write_text(_RCCL_CHILD.format(repo=str(REPO), golden=str(REPO / "tests" / "golden"), comm=comm))
     env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(29900 + os.getpid() % 90))
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=600)
