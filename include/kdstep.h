@@ -414,8 +414,10 @@ int kd_model_set_trainable(kd_model* m, int vision, int projector, int language)
  * stream every layer adds into: SigLIP encoder, Qwen2 decoder) in fp32 — the residual adds
  * in the o_proj / fc2 / down_proj GEMM epilogues in fp32, the norms read fp32 — instead of
  * rounding it to bf16 after every add (the reference's own precision: fp32 in LB / FB, the
- * residual adds of fp16 autocast in DT, which run in fp32).  Default off; not with fp8
- * weights.  Changes the forward / backward workspace sizes. */
+ * residual adds of fp16 autocast in DT, which run in fp32).  Default off.  The fp8 GEMM adds
+ * a bf16 residual only: a tower whose residual linears (SigLIP out_proj / fc2, Qwen2 o_proj /
+ * down_proj) run in fp8 (kd_model_set_fp8_families) keeps a bf16 stream.  Changes the
+ * forward / backward workspace sizes. */
 int kd_model_set_residual_f32(kd_model* m, int vision, int language);
 
 /* fp8 teacher (BASELINE config c4): e4m3 copies of every linear weight the forward's GEMMs

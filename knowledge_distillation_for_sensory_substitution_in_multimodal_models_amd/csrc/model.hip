@@ -1045,9 +1045,16 @@ int kd_model_set_trainable(kd_model* m, int vision, int projector, int language)
     return KD_OK;
 }
 
+// the fp8 GEMM epilogue adds a bf16 residual only: a tower whose residual-adding linears (SigLIP
+// out_proj / fc2, Qwen2 o_proj / down_proj) run in fp8 keeps a bf16 residual stream
+static bool fp8_stream_ok(bool f8, int fam, int rf32_v, int rf32_t) {
+    return !f8 || ((!rf32_v || !(fam & KD_FP8_VISION)) && (!rf32_t || !(fam & (KD_FP8_LM_ATTN | KD_FP8_LM_MLP))));
+}
+
 int kd_model_set_residual_f32(kd_model* m, int vision, int language) {
     KD_CHECK_ARG(m, "kd_model_set_residual_f32: null model");
-    KD_CHECK_ARG(!m->f8q || !(vision || language), "kd_model_set_residual_f32: not with fp8 weights bound");
+    KD_CHECK_ARG(fp8_stream_ok(m->f8q, m->f8_families, vision, language),
+                 "kd_model_set_residual_f32: the tower's residual linears run in fp8 (bf16 residual only)");
     m->rf32_v = vision != 0;
     m->rf32_t = language != 0;
     return KD_OK;
@@ -1072,6 +1079,8 @@ int kd_model_quantize_fp8(const kd_model* m, void* q, float* scales, void* strea
 int kd_model_set_fp8_families(kd_model* m, int families) {
     KD_CHECK_ARG(m, "kd_model_set_fp8_families: null model");
     KD_CHECK_ARG((families & ~KD_FP8_ALL) == 0, "kd_model_set_fp8_families: unknown family bits");
+    KD_CHECK_ARG(fp8_stream_ok(m->f8q, families, m->rf32_v, m->rf32_t),
+                 "kd_model_set_fp8_families: an fp32 residual stream's residual linears cannot run in fp8");
     m->f8_families = families;
     return KD_OK;
 }
@@ -1081,7 +1090,8 @@ int kd_model_set_fp8(kd_model* m, const void* q, const float* scales) {
     KD_CHECK_ARG((q == nullptr) == (scales == nullptr), "kd_model_set_fp8: q and scales go together");
     KD_CHECK_ARG(!q || !m->g, "kd_model_set_fp8: fp8 weights are for a frozen (no-grad) model, e.g. the teacher");
     KD_CHECK_ALIGN(q, 16, "kd_model_set_fp8: q must be 16-B aligned");
-    KD_CHECK_ARG(!q || !(m->rf32_v || m->rf32_t), "kd_model_set_fp8: the fp8 path keeps bf16 residual streams");
+    KD_CHECK_ARG(fp8_stream_ok(q != nullptr, m->f8_families, m->rf32_v, m->rf32_t),
+                 "kd_model_set_fp8: an fp32 residual stream's residual linears cannot run in fp8");
     m->f8q = (const uint8_t*)q;
     m->f8s = scales;
     return KD_OK;

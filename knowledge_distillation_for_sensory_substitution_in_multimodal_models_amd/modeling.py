@@ -389,12 +389,15 @@ class LlavaOnevisionModel:
                 self.P.grad.data_ptr() if trainable else None, C.byref(h))
         self._h = h
         self.fp8 = False
-        # the trainable model (the student) keeps both residual streams in fp32, as the
-        # reference's fp32 / autocast step does: with a bf16 stream the rounding after every
-        # residual add moved the tiny fixtures' gradient norm by +0.12 % (tools/grad_bias_study.py)
+        # fp32 residual streams (kd_model_set_residual_f32), as the reference's fp32 / autocast
+        # step keeps them: the student both towers; the teacher its SigLIP tower (cheap: 1152
+        # wide; its pooled post-LN features feed NT-Xent) but not its 3584-wide Qwen2 stream.
+        # With bf16 streams the tiny fixtures' pooled ViT features sat 1.7-2.0 % from the fp32
+        # reference, with fp32 streams 0.15-0.17 % (tools/vit_feature_check.py), and the student
+        # rounding after every residual add moved the gradient norm by +0.12 % (tools/grad_bias_study.py)
         self.residual_f32 = (False, False)
-        if trainable:
-            self.set_residual_f32(True, True)
+        self.fp8_families = 0
+        self.set_residual_f32(*self._default_streams())
 
     def set_residual_f32(self, vision: bool, language: bool):
         """fp32 residual streams of the SigLIP / Qwen2 towers (kd_model_set_residual_f32)."""
@@ -460,6 +463,12 @@ class LlavaOnevisionModel:
         if self.P.trainable:
             raise RuntimeError("fp8 weights are for the frozen teacher (no grad buffer)")
         fam = FP8_FAMILIES[families] if isinstance(families, str) else int(families)
+        NV.call("kd_model_set_fp8", self._h, None, None)   # unbind while the policy changes
+        # the fp8 GEMM adds a bf16 residual only: a tower whose residual linears go fp8 keeps a
+        # bf16 stream (the defaults otherwise: _default_streams)
+        v, t = self._default_streams()
+        self.set_residual_f32(v and not fam & NV.KD_FP8_VISION,
+                              t and not fam & (NV.KD_FP8_LM_ATTN | NV.KD_FP8_LM_MLP))
         NV.call("kd_model_set_fp8_families", self._h, fam)
         self.fp8_families = fam
         lib = NV.lib()
@@ -474,8 +483,14 @@ class LlavaOnevisionModel:
     def disable_fp8(self):
         NV.call("kd_model_set_fp8", self._h, None, None)
         self._f8q = self._f8s = None
+        self.set_residual_f32(*self._default_streams())
         self._ws = {}
         self.fp8 = False
+
+    def _default_streams(self):
+        """(vision, language) fp32 residual streams: both for the trainable student, the
+        SigLIP tower only for a frozen teacher."""
+        return True, bool(self.P.trainable)
 
     def _workspace(self, key, nbytes):
         """One cached workspace per call shape: a save=1 forward's workspace holds the

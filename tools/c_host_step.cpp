@@ -135,6 +135,7 @@ int main(int argc, char** argv) {
     }
     kd_model *teacher = nullptr, *student = nullptr;
     KD(kd_model_create(&tc, tw, nullptr, &teacher));
+    KD(kd_model_set_residual_f32(teacher, 1, 0));   // the drop-in module's teacher: fp32 SigLIP stream
     KD(kd_model_create(&sc, sw, grad, &student));
     KD(kd_model_set_residual_f32(student, 1, 1));   // fp32 residual streams, as the drop-in module's student
 
