@@ -282,6 +282,8 @@ def main():
                     help="one stream: student forward and the weight gradients on the main stream (profiling)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
     ap.add_argument("--teacher-bf16", action="store_true", help="c4 with the bf16 teacher instead of fp8")
+    ap.add_argument("--fp8-families", default=None,
+                    help="c4: which teacher linear families run fp8 (modeling.FP8_FAMILIES: all, lm, lm_body, lm_mlp)")
     ap.add_argument("--no-teacher-rate", action="store_true",
                     help="skip the teacher-forward rate pass (profiling runs: its launches would enter the "
                          "roofline kernel's rocprof average)")
@@ -300,7 +302,7 @@ def main():
     B = a.batch or cfg["batch"]
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
-    teacher_fp8 = bool(cfg.get("teacher_fp8")) and not a.teacher_bf16
+    teacher_fp8 = False if a.teacher_bf16 else (a.fp8_families or cfg.get("teacher_fp8") or False)
     m, opt = build(cfg, dev, teacher_fp8=teacher_fp8)
     m.concurrent_student = not a.serial
     m.student_model.wlane.serial = a.serial   # --serial: one stream for everything (profiling)
@@ -443,7 +445,7 @@ def main():
         "cpu_baseline": None,
     }
     if teacher_fp8:
-        out["dtype"] = "bf16 (student, loss) + fp8 e4m3 teacher linears"
+        out["dtype"] = f"bf16 (student, loss) + fp8 e4m3 teacher linears ({m.teacher_fp8})"
         if rank == 0:
             out["fp8_teacher_delta"] = fp8_teacher_delta(m, batches[0])
     if rank == 0 and not a.no_delta:

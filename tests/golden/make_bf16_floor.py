@@ -6,7 +6,7 @@ For every tiny end-to-end fixture (tests/golden/model_*.npz, the reference's own
 fp32) the CPU oracle (oracle/model.py, pinned to those fixtures in fp32) is run again with
 bf16 weights and activations (torch autograd on the CPU): how far a plain bf16 run of the
 reference's arithmetic lands from the fp32 reference.  Recorded per kind, in
-tests/golden/bf16_floor.json: the gradient's total norm, and on the fixture's sampled
+tests/golden/bf16_floor.json: the step's total loss, the gradient's total norm, and on the fixture's sampled
 student-logit rows the fraction of elements within the north-star |d| <= 1e-4 + 1e-3 |ref|
 and the largest |d|.  tests/test_kd_step_gpu.py holds the HIP path (bf16 storage, fp32
 accumulation) to this floor where the north-star tolerance is below bf16 resolution (raw
@@ -35,13 +35,14 @@ ATOL, RTOL = 1e-4, 1e-3
 
 def floor(name):
     _, exp = load(name)
-    _, g, logits = oracle_grads(name, torch.bfloat16, with_logits=True)
+    total, g, logits = oracle_grads(name, torch.bfloat16, with_logits=True)
     rows = exp["logit_rows"].tolist()
     st = int(exp["logit_col_stride"])
     got = logits[:, rows, ::st].float().numpy()
     ref = exp["s_logit_rows"]
     err = np.abs(got - ref)
-    return dict(grad_total_norm=grad_total_norm(g), ref_grad_total_norm=float(exp["grad_total_norm"]),
+    return dict(total=float(total), ref_total=float(exp["total"]),
+                grad_total_norm=grad_total_norm(g), ref_grad_total_norm=float(exp["grad_total_norm"]),
                 logit_frac_within_north_star=float((err <= ATOL + RTOL * np.abs(ref)).mean()),
                 logit_max_abs=float(err.max()), logit_rms_ref=float(math.sqrt(float((ref ** 2).mean()))))
 

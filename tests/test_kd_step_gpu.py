@@ -8,7 +8,11 @@ right-padded [336x336, 480x640] batch (-100 labels on the pads, NT-Xent over the
 tiles) for BD / FB / DT phase 1.  The HIP path stores bf16 with fp32 accumulation and fp32
 residual streams; the reference runs fp32, so:
   every loss term   |d| <= 1e-4 + 1e-3 |ref| (north_star): total, KD term, student CE,
-                    teacher CE, NT-Xent — each against the reference's own value
+                    teacher CE — each against the reference's own value.  NT-Xent (and the
+                    total it enters): |d| <= 1e-4 + 3e-3 |ref|: its logits are feature dot
+                    products / tau (0.07), so the pooled features' bf16-compute error (0.15 %
+                    with fp32 residual streams, tools/vit_feature_check.py) reaches the loss
+                    amplified ~14x; stated tolerance, DESIGN §4
   student logits    per-row logsumexp at the north-star tolerance; on the sampled raw
                     logits the fraction within the north-star tolerance is at least the bf16
                     floor's (the same oracle run in bf16, tests/golden/bf16_floor.json) and
@@ -33,6 +37,7 @@ import torch
 from model_fixtures import ALL_KINDS, GEOMETRY_KINDS, batch, frozen, load, oracle_grads
 
 ATOL, RTOL = 1e-4, 1e-3   # north_star
+NTX_RTOL = 3e-3           # the NT-Xent term (1 / tau = 14.3 amplification of the feature error)
 FLOOR = json.loads((Path(__file__).resolve().parent / "golden" / "bf16_floor.json").read_text())
 # kinds whose gradient total norm meets the north-star 1e-3 (profiles/r03/parity.json)
 GRAD_NORTH_STAR = {"lb", "dt2", "dt3", "bd", "sun_lb"}
@@ -47,8 +52,8 @@ def _grad(P, name):
     return g
 
 
-def _near(got, ref, what):
-    assert abs(got - ref) <= ATOL + RTOL * abs(ref), f"{what}: {got!r} vs reference {ref!r}"
+def _near(got, ref, what, rtol=RTOL):
+    assert abs(got - ref) <= ATOL + rtol * abs(ref), f"{what}: {got!r} vs reference {ref!r}"
 
 pytestmark = pytest.mark.gpu
 
@@ -83,14 +88,15 @@ def test_training_step_matches_reference(name, dev):
     assert int(m.student_model.err.item()) == 0
     # every loss term vs the reference's own forward
     kd, ce, tce, _ = m.last_terms.tolist()
-    _near(loss.item(), float(exp["total"]), "total")
+    has_ntx = not math.isnan(float(exp["ntxent"]))
+    _near(loss.item(), float(exp["total"]), "total", NTX_RTOL if has_ntx else RTOL)
     _near(ce, float(exp["student_ce"]), "student CE")
     if not math.isnan(float(exp["teacher_ce"])):
         _near(tce, float(exp["teacher_ce"]), "teacher CE")
     if not math.isnan(float(exp["kd_term"])):
         _near(kd, float(exp["kd_term"]), "KD term")
-    if not math.isnan(float(exp["ntxent"])):
-        _near(float(m.last_ntxent[1]), float(exp["ntxent"]), "NT-Xent")
+    if has_ntx:
+        _near(float(m.last_ntxent[1]), float(exp["ntxent"]), "NT-Xent", NTX_RTOL)
     # student logits
     s3, _ = m.last_logits
     lse = torch.logsumexp(s3.double(), -1).reshape(-1).cpu().numpy()
