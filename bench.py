@@ -12,8 +12,9 @@ architectures (no checkpoints are reachable offline).
 
 Configs (BASELINE.json): c1 = logit-based LoCa (T=1) bs 4 per GPU [default];
 c2 = feature-based (NT-Xent + KL) bs 8 per GPU; c3 = double-trouble phase 2 (LoCa, ViT
-frozen) bs 8 per GPU; c4 = double-trouble phase 3 bs 8 per GPU with the fp8 (e4m3) teacher
-(per-channel weight / per-token activation scales, fp8 MFMA GEMMs; --teacher-bf16 for bf16).
+frozen) bs 8 per GPU; c4 = double-trouble phase 3 bs 8 per GPU with the fp8 (e4m3) teacher: its Qwen2 MLPs
+(gate|up, down: 70 % of the teacher FLOPs) on fp8 MFMA GEMMs with per-channel weight /
+per-token activation scales (--fp8-families all|lm|lm_body|lm_mlp; --teacher-bf16 for bf16).
 Per-GPU work is fixed as N grows (weak scaling); value = samples of all ranks / max time.
 """
 from __future__ import annotations
@@ -37,8 +38,8 @@ CONFIGS = {
     "c1": dict(kind="lb", phase=0, batch=4, desc="logit-based KD (LoCa, T=1), 7B->0.5B, 336x336"),
     "c2": dict(kind="fb", phase=0, batch=8, desc="feature-based KD (NT-Xent + KL), 7B->0.5B, 336x336"),
     "c3": dict(kind="dt", phase=2, batch=8, desc="double-trouble phase 2 (LoCa + CE, ViT frozen)"),
-    "c4": dict(kind="dt", phase=3, batch=8, teacher_fp8=True,
-               desc="double-trouble phase 3 (0.8 LoCa + CE), fp8 (e4m3) teacher"),
+    "c4": dict(kind="dt", phase=3, batch=8, teacher_fp8="lm_mlp",
+               desc="double-trouble phase 3 (0.8 LoCa + CE), fp8 (e4m3) teacher MLPs"),
 }
 
 # algorithmic FLOPs per sample, L = 1536, 2 tiles
@@ -262,7 +263,9 @@ def fp8_teacher_delta(m, batch):
     names = ("kd_term", "student_ce", "teacher_ce", "total")
     return dict(teacher_logits_rel_l2=round(rel, 5), teacher_logits_cosine=round(cos, 6),
                 terms={n: dict(fp8=a, bf16=b, rel=abs(a - b) / abs(b) if b else None) for n, a, b in zip(names, tf, tb)},
-                tolerance="tests/test_fp8_gpu.py: rel-L2 <= 0.15, cosine >= 0.99, KD term rel <= 0.15")
+                tolerance="stated for the lm_mlp policy at full depth (DESIGN §4): teacher-logit rel-L2 <= 0.27, "
+                          "cosine >= 0.96, KD term rel <= 0.01; tests/test_fp8_gpu.py at depth 8: rel-L2 <= 0.18, "
+                          "cosine >= 0.98")
 
 
 def main():

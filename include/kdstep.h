@@ -178,7 +178,22 @@ typedef struct {
     const float* b_scale;     /* fp8 path: per-row scale of B [N] (per output channel)           */
     int32_t residual_dtype;   /* kd_dtype of residual: KD_DTYPE_BF16 (0) or KD_DTYPE_F32 (an fp32
                                  residual stream; then C must be fp32 and act NONE; bf16 path only) */
+    const struct kd_qkv_scatter* qkv;   /* optional: q|k|v scatter epilogue (below); C unused */
 } kd_gemm_desc;
+/* q|k|v scatter epilogue of a fused projection GEMM (the attention input of SigLIP / Qwen2:
+ * HF5 siglip :250-270, qwen2 :80-110 view / transpose / apply_rotary_pos_emb): the output tile,
+ * bias added and rounded to bf16 as the plain GEMM's C, is written straight to head-major
+ * q [B, nq, S, hdp], k / v [B, nkv, S, hdp] (rows m = b * S + s; columns [q heads | k heads |
+ * v heads] of hd), RoPE rotate_half applied to q and k when cos_t / sin_t ([S, hd/2] fp32) are
+ * given, the [hd, hdp) padding zeroed — kd_qkv_split's result bit for bit, without C's round
+ * trip through HBM.  K-major bf16 operands, no activation / residual / aux / accumulate /
+ * split-K, the tiled kernels' shapes (M, N >= 128, M * N >= 2^20); hd % 8 == 0; with RoPE
+ * hd % 16 == 0 and 128 % hd == 0. */
+typedef struct kd_qkv_scatter {
+    void* q; void* k; void* v;
+    const float* cos_t; const float* sin_t;
+    int32_t S, nq, nkv, hd, hdp;
+} kd_qkv_scatter;
 /* fp8 path (ab_dtype = KD_DTYPE_FP8_E4M3; the fp8 teacher of BASELINE config c4): A and B are
  * OCP e4m3 bytes, both K-major, K % 16 == 0, lda / ldb % 16 == 0 (bytes = elements), 16-B
  * aligned; C = epilogue(alpha * a_scale[m] * b_scale[n] * sum_k qa[m][k] qb[n][k]) with the

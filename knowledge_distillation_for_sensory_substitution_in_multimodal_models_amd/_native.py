@@ -73,7 +73,13 @@ class KdGemmDesc(C.Structure):
         ("split_k", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64),
         ("ab_dtype", C.c_int32), ("a_scale", C.c_void_p), ("b_scale", C.c_void_p),
         ("residual_dtype", C.c_int32),
+        ("qkv", C.c_void_p),
     ]
+
+
+class KdQkvScatter(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("k", C.c_void_p), ("v", C.c_void_p), ("cos_t", C.c_void_p), ("sin_t", C.c_void_p),
+                ("S", C.c_int32), ("nq", C.c_int32), ("nkv", C.c_int32), ("hd", C.c_int32), ("hdp", C.c_int32)]
 
 
 class KdAttnDesc(C.Structure):

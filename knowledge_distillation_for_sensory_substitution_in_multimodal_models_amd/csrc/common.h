@@ -113,4 +113,10 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// RoPE rotate_half pair (HF5 qwen2 apply_rotary_pos_emb), the one arithmetic shared by
+// k_qkv_split and the q|k|v scatter GEMM epilogue: first half x1 -> x1 cos - x2 sin, second
+// half x2 -> x2 cos + x1 sin (explicit fma: both kernels round identically)
+__device__ __forceinline__ float rope_first(float x1, float x2, float cs, float sn) { return fmaf(x1, cs, -(x2 * sn)); }
+__device__ __forceinline__ float rope_second(float x2, float x1, float cs, float sn) { return fmaf(x2, cs, x1 * sn); }
+
 }  // namespace kd

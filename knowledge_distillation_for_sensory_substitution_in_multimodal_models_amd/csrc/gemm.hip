@@ -42,6 +42,13 @@ struct GemmP {
     float alpha;
     int c_f32, accumulate, bias_f32, act, res_mod;
     int res_f32;           // residual is fp32 (the fp32 residual stream; C is then fp32 too)
+    // q|k|v scatter epilogue (kd_gemm_desc.qkv; forward K-major GEMMs on the tiled kernels): the
+    // tile (bias added, rounded to bf16 as the unfused GEMM output) goes straight to head-major
+    // q / k / v [B, heads, S, hdp] with RoPE on q and k (cos / sin [S, hd/2]) and the [hd, hdp)
+    // padding zeroed — k_qkv_split's arithmetic, without the [M, N] round trip through HBM
+    bf16 *sq, *sk, *sv;
+    const float *rcos, *rsin;
+    int sS, snq, snkv, shd, shdp;
     int64_t kchunk;        // split-K: K elements per split (gridDim.y splits)
     int64_t split_stride;  // split-K: fp32 elements between consecutive partial planes
     int glu;               // SwiGLU epilogue (v8, K-major): I = N/2; B rows [0,I) gate, [I,2I) up; 0 = off
@@ -551,6 +558,46 @@ __device__ __forceinline__ void load_bias(const GemmP& p, const int (&cols)[NT],
     }
 }
 
+// q|k|v scatter flush: LDS bf16 image rows [0, ROWS) x BN -> head-major q / k / v (+RoPE), every
+// head of the tile whole in it (256 % hd == 0 or no RoPE), 8-column chunks (hd % 8 == 0)
+template <int ROWS, int BN, int NTHR>
+__device__ __forceinline__ void epi_flush_qkv(const GemmP& p, const char* smem, int rs, int m0, int n0, int tid) {
+    constexpr int CPR = BN / 8;
+    const int hd = p.shd, hh = hd >> 1, hdp = p.shdp, S = p.sS, nq = p.snq, nkv = p.snkv;
+#pragma unroll 2
+    for (int idx = tid; idx < ROWS * CPR; idx += NTHR) {
+        const int lr = idx / CPR, c = idx % CPR;
+        const int row = m0 + lr, col = n0 + c * 8;
+        if (row >= p.M || col >= p.N) continue;
+        const int head = col / hd, d0 = col - head * hd;
+        bf16* base;
+        int hidx, nh;
+        if (head < nq) { base = p.sq; hidx = head; nh = nq; }
+        else if (head < nq + nkv) { base = p.sk; hidx = head - nq; nh = nkv; }
+        else { base = p.sv; hidx = head - nq - nkv; nh = nkv; }
+        const int b = row / S, s = row - b * S;
+        bf16* drow = base + (((int64_t)b * nh + hidx) * S + s) * hdp;
+        bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
+        if (p.rcos && head < nq + nkv) {
+            const bool first = d0 < hh;
+            const int pc = first ? c * 8 + hh : c * 8 - hh;   // the rotate_half partner, same head, same tile
+            const bf16x8 pv = *(const bf16x8*)(smem + lr * rs + pc * 2);
+            const int i = first ? d0 : d0 - hh;
+            const f32x4 c0 = *(const f32x4*)(p.rcos + (int64_t)s * hh + i), c1 = *(const f32x4*)(p.rcos + (int64_t)s * hh + i + 4);
+            const f32x4 s0 = *(const f32x4*)(p.rsin + (int64_t)s * hh + i), s1 = *(const f32x4*)(p.rsin + (int64_t)s * hh + i + 4);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float cs = e < 4 ? c0[e] : c1[e - 4], sn = e < 4 ? s0[e] : s1[e - 4];
+                const float x = (float)v[e], y = (float)pv[e];
+                v[e] = (bf16)(first ? rope_first(x, y, cs, sn) : rope_second(x, y, cs, sn));
+            }
+        }
+        *(bf16x8*)(drow + d0) = v;
+        if (d0 + 8 == hd)
+            for (int d = hd; d < hdp; d += 8) *(bf16x8*)(drow + d) = (bf16x8){};
+    }
+}
+
 // HAS_ACT: the activation epilogue is instantiated for the forward (K-major x K-major) kernels
 // only; the launcher rejects an activation with MN-major operands or an fp32 output.
 template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2, bool HAS_ACT = true>
@@ -569,6 +616,12 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
         load_bias<NT>(p, cols, bcol);
     }
     constexpr int RS16 = BN * 2 + 16, RS32 = BN * 4 + 16;
+    if (HAS_ACT && p.sq) {   // q|k|v scatter (+RoPE) straight from the bf16 tile
+        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        __syncthreads();
+        epi_flush_qkv<BM, BN, NTHR>(p, smem, RS16, m0, n0, tid);
+        return;
+    }
     if (p.act == KD_ACT_DGELU_TANH || p.act == KD_ACT_DSWIGLU) {   // aux is READ (the forward pre-activation)
         epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
@@ -1693,12 +1746,13 @@ int launch_quant_rows_f8(const void* x, int64_t ldx, int R, int K, void* q, int6
 
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d != nullptr, "gemm: null descriptor");
-    KD_CHECK_ARG(d->A && d->B && d->C, "gemm: null operand");
+    KD_CHECK_ARG(d->A && d->B && (d->C || d->qkv), "gemm: null operand");
     KD_CHECK_SHAPE(d->M > 0 && d->N > 0 && d->K > 0, "gemm: empty shape");
     KD_CHECK_ARG(d->a_layout == KD_LAYOUT_K_MAJOR || d->a_layout == KD_LAYOUT_MN_MAJOR, "gemm: a_layout");
     KD_CHECK_ARG(d->b_layout == KD_LAYOUT_K_MAJOR || d->b_layout == KD_LAYOUT_MN_MAJOR, "gemm: b_layout");
     KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16 || d->c_dtype == KD_DTYPE_F32, "gemm: c_dtype");
     KD_CHECK_ARG(d->ab_dtype == KD_DTYPE_BF16 || d->ab_dtype == KD_DTYPE_FP8_E4M3, "gemm: ab_dtype");
+    KD_CHECK_ARG(!d->qkv || d->ab_dtype == KD_DTYPE_BF16, "gemm qkv: bf16 operands only");
     if (d->ab_dtype == KD_DTYPE_FP8_E4M3) return launch_gemm_f8(d, stream_);
     KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_DSWIGLU, "gemm: act");
     const bool dact = d->act == KD_ACT_DGELU_TANH || d->act == KD_ACT_DSWIGLU;
@@ -1728,7 +1782,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     } else {
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldb >= d->N, "gemm: MN-major B needs N % 8 == 0, ldb >= N");
     }
-    KD_CHECK_SHAPE(d->ldc >= (d->act == KD_ACT_SWIGLU ? d->N / 2 : d->N), "gemm: ldc < N (N/2 for swiglu)");
+    KD_CHECK_SHAPE(d->qkv || d->ldc >= (d->act == KD_ACT_SWIGLU ? d->N / 2 : d->N), "gemm: ldc < N (N/2 for swiglu)");
     KD_CHECK_SHAPE(!d->residual || d->ldr >= d->N, "gemm: ldr < N");
     KD_CHECK_ARG(!d->residual || d->residual_dtype == KD_DTYPE_BF16 ||
                  (d->residual_dtype == KD_DTYPE_F32 && d->c_dtype == KD_DTYPE_F32 && d->act == KD_ACT_NONE),
@@ -1745,21 +1799,41 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.act = d->act;
     p.res_mod = d->residual_row_mod;
     p.res_f32 = d->residual && d->residual_dtype == KD_DTYPE_F32;
+    p.sq = p.sk = p.sv = nullptr; p.rcos = p.rsin = nullptr;
+    p.sS = p.snq = p.snkv = p.shd = p.shdp = 0;
+    if (d->qkv) {
+        const kd_qkv_scatter& q = *d->qkv;
+        const bool rope = q.cos_t != nullptr;
+        KD_CHECK_ARG(q.q && q.k && q.v && (rope == (q.sin_t != nullptr)), "gemm qkv: null q / k / v or cos without sin");
+        KD_CHECK_ARG(d->act == KD_ACT_NONE && !d->residual && !d->aux && !d->accumulate && d->c_dtype == KD_DTYPE_BF16 &&
+                     d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR && d->split_k <= 1,
+                     "gemm qkv: K-major operands, no activation / residual / aux / accumulate / split-K");
+        KD_CHECK_SHAPE(q.S > 0 && d->M % q.S == 0 && q.nq > 0 && q.nkv > 0 && d->N == (q.nq + 2 * q.nkv) * q.hd &&
+                       q.hd % 8 == 0 && q.hdp % 8 == 0 && q.hdp >= q.hd && (!rope || (q.hd % 16 == 0 && 128 % q.hd == 0)),
+                       "gemm qkv: N = (nq + 2 nkv) hd, M % S == 0, hd / hdp % 8 == 0, RoPE heads dividing 128");
+        KD_CHECK_ALIGN(q.q, 16, "gemm qkv: q must be 16-B aligned");
+        KD_CHECK_ALIGN(q.k, 16, "gemm qkv: k must be 16-B aligned");
+        KD_CHECK_ALIGN(q.v, 16, "gemm qkv: v must be 16-B aligned");
+        p.sq = (bf16*)q.q; p.sk = (bf16*)q.k; p.sv = (bf16*)q.v; p.rcos = q.cos_t; p.rsin = q.sin_t;
+        p.sS = q.S; p.snq = q.nq; p.snkv = q.nkv; p.shd = q.hd; p.shdp = q.hdp;
+    }
     p.kchunk = d->K; p.split_stride = 0; p.glu = 0; p.tile0 = 0;
     p.sa = p.sb = nullptr; p.gx = 0; p.gy = 1;
     p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr;
     p.gm = 0;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
-    const bool c_ok16 = (d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0) && (!d->residual || ((d->ldr % 8 == 0) &&
-                        ((uintptr_t)d->residual % 16 == 0)));
+    const bool c_ok16 = (d->qkv || ((d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0))) &&
+                        (!d->residual || ((d->ldr % 8 == 0) && ((uintptr_t)d->residual % 16 == 0)));
     const bool big_ok = d->N % 8 == 0 && c_ok16 && d->M >= 128 && d->N >= 128 &&
                         ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
                         (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
                         (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
     KD_CHECK_ARG(!dact || big_ok, "gemm backward activation: needs the tiled kernels (M, N >= 128, M*N >= 2^20)");
+    KD_CHECK_ARG(!d->qkv || (big_ok && d->variant != 1 && d->variant != 21),
+                 "gemm qkv: needs the tiled kernels (M, N >= 128, M*N >= 2^20)");
     kd_gemm_desc d1;
-    if (dact && d->split_k != 1) {   // the fused backward activation is never split-K
+    if ((dact || d->qkv) && d->split_k != 1) {   // the fused backward activation / q|k|v scatter are never split-K
         d1 = *d;
         d1.split_k = 1;
         d = &d1;

@@ -301,8 +301,8 @@ __global__ void k_qkv_split(const bf16* __restrict__ qkv, int64_t ld, bf16* __re
 #pragma unroll
                 for (int e = 0; e < VEC; ++e) {
                     const float x1 = (float)a[e], x2 = (float)c2[e], cs = cr[e], sn = sr[e];
-                    a[e] = (bf16)(x1 * cs - x2 * sn);
-                    c2[e] = (bf16)(x2 * cs + x1 * sn);
+                    a[e] = (bf16)rope_first(x1, x2, cs, sn);
+                    c2[e] = (bf16)rope_second(x2, x1, cs, sn);
                 }
             }
             *(vec_t*)(drow + i) = a;

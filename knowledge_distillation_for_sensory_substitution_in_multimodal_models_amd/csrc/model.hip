@@ -264,6 +264,7 @@ struct GemmArgs {
     int bias_f32 = 0;
     int split_k = 0;
     int res_f32 = 0;   // fp32 residual (then c_f32 too)
+    const kd_qkv_scatter* qkv = nullptr;   // q|k|v scatter epilogue (C unused)
 };
 
 // split-K default of the runtime's GEMMs (KD_GEMM_SPLIT_K: 0 = the cost model, 1 = never split)
@@ -286,6 +287,7 @@ int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int6
     d.act = g.act;
     d.residual = g.residual; d.ldr = g.ldr;
     d.residual_dtype = g.res_f32 ? KD_DTYPE_F32 : KD_DTYPE_BF16;
+    d.qkv = g.qkv;
     d.aux = g.aux; d.ld_aux = g.ld_aux;
     d.residual_row_mod = g.residual_row_mod;
     d.split_k = g.split_k ? g.split_k : g_split_default;
@@ -515,6 +517,33 @@ int lin(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int N, int K, const
     return gemm_timed(&d, s);
 }
 
+// the fused q|k|v projection + view / transpose (+ RoPE) of the attention input: one GEMM whose
+// epilogue writes head-major q / k / v (kd_qkv_scatter) where the tiled kernels take the shape
+// and the weight is on the bf16 path; else the GEMM into `qkv` and k_qkv_split (same bits).
+// KD_FUSE_QKV=0 turns the fusion off (A/B).
+static const bool g_fuse_qkv = [] {
+    const char* e = std::getenv("KD_FUSE_QKV");
+    return !(e && e[0] == '0');
+}();
+
+int qkv_proj(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int K, const bf16* x, int widx, const void* bias,
+             bf16* qkv, void* q, void* k, void* v, const float* cs, const float* sn, int B, int S, int nq, int nkv,
+             int hd, int hdp) {
+    const int N = (nq + 2 * nkv) * hd;
+    GemmArgs g;
+    g.bias = bias;
+    const bool fp8 = m->f8q && m->soff[widx] >= 0 && (m->fam[widx] & m->f8_families);
+    if (g_fuse_qkv && !fp8 && M >= 128 && N >= 128 && N % 8 == 0 && (int64_t)M * N >= ((int64_t)1 << 20) &&
+        hd % 8 == 0 && hdp % 8 == 0 && (!cs || (hd % 16 == 0 && 128 % hd == 0))) {
+        kd_qkv_scatter sc{q, k, v, cs, sn, S, nq, nkv, hd, hdp};
+        g.qkv = &sc;
+        g.split_k = 1;
+        return gemm(s, P.splitk, M, N, K, km(x, K), km(m->W(widx), K), nullptr, 0, g);
+    }
+    KD_TRY(lin(m, P, s, M, N, K, x, K, widx, qkv, N, g));
+    return launch_qkv_split(qkv, N, q, k, v, cs, sn, B, S, nq, nkv, hd, hdp, s);
+}
+
 int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dtype, int NI, int save, void* post,
                    hipStream_t s) {
     const Cfg& C = m->C;
@@ -538,12 +567,8 @@ int vision_forward(kd_model* m, const FwdPlan& P, const void* pixels, int px_dty
         void* x_out = (i + 1 < c.v_layers) ? P.vl[i + 1].x : P.x_vis_last;
         KD_TRY(launch_norm_fwd(0, b.x, D, m->W(m->vis(i, VLN1W)), m->W(m->vis(i, VLN1B)), b.h, D, save ? b.m1 : nullptr,
                                save ? b.r1 : nullptr, NT, D, c.v_eps, s, f32));
-        {
-            GemmArgs g;
-            g.bias = m->W(m->vis(i, VQB));
-            KD_TRY(lin(m, P, s, NT, 3 * D, D, b.h, D, m->vis(i, VQW), P.qkv_v, 3 * D, g));
-        }
-        KD_TRY(launch_qkv_split(P.qkv_v, 3 * D, b.q, b.k, b.v, nullptr, nullptr, NI, np, c.v_heads, c.v_heads, hd, hdp, s));
+        KD_TRY(qkv_proj(m, P, s, NT, D, b.h, m->vis(i, VQW), m->W(m->vis(i, VQB)), P.qkv_v, b.q, b.k, b.v, nullptr,
+                        nullptr, NI, np, c.v_heads, c.v_heads, hd, hdp));
         {
             kd_attn_desc a{b.q, b.k, b.v, b.o, save ? b.lse : nullptr, NI, c.v_heads, c.v_heads, np, hd, hdp, 0};
             KD_TRY(launch_attn_fwd(&a, s));
@@ -594,14 +619,10 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
         void* x_out = (i + 1 < c.t_layers) ? P.ll[i + 1].x : P.x_lm_last;
         KD_TRY(launch_norm_fwd(1, b.x, H, m->W(m->lm(i, LINW)), nullptr, b.h, H, nullptr, save ? b.r1 : nullptr, M, H,
                                c.t_eps, s, f32));
-        {
-            GemmArgs g;
-            g.bias = m->W(m->lm(i, LQB));
-            KD_TRY(lin(m, P, s, M, qd + 2 * kvd, H, b.h, H, m->lm(i, LQW), P.qkv_t, qd + 2 * kvd, g));
-        }
         void* k = kv_k ? kv_k[i] : b.k;
         void* v = kv_v ? kv_v[i] : b.v;
-        KD_TRY(launch_qkv_split(P.qkv_t, qd + 2 * kvd, b.q, k, v, cs, sn, B, L, c.t_heads, c.t_kv_heads, hd, hd, s));
+        KD_TRY(qkv_proj(m, P, s, M, H, b.h, m->lm(i, LQW), m->W(m->lm(i, LQB)), P.qkv_t, b.q, k, v, cs, sn, B, L,
+                        c.t_heads, c.t_kv_heads, hd, hd));
         {
             kd_attn_desc a{b.q, k, v, b.o, save ? b.lse : nullptr, B, c.t_heads, c.t_kv_heads, L, hd, hd, 1};
             KD_TRY(launch_attn_fwd(&a, s));

@@ -224,6 +224,25 @@ def _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate
     return d, out, M, N, K, la, lb
 
 
+def gemm_qkv(x: torch.Tensor, w: torch.Tensor, bias, q, k, v, S: int, nq: int, nkv: int, hd: int, hdp: int,
+             cos=None, sin=None, variant: int = 0):
+    """Fused q|k|v projection: x [M, K] @ w[N, K]^T + bias written straight to head-major q
+    [B, nq, S, hdp], k / v [B, nkv, S, hdp] (+ RoPE with cos / sin [S, hd/2] fp32), the
+    padding zeroed (include/kdstep.h kd_qkv_scatter) — equal to gemm() + qkv_split()."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _require(t, torch.bfloat16, f"gemm_qkv.{n}")
+        if not t.is_contiguous():
+            raise RuntimeError(f"gemm_qkv.{n}: contiguous head-major tensor expected")
+    sc = NV.KdQkvScatter(q.data_ptr(), k.data_ptr(), v.data_ptr(), _ptr(cos), _ptr(sin), int(S), int(nq), int(nkv),
+                         int(hd), int(hdp))
+    d, _, M, N, K, la, lb = _gemm_desc(x, w, q.view(-1, 1), bias, None, None, None, 1.0, None, False,
+                                       torch.bfloat16, 0, variant, 1)
+    d.C, d.ldc = None, 0
+    d.qkv = C.cast(C.pointer(sc), C.c_void_p)
+    NV.call("kd_gemm", C.byref(d), _stream())
+    return q, k, v
+
+
 def gemm_plan(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
               residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
               out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0):

@@ -108,10 +108,11 @@ def test_gemm_fp8_teacher_shape_sampled(dev):
 
 
 def test_fp8_teacher_end_to_end_tiny(dev):
-    """LogitBasedKD with the teacher's linears on the fp8 path vs the same module with the bf16
-    teacher, same weights and batch: the student side is untouched (student CE bit-equal), the
-    teacher logits stay within rel-L2 5e-2 of the bf16 teacher's, and the KD term within 5e-2
-    relative (stated tolerance of the fp8 teacher)."""
+    """LogitBasedKD with every teacher linear on the fp8 path vs the same module with the bf16
+    teacher, same weights and batch (tiny widths, 2 layers): the student side is untouched
+    (student CE bit-equal), the teacher logits stay within rel-L2 0.15 / cosine 0.99 of the
+    bf16 teacher's and the KD term within 0.15 relative.  The full-width depth tolerance is
+    test_fp8_teacher_depth8_real_widths."""
     import sys
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
@@ -136,3 +137,33 @@ def test_fp8_teacher_end_to_end_tiny(dev):
           f"(rel {kd_rel:.4f}); teacher CE {terms_f[2]:.6g} vs {terms_b[2]:.6g}")
     assert 0 < rel <= 0.15 and cos >= 0.99, (rel, cos)
     assert kd_rel <= 0.15, (terms_f[0], terms_b[0])
+
+
+@pytest.mark.parametrize("families,max_rel,min_cos", [("lm_mlp", 0.18, 0.98), ("all", 0.32, 0.95)])
+def test_fp8_teacher_depth8_real_widths(families, max_rel, min_cos, dev):
+    """The 7B teacher at its real widths, 8 Qwen2 + 8 SigLIP layers, one 336x336 sample: the
+    fp8 policy's logits against the bf16 teacher's (same weights).  Stated tolerances (DESIGN
+    §4; measured 0.155 / 0.988 for lm_mlp — BASELINE c4's default — and 0.284 / 0.960 for all,
+    profiles/r03/fp8_depth_policies.json).  e4m3 costs ~3.7 % rel-L2 per GEMM output whatever
+    the scaling and the errors add in quadrature along the forward, so the bound grows with
+    depth (full depth: 0.249 / 0.969 and 0.478 / 0.886)."""
+    from dataclasses import replace
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import (TEACHER_7B,
+                                                                                                   LlavaOnevisionModel)
+    cfg = replace(TEACHER_7B, vision=replace(TEACHER_7B.vision, layers=8), text=replace(TEACHER_7B.text, layers=8))
+    t = LlavaOnevisionModel(cfg, dev, trainable=False, seed=1)
+    b = synthetic_batch(1, dev, L=1536, seed=0)
+    out = {}
+    for fam in (None, families):
+        if fam:
+            t.enable_fp8(fam)
+        with torch.no_grad():
+            f = t.forward(b["rgb_input_ids"], b["rgb_pixel_values"], b["image_sizes"], want_logits=True)
+        torch.cuda.synchronize()
+        out[fam] = f["logits"].float()
+    lb, lf = out[None], out[families]
+    rel = float((lf - lb).norm() / lb.norm())
+    cos = float((lf * lb).sum() / (lf.norm() * lb.norm()))
+    print(f"fp8 {families} depth 8: logits rel-L2 {rel:.4f} cosine {cos:.5f}")
+    assert 0 < rel <= max_rel and cos >= min_cos, (rel, cos)

@@ -346,3 +346,36 @@ def test_fused_backward_activation(variant, M, N, K, dev):
     x = pre.float().requires_grad_(True)
     torch.nn.functional.gelu(x, approximate="tanh").backward(v.float())
     _check(out, x.grad)
+
+
+@pytest.mark.parametrize("shape,variant", [
+    ("teacher", 0), ("teacher", 16), ("teacher", 6), ("student", 0), ("student", 5), ("student", 7),
+    ("siglip", 0), ("siglip", 16), ("siglip", 6)])
+def test_qkv_scatter_epilogue_equals_gemm_then_split(shape, variant, dev):
+    """The fused q|k|v projection (kd_qkv_scatter epilogue: bias, bf16 rounding, head-major
+    scatter, RoPE on q / k, zeroed padding) equals the plain GEMM followed by k_qkv_split bit
+    for bit, in every tiled kernel: the Qwen2-7B (28q / 4kv, hd 128), Qwen2-0.5B (14q / 2kv,
+    hd 64) and SigLIP (16 heads, hd 72 padded to 96, no RoPE) attention inputs."""
+    ops = _ops()
+    B, S, K, nq, nkv, hd, hdp, rope = {
+        "teacher": (2, 1536, 3584, 28, 4, 128, 128, True),
+        "student": (2, 1536, 896, 14, 2, 64, 64, True),
+        "siglip": (4, 729, 1152, 16, 16, 72, 96, False)}[shape]
+    M, N = B * S, (nq + 2 * nkv) * hd
+    x = _rand(M, K, dev=dev, seed=31)
+    w = _rand(N, K, dev=dev, seed=32, scale=0.05)
+    bias = _rand(N, dev=dev, seed=33)
+    cos = sin = None
+    if rope:
+        inv = 1.0 / (1e6 ** (torch.arange(0, hd, 2, dtype=torch.float32) / hd))
+        f = torch.arange(S, dtype=torch.float32)[:, None] * inv[None]
+        cos, sin = f.cos().to(dev).contiguous(), f.sin().to(dev).contiguous()
+    qkv = ops.gemm(x, w, bias=bias, variant=variant, split_k=1)
+    q0, k0, v0 = ops.qkv_split(qkv, B, S, nq, nkv, hd, hdp, cos, sin)
+    q = torch.full((B, nq, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)   # garbage: the padding must be zeroed
+    k = torch.full((B, nkv, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)
+    v = torch.full((B, nkv, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)
+    ops.gemm_qkv(x, w, bias, q, k, v, S, nq, nkv, hd, hdp, cos, sin, variant=variant)
+    torch.cuda.synchronize()
+    for got, ref, n in ((q, q0, "q"), (k, k0, "k"), (v, v0, "v")):
+        assert torch.equal(got, ref), f"{n}: {int((got != ref).sum())} elements differ"

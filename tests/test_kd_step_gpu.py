@@ -40,7 +40,7 @@ ATOL, RTOL = 1e-4, 1e-3   # north_star
 NTX_RTOL = 3e-3           # the NT-Xent term (1 / tau = 14.3 amplification of the feature error)
 FLOOR = json.loads((Path(__file__).resolve().parent / "golden" / "bf16_floor.json").read_text())
 # kinds whose gradient total norm meets the north-star 1e-3 (profiles/r03/parity.json)
-GRAD_NORTH_STAR = {"lb", "dt2", "dt3", "bd", "sun_lb"}
+GRAD_NORTH_STAR = {"lb", "dt2", "dt3", "bd", "fb", "sun_lb", "mix_fb"}
 
 
 def _grad(P, name):
