@@ -390,7 +390,7 @@ def main():
     fwd = ops.TIMER.summary("gemm_kk_swiglu")
     fwd8 = ops.TIMER.summary("gemm_f8_swiglu")
     traffic = None   # PMC HBM bytes per launch of that kernel (tools/pmc_bench.sh -> profiles/)
-    for rd in ("r02", "r01"):
+    for rd in ("r03", "r02", "r01"):
         tpath = REPO / "profiles" / rd / "pmc_traffic.json"
         if tpath.exists():
             fg = json.load(open(tpath)).get("roofline_kernel")

@@ -401,36 +401,44 @@ constexpr size_t gemm2_lds() {
 }
 
 
+// Accumulator layout of the 256-row kernels (v3, v8, v9): the MFMA is issued with the B
+// fragment as its A operand and the A fragment as its B operand, i.e. it computes the 16x16
+// tile of C^T, so lane l holds C[row = l & 15][cols 4 (l >> 4) .. +3] — four CONSECUTIVE
+// columns of one row.  The epilogue's LDS staging is then one 8-B (bf16) / 16-B (fp32) store
+// per lane and 16x16 tile instead of four 2-B / 4-B stores (4x fewer LDS write instructions
+// in a store-issue-bound epilogue), and a lane's bias is 4 consecutive columns.
+__device__ __forceinline__ int acc_row(int lane) { return lane & 15; }
+__device__ __forceinline__ int acc_col(int lane) { return (lane >> 4) * 4; }
+
 // Epilogue of the 256-row kernels. Every condition is wave-uniform and hoisted out of the
 // per-element loops (a per-element switch on the activation compiled to ~2,800 branches
 // and dominated the v8 tile time); the accumulators are only read (so v8's stay in the
 // AGPR file), one 16x16 tile at a time, into an LDS image that is then written out in
 // 16-B row chunks: pre = alpha*acc + bias -> [aux <- pre] -> C <- act(pre) (+ resid, + C).
 template <int ACT, int TM, int TN, int MT, int NT, bool F32>
-__device__ __forceinline__ void epi_to_lds(const f32x4 (&acc)[MT][NT], char* smem, int rs, float alpha, const float (&bcol)[NT],
-                                           int wm, int wn, int lane, int r_lo, int r_hi) {
+__device__ __forceinline__ void epi_to_lds(const f32x4 (&acc)[MT][NT], char* smem, int rs, float alpha,
+                                           const f32x4 (&bcol)[NT], int wm, int wn, int lane, int r_lo, int r_hi) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
         const int lr0 = wm * TM + i * 16;
         if (lr0 < r_lo || lr0 >= r_hi) continue;
+        const int lr = lr0 - r_lo + acc_row(lane);
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const f32x4 a = acc[i][j];
+            const int lc = wn * TN + j * 16 + acc_col(lane);
+            float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float v = apply_act(a[r] * alpha + bcol[j], ACT);
-                const int lr = lr0 - r_lo + (lane >> 4) * 4 + r;
-                const int lc = wn * TN + j * 16 + (lane & 15);
-                if (F32) *(float*)(smem + lr * rs + lc * 4) = v;
-                else *(bf16*)(smem + lr * rs + lc * 2) = (bf16)v;
-            }
+            for (int r = 0; r < 4; ++r) v[r] = apply_act(a[r] * alpha + bcol[j][r], ACT);
+            if (F32) *(f32x4*)(smem + lr * rs + lc * 4) = (f32x4){v[0], v[1], v[2], v[3]};
+            else *(bf16x4*)(smem + lr * rs + lc * 2) = (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         }
     }
 }
 
 template <int TM, int TN, int MT, int NT, bool F32>
 __device__ __forceinline__ void epi_to_lds_act(int act, const f32x4 (&acc)[MT][NT], char* smem, int rs, float alpha,
-                                               const float (&bcol)[NT], int wm, int wn, int lane, int r_lo, int r_hi) {
+                                               const f32x4 (&bcol)[NT], int wm, int wn, int lane, int r_lo, int r_hi) {
     switch (act) {
         case KD_ACT_GELU_TANH: epi_to_lds<KD_ACT_GELU_TANH, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
         case KD_ACT_GELU_ERF: epi_to_lds<KD_ACT_GELU_ERF, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
@@ -536,6 +544,28 @@ __device__ __forceinline__ void epi_flush_dact(const GemmP& p, const char* smem,
     }
 }
 
+// bias of NT groups of 4 consecutive columns (the transposed accumulator layout), the dtype
+// branch outside the loads so all NT vector loads are in flight together (cols[j] % 4 == 0;
+// N % 8 == 0 on the tiled kernels: the clamp keeps the 4 columns inside [0, N))
+template <int NT>
+__device__ __forceinline__ void load_bias4(const GemmP& p, const int (&cols)[NT], f32x4 (&b)[NT]) {
+    if (p.bias_f32) {
+        const float* bp = (const float*)p.bias;
+        f32x4 t[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) t[j] = *(const f32x4*)(bp + cols[j]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) b[j] = t[j];
+    } else {
+        const bf16* bp = (const bf16*)p.bias;
+        bf16x4 t[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) t[j] = *(const bf16x4*)(bp + cols[j]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) b[j] = (f32x4){(float)t[j][0], (float)t[j][1], (float)t[j][2], (float)t[j][3]};
+    }
+}
+
 // bias of NT columns with the dtype branch outside the loads, so all NT loads are in flight
 // together: a per-element `bias_f32 ? f32 : bf16` select made hipcc wait for each load in turn
 // (NT dependent memory round trips per tile: +22-24 us on the 7B q|k|v GEMM, 28 calls a step)
@@ -606,14 +636,14 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
     const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
     float alpha = p.alpha;
     if (p.alpha_dev) alpha *= *p.alpha_dev;
-    float bcol[NT];
+    f32x4 bcol[NT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bcol[j] = 0.f;
+    for (int j = 0; j < NT; ++j) bcol[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     if (p.bias) {
         int cols[NT];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) cols[j] = min(n0 + wn * TN + j * 16 + (lane & 15), p.N - 1);
-        load_bias<NT>(p, cols, bcol);
+        for (int j = 0; j < NT; ++j) cols[j] = min(n0 + wn * TN + j * 16 + acc_col(lane), p.N - 4);
+        load_bias4<NT>(p, cols, bcol);
     }
     constexpr int RS16 = BN * 2 + 16, RS32 = BN * 4 + 16;
     if (HAS_ACT && p.sq) {   // q|k|v scatter (+RoPE) straight from the bf16 tile
@@ -662,9 +692,9 @@ __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[
                                              int wn, int lane, int tid) {
     float alpha = p.alpha;
     if (p.alpha_dev) alpha *= *p.alpha_dev;
-    float bcol[NT];
+    f32x4 bcol[NT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bcol[j] = 0.f;
+    for (int j = 0; j < NT; ++j) bcol[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     constexpr int RS = 256 * 2 + 16;
     epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS, alpha, bcol, wm, wn, lane, 0, 256);
     __syncthreads();
@@ -763,7 +793,7 @@ __global__ void __launch_bounds__(NTH2, 1) k_gemm3(GemmP p_) {
         }                                                                                                 \
         _Pragma("unroll") for (int i = 0; i < MT; ++i)                                                    \
             _Pragma("unroll") for (int j = 0; j < NT; ++j)                                                \
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CUR_A[i], CUR_B[j], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CUR_B[j], CUR_A[i], acc[i][j], 0, 0, 0); \
         _Pragma("unroll") for (int k = 0; k < G; ++k) {                                                   \
             __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                            \
             __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                            \
@@ -970,23 +1000,23 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         const int t_ = t + (SL);                                                                              \
         const char* na_ = smem + (((SL) + 1) % NS8) * SS;                                                     \
         _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
-            mfma_agpr(acc[u][0], CA[u], CB[0]); KD_SB                                                         \
+            mfma_agpr(acc[u][0], CB[0], CA[u]); KD_SB                                                         \
             dma(t_ + NS8, (SL), u, FT{}); KD_SB                                                               \
-            mfma_agpr(acc[u][1], CA[u], CB[1]); KD_SB                                                         \
+            mfma_agpr(acc[u][1], CB[1], CA[u]); KD_SB                                                         \
             if (u < 4) NA[2 * u] = frag2<256, A_MN>(na_, ra + 2 * u * 16, lane);                              \
             KD_SB                                                                                             \
-            mfma_agpr(acc[u][2], CA[u], CB[2]); mfma_agpr(acc[u][3], CA[u], CB[3]); KD_SB                     \
+            mfma_agpr(acc[u][2], CB[2], CA[u]); mfma_agpr(acc[u][3], CB[3], CA[u]); KD_SB                     \
             if (u < 4) NB[2 * u] = frag2<256, B_MN>(na_ + SA, cb + 2 * u * 16, lane);                         \
             KD_SB                                                                                             \
-            mfma_agpr(acc[u][4], CA[u], CB[4]); mfma_agpr(acc[u][5], CA[u], CB[5]); KD_SB                     \
+            mfma_agpr(acc[u][4], CB[4], CA[u]); mfma_agpr(acc[u][5], CB[5], CA[u]); KD_SB                     \
             if (u < 4) NA[2 * u + 1] = frag2<256, A_MN>(na_, ra + (2 * u + 1) * 16, lane);                    \
             KD_SB                                                                                             \
-            mfma_agpr(acc[u][6], CA[u], CB[6]); KD_SB                                                         \
+            mfma_agpr(acc[u][6], CB[6], CA[u]); KD_SB                                                         \
             if (u < 4) NB[2 * u + 1] = frag2<256, B_MN>(na_ + SA, cb + (2 * u + 1) * 16, lane);               \
             if (u == 7) KD_G8_SYNC()                                                                          \
             KD_SB                                                                                             \
-            if (u == 7) mfma_agpr_last(acc[u][7], CA[u], CB[7], t_ + 1 == nk);                                \
-            else mfma_agpr(acc[u][7], CA[u], CB[7]);                                                          \
+            if (u == 7) mfma_agpr_last(acc[u][7], CB[7], CA[u], t_ + 1 == nk);                                \
+            else mfma_agpr(acc[u][7], CB[7], CA[u]);                                                          \
             KD_SB                                                                                             \
         }                                                                                                     \
     }
@@ -1189,8 +1219,8 @@ __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if (i == 7 && j == 3) mfma_agpr_last(acc[i][j], fa[i], fb[j], t + 1 == nk);
-                else mfma_agpr(acc[i][j], fa[i], fb[j]);
+                if (i == 7 && j == 3) mfma_agpr_last(acc[i][j], fb[j], fa[i], t + 1 == nk);
+                else mfma_agpr(acc[i][j], fb[j], fa[i]);
             }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
