@@ -1,3 +1,6 @@
+# GPU pass for a library A/B (run under gpurun): the whole -m gpu suite on the in-tree library,
+# then the c1 bench alternating the in-tree build ("new") and tools/variants/libkdstep_base.so
+# ("base", loaded through KDSTEP_LIB), with the fused q|k|v epilogue on and off (KD_FUSE_QKV).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

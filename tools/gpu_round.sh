@@ -7,6 +7,7 @@
 # prof   : rocprofv3 --kernel-trace --stats of a serialized bench (its roofline-kernel average
 #          is what bench.py's HIP-event pass measures)
 # step   : kernel trace of the concurrent (default) bench -> gpurun_out/step_breakdown.txt
+# blas   : PMC clock / MFMA-busy of kd_gemm vs hipBLASLt on the two big shapes (tools/pmc_vs_blas.sh)
 # pmc    : HBM traffic per kernel (tools/pmc_bench.sh, two --pmc passes)
 # Every step has its own time limit; the first failure ends the script.
 set -o pipefail
@@ -29,6 +30,8 @@ for s in $STEPS; do
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-teacher-rate --no-cpu-baseline --no-delta $BENCH_ARGS > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; } ;;
     step)   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/profstep -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-delta --no-timer --no-teacher-rate $BENCH_ARGS > gpurun_out/profstep.log 2>&1 || { echo "profstep failed"; tail -20 gpurun_out/profstep.log; exit 1; }
             python3 tools/step_breakdown.py $(ls gpurun_out/profstep/*/run_results.db gpurun_out/profstep/run_results.db 2>/dev/null | head -1) 40 > gpurun_out/step_breakdown.txt 2>&1; head -45 gpurun_out/step_breakdown.txt ;;
+    blas)   bash tools/pmc_vs_blas.sh > gpurun_out/pmc_blas.log 2>&1 || { echo "pmc_vs_blas failed"; tail -10 gpurun_out/pmc_blas.log; exit 1; }
+            cat gpurun_out/pmc_blas/summary.txt ;;
     pmc)    bash tools/pmc_bench.sh > gpurun_out/pmc_bench.log 2>&1 || { echo "pmc failed"; tail -10 gpurun_out/pmc_bench.log; exit 1; } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
