@@ -21,7 +21,9 @@
 //   dS goes through LDS once for dQ += dS K, accumulated with fp32 atomics.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
+#include <utility>
 #include <type_traits>
 
 namespace kd {
@@ -319,6 +321,613 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     }
 }
 
+// ------------------------------------------------------- forward, 32x32x16 MFMAs ----
+// The 16x16x32 kernel above is bound by VECTOR ISSUE, not by the matrix pipe: a 16x16x32
+// MFMA holds its SIMD's vector issue for 8 of its 16 cycles, so with ~170 softmax VALU per
+// 64 MFMAs (32 exps at 8 cycles) a SIMD's two waves need ~2,700 issue cycles per 2,048 MFMA
+// cycles (MFMA pipe ~35% busy, measured 25%). A 32x32x16 MFMA holds issue for 8 of its 32
+// cycles: the same FLOPs leave 3x the issue slots for the softmax.
+//   S^T (32 keys x 32 queries) = K Q^T: lane l owns query l & 31, keys 8(i>>2) + 4(l>>5) + (i&3)
+//   in register i; two such tiles per 64-key tile = 32 scores per lane, the other 32 in lane
+//   l ^ 32 (row max: one v_permlane32_swap). The accumulator IS the B operand of the PV
+//   product (registers 8s'..8s'+7 -> k-step s' in the permuted key order), and the V^T A
+//   operand is read in that same order by two ds_read_b64_tr_b16 per MFMA (keys 16s + 4h + q
+//   and 16s + 8 + 4h + q). O^T (32 dims x 32 queries) keeps the query on the lane: the online
+//   rescale stays lane-local.
+// Per wave: 32 queries (4 waves = 128 rows per workgroup, as k_attn_fwd<.., NQ = 2>); per
+// 64-key tile 16 QK^T + 16 PV MFMAs of 32 cycles (hd 128). Causal: a wave skips the MFMAs of
+// tiles wholly above its diagonal (the workgroup still stages them for its other waves).
+
+// V image swizzle for the 32x32x16 transposed reads: a 32-lane half reads 4 consecutive rows
+// x 64 B; the XOR moves the 4 rows into 4 different 64-B bank blocks (256-B rows: chunk ^ 4(r&3);
+// 128-B rows: rows r and r+2 share banks, chunk ^ 4((r>>1)&1))
+template <int RB> __device__ __forceinline__ int swV32(int r) { return RB == 256 ? ((r & 3) << 2) : (((r >> 1) & 1) << 2); }
+
+template <int HDP, bool VIMG>
+__device__ __forceinline__ void stage_kv32(char* lds, const bf16* slab, int row0, int S, int wid, int lane) {
+    constexpr int RB = Geo<HDP>::RB;
+    constexpr int ROWS_PER = 1024 / RB, CH = RB / 16, NINSTR = 64 / ROWS_PER;
+    const int rows_valid = min(64, S - row0);
+    auto rs = rsrc(slab + (int64_t)row0 * HDP, rows_valid <= 0 ? 0u : (uint32_t)(rows_valid * HDP * 2));
+#pragma unroll
+    for (int s = 0; s < NINSTR / 4; ++s) {
+        const int i = wid * (NINSTR / 4) + s;
+        const int r = i * ROWS_PER + lane / CH;
+        const int c = lane % CH;
+        const int gc = c ^ (VIMG ? swV32<RB>(r) : swK<RB>(r));
+        const uint32_t voff = (gc * 8 < HDP) ? (uint32_t)((r * HDP + gc * 8) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(lds + i * 1024), 16, voff, 0, 0, 0);
+    }
+}
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
+    bf16x8 r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+    return r;
+}
+
+
+// v of lanes l & 31 and (l & 31) + 32 in every lane (one v_permlane32_swap): max / sum over the
+// two halves, in the same operand order in both (bit-identical results)
+__device__ __forceinline__ float half_max(float v) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float v) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Register staging of one 64-row K or V tile (RS build of k_attn_fwd32): the attention guide
+// measures LDS-DMA pieces at 100-185 issue cycles each inside a phase that also reads LDS, and
+// a wave-tile here issues 8 of them (as many cycles as its 32 MFMAs); a buffer load to VGPRs
+// plus a ds_write_b128 costs a fraction of that. Piece pi (1 KiB) = rows [pi R, pi R + R),
+// R = 1024 / RB; lane -> row pi R + lane / CH, logical 16-B chunk lane % CH, written to the
+// swizzled LDS position. Rows >= S and chunks past HDP load as zeros (buffer range check).
+template <int HDP> struct Stage {
+    static constexpr int RB = Geo<HDP>::RB, R = 1024 / RB, CH = RB / 16, NL = 64 / R / 4;   // pieces per wave
+    uint32_t goff;         // per-lane global byte offset inside a piece (OOB past HDP)
+    uint32_t kw[NL], vw;   // per-lane LDS byte offsets of the K pieces (swK depends on the piece) and V
+    __device__ __forceinline__ void init(int wid, int lane) {
+        const int c = lane % CH, rr = lane / CH;
+        goff = (c * 8 < HDP) ? (uint32_t)((rr * HDP + c * 8) * 2) : OOB;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            const int r = (wid * NL + i) * R + rr;
+            kw[i] = (uint32_t)(r * RB + ((c ^ swK<RB>(r)) << 4));
+        }
+        const int r0 = wid * NL * R + rr;   // swV32 is the same for every piece of the wave
+        vw = (uint32_t)(r0 * RB + ((c ^ swV32<RB>(r0)) << 4));
+    }
+    __device__ __forceinline__ void load(u32x4 (&st)[NL], const bf16* slab, int row0, int S, int wid) const {
+        const int rows_valid = min(64, S - row0);
+        const auto rs = rsrc(slab + (int64_t)row0 * HDP, rows_valid <= 0 ? 0u : (uint32_t)(rows_valid * HDP * 2));
+#pragma unroll
+        for (int i = 0; i < NL; ++i)
+            st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, goff, (wid * NL + i) * R * HDP * 2, 0));
+    }
+    __device__ __forceinline__ void write_k(char* lds, const u32x4 (&st)[NL]) const {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) *(u32x4*)(lds + kw[i]) = st[i];
+    }
+    __device__ __forceinline__ void write_v(char* lds, const u32x4 (&st)[NL]) const {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) *(u32x4*)(lds + vw + i * 1024) = st[i];
+    }
+};
+
+// ST (diagnostic build, KD_ATTN_FWD_V=34, tools/stamp_attn.py): per-wave s_memtime totals
+// (prologue, tile compute, end-of-tile wait + barrier, epilogue, whole wave, tiles computed)
+// written as uint32 over the wave's own first Q row after its Q fragments are loaded (the
+// tool passes a scratch Q; nothing else reads that row: Q rows belong to one workgroup)
+template <int HDP, bool CAUSAL, bool RS, bool ST = false>
+__global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
+    uint64_t st_t0 = 0, st_pro = 0, st_cmp = 0, st_bar = 0, st_prev = 0;
+    int st_n = 0;
+    uint64_t st_r0 = 0;
+    if (ST) { st_t0 = __builtin_amdgcn_s_memtime(); st_r0 = __builtin_amdgcn_s_memrealtime(); }
+    constexpr int RB = Geo<HDP>::RB;
+    constexpr int TILE = 64 * RB;
+    constexpr int KS = HDP == 96 ? 5 : HDP / 16;               // 16-deep QK^T steps (hd <= 16 KS)
+    constexpr int ND = HDP == 64 ? 2 : (HDP == 96 ? 3 : 4);    // 32-dim O^T tiles
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][K TILE | V TILE]
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r32 = lane & 31, hf = lane >> 5;
+    const int nqb = (p.S + 127) / 128;
+    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
+    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
+    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
+    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const int q0 = qb * 128 + wid * 32;   // the wave's first query (uniform)
+    const int myq = q0 + r32;
+
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+        qf[kk] = myq < p.S ? *(const bf16x8*)(Q + (int64_t)myq * HDP + kk * 16 + 8 * hf) : (bf16x8){};
+    f32x16 o[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+    float m = -INFINITY, l = 0.f;
+
+    const int nkv_all = (p.S + 63) / 64;
+    const int nkv = CAUSAL ? min((qb + 1) * 2, nkv_all) : nkv_all;
+    const int nkv_w = CAUSAL ? min(nkv, (q0 + 31) / 64 + 1) : nkv;   // tiles with a key <= the wave's last query
+    Stage<HDP> stg;
+    u32x4 stk[Stage<HDP>::NL], stv[Stage<HDP>::NL];
+    if (RS) {
+        stg.init(wid, lane);
+        stg.load(stk, K, 0, p.S, wid);
+        stg.load(stv, V, 0, p.S, wid);
+        stg.write_k(smem, stk);
+        stg.write_v(smem + TILE, stv);
+    } else {
+        stage_kv32<HDP, false>(smem, K, 0, p.S, wid, lane);
+        stage_kv32<HDP, true>(smem + TILE, V, 0, p.S, wid, lane);
+    }
+    // per-lane LDS byte offsets; buffer, 32-key sub-tile and 16-key step are immediates
+    uint32_t koff[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+        koff[kk] = (uint32_t)(uintptr_t)smem + r32 * RB + (((2 * kk + hf) ^ swK<RB>(r32)) << 4);
+    uint32_t vaddr[ND];
+    {
+        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+        const int row = 4 * hf + ((lane >> 2) & 3);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            const int col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            vaddr[d] = sbase + TILE + row * RB + ((((col >> 3) ^ swV32<RB>(row))) << 4) + ((col & 4) << 1);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ST) { st_prev = __builtin_amdgcn_s_memtime(); st_pro = st_prev - st_t0; }
+
+    auto tile = [&](const int t, auto buf_c) {
+        constexpr int BUF = decltype(buf_c)::value;
+        if (t + 1 < nkv) {
+            if (RS) {   // loads now, LDS writes after this tile's reads (buffer BUF ^ 1 is free:
+                        // every wave passed the barrier that ended tile t - 1, its last reader)
+                stg.load(stk, K, (t + 1) * 64, p.S, wid);
+                stg.load(stv, V, (t + 1) * 64, p.S, wid);
+            } else {
+                char* nb = smem + (BUF ^ 1) * 2 * TILE;
+                stage_kv32<HDP, false>(nb, K, (t + 1) * 64, p.S, wid, lane);
+                stage_kv32<HDP, true>(nb + TILE, V, (t + 1) * 64, p.S, wid, lane);
+            }
+        }
+        if (t < nkv_w) {
+            // S^T = K Q^T: the K fragments by asm ds_read_b128 with counted waits (the builtin
+            // loads were each waited for right before their MFMA: the compiler reused one
+            // register set). Sub-tile 0's reads go out first; each of sub-tile 1's reads is
+            // issued after the MFMA that frees its registers' counterpart.
+            f32x16 sc[2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) sc[kt][i] = 0.f;
+            u32x4 ka[KS], kb[KS];
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk)
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ka[kk]) : "v"(koff[kk]), "i"(BUF * 2 * TILE));
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(KS - 1) : "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ka[kk]), qf[kk], sc[0], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kb[kk]) : "v"(koff[kk]), "i"(BUF * 2 * TILE + 32 * RB));
+            }
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(KS - 1 - kk) : "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kb[kk]), qf[kk], sc[1], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // mask only on tiles that cross the diagonal or the sequence end (uniform test)
+            if (t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > q0)) {
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int key = t * 64 + 32 * kt + 8 * (i >> 2) + 4 * hf + (i & 3);
+                        if (key >= p.S || (CAUSAL && key > myq)) sc[kt][i] = -INFINITY;
+                    }
+            }
+            float mt = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sc[kt][i]);
+            mt = half_max(mt);
+            // online softmax in the log2 domain with the lazy rescale of k_attn_fwd (the
+            // reference max moves only when the tile's max exceeds it by more than 8)
+            const float mts = mt * p.scale_log2;
+            const bool move = mts > m + 8.f;
+            if (__ballot(move)) {
+                const float mn = move ? mts : m;
+                const float alpha = __builtin_amdgcn_exp2f(m - mn);
+                l *= alpha;
+#pragma unroll
+                for (int d = 0; d < ND; ++d) o[d] *= alpha;
+                m = mn;
+            }
+            const float mref = (m == -INFINITY) ? 0.f : m;
+            float ls[4] = {0.f, 0.f, 0.f, 0.f};   // four independent add chains
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][i], p.scale_log2, -mref));
+                    sc[kt][i] = e;
+                    ls[i & 3] += e;
+                }
+            l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+            bf16x8 pf[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[s][j] = (bf16)sc[s >> 1][8 * (s & 1) + j];
+            // O^T += V^T P^T: per 32-dim tile 8 transposed reads (4 key steps x 2 halves), the
+            // next tile's reads in flight while this one's MFMAs run
+            u32x2 vr[2][8];
+#define KD_F32_RD(D, SET)                                                                                        \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                                              \
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[SET][2 * s]) : "v"(vaddr[D]), "i"(BUF * 2 * TILE + (16 * s) * RB));     \
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[SET][2 * s + 1]) : "v"(vaddr[D]), "i"(BUF * 2 * TILE + (16 * s + 8) * RB)); \
+    }
+#define KD_F32_MM(D, SET)                                                                                        \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                                              \
+        const bf16x8 vf = cat4(__builtin_bit_cast(bf16x4, vr[SET][2 * s]), __builtin_bit_cast(bf16x4, vr[SET][2 * s + 1])); \
+        o[D] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], o[D], 0, 0, 0);                                 \
+    }
+#define KD_F32_WAIT(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory"); __builtin_amdgcn_sched_barrier(0);
+            KD_F32_RD(0, 0)
+            KD_F32_RD(1, 1)
+            KD_F32_WAIT(8)
+            KD_F32_MM(0, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ND > 2) { KD_F32_RD(2, 0) KD_F32_WAIT(8) }
+            else { KD_F32_WAIT(0) }
+            KD_F32_MM(1, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ND > 2) {
+                if constexpr (ND > 3) { KD_F32_RD(3, 1) KD_F32_WAIT(8) }
+                else { KD_F32_WAIT(0) }
+                KD_F32_MM(2, 0)
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (ND > 3) {
+                    KD_F32_WAIT(0)
+                    KD_F32_MM(3, 1)
+                }
+            }
+#undef KD_F32_RD
+#undef KD_F32_MM
+#undef KD_F32_WAIT
+        }
+        if (RS && t + 1 < nkv) {
+            char* nb = smem + (BUF ^ 1) * 2 * TILE;
+            stg.write_k(nb, stk);
+            stg.write_v(nb + TILE, stv);
+        }
+        uint64_t ta = 0;
+        if (ST) { ta = __builtin_amdgcn_s_memtime(); st_cmp += ta - st_prev; st_n += t < nkv_w; }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (ST) { st_prev = __builtin_amdgcn_s_memtime(); st_bar += st_prev - ta; }
+    };
+    int t = 0;
+    for (; t + 1 < nkv; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        tile(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
+    l = half_sum(l);
+    if (ST) {
+        const uint64_t te = __builtin_amdgcn_s_memtime();
+        if (lane == 0) {
+            uint32_t* w = (uint32_t*)(const_cast<bf16*>(Q) + (int64_t)q0 * HDP);
+            w[0] = (uint32_t)st_pro; w[1] = (uint32_t)st_cmp; w[2] = (uint32_t)st_bar;
+            w[3] = (uint32_t)(te - st_prev); w[4] = (uint32_t)(te - st_t0); w[5] = (uint32_t)st_n; w[6] = (uint32_t)nkv;
+            w[7] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - st_r0);   // 100 MHz ticks
+        }
+    }
+    if (myq < p.S) {
+        const float inv = 1.f / l;
+        bf16* orow = p.o + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int dd = 32 * d + 8 * g + 4 * hf;
+                if (dd < p.hd) {
+                    bf16x4 w;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[d][4 * g + r] * inv);
+                    *(bf16x4*)(orow + dd) = w;
+                }
+            }
+        if (hf == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq] = (m + log2f(l)) * 0.6931471805599453f;
+    }
+}
+
+// k_attn_fwd32 software-pipelined at 32-key sub-tile granularity. In k_attn_fwd32 every step
+// of a tile waits on the previous one (QK^T -> max -> exp -> PV), and with two waves per SIMD
+// the waves spent ~half their lifetime stalled on those dependencies (SQ_WAIT_INST_ANY), the
+// matrix pipe 34% busy. Here, per sub-tile u (32 keys; S(u) already computed):
+//   phase A: the QK^T MFMAs of sub-tile u+1, and between them the row max / rescale test /
+//            exps of sub-tile u and the transposed V reads of PV(u)
+//   phase B: the PV(u) MFMAs, and between them the bf16 packing of P(u), the row-sum adds and
+//            the K fragment reads of sub-tile u+2
+// Every LDS read is inline asm and every group is pinned by sched_barrier, so the instruction
+// stream is the one written here. Rule for the asm reads (the round-2 fault class): a register
+// an asm read is still filling never crosses a basic-block boundary, and the s_waitcnt that
+// retires it names it as an in/out operand, so no compiler copy of it can be placed before
+// the wait (a PHI copy at a branch merge did exactly that in a first version: wrong outputs
+// whenever a workgroup had one K/V tile). Hence the V^T reads of PV(u) are issued only after
+// phase A's rescale branch and retired at the start of phase B, and the K reads of sub-tile
+// u + 2 are retired at the end of phase B. The K image is read two
+// sub-tiles ahead: tile t+1's K must have landed while tile t is processed, so the K ring is
+// filled one tile ahead of the V ring (LDS: K slots [0, 2 TILE), V slots [2 TILE, 4 TILE)).
+// The causal per-wave skip is per sub-tile (a wave stops at its diagonal sub-tile).
+// LDS reads with an immediate offset (asm: not tracked by the compiler's lgkmcnt; the caller
+// waits). Functions, not asm in the generic lambdas below (clang rejects captured asm operands
+// there).
+template <int OFF> __device__ __forceinline__ void lds_b128(u32x4& dst, uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+template <int OFF> __device__ __forceinline__ void lds_tr16(u32x2& dst, uint32_t addr) {
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+
+// s_waitcnt lgkmcnt(0) that the compiler sees as (re)defining the N registers of r: no use or
+// copy of them can be scheduled before it (asm reads are invisible to its own lgkmcnt tracking)
+template <int N, typename T> __device__ __forceinline__ void wait_lgkm0_def(T (&r)[N]) {
+    static_assert(N <= 16, "wait_lgkm0_def: at most 16 registers");
+    if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) :: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) :: "memory");
+    else if constexpr (N == 8)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]) :: "memory");
+    else if constexpr (N == 12)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
+                     "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]) :: "memory");
+    else if constexpr (N == 16)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
+                     "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15]) :: "memory");
+    else static_assert(N == 4, "wait_lgkm0_def: unsupported count");
+}
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F> __device__ __forceinline__ void static_for(F&& f) {
+    static_for_(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int HDP, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) k_attn_fwd32p(AttnP p) {
+    constexpr int RB = Geo<HDP>::RB;
+    constexpr int TILE = 64 * RB;
+    constexpr int KS = HDP == 96 ? 5 : HDP / 16;               // 16-deep QK^T steps
+    constexpr int ND = HDP == 64 ? 2 : (HDP == 96 ? 3 : 4);    // 32-dim O^T tiles
+    constexpr int NV = 4 * ND;                                 // V^T reads per sub-tile
+    constexpr int VPS = (NV + KS - 3) / (KS - 2);              // V^T reads per phase-A slot 2..KS-1
+    static_assert(KS <= 2 * ND, "phase B issues one K read per PV MFMA");
+    static_assert(NV <= 16 && KS <= 16, "at most 16 LDS reads in flight (as k_attn_fwd: issue stalls at the counter limit)");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r32 = lane & 31, hf = lane >> 5;
+    const int nqb = (p.S + 127) / 128;
+    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
+    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
+    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
+    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const int q0 = qb * 128 + wid * 32;
+    const int myq = q0 + r32;
+
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+        qf[kk] = myq < p.S ? *(const bf16x8*)(Q + (int64_t)myq * HDP + kk * 16 + 8 * hf) : (bf16x8){};
+    f32x16 o[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+    float m = -INFINITY, l = 0.f;
+
+    const int nkv_all = (p.S + 63) / 64;
+    const int nkv = CAUSAL ? min((qb + 1) * 2, nkv_all) : nkv_all;
+    const int nsub_all = (p.S + 31) / 32;
+    const int nsub_w = CAUSAL ? min(nsub_all, q0 / 32 + 1) : nsub_all;   // the wave's sub-tiles
+
+    const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+    uint32_t koff[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) koff[kk] = sbase + r32 * RB + (((2 * kk + hf) ^ swK<RB>(r32)) << 4);
+    uint32_t vaddr[ND];
+    {
+        const int row = 4 * hf + ((lane >> 2) & 3);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            const int col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            vaddr[d] = sbase + 2 * TILE + row * RB + ((((col >> 3) ^ swV32<RB>(row))) << 4) + ((col & 4) << 1);
+        }
+    }
+    // K(0) -> K slot 0, V(0) -> V slot 0, K(1) -> K slot 1
+    stage_kv32<HDP, false>(smem, K, 0, p.S, wid, lane);
+    stage_kv32<HDP, true>(smem + 2 * TILE, V, 0, p.S, wid, lane);
+    if (nkv > 1) stage_kv32<HDP, false>(smem + TILE, K, 64, p.S, wid, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    u32x4 kf[KS];   // K fragments of the sub-tile whose QK^T runs next
+    f32x16 sc;      // S^T of the current sub-tile (raw scores, then exps)
+    auto kread = [&](auto kk_c, auto off_c) {
+        constexpr int KK = decltype(kk_c)::value, OFF = decltype(off_c)::value;
+        lds_b128<OFF>(kf[KK], koff[KK]);
+    };
+#define KD_WAIT(N) asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(N) : "memory")
+#define KD_SB __builtin_amdgcn_sched_barrier(0)
+    // prologue: S(0) from K(0) rows 0-31, then the reads of K(0) rows 32-63 (sub-tile 1)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sc[i] = 0.f;
+    static_for<KS>([&](auto kk_c) { kread(kk_c, std::integral_constant<int, 0>{}); });
+    KD_WAIT(0);
+    KD_SB;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[kk]), qf[kk], sc, 0, 0, 0);
+    KD_SB;
+    static_for<KS>([&](auto kk_c) { kread(kk_c, std::integral_constant<int, 32 * RB>{}); });
+    wait_lgkm0_def<KS>(kf);
+    __syncthreads();   // every wave's K(0) reads are done before K(2) overwrites slot 0
+
+    // one 32-key sub-tile u = 2t + H2: V(t) in V slot BUF; its successor's K fragments are in
+    // kf (in flight); the K of sub-tile u + 2 is K(t+1) in slot BUF ^ 1
+    auto sub = [&](const int u, auto buf_c, auto h2_c) {
+        constexpr int BUF = decltype(buf_c)::value, H2 = decltype(h2_c)::value;
+        constexpr int VOFF = BUF * TILE + H2 * 32 * RB;
+        constexpr int KNEXT = (BUF ^ 1) * TILE + H2 * 32 * RB;
+        f32x16 sn;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sn[i] = 0.f;
+        u32x2 vr[NV];   // read vi: k-step vi / (2 ND), dims tile (vi / 2) % ND, key half vi & 1
+        auto vread = [&](auto vi_c) {
+            constexpr int VI = decltype(vi_c)::value;
+            constexpr int S_ = VI / (2 * ND), D_ = (VI / 2) % ND, HS = VI & 1;
+            lds_tr16<VOFF + (16 * S_ + 8 * HS) * RB>(vr[VI], vaddr[D_]);
+        };
+        const bool diag = (32 * u + 31 >= p.S) || (CAUSAL && 32 * u + 31 > q0);
+        float mt = -INFINITY, mref = 0.f;
+        float ls[4] = {0.f, 0.f, 0.f, 0.f};
+        // ---- phase A: QK^T(u+1) || V^T reads of PV(u) || max, rescale, exps of S(u)
+        static_for<KS>([&](auto kk_c) {
+            constexpr int KKc = decltype(kk_c)::value;
+            KD_SB;
+            // pin the MFMA between this slot's wait and the next slot (the DAG scheduler otherwise
+            // sinks all but the first two to the end of phase A): its operand passes through an
+            // empty volatile asm here, and its result through one at the end of the slot
+            asm volatile("" : "+v"(kf[KKc]));
+            sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[KKc]), qf[KKc], sn, 0, 0, 0);
+            KD_SB;
+            static_for<VPS>([&](auto j_c) {
+                constexpr int VI = VPS * (KKc - 2) + decltype(j_c)::value;
+                if constexpr (KKc >= 2 && VI < NV) vread(std::integral_constant<int, VI>{});
+            });
+            if constexpr (KKc == 0) {
+                if (diag) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int key = 32 * u + 8 * (i >> 2) + 4 * hf + (i & 3);
+                        if (key >= p.S || (CAUSAL && key > myq)) sc[i] = -INFINITY;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) mt = fmaxf(mt, sc[i]);
+            } else if constexpr (KKc == 1) {
+#pragma unroll
+                for (int i = 8; i < 16; ++i) mt = fmaxf(mt, sc[i]);
+                mt = half_max(mt);
+                // lazy rescale (k_attn_fwd): the reference max moves only by more than 8
+                const float mts = mt * p.scale_log2;
+                const bool move = mts > m + 8.f;
+                if (__ballot(move)) {
+                    const float mn = move ? mts : m;
+                    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+                    l *= alpha;
+#pragma unroll
+                    for (int d = 0; d < ND; ++d) o[d] *= alpha;
+                    m = mn;
+                }
+                mref = (m == -INFINITY) ? 0.f : m;
+            } else {
+                constexpr int E0 = (KKc - 2) * 16 / (KS - 2), E1 = (KKc - 1) * 16 / (KS - 2);
+#pragma unroll
+                for (int i = E0; i < E1; ++i) {
+                    const float e = __builtin_amdgcn_exp2f(fmaf(sc[i], p.scale_log2, -mref));
+                    sc[i] = e;
+                    ls[i & 3] += e;
+                }
+            }
+            KD_SB;
+            asm volatile("" :: "v"(sn));
+        });
+        // ---- phase B: PV(u) || P(u) packing, row sums, K reads of sub-tile u + 2
+        KD_SB;
+        wait_lgkm0_def<NV>(vr);
+        KD_SB;
+        bf16x8 pf[2];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[0][j] = (bf16)sc[j];
+        static_for<2 * ND>([&](auto j_c) {
+            constexpr int J = decltype(j_c)::value, S_ = J / ND, D_ = J % ND;
+            KD_SB;
+            const bf16x8 vf = cat4(__builtin_bit_cast(bf16x4, vr[2 * J]), __builtin_bit_cast(bf16x4, vr[2 * J + 1]));
+            o[D_] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[S_], o[D_], 0, 0, 0);
+            KD_SB;
+            if constexpr (J < KS) kread(std::integral_constant<int, J>{}, std::integral_constant<int, KNEXT>{});
+            if constexpr (J == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[1][j] = (bf16)sc[8 + j];
+            }
+            if constexpr (J == 1) l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+        });
+        KD_SB;
+        wait_lgkm0_def<KS>(kf);
+        KD_SB;
+        sc = sn;
+    };
+    auto tile = [&](const int t, auto buf_c) {
+        constexpr int BUF = decltype(buf_c)::value;
+        // K(t+2) -> K slot BUF (K(t) was last read in tile t-1), V(t+1) -> V slot BUF ^ 1
+        if (t + 2 < nkv) stage_kv32<HDP, false>(smem + BUF * TILE, K, (t + 2) * 64, p.S, wid, lane);
+        if (t + 1 < nkv) stage_kv32<HDP, true>(smem + 2 * TILE + (BUF ^ 1) * TILE, V, (t + 1) * 64, p.S, wid, lane);
+        if (2 * t < nsub_w) sub(2 * t, buf_c, std::integral_constant<int, 0>{});
+        if (2 * t + 1 < nsub_w) sub(2 * t + 1, buf_c, std::integral_constant<int, 1>{});
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+#undef KD_WAIT
+#undef KD_SB
+    int t = 0;
+    for (; t + 1 < nkv; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        tile(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
+    l = half_sum(l);
+    if (myq < p.S) {
+        const float inv = 1.f / l;
+        bf16* orow = p.o + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int dd = 32 * d + 8 * g + 4 * hf;
+                if (dd < p.hd) {
+                    bf16x4 w;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[d][4 * g + r] * inv);
+                    *(bf16x4*)(orow + dd) = w;
+                }
+            }
+        if (hf == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq] = (m + log2f(l)) * 0.6931471805599453f;
+    }
+}
+
 // ------------------------------------------------------------------ backward ----
 struct AttnBwdP {
     const bf16* q; const bf16* k; const bf16* v;   // [B, heads, S, HDP]
@@ -376,13 +985,6 @@ __device__ __forceinline__ bf16x4 tr_read_k_asm(const char* lds, int r, int d) {
     u32x2 v;
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)a));
     return __builtin_bit_cast(bf16x4, v);
-}
-
-__device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
-    bf16x8 r;
-    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
-    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
-    return r;
 }
 
 // dK / dV for 64 keys of ONE query head (4 waves x 16 keys, key on the lane), looping
@@ -811,13 +1413,24 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
             d->B, d->H, d->HKV, d->S, d->hd, (float)(1.4426950408889634 / std::sqrt((double)d->hd))};
     // NQ query sub-tiles per wave (KD_ATTN_FWD_NQ=1 restores one, for A/B)
     static const int nq = [] { const char* e = std::getenv("KD_ATTN_FWD_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
-    dim3 grid(d->H, d->B, (d->S + 64 * nq - 1) / (64 * nq));
+    // KD_ATTN_FWD_V (A/B and diagnostics): unset / 32 = k_attn_fwd32 (LDS-DMA staging), 35 = its
+    // register-staged build, 33 = the sub-tile-pipelined k_attn_fwd32p, 34 = the stamp build,
+    // 16 = the 16x16x32 k_attn_fwd
+    // (read per call, so a test can switch variants inside one process)
+    const char* fve = std::getenv("KD_ATTN_FWD_V");
+    const int fv = fve ? std::atoi(fve) : 0;
+    const bool v16 = fv == 16;
+    dim3 grid(d->H, d->B, v16 ? (d->S + 64 * nq - 1) / (64 * nq) : (d->S + 127) / 128);
     hipStream_t st = as_stream(stream_);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem = 2 * 2 * 64 * rb;
 #define LAUNCH(HD, C)                                                                                \
     do {                                                                                             \
-        if (nq == 2) hipLaunchKernelGGL((k_attn_fwd<HD, C, 2>), grid, dim3(256), smem, st, p);       \
+        if (fv == 0 || fv == 32) hipLaunchKernelGGL((k_attn_fwd32<HD, C, false>), grid, dim3(256), smem, st, p); \
+        else if (fv == 35) hipLaunchKernelGGL((k_attn_fwd32<HD, C, true>), grid, dim3(256), smem, st, p); \
+        else if (fv == 33) hipLaunchKernelGGL((k_attn_fwd32p<HD, C>), grid, dim3(256), smem, st, p); \
+        else if (fv == 34) hipLaunchKernelGGL((k_attn_fwd32<HD, C, false, true>), grid, dim3(256), smem, st, p); \
+        else if (nq == 2) hipLaunchKernelGGL((k_attn_fwd<HD, C, 2>), grid, dim3(256), smem, st, p);  \
         else hipLaunchKernelGGL((k_attn_fwd<HD, C, 1>), grid, dim3(256), smem, st, p);               \
     } while (0)
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }

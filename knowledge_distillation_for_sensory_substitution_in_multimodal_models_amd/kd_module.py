@@ -170,7 +170,7 @@ class _ErrorWatch:
         # forward, before the next step's teacher forward: all on this stream)
         self.snapshot = self.words.clone()
         self.host[slot].copy_(self.words[0:6], non_blocking=True)
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(blocking=True)   # a host wait on it sleeps instead of spinning
         ev.record()
         self.pending.append((ev, slot, info))
 

@@ -1,7 +1,9 @@
 """Flash attention fwd/bwd (kd_attn_fwd / kd_attn_bwd) against a torch fp32 reference.
 
 Inputs are bf16; the reference runs in fp32 on the same bf16 values.  Tolerances:
-o (bf16 out, P rounded to bf16 in the kernel): |err| <= 2e-2 * rms(ref) + 1e-2 |ref|;
+o (bf16 out, P rounded to bf16 in the kernel): |err| <= 2e-2 * rms(ref) + 2e-2 |ref| + 2^-8 (P|V|)
+(the last term bounds the bf16 rounding of P, which dominates where a row's output cancels to ~0:
+an early causal row of the 28-head teacher at S = 1536 sits at 3e-3 there);
 lse 1e-4 relative; grads 8e-2 * rms(ref) + 3e-2 |ref|: P and dS enter the MFMAs as bf16
 (as in FlashAttention-2) and the outputs are bf16; the worst elements are early causal
 rows (1-2 visible keys, O(1) gradients) where one bf16 ulp of dS is ~5% of rms(grad).
@@ -33,10 +35,17 @@ def _ref(q, k, v, causal, hd):
     return o, lse
 
 
-def _close(got, ref, tol, rtol=None):
+def _ref_pabs(q, k, v, causal, hd):
+    """softmax(s) @ |v|: the scale of the bf16-P rounding error of each output element"""
+    return _ref(q, k, v.abs(), causal, hd)[0]
+
+
+def _close(got, ref, tol, rtol=None, extra=None):
     ref = ref.float()
     err = (got.float() - ref).abs()
     bound = tol * ref.pow(2).mean().sqrt() + (tol if rtol is None else rtol) * ref.abs()
+    if extra is not None:
+        bound = bound + extra
     assert bool((err <= bound).all()), f"max err {err.max().item():.3e}, rms ref {ref.pow(2).mean().sqrt().item():.3e}"
 
 
@@ -48,6 +57,8 @@ CASES = [  # B, H, HKV, S, hd, hdp, causal
     (1, 3, 3, 100, 64, 64, False),
     (1, 14, 2, 1536, 64, 64, True),       # student at the step's full sequence length
     (1, 16, 16, 729, 72, 96, False),      # SigLIP, all heads
+    (1, 28, 4, 1536, 128, 128, True),     # teacher at the step's full sequence length
+    (1, 2, 2, 33, 128, 128, False),       # one partial 64-key tile, 33 of 128 query rows
 ]
 
 
@@ -65,9 +76,35 @@ def test_attn_fwd(B, H, HKV, S, hd, hdp, causal, dev):
     ops = _ops()
     q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev)
     o, lse = ops.attn_fwd(q, k, v, hd, causal)
-    ro, rlse = _ref(q[..., :hd].float(), k[..., :hd].float(), v[..., :hd].float(), causal, hd)
-    _close(o, ro.permute(0, 2, 1, 3), 2e-2)
+    qf, kf, vf = q[..., :hd].float(), k[..., :hd].float(), v[..., :hd].float()
+    ro, rlse = _ref(qf, kf, vf, causal, hd)
+    pabs = _ref_pabs(qf, kf, vf, causal, hd).permute(0, 2, 1, 3)
+    _close(o, ro.permute(0, 2, 1, 3), 2e-2, extra=2.0 ** -8 * pabs)
     assert (lse - rlse).abs().max().item() < 1e-3 * rlse.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("variant", ["16", "32"])
+@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", [CASES[1], CASES[2], CASES[3], CASES[7], CASES[8]])
+def test_attn_fwd_variants_agree(B, H, HKV, S, hd, hdp, causal, variant, dev):
+    """The pipelined 32x32x16 kernel (default), the unpipelined one (KD_ATTN_FWD_V=32) and the
+    16x16x32 one (=16) compute the same softmax; they differ only in the fp32 summation order
+    of the scores / row sums and the sub-tile width of the lazy rescale (which changes the
+    bf16 rounding of P): outputs within 2^-7 (|o| + P|V|), lse within 1e-5 relative."""
+    import os
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev)
+    outs = []
+    try:
+        for var in ("0", variant):
+            os.environ["KD_ATTN_FWD_V"] = var   # read by the launcher on every call
+            outs.append(ops.attn_fwd(q, k, v, hd, causal))
+    finally:
+        os.environ.pop("KD_ATTN_FWD_V", None)
+    (o0, l0), (o1, l1) = outs
+    d = (o0.float() - o1.float()).abs()
+    pabs = _ref_pabs(q[..., :hd].float(), k[..., :hd].float(), v[..., :hd].float(), causal, hd).permute(0, 2, 1, 3)
+    assert bool((d <= 2.0 ** -7 * (o0.float().abs() + pabs) + 1e-4).all()), d.max().item()
+    assert (l0 - l1).abs().max().item() <= 1e-5 * l0.abs().max().item() + 1e-5
 
 
 @pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
