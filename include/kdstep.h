@@ -169,7 +169,9 @@ typedef struct {
                                  17-19 diagnostic builds of 16 (tools/stamp_gemm.py, tools/ablate_gemm.py);
                                  20 256x256 8-wave ping-pong (two wave groups alternate on each SIMD);
                                  21 stream-K on 16 (256 workgroups take equal runs of the tiles' k-steps,
-                                 shared tiles folded from fp32 partial planes; needs workspace) */
+                                 shared tiles folded from fp32 partial planes; needs workspace);
+                                 22 16 with register staging instead of LDS-DMA (K-major operands;
+                                 measured slower, kept for A/B: tools/ab_gemm_rs.py) */
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;

@@ -892,10 +892,23 @@ __device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, i
 // then carries no pre-activation output); bit 1 drops the in-loop DMA (timing ablation:
 // WRONG results); bit 6 re-reads stage 0 for every stage (same addresses, L2-hot:
 // separates issue cost from memory-system cost; WRONG results).
+// Bit 3 (K-major x K-major only): REGISTER staging instead of LDS-DMA. A k-step's 64
+// MFMAs (16x16x32, each holding the SIMD's vector issue for 8 of its 16 cycles) leave 512
+// issue cycles for everything else, and its 8 LDS-DMA pieces cost ~60 each (more beside
+// 16 fragment reads: MI355X_MICROARCH constants table) — the measured step is 1243 cycles,
+// not 1024, and the kernel keeps the matrix pipe 65-66% busy where hipBLASLt keeps it 77-81%
+// (profiles/r03/pmc_vs_blas.txt). Here unit u of step t writes piece u of stage t+4 (loaded
+// during step t-1) into slot t%4 with one ds_write_b128 at the same lane-linear position the
+// DMA wrote, then loads piece u of stage t+5 into the same 4 VGPRs (buffer load, the same
+// pre-swizzled source offset): same LDS image, same ring, same barriers. Measured (forced
+// variant 22, tools/ab_gemm_rs.py): bit-exact, and 2-11% SLOWER than the LDS-DMA build on every
+// forward shape of the step (gate|up+SwiGLU 1291 -> 1379 us, lm_head 5320 -> 5808 us): the DMA
+// issue is not what holds v8 below hipBLASLt's MFMA-busy fraction. Kept as a forced variant only.
 // one 256x256 output tile over p's K range (the whole K, a split-K plane or a stream-K piece)
 template <bool A_MN, bool B_MN, int EXP>
 __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     constexpr bool STAMP = EXP & 1, NODMA = EXP & 2, HOT = EXP & 64;
+    constexpr bool RS = (EXP & 8) && !A_MN && !B_MN;
     uint32_t* stamps = nullptr;
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
     uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
@@ -957,18 +970,58 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     };
     using FullT = std::integral_constant<bool, true>;
     using PartT = std::integral_constant<bool, false>;
+    // register staging (RS): piece u of stage st -> rsb[u] (the DMA's source offsets), and
+    // rsb[u] -> its lane-linear 16 B of slot sl
+    u32x4 rsb[8];
+    auto rs_load = [&](int st, int u, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        const bool isA = u < 4;
+        const int i = wid * 4 + (u & 3);
+        uint32_t v = isA ? va[u & 3] : vb[u & 3];
+        int soff = st * BK2 * 2;
+        if (!FULL) {
+            const int kleft = K - st * BK2;
+            if (kleft < BK2) {
+                const int row = 16 * i + (lane >> 2);
+                const int gc = (lane & 3) ^ f4(row);
+                if (gc * 8 >= kleft) v = OOB;
+                if (kleft <= 0) soff = 0;
+            }
+        }
+        rsb[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(isA ? rsAk : rsBk, v, soff, 0));
+    };
+    auto rs_write = [&](int sl, int u) {
+        const int i = wid * 4 + (u & 3);
+        *(u32x4*)(smem + sl * SS + (u < 4 ? 0 : SA) + i * 1024 + lane * 16) = rsb[u];
+    };
     f32x4 acc[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int ra = wm * 128, cb = wn * 128;
+    if (RS) {   // stages 0..3 into slots 0..3 (two register sets in flight), then stage 4 -> rsb
+        u32x4 alt[8];
 #pragma unroll
-    for (int st = 0; st < NS8; ++st)
+        for (int u = 0; u < 8; ++u) rs_load(0, u, PartT{});
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dma(st, st, u, PartT{});
-    if (NODMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
+        for (int st = 0; st < NS8; ++st) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) alt[u] = rsb[u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) rs_load(st + 1, u, PartT{});
+#pragma unroll
+            for (int u = 0; u < 8; ++u) *(u32x4*)(smem + st * SS + (u < 4 ? 0 : SA) + (wid * 4 + (u & 3)) * 1024 + lane * 16) = alt[u];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+#pragma unroll
+        for (int st = 0; st < NS8; ++st)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) dma(st, st, u, PartT{});
+        if (NODMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
+    }
     __builtin_amdgcn_s_barrier();
     uint64_t tprev = 0;
     if (STAMP) { tprev = __builtin_amdgcn_s_memtime(); s_pro = tprev - ts0; }
@@ -985,7 +1038,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         uint64_t ta_ = 0, tb_ = 0;                                                                            \
         if (STAMP) ta_ = __builtin_amdgcn_s_memtime();                                                        \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                    \
-        if (!NODMA) wait_vm<16>();                                                                            \
+        if (!NODMA && !RS) wait_vm<16>();                                                                     \
         __builtin_amdgcn_s_barrier();                                                                         \
         if (STAMP) {                                                                                          \
             tb_ = __builtin_amdgcn_s_memtime();                                                               \
@@ -1001,7 +1054,9 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         const char* na_ = smem + (((SL) + 1) % NS8) * SS;                                                     \
         _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
             mfma_agpr(acc[u][0], CB[0], CA[u]); KD_SB                                                         \
-            dma(t_ + NS8, (SL), u, FT{}); KD_SB                                                               \
+            if (RS) { rs_write((SL), u); rs_load(t_ + NS8 + 1, u, FT{}); }                                    \
+            else dma(t_ + NS8, (SL), u, FT{});                                                                \
+            KD_SB                                                                                             \
             mfma_agpr(acc[u][1], CB[1], CA[u]); KD_SB                                                         \
             if (u < 4) NA[2 * u] = frag2<256, A_MN>(na_, ra + 2 * u * 16, lane);                              \
             KD_SB                                                                                             \
@@ -1021,7 +1076,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         }                                                                                                     \
     }
     int t = 0;
-    for (; t + 2 * NS8 <= nk_full; t += NS8) {   // every DMA of these steps lies inside K
+    for (; t + 2 * NS8 + (RS ? 1 : 0) <= nk_full; t += NS8) {   // every DMA / staged load of these steps lies inside K
         KD_G8_STEP(0, xa, xb, ya, yb, FullT)
         KD_G8_STEP(1, ya, yb, xa, xb, FullT)
         KD_G8_STEP(2, xa, xb, ya, yb, FullT)
@@ -1797,7 +1852,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldc >= w && d->ld_aux >= w && d->ldc % 8 == 0 && d->ld_aux % 8 == 0 &&
                        (uintptr_t)d->aux % 16 == 0, "gemm backward activation: ldc / ld_aux >= N (2N for dswiglu), 16-B rows");
     }
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 21), "gemm: unknown variant");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 22), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     KD_CHECK_SHAPE(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
@@ -1881,12 +1936,14 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
         pk.gx = (int)grid.x; pk.gy = 1;
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
+        else if (d->variant == 22)
+            hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
         return KD_OK;
     }
     const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,
-                                    // 16 v8 256x256 (4 waves, AGPR accumulators), 17-19 v8 diagnostics
+                                    // 16 v8 256x256 (4 waves, AGPR accumulators), 17-19 v8 diagnostics, 22 v8 register-staged (negative result, kept for A/B)
     if (force != 1 && big_ok) {
         const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
         const int tbm = pl.var == 4 ? 128 : 256, tbn = pl.var == 3 ? 128 : 256;
@@ -1941,6 +1998,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                     case 17: L8K(1) break;
                     case 18: L8K(2) break;
                     case 19: L8K(64) break;
+                    case 22: L8K(8) break;
                     default: L8(0) break;
                 }
 #undef L8K

@@ -379,3 +379,29 @@ def test_qkv_scatter_epilogue_equals_gemm_then_split(shape, variant, dev):
     torch.cuda.synchronize()
     for got, ref, n in ((q, q0, "q"), (k, k0, "k"), (v, v0, "v")):
         assert torch.equal(got, ref), f"{n}: {int((got != ref).sum())} elements differ"
+
+
+@pytest.mark.parametrize("M,N,K", [(6144 // 4, 896, 4864 // 2), (1456, 1152, 1152), (304, 520, 600), (4096, 4096, 4096),
+                                   (5832 // 4, 4304, 1152), (512, 512, 2248), (256, 768, 32), (300, 272, 4304)])
+def test_register_staged_v8_bitexact(M, N, K, dev):
+    """The register-staged v8 build (variant 22: buffer loads to VGPRs + ds_write_b128 instead of
+    LDS-DMA, the same LDS image) accumulates over the same k32 MFMA sequence as v8: bit for bit
+    equal, plain and with the epilogue (bias, gelu, residual, aux) and the SwiGLU build; K tails
+    of every length, partial tiles, K shorter than the prefetch ring."""
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=120)
+    w = _rand(N, K, dev=dev, seed=121, scale=0.05)
+    assert torch.equal(ops.gemm(a, w, variant=22, split_k=1), ops.gemm(a, w, variant=16, split_k=1))
+    bias = _rand(N, dev=dev, seed=122)
+    res = _rand(M, N, dev=dev, seed=123)
+    ax16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    ax22 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    o16 = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=res, aux=ax16, variant=16, split_k=1)
+    o22 = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=res, aux=ax22, variant=22, split_k=1)
+    assert torch.equal(o22, o16) and torch.equal(ax22, ax16)
+    if N % 256 == 0:
+        g16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        g22 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        s16 = ops.gemm(a, w, act="swiglu", aux=g16, variant=16)
+        s22 = ops.gemm(a, w, act="swiglu", aux=g22, variant=22)
+        assert torch.equal(s22, s16) and torch.equal(g22, g16)
