@@ -909,6 +909,7 @@ template <bool A_MN, bool B_MN, int EXP>
 __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     constexpr bool STAMP = EXP & 1, NODMA = EXP & 2, HOT = EXP & 64;
     constexpr bool RS = (EXP & 8) && !A_MN && !B_MN;
+
     uint32_t* stamps = nullptr;
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
     uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;

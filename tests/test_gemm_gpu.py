@@ -405,3 +405,4 @@ def test_register_staged_v8_bitexact(M, N, K, dev):
         s16 = ops.gemm(a, w, act="swiglu", aux=g16, variant=16)
         s22 = ops.gemm(a, w, act="swiglu", aux=g22, variant=22)
         assert torch.equal(s22, s16) and torch.equal(g22, g16)
+
