@@ -1190,6 +1190,222 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
     }
 }
 
+// k_attn_bwd_dkdv with TWO 16-key sub-tiles per wave (4 waves x 32 keys = 128 keys per
+// workgroup): every Q / dO row fragment and every transposed dO^T / Q^T read from LDS feeds
+// both sub-tiles' MFMAs. With one 16-key sub-tile a wave moves ~1 KiB of LDS per MFMA
+// (SigLIP: 44 KiB of fragment reads per 44 MFMAs per query tile, the CU's 256 B/clk at the
+// full MFMA rate): the kernel was LDS-bound at ~0.15 of peak. The 64-row query tile is taken
+// in two 32-row halves so the S / dP registers do not double. Same arithmetic per element as
+// k_attn_bwd_dkdv (bit-identical outputs).
+template <int HDP, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv2(AttnBwdP p) {
+    constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
+    constexpr int TILE = 64 * RB, BUF = 2 * TILE + 512;
+    constexpr bool HALF = HDP == 96;
+    constexpr int KSF = HALF ? KS - 1 : KS;
+    extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][Q TILE | dO TILE | lse2 64 | delta 64]
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, li = lane & 15;
+    const int kb0 = blockIdx.z * 128;
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int grp = p.H / p.HKV, kvh = h / grp;
+    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
+    const bf16* dO = p.dO + ((int64_t)b * p.S * p.H + h) * p.hd;
+    const float* LSE = p.lse + ((int64_t)b * p.H + h) * p.S;
+    const float* DEL = p.delta + ((int64_t)b * p.H + h) * p.S;
+    const int64_t ldo = (int64_t)p.H * p.hd;
+    const int kw0 = kb0 + wid * 32;   // the wave's first key (uniform)
+    int mykey[2];
+    bf16x8 kf[2][KS], vf[2][KS];
+    bf16x4 kh[2], vh[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        mykey[c] = kw0 + 16 * c + li;
+        kh[c] = (bf16x4){}; vh[c] = (bf16x4){};
+#pragma unroll
+        for (int kk = 0; kk < KSF; ++kk) {
+            if (mykey[c] < p.S) {
+                kf[c][kk] = *(const bf16x8*)(K + (int64_t)mykey[c] * HDP + kk * 32 + 8 * g);
+                vf[c][kk] = *(const bf16x8*)(V + (int64_t)mykey[c] * HDP + kk * 32 + 8 * g);
+            } else {
+                kf[c][kk] = (bf16x8){}; vf[c][kk] = (bf16x8){};
+            }
+        }
+        if (HALF && mykey[c] < p.S) {
+            kh[c] = *(const bf16x4*)(K + (int64_t)mykey[c] * HDP + KSF * 32 + 4 * g);
+            vh[c] = *(const bf16x4*)(V + (int64_t)mykey[c] * HDP + KSF * 32 + 4 * g);
+        }
+    }
+    f32x4 dk[2][DT], dv[2][DT];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int d = 0; d < DT; ++d) { dk[c][d] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[c][d] = dk[c][d]; }
+
+    int qoff[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) qoff[kk] = li * RB + (((kk * 4 + g) ^ swK<RB>(li)) << 4);
+    const int qhoff = li * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(li)) << 4) + (g & 1) * 8;
+    int troff[DT];
+    {
+        const int r = 4 * g + (li >> 2);
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+            troff[d] = r * RB + (((2 * d + ((li & 3) >> 1)) ^ swK<RB>(r)) << 4) + (li & 1) * 8;
+    }
+
+    const int nqt = (p.S + 63) / 64;
+    const int qt0 = CAUSAL ? kb0 / 64 : 0;
+    float lse_nx = 0.f;
+    auto stage = [&](char* buf, int qt) {
+        stage_kv<HDP, false>(buf, Q, qt * 64, p.S, wid, lane);
+        stage_rows_dma<HDP>(buf + TILE, dO, ldo, p.hd, qt * 64, p.S, wid, lane);
+        if (wid == 0) {
+            lse_nx = qt * 64 + lane < p.S ? LSE[qt * 64 + lane] : 0.f;
+            stage_vec64((float*)(buf + 2 * TILE + 256), DEL, qt * 64, p.S, lane);
+        }
+    };
+    auto put_lse = [&](char* buf) {
+        if (wid == 0) ((float*)(buf + 2 * TILE))[lane] = lse_nx * 1.4426950408889634f;
+    };
+    stage(smem, qt0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    put_lse(smem);
+    __syncthreads();
+    for (int qt = qt0; qt < nqt; ++qt) {
+        const int cur = (qt - qt0) & 1;
+        if (qt + 1 < nqt) stage(smem + (cur ^ 1) * BUF, qt + 1);
+        const char* lQ = smem + cur * BUF;
+        const char* lO = lQ + TILE;
+        const float* lL = (const float*)(lQ + 2 * TILE);
+        const float* lD = lL + 64;
+        const int q0 = qt * 64;
+        const uint32_t bq = (uint32_t)(uintptr_t)lQ;
+        // a 32-row half with no query at or past any of this wave's keys contributes nothing
+        // (causal: every P is 0); skip its MFMAs (uniform)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int qh0 = q0 + 32 * ks;
+            if (CAUSAL && qh0 + 31 < kw0) continue;
+            // S, dP for query rows qh0 + 16qs' + 4g + r (qs' = 0, 1) and both key sub-tiles
+            f32x4 s[2][2], dp[2][2];
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const int qs = 2 * ks + qq;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) { s[c][qq] = (f32x4){0.f, 0.f, 0.f, 0.f}; dp[c][qq] = s[c][qq]; }
+#pragma unroll
+                for (int kk = 0; kk < KSF; ++kk) {
+                    const bf16x8 qa = *(const bf16x8*)(lQ + qoff[kk] + qs * 16 * RB);
+                    const bf16x8 oa = *(const bf16x8*)(lO + qoff[kk] + qs * 16 * RB);
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        s[c][qq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[c][kk], s[c][qq], 0, 0, 0);
+                        dp[c][qq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[c][kk], dp[c][qq], 0, 0, 0);
+                    }
+                }
+                if (HALF) {
+                    const bf16x4 qa = *(const bf16x4*)(lQ + qhoff + qs * 16 * RB);
+                    const bf16x4 oa = *(const bf16x4*)(lO + qhoff + qs * 16 * RB);
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        s[c][qq] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(qa, kh[c], s[c][qq], 0, 0, 0);
+                        dp[c][qq] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(oa, vh[c], dp[c][qq], 0, 0, 0);
+                    }
+                }
+            }
+            if (qh0 + 31 >= p.S || kw0 + 31 >= p.S || (CAUSAL && kw0 + 31 > qh0)) {
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int q = qh0 + 16 * qq + 4 * g + r;
+                            if (q >= p.S || mykey[c] >= p.S || (CAUSAL && mykey[c] > q)) s[c][qq][r] = -INFINITY;
+                        }
+            }
+            const f32x2 sl2 = {p.scale_log2, p.scale_log2};
+            bf16x8 pfr[2], dsf[2];
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const int qs = 2 * ks + qq;
+                const f32x4 l2 = *(const f32x4*)(lL + 16 * qs + 4 * g), dl = *(const f32x4*)(lD + 16 * qs + 4 * g);
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        const f32x2 x = f32x2{s[c][qq][r], s[c][qq][r + 1]} * sl2 - f32x2{l2[r], l2[r + 1]};
+                        const f32x2 pv = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+                        const f32x2 ds = pv * (f32x2{dp[c][qq][r], dp[c][qq][r + 1]} - f32x2{dl[r], dl[r + 1]});
+                        pfr[c][4 * qq + r] = (bf16)pv[0]; pfr[c][4 * qq + r + 1] = (bf16)pv[1];
+                        dsf[c][4 * qq + r] = (bf16)ds[0]; dsf[c][4 * qq + r + 1] = (bf16)ds[1];
+                    }
+            }
+            // dV^T += dO^T P ; dK^T += Q^T dS: each transposed read feeds both key sub-tiles
+            bf16x4 o0[DT], o1[DT], x0[DT], x1[DT];
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
+                const uint32_t a = bq + troff[d];
+                if (ks == 0) {
+                    o0[d] = tr_read_off<TILE>(a);
+                    o1[d] = tr_read_off<TILE + 16 * RB>(a);
+                    x0[d] = tr_read_off<0>(a);
+                    x1[d] = tr_read_off<16 * RB>(a);
+                } else {
+                    o0[d] = tr_read_off<TILE + 32 * RB>(a);
+                    o1[d] = tr_read_off<TILE + 48 * RB>(a);
+                    x0[d] = tr_read_off<32 * RB>(a);
+                    x1[d] = tr_read_off<48 * RB>(a);
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
+                const bf16x8 ov = cat4(o0[d], o1[d]), xv = cat4(x0[d], x1[d]);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    dv[c][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ov, pfr[c], dv[c][d], 0, 0, 0);
+                    dk[c][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xv, dsf[c], dk[c][d], 0, 0, 0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (qt + 1 < nqt) put_lse(smem + (cur ^ 1) * BUF);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (mykey[c] >= p.S) continue;
+        if (grp == 1) {
+            bf16* dKr = p.dk + ((int64_t)(b * p.HKV + kvh) * p.S + mykey[c]) * HDP;
+            bf16* dVr = p.dv + ((int64_t)(b * p.HKV + kvh) * p.S + mykey[c]) * HDP;
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
+                const int dd = d * 16 + 4 * g;
+                bf16x4 wk, wv;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(dk[c][d][r] * p.scale); wv[r] = (bf16)dv[c][d][r]; }
+                *(bf16x4*)(dKr + dd) = wk;
+                *(bf16x4*)(dVr + dd) = wv;
+            }
+        } else {
+            float* dKr = p.dkp + ((int64_t)(b * p.H + h) * p.S + mykey[c]) * HDP;
+            float* dVr = p.dvp + ((int64_t)(b * p.H + h) * p.S + mykey[c]) * HDP;
+#pragma unroll
+            for (int d = 0; d < DT; ++d) {
+                const int dd = d * 16 + 4 * g;
+                *(f32x4*)(dKr + dd) = dk[c][d];
+                *(f32x4*)(dVr + dd) = dv[c][d];
+            }
+        }
+    }
+}
+
 // dK[b,kvh] = scale * sum_{h in group} dKp[b,h], dV likewise (d < 16*DT columns)
 __global__ void k_attn_group_sum(const float* __restrict__ dkp, const float* __restrict__ dvp, bf16* __restrict__ dk,
                                  bf16* __restrict__ dv, int B, int H, int HKV, int S, int hdp, int dcols, float scale) {
@@ -1441,6 +1657,20 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     return KD_OK;
 }
 
+// dK / dV launch: the two-sub-tile kernel for head dims 64 / 96 (at 128 its 2 x 2 x DT
+// accumulator tiles do not fit beside the fragments: the one-sub-tile kernel there; the 7B
+// teacher never runs a backward)
+template <int HD, bool C>
+void launch_dkdv(bool kv16, dim3 grid, size_t smem, hipStream_t st, const AttnBwdP& p) {
+    if constexpr (HD == 128) {
+        grid.z = (p.S + 63) / 64;
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<HD, C>), grid, dim3(256), smem, st, p);
+    } else {
+        if (kv16) hipLaunchKernelGGL((k_attn_bwd_dkdv<HD, C>), grid, dim3(256), smem, st, p);
+        else hipLaunchKernelGGL((k_attn_bwd_dkdv2<HD, C>), grid, dim3(256), smem, st, p);
+    }
+}
+
 size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d) {
     if (!d || d->HKV <= 0 || d->H == d->HKV) return 0;
     return (size_t)2 * d->B * d->H * d->S * d->hdp * 4;
@@ -1470,7 +1700,11 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, d->lse, d->delta,
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
                (float)(sc * 1.4426950408889634)};
-    dim3 grid(d->H, d->B, (d->S + 63) / 64);
+    // dK / dV: two 16-key sub-tiles per wave by default; KD_ATTN_BWD_V=16 selects the one-sub-tile
+    // kernel (A/B; read per call)
+    const char* bve = std::getenv("KD_ATTN_BWD_V");
+    const bool kv16 = bve && std::atoi(bve) == 16;
+    dim3 grid(d->H, d->B, kv16 ? (d->S + 63) / 64 : (d->S + 127) / 128);
     static const int nq_dq = [] { const char* e = std::getenv("KD_ATTN_DQ_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
     dim3 grid_q(d->H, d->B, (d->S + 64 * nq_dq - 1) / (64 * nq_dq));
     const int rb = d->hdp == 64 ? 128 : 256;
@@ -1478,7 +1712,7 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     const size_t smem_q = 2 * 2 * 64 * rb;
 #define LAUNCH(HD, C)                                                                         \
     do {                                                                                      \
-        hipLaunchKernelGGL((k_attn_bwd_dkdv<HD, C>), grid, dim3(256), smem_kv, st, p);       \
+        launch_dkdv<HD, C>(kv16, grid, smem_kv, st, p);                                     \
         KD_LAUNCH_CHECK("k_attn_bwd_dkdv");                                                   \
         if (nq_dq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p); \
         else hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 1>), grid_q, dim3(256), smem_q, st, p);            \

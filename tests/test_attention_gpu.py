@@ -123,3 +123,27 @@ def test_attn_bwd(B, H, HKV, S, hd, hdp, causal, dev):
     _close(dq[..., :hd], qf.grad, 8e-2, 3e-2)
     _close(dk[..., :hd], kf.grad, 8e-2, 3e-2)
     _close(dv[..., :hd], vf.grad, 8e-2, 3e-2)
+
+
+@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", [CASES[0], CASES[1], CASES[3], CASES[4], CASES[5], CASES[6]])
+def test_attn_bwd_dkdv_variants_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
+    """dK / dV with two 16-key sub-tiles per wave (default) == the one-sub-tile kernel
+    (KD_ATTN_BWD_V=16) bit for bit: the same MFMA sequence and arithmetic per element; only the
+    sharing of LDS fragments between the sub-tiles differs (and fully masked causal query
+    halves are skipped, which adds exact zeros)."""
+    import os
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=4)
+    o, lse = ops.attn_fwd(q, k, v, hd, causal)
+    g = torch.Generator().manual_seed(5)
+    do = torch.randn(B, S, H, hd, generator=g).to(dev, torch.bfloat16)
+    outs = []
+    try:
+        for var in ("0", "16"):
+            os.environ["KD_ATTN_BWD_V"] = var
+            outs.append(ops.attn_bwd(q, k, v, o, do, lse, hd, causal))
+    finally:
+        os.environ.pop("KD_ATTN_BWD_V", None)
+    (dq0, dk0, dv0), (dq1, dk1, dv1) = outs
+    sl = (Ellipsis, slice(0, hd))   # the head-dim padding [hd, hdp) is not an output
+    assert torch.equal(dk0[sl], dk1[sl]) and torch.equal(dv0[sl], dv1[sl]) and torch.equal(dq0[sl], dq1[sl])
