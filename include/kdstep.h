@@ -96,6 +96,13 @@ typedef struct {
                                bf16) instead of a bf16-rounded -1/n_valid (a systematic
                                bias of the whole gradient).  NULL: c = 1.               */
     int32_t dscale_given;   /* 1: read c from *dscale (an earlier call's; loss groups)    */
+    /* optional: the lm_head GEMMs' row statistics (kd_gemm_desc.row_stats) of THESE rows — the
+       student's with row_stats_vs = V_s and inv_t = 1/T, the teacher's with row_stats_vs = V_s,
+       inv_t = 1/T and top-2 — instead of the loss's own pass over both logit tensors
+       (k_row_stats). Same values up to fp32 summation order. Both or neither (KD_LOSS_NONE:
+       the student's alone). */
+    const float* s_row_stats;
+    const float* t_row_stats;
 } kd_loss_params;
 
 /* loss_out (device float[4]): [0] KD term (mean, incl. T^2, unweighted)
@@ -181,6 +188,20 @@ typedef struct {
     int32_t residual_dtype;   /* kd_dtype of residual: KD_DTYPE_BF16 (0) or KD_DTYPE_F32 (an fp32
                                  residual stream; then C must be fp32 and act NONE; bf16 path only) */
     const struct kd_qkv_scatter* qkv;   /* optional: q|k|v scatter epilogue (below); C unused */
+    /* optional: per-row softmax statistics of C, emitted by the epilogue (the lm_head GEMM feeding
+       kd_loss_fwd_bwd: the loss then skips its own pass over the logits, DT:155-192). For every
+       row m and 256-column tile j, 8 floats at row_stats + (m * ceil(N / 256) + j) * 8, over the
+       tile's bf16-rounded C (what the loss reads):
+         [0] max over the tile's columns < N        [1] sum exp(c - [0])
+         [2] max over its columns < row_stats_vs    [3] sum exp((c - [2]) * row_stats_inv_t)
+         [4..7] top-2 over columns < row_stats_vs: value, index (int32 bits), value, index
+                (larger value first, lower index on ties; only when row_stats_top2)
+       Requires bf16 C, K-major bf16 operands, no bias / activation / residual / aux /
+       accumulate; runs the 256x256 kernel without split-K. */
+    float* row_stats;
+    int32_t row_stats_vs;      /* column bound of [2..7] (the student vocab V_s); <= 0: N */
+    float row_stats_inv_t;     /* 1 / T of [3] */
+    int32_t row_stats_top2;
 } kd_gemm_desc;
 /* q|k|v scatter epilogue of a fused projection GEMM (the attention input of SigLIP / Qwen2:
  * HF5 siglip :250-270, qwen2 :80-110 view / transpose / apply_rotary_pos_emb): the output tile,
@@ -461,6 +482,12 @@ typedef enum {
     KD_FP8_ALL = 31
 } kd_fp8_family;
 int kd_model_set_fp8_families(kd_model* m, int families);
+
+/* Row statistics of the lm_head logits (kd_gemm_desc.row_stats, same layout), written by the
+ * lm_head GEMM's epilogue of every later kd_model_forward that produces logits: partials fp32
+ * [B*L, ceil(vocab / 256), 8]; vs / inv_t / top2 as kd_gemm_desc.row_stats_*.  The lm_head then
+ * runs bf16 (an fp8 lm_head family is ignored while this is set).  partials = NULL turns it off. */
+int kd_model_set_row_stats(kd_model* m, float* partials, int vs, float inv_t, int top2);
 
 /* Forward.  ids int64 [B, L]; pixels [n_tiles, 3, image, image] (kd_dtype: the batch's
  * vision tiles, e.g. the compact real tiles of kd_anyres_batch_map(tiles = 0)); src int32 [B*L]

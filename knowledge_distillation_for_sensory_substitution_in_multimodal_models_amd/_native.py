@@ -43,6 +43,8 @@ class KdLossParams(C.Structure):
         ("row_base", C.c_int32),
         ("dscale", C.c_void_p),
         ("dscale_given", C.c_int32),
+        ("s_row_stats", C.c_void_p),
+        ("t_row_stats", C.c_void_p),
     ]
 
 
@@ -74,6 +76,8 @@ class KdGemmDesc(C.Structure):
         ("ab_dtype", C.c_int32), ("a_scale", C.c_void_p), ("b_scale", C.c_void_p),
         ("residual_dtype", C.c_int32),
         ("qkv", C.c_void_p),
+        ("row_stats", C.c_void_p), ("row_stats_vs", C.c_int32), ("row_stats_inv_t", C.c_float),
+        ("row_stats_top2", C.c_int32),
     ]
 
 
@@ -179,6 +183,7 @@ SIGNATURES = {
     "kd_model_quantize_fp8": (_i32, [_vp, _vp, _vp, _vp]),
     "kd_model_set_fp8": (_i32, [_vp, _vp, _vp]),
     "kd_model_set_fp8_families": (_i32, [_vp, _i32]),
+    "kd_model_set_row_stats": (_i32, [_vp, _vp, _i32, _f32, _i32]),
     "kd_model_forward_workspace_size": (_sz, [_vp, _i32, _i32, _i32, _i32]),
     "kd_model_forward": (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _sz, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp]),

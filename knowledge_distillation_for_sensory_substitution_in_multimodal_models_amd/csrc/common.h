@@ -85,6 +85,24 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// top-2 with deterministic tie-break: larger value first, lower index on ties (the KD loss's
+// teacher klogits, DT:170-171; used by k_row_stats and the lm_head GEMM's row statistics).
+// Branch-free (selects only): the if/else-if form made hipcc keep (v1, i1, v2, i2) in a
+// scratch array indexed per lane (36 B of private memory, a scratch round trip per push).
+__device__ __forceinline__ bool top2_better(float a, int ia, float b, int ib) {
+    return a > b || (a == b && ia < ib);
+}
+__device__ __forceinline__ void top2_push(float v, int i, float& v1, int& i1, float& v2, int& i2) {
+    const bool b1 = top2_better(v, i, v1, i1);
+    const bool b2 = top2_better(v, i, v2, i2);
+    const float nv2 = b1 ? v1 : (b2 ? v : v2);
+    const int ni2 = b1 ? i1 : (b2 ? i : i2);
+    v1 = b1 ? v : v1;
+    i1 = b1 ? i : i1;
+    v2 = nv2;
+    i2 = ni2;
+}
+
 // Block-wide sum over NW waves using a caller-provided LDS scratch of >= NW floats.
 template <int NW>
 __device__ __forceinline__ float block_sum(float v, float* scratch) {

@@ -59,6 +59,10 @@ struct GemmP {
     // hidden kernel arguments, and the HIP runtime's per-stream kernel-argument pool (~1 MB)
     // then holds ~2000 queued GEMM launches instead of ~5000 before hipLaunchKernel blocks
     int gx, gy;
+    // per-row softmax statistics of the bf16 tile (kd_gemm_desc.row_stats; v8, K-major forward)
+    float* rst;
+    int rst_nt, rst_vs, rst_top2;
+    float rst_inv_t;
     // stream-K (v8): the launch's sk_grid workgroups split the tiles' sk_steps-deep K loops
     // evenly (one workgroup's run may cover the end of one tile and the start of the next);
     // a tile covered by several workgroups gets fp32 partial planes in sk_ws (plane stride
@@ -628,9 +632,85 @@ __device__ __forceinline__ void epi_flush_qkv(const GemmP& p, const char* smem, 
     }
 }
 
+// Row statistics of the staged bf16 tile (kd_gemm_desc.row_stats): one thread per tile row
+// (256 rows, 256 threads), one online pass over its 256 LDS values, the arithmetic of
+// k_row_stats (__expf, chunk-filtered top-2) on the bf16-rounded values the loss reads.
+// Measured cost (tools/rst_cost.py): +1170 us on the 7B lm_head (+22%), +374 us on the 0.5B one
+// -- 1-2 exps per element run with one wave per SIMD and nothing to overlap them with, which is
+// more than the separate HBM-bound k_row_stats pass it removes (0.93 ms a step), so the step
+// keeps that pass by default.  LDS rows are RS-byte strided (RS / 4 = 4 mod 64 banks).
+__device__ __forceinline__ void epi_row_stats(const GemmP& p, const char* smem, int rs, int m0, int n0, int tid) {
+    const int row = m0 + tid;
+    if (row >= p.M) return;
+    const int ncols = min(256, p.N - n0);
+    const int nvs = max(0, min(ncols, (p.rst_vs > 0 ? p.rst_vs : p.N) - n0));
+    const bf16x8* rp = (const bf16x8*)(smem + tid * rs);
+    // one online pass (k_row_stats' arithmetic): the max moves chunk by chunk and rescales the
+    // sums; at T = 1 one exp per element feeds both sums (the sum below vs is kept relative to
+    // the running max of all columns and rebased on the max below vs at the end)
+    float m_all = -INFINITY, m_vs = -INFINITY, v1 = -INFINITY, v2 = -INFINITY;
+    float z1 = 0.f, zt = 0.f;
+    int i1 = 0x7fffffff, i2 = 0x7fffffff;
+    const bool top2 = p.rst_top2 != 0;
+    const float invT = p.rst_inv_t;
+    const bool t1 = invT == 1.f;
+    const int nch = ncols / 8, nvch = nvs / 8;
+    for (int c0 = 0; c0 < nch; c0 += 4) {
+        bf16x8 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = c0 + u < nch ? rp[c0 + u] : (bf16x8){};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u;
+            if (c >= nch) break;
+            float f[8], cm = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { f[j] = (float)x[u][j]; cm = fmaxf(cm, f[j]); }
+            if (cm > m_all) {
+                if (m_all != -INFINITY) {
+                    const float sc = __expf(m_all - cm);
+                    z1 *= sc;
+                    if (t1) zt *= sc;
+                }
+                m_all = cm;
+            }
+            const bool in_vs = c < nvch;
+            float e1 = 0.f, et = 0.f;
+            if (t1) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) e1 += __expf(f[j] - m_all);
+                et = e1;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) e1 += __expf(f[j] - m_all);
+                if (in_vs) {
+                    if (cm > m_vs) { if (m_vs != -INFINITY) zt *= __expf((m_vs - cm) * invT); m_vs = cm; }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) et += __expf((f[j] - m_vs) * invT);
+                }
+            }
+            z1 += e1;
+            if (in_vs) {
+                zt += et;
+                if (t1) m_vs = fmaxf(m_vs, cm);
+                const int col = n0 + 8 * c;
+                if (top2 && (cm > v2 || (cm == v2 && col < i2))) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) top2_push(f[j], col + j, v1, i1, v2, i2);
+                }
+            }
+        }
+    }
+    if (t1 && m_vs != -INFINITY) zt *= __expf(m_all - m_vs);   // sum exp(c - m_vs) below vs
+    float* o = p.rst + ((int64_t)row * p.rst_nt + n0 / 256) * 8;
+    *(f32x4*)o = (f32x4){m_all, z1, m_vs, nvs > 0 ? zt : 0.f};
+    *(f32x4*)(o + 4) = (f32x4){v1, __int_as_float(i1), v2, __int_as_float(i2)};
+}
+
 // HAS_ACT: the activation epilogue is instantiated for the forward (K-major x K-major) kernels
 // only; the launcher rejects an activation with MN-major operands or an fp32 output.
-template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2, bool HAS_ACT = true>
+template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2, bool HAS_ACT = true,
+          bool RST = false>
 __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int n0, int wm,
                                           int wn, int lane, int tid) {
     const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
@@ -670,6 +750,7 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
         else epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
         epi_flush_sel<BM, BN, NTHR, false>(p, smem, RS16, p.C, p.ldc, m0, n0, tid, full, res, accum);
+        if constexpr (RST) epi_row_stats(p, smem, RS16, m0, n0, tid);
     } else {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {   // fp32: two half tiles of BM/2 rows
@@ -909,6 +990,10 @@ template <bool A_MN, bool B_MN, int EXP>
 __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     constexpr bool STAMP = EXP & 1, NODMA = EXP & 2, HOT = EXP & 64;
     constexpr bool RS = (EXP & 8) && !A_MN && !B_MN;
+    // bit 5: the epilogue also writes the tile's row statistics (kd_gemm_desc.row_stats, the
+    // lm_head GEMMs of the KD step): a build of its own, so the plain forward kernel carries none
+    // of that code and the lm_head launches are their own line in a kernel trace
+    constexpr bool RSTATS = (EXP & 32) && !A_MN && !B_MN;
 
     uint32_t* stamps = nullptr;
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
@@ -1104,7 +1189,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     if (STAMP) { te0 = __builtin_amdgcn_s_memtime(); s_units += te0 - tprev; }
     __syncthreads();
     if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
-    else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+    else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN, RSTATS>(p, acc, smem, m0, n0, wm, wn, lane, tid);
     if (STAMP) {
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         s_epi = te1 - te0;
@@ -1907,6 +1992,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.sa = p.sb = nullptr; p.gx = 0; p.gy = 1;
     p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr;
     p.gm = 0;
+    p.rst = nullptr; p.rst_nt = p.rst_vs = p.rst_top2 = 0; p.rst_inv_t = 1.f;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->qkv || ((d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0))) &&
@@ -1923,6 +2009,24 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         d1 = *d;
         d1.split_k = 1;
         d = &d1;
+    }
+    if (d->row_stats) {   // the lm_head GEMM with the KD loss's row statistics, on v8 (no split)
+        KD_CHECK_ARG(!amn && !bmn && d->c_dtype == KD_DTYPE_BF16 && !d->bias && d->act == KD_ACT_NONE && !d->residual &&
+                         !d->aux && !d->accumulate && !d->qkv && d->ab_dtype == KD_DTYPE_BF16,
+                     "gemm row_stats: K-major bf16 operands, bf16 C, no bias / act / residual / aux / accumulate");
+        KD_CHECK_SHAPE(d->N % 8 == 0 && (d->row_stats_vs <= 0 || d->row_stats_vs % 8 == 0) && big_ok,
+                       "gemm row_stats: N and row_stats_vs multiples of 8, the tiled kernels' shapes");
+        KD_CHECK_ARG(d->row_stats_inv_t > 0.f, "gemm row_stats: row_stats_inv_t must be > 0");
+        KD_CHECK_ALIGN(d->row_stats, 16, "gemm row_stats: 16-B aligned");
+        GemmP pk = p;
+        pk.rst = d->row_stats; pk.rst_nt = ceil_div(d->N, 256); pk.rst_vs = d->row_stats_vs;
+        pk.rst_inv_t = d->row_stats_inv_t; pk.rst_top2 = d->row_stats_top2 ? 1 : 0;
+        pk.gm = pick_gm(ceil_div(d->M, 256), ceil_div(d->N, 256));
+        const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256), 1);
+        pk.gx = (int)grid.x; pk.gy = 1; pk.tile0 = 0;
+        hipLaunchKernelGGL((k_gemm8<false, false, 32>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        KD_LAUNCH_CHECK("k_gemm8 (row stats)");
+        return KD_OK;
     }
     if (d->act == KD_ACT_SWIGLU) {   // fused gate|up GEMM + silu(gate) * up, on v8
         KD_CHECK_SHAPE(d->N % 256 == 0 && d->M >= 1, "gemm swiglu: N = 2I needs I % 128 == 0");

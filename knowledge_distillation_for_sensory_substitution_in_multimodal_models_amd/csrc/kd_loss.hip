@@ -78,23 +78,7 @@ inline Layout make_layout(int B, int L, int V) {
     return lo;
 }
 
-// top-2 with deterministic tie-break: larger value first, lower index on ties.
-__device__ __forceinline__ bool better(float a, int ia, float b, int ib) {
-    return a > b || (a == b && ia < ib);
-}
-// Branch-free (selects only): the if/else-if form made hipcc keep (v1, i1, v2, i2) in a
-// scratch array indexed per lane (36 B of private memory, a scratch round trip per push
-// and per chunk test in k_row_stats' teacher loop).
-__device__ __forceinline__ void top2_push(float v, int i, float& v1, int& i1, float& v2, int& i2) {
-    const bool b1 = better(v, i, v1, i1);
-    const bool b2 = better(v, i, v2, i2);
-    const float nv2 = b1 ? v1 : (b2 ? v : v2);
-    const int ni2 = b1 ? i1 : (b2 ? i : i2);
-    v1 = b1 ? v : v1;
-    i1 = b1 ? i : i1;
-    v2 = nv2;
-    i2 = ni2;
-}
+// top2_push / top2_better: common.h
 
 // merge an online (max, sum-exp-at-invT) pair
 __device__ __forceinline__ void lse_merge(float& m, float& z, float m2, float z2, float invT) {
@@ -117,13 +101,19 @@ __device__ __forceinline__ void report_label(int* err, int* err_ext, int bit, in
     }
 }
 
+// PART: the per-row max / sum-exp / top-2 come from the lm_head GEMMs' epilogue partials
+// (kd_gemm_desc.row_stats: [rows, ceil(V / 256), 8] per model, merged with the same lse_merge /
+// top2_push as the wave reductions below) instead of a pass over both logit tensors; the label
+// gathers, the CE and the LoCa override values are unchanged (a few single-element reads).
+template <bool PART>
 __global__ void __launch_bounds__(NT)
 k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
             const bf16* __restrict__ S_, int64_t ld_s, int V_s,
             const int64_t* __restrict__ labels, int L, int rows,
             int variant, float invT, float alpha, int want_tce,
             RowStats* __restrict__ stats, int* __restrict__ lab_last,
-            int* __restrict__ klo_last, int* __restrict__ err, int* __restrict__ err_ext, int row_base) {
+            int* __restrict__ klo_last, int* __restrict__ err, int* __restrict__ err_ext, int row_base,
+            const float* __restrict__ s_part, const float* __restrict__ t_part) {
     __shared__ float sm[NW * 8];
     __shared__ int si[NW * 2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -131,8 +121,32 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
     for (int r = blockIdx.x; r < rows; r += gridDim.x) {
         const bf16* srow = S_ + (int64_t)r * ld_s;
         const bf16* trow = has_t ? T_ + (int64_t)r * ld_t : nullptr;
-        // ---- student: max / sum-exp at T and at 1 (same max); RS_U chunks in flight per lane
         float ms = -INFINITY, zs = 0.f, zs1 = 0.f;
+        float mt = -INFINITY, zt = 0.f, mtf = -INFINITY, ztf = 0.f;
+        float v1 = -INFINITY, v2 = -INFINITY;
+        int i1 = 0x7fffffff, i2 = 0x7fffffff;
+        if constexpr (PART) {
+            // student tiles {max, sum at 1, max below V_s (= the same), sum at 1/T}; teacher tiles
+            // {max over V_t, sum at 1, max over V_s, sum at 1/T, top-2}
+            const int nts = (V_s + 255) / 256, ntt = (V_t + 255) / 256;
+            for (int j = tid; j < nts; j += NT) {
+                const f32x4 a = *(const f32x4*)(s_part + ((int64_t)r * nts + j) * 8);
+                float mm = ms;
+                lse_merge(ms, zs, a[2], a[3], invT);
+                lse_merge(mm, zs1, a[0], a[1], 1.f);
+            }
+            if (has_t) {
+                for (int j = tid; j < ntt; j += NT) {
+                    const f32x4 a = *(const f32x4*)(t_part + ((int64_t)r * ntt + j) * 8);
+                    const f32x4 c = *(const f32x4*)(t_part + ((int64_t)r * ntt + j) * 8 + 4);
+                    lse_merge(mtf, ztf, a[0], a[1], 1.f);
+                    lse_merge(mt, zt, a[2], a[3], invT);
+                    top2_push(c[0], __float_as_int(c[1]), v1, i1, v2, i2);
+                    top2_push(c[2], __float_as_int(c[3]), v1, i1, v2, i2);
+                }
+            }
+        } else {
+        // ---- student: max / sum-exp at T and at 1 (same max); RS_U chunks in flight per lane
         const bool t1 = invT == 1.f;   // T = 1 (LB): the two sums coincide, one exp per element
         for (int v0 = tid * 8; v0 < V_s; v0 += NT * 8 * RS_U) {
             bf16x8 xs[RS_U];
@@ -162,9 +176,6 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
         }
         if (t1) zs1 = zs;
         // ---- teacher: max/sum over V_s at T, top-2 over V_s; max/sum over V_t at 1
-        float mt = -INFINITY, zt = 0.f, mtf = -INFINITY, ztf = 0.f;
-        float v1 = -INFINITY, v2 = -INFINITY;
-        int i1 = 0x7fffffff, i2 = 0x7fffffff;
         if (has_t) {
             for (int v0 = tid * 8; v0 < V_t; v0 += NT * 8 * RS_U) {
                 bf16x8 xt[RS_U];
@@ -216,6 +227,8 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
             }
         }
         if (has_t && want_tce && t1 && mt != -INFINITY) zt *= __expf(mtf - mt);   // sum exp(t - mt) over V_s
+        }
+
         // ---- wave reductions
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -746,9 +759,19 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
             return fail(KD_ERR_LAUNCH, "kd_loss: memset tables");
     }
     const int grid = rows < 2048 ? rows : 2048;
-    hipLaunchKernelGGL(k_row_stats, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
-                       V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
-                       lab_last, klo_last, err, p.err_out, p.row_base);
+    const bool part = p.s_row_stats != nullptr;
+    if (part) {
+        KD_CHECK_ARG(!T_ || p.t_row_stats, "kd_loss: s_row_stats without t_row_stats");
+        KD_CHECK_ALIGN(p.s_row_stats, 16, "kd_loss: s_row_stats must be 16-B aligned");
+        KD_CHECK_ALIGN(p.t_row_stats, 16, "kd_loss: t_row_stats must be 16-B aligned");
+        hipLaunchKernelGGL(k_row_stats<true>, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
+                           V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
+                           lab_last, klo_last, err, p.err_out, p.row_base, p.s_row_stats, p.t_row_stats);
+    } else {
+        hipLaunchKernelGGL(k_row_stats<false>, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
+                           V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
+                           lab_last, klo_last, err, p.err_out, p.row_base, nullptr, nullptr);
+    }
     KD_LAUNCH_CHECK("k_row_stats");
     if (variant == KD_LOSS_LOCA) {
         const int nb = (V_s + 255) / 256;

@@ -204,6 +204,10 @@ struct kd_model {
     std::vector<int64_t> soff;   // per spec: first scale index (-1: not an fp8 linear)
     std::vector<int> fam;        // per spec: its kd_fp8_family bit (0: not an fp8 linear)
     int f8_families = KD_FP8_ALL;   // which families run on the fp8 path (kd_model_set_fp8_families)
+    // lm_head row statistics for the KD loss (kd_model_set_row_stats); nullptr = off
+    float* rst = nullptr;
+    int rst_vs = 0, rst_top2 = 0;
+    float rst_inv_t = 1.f;
     int64_t n_scales = 0;
     // spec indices
     int i_patch_w = 0, i_patch_b = 1, i_pos = 2, i_vis0 = 3, i_post_w, i_post_b, i_p1w, i_p1b, i_p2w, i_p2b, i_newline,
@@ -265,6 +269,9 @@ struct GemmArgs {
     int split_k = 0;
     int res_f32 = 0;   // fp32 residual (then c_f32 too)
     const kd_qkv_scatter* qkv = nullptr;   // q|k|v scatter epilogue (C unused)
+    float* row_stats = nullptr;            // lm_head row statistics (kd_gemm_desc.row_stats)
+    int rs_vs = 0, rs_top2 = 0;
+    float rs_inv_t = 1.f;
 };
 
 // split-K default of the runtime's GEMMs (KD_GEMM_SPLIT_K: 0 = the cost model, 1 = never split)
@@ -292,6 +299,7 @@ int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int6
     d.residual_row_mod = g.residual_row_mod;
     d.split_k = g.split_k ? g.split_k : g_split_default;
     if (d.split_k != 1 && ws) { d.workspace = ws; d.workspace_bytes = SPLITK_WS; }
+    d.row_stats = g.row_stats; d.row_stats_vs = g.rs_vs; d.row_stats_inv_t = g.rs_inv_t; d.row_stats_top2 = g.rs_top2;
     return gemm_timed(&d, s);
 }
 
@@ -499,7 +507,7 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int n_tiles, int save, voi
 // GEMM against the e4m3 weight rows and their per-channel scales (kdstep.h, fp8 path).
 int lin(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int N, int K, const bf16* x, int64_t ldx, int widx,
         void* out, int64_t ldo, const GemmArgs& g) {
-    if (!m->f8q || m->soff[widx] < 0 || !(m->fam[widx] & m->f8_families))
+    if (!m->f8q || m->soff[widx] < 0 || !(m->fam[widx] & m->f8_families) || g.row_stats)
         return gemm(s, P.splitk, M, N, K, km(x, ldx), km(m->W(widx), K), out, ldo, g);
     KD_TRY(launch_quant_rows_f8(x, ldx, M, K, P.qa, K, P.sa, s));
     kd_gemm_desc d;
@@ -1097,6 +1105,14 @@ int kd_model_quantize_fp8(const kd_model* m, void* q, float* scales, void* strea
     return KD_OK;
 }
 
+int kd_model_set_row_stats(kd_model* m, float* partials, int vs, float inv_t, int top2) {
+    KD_CHECK_ARG(m, "kd_model_set_row_stats: null model");
+    KD_CHECK_ARG(!partials || inv_t > 0.f, "kd_model_set_row_stats: inv_t must be > 0");
+    KD_CHECK_ALIGN(partials, 16, "kd_model_set_row_stats: partials must be 16-B aligned");
+    m->rst = partials; m->rst_vs = vs; m->rst_inv_t = inv_t; m->rst_top2 = top2 ? 1 : 0;
+    return KD_OK;
+}
+
 int kd_model_set_fp8_families(kd_model* m, int families) {
     KD_CHECK_ARG(m, "kd_model_set_fp8_families: null model");
     KD_CHECK_ARG((families & ~KD_FP8_ALL) == 0, "kd_model_set_fp8_families: unknown family bits");
@@ -1162,6 +1178,7 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
     KD_TRY(lm_forward(m, P, rope_cos, rope_sin, B, L, save, hn, kv_k, kv_v, s));
     if (logits) {
         GemmArgs g;
+        if (m->rst) { g.row_stats = m->rst; g.rs_vs = m->rst_vs; g.rs_inv_t = m->rst_inv_t; g.rs_top2 = m->rst_top2; }
         KD_TRY(lin(m, P, s, M, c.t_vocab, H, (const bf16*)hn, H, m->i_head, logits, c.t_vocab, g));
     }
     return KD_OK;

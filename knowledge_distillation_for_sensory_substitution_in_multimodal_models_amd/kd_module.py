@@ -26,6 +26,8 @@ from __future__ import annotations
 import contextlib
 import inspect
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -264,6 +266,9 @@ class _KDBase(_Base):
         self._errors = _ErrorWatch(dev)
         self._errors.bind(self.student_model, self.teacher_model)
         self.keep_logits = False         # tests: keep the step's logits in last_logits
+        # KD_FUSE_ROWSTATS=1: the lm_head epilogues emit the KD loss's row statistics.  Off by
+        # default: measured slower (profiles/r03/row_stats_fusion_ab.txt)
+        self.fuse_row_stats = os.environ.get("KD_FUSE_ROWSTATS", "0") == "1"
         self.last_terms = None
         self.last_ntxent = None
         self.last_logits = None
@@ -335,10 +340,10 @@ class _KDBase(_Base):
         return [opt], [sched]
 
     # ------------------------------------------------------------- the step ----
-    def _teacher_forward(self, batch, need_feats):
+    def _teacher_forward(self, batch, need_feats, row_stats=None):
         tfwd = self.teacher_model.forward(batch["rgb_input_ids"], batch["rgb_pixel_values"], batch["image_sizes"],
-                                          save=False, want_post_ln=need_feats, want_logits=True)
-        return tfwd["logits"], tfwd.get("post_ln")
+                                          save=False, want_post_ln=need_feats, want_logits=True, row_stats=row_stats)
+        return tfwd["logits"], tfwd.get("post_ln"), tfwd.get("row_stats")
 
     def _groups(self, B):
         G = self.loss_group_size or B
@@ -368,13 +373,20 @@ class _KDBase(_Base):
         if self._opt_pending:
             side.wait_event(self._opt_done)
             self._opt_pending = False
-        t_logits = t_post = None
+        # the lm_head epilogues emit the loss's per-row softmax statistics (kd_gemm_desc.row_stats)
+        # so the loss does not read both logit tensors once more just for them (KD_FUSE_ROWSTATS=1;
+        # default: the loss's own pass)
+        Vs_ = s.cfg.text.vocab
+        fuse = self.fuse_row_stats
+        t_logits = t_post = t_rst = None
         if self.uses_teacher:
-            t_logits, t_post = self._teacher_forward(batch, need_feats)
+            t_logits, t_post, t_rst = self._teacher_forward(batch, need_feats,
+                                                            (Vs_, 1.0 / T, True) if fuse else None)
         with torch.cuda.stream(side):
             sfwd = s.forward(batch["depth_input_ids"], batch["depth_pixel_values"], image_sizes, save=train,
-                             want_post_ln=need_feats, want_logits=True)
+                             want_post_ln=need_feats, want_logits=True, row_stats=(Vs_, 1.0 / T, False) if fuse else None)
             s_logits = sfwd.pop("logits")
+            s_rst = sfwd.pop("row_stats", None)
         main.wait_stream(side)
         Vs = s_logits.shape[1]
         s3 = s_logits.view(B, L, Vs)
@@ -385,13 +397,20 @@ class _KDBase(_Base):
         # element of every row is then ~ -1, exact in bf16, instead of the same bf16-rounded
         # -1/n_valid in every row, a systematic +0.13 % on the whole gradient (tools/grad_bias_study.py)
         dscale = torch.empty(1, dtype=torch.float32, device=s_logits.device) if train else None
+        if s_rst is not None and t3 is not None and t_rst is None:
+            s_rst = None   # both or neither
+        rs = slice(0, 0)
         for g in range(ng):   # loss groups: mean over groups of each group's loss
             sl = slice(g * G, (g + 1) * G)
+            rs = slice(g * G * L, (g + 1) * G * L)
             ops.kd_loss_fwd_bwd(s3[sl], None if t3 is None else t3[sl], labels[sl], variant,
                                 temperature=T, alpha=0.8, kd_weight=kd_w, ce_weight=ce_w, grad_scale=1.0 / ng,
                                 want_grad=train, loss_out=loss4, out_scale=1.0 / ng, accumulate=g > 0,
                                 dlogits_out=None if dlogits is None else dlogits[sl], err_out=self._errors.kd,
-                                row_base=g * G * L, dscale=dscale, dscale_given=g > 0)
+                                row_base=g * G * L, dscale=dscale, dscale_given=g > 0,
+                                s_row_stats=None if s_rst is None else s_rst[rs],
+                                t_row_stats=None if (s_rst is None or t_rst is None) else t_rst[rs])
+        del s_rst, t_rst
         if self.keep_logits:
             self.last_logits = (s3, t3)
             self.last_post = (sfwd.get("post_ln"), t_post)

@@ -514,7 +514,7 @@ class LlavaOnevisionModel:
 
     # ========================================================= full model ====
     def forward(self, input_ids, pixel_values, image_sizes, save: bool = False, want_post_ln: bool = False,
-                kv_out: list | None = None, want_logits: bool = False):
+                kv_out: list | None = None, want_logits: bool = False, row_stats: tuple | None = None):
         """LlavaOnevisionForConditionalGeneration.forward (kd_model_forward).
 
         input_ids [B, L] int64 (device), pixel_values [B, P, 3, 384, 384] (bf16 / fp32),
@@ -522,7 +522,9 @@ class LlavaOnevisionModel:
         [B*L, H]), `post_ln` (vision post_layernorm output, the reference's hook, DT:110-121),
         `logits` [B*L, V] (want_logits), `tile_counts` (each sample's real vision tiles, the
         post_ln row groups) and, with save, the workspace the backward reads.
-        kv_out (a list) receives each layer's roped (k, v) [B, kv_heads, L, head_dim]."""
+        kv_out (a list) receives each layer's roped (k, v) [B, kv_heads, L, head_dim].
+        row_stats = (vs, inv_t, top2) with want_logits: `row_stats` [B*L, ceil(V/256), 8] fp32, the
+        lm_head epilogue's per-row softmax statistics for the KD loss (kd_model_set_row_stats)."""
         T, V = self.cfg.text, self.cfg.vision
         B, L = input_ids.shape
         P = pixel_values.shape[1]
@@ -559,10 +561,21 @@ class LlavaOnevisionModel:
             kv_out.extend(zip(ks, vs))
             kvk = (C.c_void_p * T.layers)(*[k.data_ptr() for k in ks])
             kvv = (C.c_void_p * T.layers)(*[v.data_ptr() for v in vs])
-        NV.call("kd_model_forward", self._h, ids.data_ptr(), px.data_ptr(), ops._DT[px.dtype], src.data_ptr(),
-                cos.data_ptr(), sin.data_ptr(), B, L, tiles, int(save), ws.data_ptr(), ws.numel(), hn.data_ptr(),
-                ops._ptr(post), ops._ptr(logits), kvk, kvv, self.err.data_ptr(), ops._stream())
+        rst = None
+        if row_stats is not None and want_logits:
+            vs, inv_t, top2 = row_stats
+            rst = torch.empty((B * L, (T.vocab + 255) // 256, 8), dtype=torch.float32, device=dev)
+            NV.call("kd_model_set_row_stats", self._h, rst.data_ptr(), int(vs), float(inv_t), int(bool(top2)))
+        try:
+            NV.call("kd_model_forward", self._h, ids.data_ptr(), px.data_ptr(), ops._DT[px.dtype], src.data_ptr(),
+                    cos.data_ptr(), sin.data_ptr(), B, L, tiles, int(save), ws.data_ptr(), ws.numel(), hn.data_ptr(),
+                    ops._ptr(post), ops._ptr(logits), kvk, kvv, self.err.data_ptr(), ops._stream())
+        finally:
+            if rst is not None:   # the handle never keeps a pointer past the call that owns it
+                NV.call("kd_model_set_row_stats", self._h, None, 0, 1.0, 0)
         out = dict(hn=hn, src=src, ids=ids, shape=(B, L, tiles), tile_counts=counts)
+        if rst is not None:
+            out["row_stats"] = rst
         if want_post_ln:
             out["post_ln"] = post
         if want_logits:

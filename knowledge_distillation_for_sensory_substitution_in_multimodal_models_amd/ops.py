@@ -109,7 +109,8 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
                     check: bool = False, loss_out: torch.Tensor | None = None, out_scale: float = 1.0,
                     accumulate: bool = False, dlogits_out: torch.Tensor | None = None,
                     err_out: torch.Tensor | None = None, row_base: int = 0,
-                    dscale: torch.Tensor | None = None, dscale_given: bool = False):
+                    dscale: torch.Tensor | None = None, dscale_given: bool = False,
+                    s_row_stats: torch.Tensor | None = None, t_row_stats: torch.Tensor | None = None):
     """Fused KD-loss forward + backward (include/kdstep.h kd_loss_fwd_bwd).
 
     student_logits [B, L, V_s] bf16 (last dim contiguous), teacher_logits [B, L, V_t] bf16,
@@ -122,7 +123,9 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
     without a host sync (kd_loss_params.err_out).  dscale (device fp32 [1]): the dlogits are
     stored relative to the scale written there (or read from there, dscale_given), which
     the consumer multiplies back in fp32 (kd_loss_params.dscale: the CE one-hot element
-    stays exact in bf16).
+    stays exact in bf16).  s_row_stats / t_row_stats (fp32 [B*L, ceil(V / 256), 8], these rows):
+    the lm_head GEMMs' row statistics (gemm(row_stats=...), modeling set_row_stats) in place of
+    the loss's own pass over the logits (kd_loss_params.s_row_stats / t_row_stats).
     """
     B, L, V_s = student_logits.shape
     _require(student_logits, torch.bfloat16, "student_logits")
@@ -152,12 +155,19 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
         _require(err_out, torch.int32, "err_out")
     if dscale is not None:
         _require(dscale, torch.float32, "dscale")
+    for nm, t, V in (("s_row_stats", s_row_stats, V_s), ("t_row_stats", t_row_stats, V_t)):
+        if t is not None:
+            _require(t, torch.float32, nm)
+            if not t.is_contiguous() or t.numel() != B * L * ((V + 255) // 256) * 8:
+                raise RuntimeError(f"{nm}: expected a contiguous [B*L, ceil(V/256), 8] fp32 block of these rows")
+    if (s_row_stats is None) != (t_row_stats is None) and teacher_logits is not None:
+        raise RuntimeError("s_row_stats and t_row_stats: both or neither")
     nbytes = NV.lib().kd_loss_workspace_size(B, L, V_s)
     ws = _workspace("kd_loss", nbytes, dev)
     prm = NV.KdLossParams(v, float(temperature), float(alpha), float(kd_weight), float(ce_weight),
                          float(grad_scale), float(clamp_min), 1 if teacher_ce else 0, float(out_scale),
                          1 if accumulate else 0, _ptr(err_out), int(row_base), _ptr(dscale),
-                         1 if dscale_given else 0)
+                         1 if dscale_given else 0, _ptr(s_row_stats), _ptr(t_row_stats))
     NV.call("kd_loss_fwd_bwd", _ptr(teacher_logits), ld_t, V_t, _ptr(student_logits),
            student_logits.stride(1), V_s, _ptr(labels), B, L, prm, _ptr(loss), _ptr(dl),
            V_s, _ptr(ws), ws.numel(), _stream())
@@ -271,7 +281,9 @@ def gemm_split_default(split_k: int):
 
 def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, act=None,
          residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
-         out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0) -> torch.Tensor:
+         out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0,
+         row_stats: torch.Tensor | None = None, row_stats_vs: int = 0, row_stats_inv_t: float = 1.0,
+         row_stats_top2: bool = False) -> torch.Tensor:
     """out[M, N] = epilogue(alpha * a[M, K] @ b[N, K]^T).
 
     split_k: 0 = library cost model (bounded by the cached GEMM_SPLITK_WS workspace),
@@ -282,11 +294,22 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
 
     act="swiglu": b = [gate; up] ([2I, K]), out [M, I] = silu(gate) * up, aux (optional)
     the [M, 2I] pre-activation (include/kdstep.h KD_ACT_SWIGLU).
+
+    row_stats: fp32 [M, ceil(N / 256), 8] receives the per-row softmax statistics of the bf16
+    output per 256-column tile (kd_gemm_desc.row_stats; the lm_head GEMMs of the KD step).
     """
     if split_k == 0:
         split_k = _SPLIT_DEFAULT[0]
     d, out, M, N, K, la, lb = _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate,
                                          out_dtype, residual_row_mod, variant, split_k)
+    if row_stats is not None:
+        _require(row_stats, torch.float32, "row_stats")
+        if not row_stats.is_contiguous() or row_stats.numel() != M * ((N + 255) // 256) * 8:
+            raise RuntimeError("row_stats: expected a contiguous fp32 [M, ceil(N/256), 8]")
+        d.row_stats = row_stats.data_ptr()
+        d.row_stats_vs = int(row_stats_vs)
+        d.row_stats_inv_t = float(row_stats_inv_t)
+        d.row_stats_top2 = 1 if row_stats_top2 else 0
     NV.call("kd_gemm", C.byref(d), _stream())
     return out
 

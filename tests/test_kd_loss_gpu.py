@@ -113,3 +113,92 @@ def test_kat1_small_vocab_against_reference(dev):
     ref = O.loca_kd_term(tb.float()[..., :19], sb.float(), torch.tensor(k["labels"]), T=1.0)
     assert float(loss[0]) == pytest.approx(ref.item(), rel=1e-5)
     assert float(loss[0]) == pytest.approx(k["loss"], rel=5e-2)
+
+
+def _tile_stats_ref(x, vs, inv_t):
+    """per-row, per-256-column-tile statistics of bf16 logits x [M, N] (kd_gemm_desc.row_stats)"""
+    M, N = x.shape
+    nt = (N + 255) // 256
+    xf = x.float()
+    out = torch.zeros(M, nt, 4)
+    for j in range(nt):
+        t = xf[:, 256 * j: min(N, 256 * (j + 1))]
+        m = t.max(1).values
+        out[:, j, 0] = m
+        out[:, j, 1] = torch.exp(t - m[:, None]).sum(1)
+        w = t[:, : max(0, min(t.shape[1], vs - 256 * j))]
+        if w.shape[1]:
+            mv = w.max(1).values
+            out[:, j, 2] = mv
+            out[:, j, 3] = torch.exp((w - mv[:, None]) * inv_t).sum(1)
+        else:
+            out[:, j, 2] = -float("inf")
+    return out
+
+
+@pytest.mark.parametrize("M,N,K,vs,T,top2", [(512, 2056, 256, 1800, 0.8, True), (520, 2048, 600, 2048, 1.0, False),
+                                             (256, 151936 // 16, 512, 151936 // 16, 1.0, True)])
+def test_gemm_row_stats(M, N, K, vs, T, top2, dev):
+    """kd_gemm_desc.row_stats: the v8 epilogue's per-row, per-tile max / sum-exp (at 1 over N,
+    at 1/T below vs) and top-2 of the bf16 output, against the same quantities from the output
+    itself (the loss reads the bf16 logits); the output is the plain GEMM's, bit for bit."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(7)
+    h = (torch.randn(M, K, generator=g)).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.2).to(dev, torch.bfloat16)
+    nt = (N + 255) // 256
+    rs = torch.full((M, nt, 8), float("nan"), dtype=torch.float32, device=dev)
+    y = ops.gemm(h, w, row_stats=rs, row_stats_vs=vs, row_stats_inv_t=1.0 / T, row_stats_top2=top2)
+    assert torch.equal(y, ops.gemm(h, w, variant=16, split_k=1))
+    ref = _tile_stats_ref(y.cpu(), vs, 1.0 / T)
+    got = rs.cpu()
+    assert torch.equal(got[:, :, 0], ref[:, :, 0])
+    assert torch.allclose(got[:, :, 1], ref[:, :, 1], rtol=2e-5, atol=0)
+    valid = ref[:, :, 2] > -float("inf")
+    assert torch.equal(got[:, :, 2][valid], ref[:, :, 2][valid])
+    assert torch.allclose(got[:, :, 3][valid], ref[:, :, 3][valid], rtol=2e-5, atol=0)
+    if top2:
+        yf = y.float().cpu()
+        rows = torch.arange(M)
+        for j in range(nt):
+            t = yf[:, 256 * j: min(N, vs, 256 * (j + 1))]
+            if t.shape[1] < 2:
+                continue
+            top = t.topk(2, dim=1).values                      # the two largest values (a multiset)
+            assert torch.equal(got[:, j, 4], top[:, 0]) and torch.equal(got[:, j, 6], top[:, 1])
+            gi1 = got[:, j, 5].contiguous().view(torch.int32).long() - 256 * j
+            gi2 = got[:, j, 7].contiguous().view(torch.int32).long() - 256 * j
+            assert torch.equal(t[rows, gi1], top[:, 0]) and torch.equal(t[rows, gi2], top[:, 1])
+            assert bool((gi1 != gi2).all())
+            # ties: the lower index first, and no lower index holding the same value was skipped
+            first1 = (t == top[:, :1]).float().argmax(1)
+            assert torch.equal(gi1, first1)
+
+
+@pytest.mark.parametrize("variant,T", [("loca", 1.0), ("loca", 0.8), ("kl", 0.8), ("kl_logtarget", 0.8), ("none", 1.0)])
+def test_loss_with_gemm_row_stats(variant, T, dev):
+    """The loss fed with the lm_head GEMMs' row statistics (s_row_stats / t_row_stats) == the
+    loss's own pass over the logits, up to fp32 summation order: terms within 2e-6 relative,
+    dlogits within one bf16 ulp (the row constants move in their last bits)."""
+    ops = _ops()
+    B, L, K, Vs, Vt = 2, 192, 384, 151936, 152064
+    g = torch.Generator().manual_seed(11)
+    hs = torch.randn(B * L, K, generator=g).to(dev, torch.bfloat16)
+    ht = torch.randn(B * L, K, generator=g).to(dev, torch.bfloat16)
+    ws = (torch.randn(Vs, K, generator=g) * 0.12).to(dev, torch.bfloat16)
+    wt = (torch.randn(Vt, K, generator=g) * 0.12).to(dev, torch.bfloat16)
+    srs = torch.empty(B * L, (Vs + 255) // 256, 8, dtype=torch.float32, device=dev)
+    trs = torch.empty(B * L, (Vt + 255) // 256, 8, dtype=torch.float32, device=dev)
+    s = ops.gemm(hs, ws, row_stats=srs, row_stats_vs=Vs, row_stats_inv_t=1.0 / T).view(B, L, Vs)
+    t = ops.gemm(ht, wt, row_stats=trs, row_stats_vs=Vs, row_stats_inv_t=1.0 / T, row_stats_top2=True).view(B, L, Vt)
+    labels = torch.randint(0, Vs, (B, L), generator=g).to(dev)
+    labels[:, :5] = -100 if variant != "loca" else labels[:, :5]
+    tt = None if variant == "none" else t
+    l0, d0 = ops.kd_loss_fwd_bwd(s, tt, labels, variant, temperature=T, check=True)
+    l1, d1 = ops.kd_loss_fwd_bwd(s, tt, labels, variant, temperature=T, check=True, s_row_stats=srs,
+                                 t_row_stats=None if tt is None else trs)
+    torch.cuda.synchronize()
+    a, b = l0.cpu().double(), l1.cpu().double()
+    assert torch.allclose(a, b, rtol=2e-6, atol=1e-9), (a, b)
+    dd = (d0.float() - d1.float()).abs()
+    assert bool((dd <= 2.0 ** -7 * d0.float().abs() + 1e-9).all()), dd.max().item()

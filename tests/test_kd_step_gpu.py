@@ -147,6 +147,31 @@ def test_training_step_matches_reference(name, dev):
         assert float(P.grad[:P.regions["vision"][1]].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("name", ["lb", "dt2"])
+def test_fused_row_stats_step_matches(name, dev):
+    """KD_FUSE_ROWSTATS=1 (the lm_head epilogues emit the loss's row statistics): every loss
+    term at the north-star tolerance against the reference and within 1e-6 |ref| of the
+    default path's (the same statistics, merged per 256-column tile instead of per row)."""
+    meta, exp = load(name)
+    kind, phase = ALL_KINDS[name]
+    terms = []
+    for fuse in (False, True):
+        m = _module(kind, phase)
+        m.fuse_row_stats = fuse
+        loss = m.training_step(batch(meta, dev), 0)
+        torch.cuda.synchronize()
+        assert int(m.student_model.err.item()) == 0
+        terms.append([loss.item()] + m.last_terms.tolist()[:3])
+    for (a, b), what in zip(zip(*terms), ("total", "KD term", "student CE", "teacher CE")):
+        if math.isnan(a):
+            continue
+        assert abs(b - a) <= 1e-6 * abs(a) + 1e-7, f"{what}: fused {b!r} vs unfused {a!r}"
+    has_ntx = not math.isnan(float(exp["ntxent"]))
+    _near(terms[1][0], float(exp["total"]), "total", NTX_RTOL if has_ntx else RTOL)
+    if not math.isnan(float(exp["kd_term"])):
+        _near(terms[1][1], float(exp["kd_term"]), "KD term")
+
+
 def test_optimizer_step_and_checkpoint_roundtrip(dev, tmp_path):
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
     meta, _ = load("lb")
