@@ -1,4 +1,4 @@
-// Flash attention forward / backward for gfx950 (MFMA 16x16x32 bf16, fp32 softmax).
+// Flash attention forward / backward for gfx950 (bf16 MFMAs, fp32 softmax).
 //
 // Replaces the attention the reference reaches through transformers:
 //   Qwen2 causal GQA (HF5 qwen2 :80-140; 7B: 28q/4kv hd128, 0.5B: 14q/2kv hd64)
@@ -9,16 +9,18 @@
 //          o / do [B, S, H, hd] bf16 (token-major: what o_proj consumes / produces);
 //          lse [B, H, S] fp32 (natural log of sum exp(score)).
 //
-// Forward (per workgroup: 64 query rows of one head, 4 waves x 16 rows):
-//   S^T = K Q^T (MFMA A = K rows from LDS, B = Q in registers) so each lane owns ONE
-//   query's scores (4 keys x 4 tiles): the softmax max/sum are lane-local plus two
-//   cross-lane xors, the O^T = V^T P^T accumulator is lane-local per query (rescale with
-//   no shuffles), and P^T's registers ARE the B operand of the PV MFMA (key order
-//   permuted consistently with the V^T fragment read by ds_read_b64_tr_b16).
-// Backward (per workgroup: 64 keys of one kv head, 4 waves x 16 keys; loops over the
-//   group's query heads and 32-row query tiles): S = Q K^T and dP = dO V^T with the key
-//   on the lane, so P / dS registers feed dV^T += dO^T P and dK^T += Q^T dS directly;
-//   dS goes through LDS once for dQ += dS K, accumulated with fp32 atomics.
+// Forward, default k_attn_fwd32 (per workgroup: 128 query rows of one head, 4 waves x 32
+//   rows, 32x32x16 MFMAs): S^T = K Q^T so each lane pair (l, l ^ 32) owns ONE query's
+//   scores; max / sum are lane-local plus one v_permlane32_swap, the O^T = V^T P^T
+//   accumulator is lane-local per query, and the S accumulator registers ARE the B operand
+//   of the PV MFMA (key order permuted consistently with the V^T fragment read by
+//   ds_read_b64_tr_b16).  k_attn_fwd (16x16x32, 64 rows per workgroup) stays for A/B
+//   (KD_ATTN_FWD_V=16).
+// Backward: dK / dV per 128 keys of one kv head (k_attn_bwd_dkdv2: 4 waves x two 16-key
+//   sub-tiles; head dim 128: k_attn_bwd_dkdv, 64 keys), looping over the group's query heads
+//   and 32-row query tiles: S = Q K^T and dP = dO V^T with the key on the lane, so P / dS
+//   registers feed dV^T += dO^T P and dK^T += Q^T dS directly.  dQ by its own kernel
+//   (k_attn_bwd_dq: S and dP recomputed per query tile, no atomics).
 #include "common.h"
 
 #include <algorithm>

@@ -309,6 +309,9 @@ __global__ void __launch_bounds__(NTH, 2) k_gemm(GemmP p) {
 // Both swizzles are conflict-free for the 16x16x32 fragment reads (checked by
 // enumeration).
 // =============================================================================
+// read-modify-write epilogues: chunks per load group (epi_flush_g; 8 measured best, no spills
+// in the k-loops) and the q|k|v scatter's (its cos / sin loads; 4 spilled in v3)
+constexpr int EPI_G = 8, QKV_G = 2;
 constexpr int BK2 = 32, NST = 4, NTH2 = 512;
 
 __device__ __forceinline__ int f4(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }  // [0,2,3,1]
@@ -451,55 +454,88 @@ __device__ __forceinline__ void epi_to_lds_act(int act, const f32x4 (&acc)[MT][N
     }
 }
 
-// LDS image rows [0, ROWS) -> global rows m0 + row_off + lr, 16-B chunks (+ resid, + dst)
+// LDS image rows [0, ROWS) -> global rows m0 + lr, 16-B chunks (+ resid, + dst).
+// A thread's chunks share one column (NTHR % CPR == 0) and step RSTEP rows; they go G at a
+// time, the G residual / old-C loads all issued before the group's first store.  Loads placed
+// after the previous chunk's store cannot be hoisted by the compiler (the store may alias
+// them), so the one-chunk-at-a-time loop kept ONE 16-B load per lane in flight and the
+// read-modify-write epilogues moved their extra bytes at ~1.7 TB/s (tools/epi_cost.py).
+template <int ROWS, int BN, int NTHR, bool F32, bool RES, bool RF, bool ACC>
+__device__ __forceinline__ void epi_flush_g(const GemmP& p, const char* smem, int rs, void* dst_, int64_t ld, int m0,
+                                            int n0, int tid, bool full) {
+    constexpr int EPC = F32 ? 4 : 8;   // elements per 16-B chunk
+    constexpr int CPR = BN / EPC;
+    static_assert(NTHR % CPR == 0 && (ROWS * CPR) % NTHR == 0, "epi_flush: chunk map");
+    constexpr int RSTEP = NTHR / CPR, PER = ROWS * CPR / NTHR, G = PER < EPI_G ? PER : EPI_G;
+    static_assert(PER % G == 0, "epi_flush: group");
+    using RT = std::conditional_t<RF, f32x4, std::conditional_t<F32, bf16x4, bf16x8>>;   // residual chunk
+    using VT = std::conditional_t<F32, f32x4, bf16x8>;                                    // C chunk
+    const int c = tid % CPR, lr0 = tid / CPR;
+    const int col = n0 + c * EPC;
+    if (!full && col >= p.N) return;
+#pragma unroll 1
+    for (int g0 = 0; g0 < PER; g0 += G) {
+        RT rv[G];
+        VT cv[G];
+        if constexpr (RES || ACC) {
+#pragma unroll
+            for (int u = 0; u < G; ++u) {   // unconditional (rows clamped): a load inside a branch got its own vmcnt(0)
+                const int row = full ? m0 + lr0 + (g0 + u) * RSTEP : min(m0 + lr0 + (g0 + u) * RSTEP, p.M - 1);
+                if constexpr (RES) {
+                    const int64_t rr = p.res_mod > 0 ? row % p.res_mod : row;
+                    if constexpr (RF) rv[u] = *(const f32x4*)((const float*)p.resid + rr * p.ldr + col);
+                    else rv[u] = *(const RT*)(p.resid + rr * p.ldr + col);
+                }
+                if constexpr (ACC) {
+                    if constexpr (F32) cv[u] = *(const f32x4*)((const float*)dst_ + (int64_t)row * ld + col);
+                    else cv[u] = *(const bf16x8*)((const bf16*)dst_ + (int64_t)row * ld + col);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int lr = lr0 + (g0 + u) * RSTEP, row = m0 + lr;
+            if (!full && row >= p.M) continue;
+            if constexpr (F32) {
+                f32x4 v = *(const f32x4*)(smem + lr * rs + c * 16);
+                if constexpr (RES) {
+                    if constexpr (RF) v += rv[u];
+                    else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] += (float)rv[u][e];
+                    }
+                }
+                if constexpr (ACC) v += cv[u];
+                *(f32x4*)((float*)dst_ + (int64_t)row * ld + col) = v;
+            } else {
+                bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
+                if constexpr (RES || ACC) {
+                    float f[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) f[e] = (float)v[e];
+                    if constexpr (RES) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) f[e] += (float)rv[u][e];
+                    }
+                    if constexpr (ACC) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) f[e] += (float)cv[u][e];
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = (bf16)f[e];
+                }
+                *(bf16x8*)((bf16*)dst_ + (int64_t)row * ld + col) = v;
+            }
+        }
+    }
+}
+
 template <int ROWS, int BN, int NTHR, bool F32, bool RES, bool ACC>
 __device__ __forceinline__ void epi_flush(const GemmP& p, const char* smem, int rs, void* dst_, int64_t ld, int m0, int n0,
                                           int tid, bool full) {
-    constexpr int EPC = F32 ? 4 : 8;   // elements per 16-B chunk
-    constexpr int CPR = BN / EPC;
-#pragma unroll 4
-    for (int idx = tid; idx < ROWS * CPR; idx += NTHR) {
-        const int lr = idx / CPR, c = idx % CPR;
-        const int row = m0 + lr, col = n0 + c * EPC;
-        if (!full && (row >= p.M || col >= p.N)) continue;
-        const int rr = RES ? (p.res_mod > 0 ? row % p.res_mod : row) : 0;
-        if (F32) {
-            f32x4 v = *(const f32x4*)(smem + lr * rs + c * 16);
-            float* o = (float*)dst_ + (int64_t)row * ld + col;
-            if (RES) {
-                if (p.res_f32) {
-                    v += *(const f32x4*)((const float*)p.resid + (int64_t)rr * p.ldr + col);
-                } else {
-                    const bf16x4 rv = *(const bf16x4*)(p.resid + (int64_t)rr * p.ldr + col);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
-                }
-            }
-            if (ACC) v += *(const f32x4*)o;
-            *(f32x4*)o = v;
-        } else {
-            bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
-            bf16* o = (bf16*)dst_ + (int64_t)row * ld + col;
-            if (RES || ACC) {
-                float f[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) f[e] = (float)v[e];
-                if (RES) {
-                    const bf16x8 rv = *(const bf16x8*)(p.resid + (int64_t)rr * p.ldr + col);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) f[e] += (float)rv[e];
-                }
-                if (ACC) {
-                    const bf16x8 cv = *(const bf16x8*)o;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) f[e] += (float)cv[e];
-                }
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = (bf16)f[e];
-            }
-            *(bf16x8*)o = v;
-        }
-    }
+    // an fp32 C reads an fp32 or a bf16 residual (p.res_f32); a bf16 C a bf16 one
+    if (F32 && RES && p.res_f32) epi_flush_g<ROWS, BN, NTHR, F32, RES, F32 && RES, ACC>(p, smem, rs, dst_, ld, m0, n0, tid, full);
+    else epi_flush_g<ROWS, BN, NTHR, F32, RES, false, ACC>(p, smem, rs, dst_, ld, m0, n0, tid, full);
 }
 
 template <int ROWS, int BN, int NTHR, bool F32>
@@ -513,39 +549,58 @@ __device__ __forceinline__ void epi_flush_sel(const GemmP& p, const char* smem, 
 
 // Backward-activation flush (KD_ACT_DGELU_TANH / KD_ACT_DSWIGLU): the staged bf16 tile is the
 // activation's output gradient v (exactly the unfused GEMM output); multiply by act'(aux)
-// with the same per-element functions as k_act_bwd / k_swiglu_bwd.
-template <int ROWS, int BN, int NTHR>
-__device__ __forceinline__ void epi_flush_dact(const GemmP& p, const char* smem, int rs, int m0, int n0, int tid, bool full) {
+// with the same per-element functions as k_act_bwd / k_swiglu_bwd.  Chunks G at a time with
+// their aux loads issued first (epi_flush_g).
+template <int ROWS, int BN, int NTHR, bool GLU>
+__device__ __forceinline__ void epi_flush_dact_g(const GemmP& p, const char* smem, int rs, int m0, int n0, int tid, bool full) {
     constexpr int CPR = BN / 8;
-    const bool glu = p.act == KD_ACT_DSWIGLU;
-#pragma unroll 4
-    for (int idx = tid; idx < ROWS * CPR; idx += NTHR) {
-        const int lr = idx / CPR, c = idx % CPR;
-        const int row = m0 + lr, col = n0 + c * 8;
-        if (!full && (row >= p.M || col >= p.N)) continue;
-        const bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
-        const bf16* ar = p.aux + (int64_t)row * p.ld_aux;
-        bf16* cr = (bf16*)p.C + (int64_t)row * p.ldc;
-        if (glu) {
-            const bf16x8 g8 = *(const bf16x8*)(ar + col), u8 = *(const bf16x8*)(ar + p.N + col);
-            bf16x8 og, ou;
+    static_assert(NTHR % CPR == 0 && (ROWS * CPR) % NTHR == 0, "epi_flush_dact: chunk map");
+    constexpr int RSTEP = NTHR / CPR, PER = ROWS * CPR / NTHR, G = PER < EPI_G ? PER : EPI_G;
+    static_assert(PER % G == 0, "epi_flush_dact: group");
+    const int c = tid % CPR, lr0 = tid / CPR;
+    const int col = n0 + c * 8;
+    if (!full && col >= p.N) return;
+#pragma unroll 1
+    for (int g0 = 0; g0 < PER; g0 += G) {
+        bf16x8 x0[G], x1[G];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                float dg, du;
-                swiglu_grad((float)v[e], (float)g8[e], (float)u8[e], dg, du);
-                og[e] = (bf16)dg;
-                ou[e] = (bf16)du;
+        for (int u = 0; u < G; ++u) {   // unconditional (rows clamped), as in epi_flush_g
+            const int row = full ? m0 + lr0 + (g0 + u) * RSTEP : min(m0 + lr0 + (g0 + u) * RSTEP, p.M - 1);
+            const bf16* ar = p.aux + (int64_t)row * p.ld_aux + col;
+            x0[u] = *(const bf16x8*)ar;
+            if constexpr (GLU) x1[u] = *(const bf16x8*)(ar + p.N);
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int lr = lr0 + (g0 + u) * RSTEP, row = m0 + lr;
+            if (!full && row >= p.M) continue;
+            const bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
+            bf16* cr = (bf16*)p.C + (int64_t)row * p.ldc + col;
+            if constexpr (GLU) {
+                bf16x8 og, ou;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float dg, du;
+                    swiglu_grad((float)v[e], (float)x0[u][e], (float)x1[u][e], dg, du);
+                    og[e] = (bf16)dg;
+                    ou[e] = (bf16)du;
+                }
+                *(bf16x8*)cr = og;
+                *(bf16x8*)(cr + p.N) = ou;
+            } else {
+                bf16x8 o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)v[e] * gelu_tanh_grad((float)x0[u][e]));
+                *(bf16x8*)cr = o;
             }
-            *(bf16x8*)(cr + col) = og;
-            *(bf16x8*)(cr + p.N + col) = ou;
-        } else {
-            const bf16x8 x8 = *(const bf16x8*)(ar + col);
-            bf16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)v[e] * gelu_tanh_grad((float)x8[e]));
-            *(bf16x8*)(cr + col) = o;
         }
     }
+}
+
+template <int ROWS, int BN, int NTHR>
+__device__ __forceinline__ void epi_flush_dact(const GemmP& p, const char* smem, int rs, int m0, int n0, int tid, bool full) {
+    if (p.act == KD_ACT_DSWIGLU) epi_flush_dact_g<ROWS, BN, NTHR, true>(p, smem, rs, m0, n0, tid, full);
+    else epi_flush_dact_g<ROWS, BN, NTHR, false>(p, smem, rs, m0, n0, tid, full);
 }
 
 // bias of NT groups of 4 consecutive columns (the transposed accumulator layout), the dtype
@@ -593,42 +648,66 @@ __device__ __forceinline__ void load_bias(const GemmP& p, const int (&cols)[NT],
 }
 
 // q|k|v scatter flush: LDS bf16 image rows [0, ROWS) x BN -> head-major q / k / v (+RoPE), every
-// head of the tile whole in it (256 % hd == 0 or no RoPE), 8-column chunks (hd % 8 == 0)
+// head of the tile whole in it (256 % hd == 0 or no RoPE), 8-column chunks (hd % 8 == 0).  A
+// thread's chunks share one column, so the head / destination tensor / rotate_half partner are
+// computed once; the rows go G at a time with their cos / sin loads issued first (epi_flush_g).
 template <int ROWS, int BN, int NTHR>
 __device__ __forceinline__ void epi_flush_qkv(const GemmP& p, const char* smem, int rs, int m0, int n0, int tid) {
     constexpr int CPR = BN / 8;
+    static_assert(NTHR % CPR == 0 && (ROWS * CPR) % NTHR == 0, "epi_flush_qkv: chunk map");
+    constexpr int RSTEP = NTHR / CPR, PER = ROWS * CPR / NTHR, G = PER < QKV_G ? PER : QKV_G;
+    static_assert(PER % G == 0, "epi_flush_qkv: group");
     const int hd = p.shd, hh = hd >> 1, hdp = p.shdp, S = p.sS, nq = p.snq, nkv = p.snkv;
-#pragma unroll 2
-    for (int idx = tid; idx < ROWS * CPR; idx += NTHR) {
-        const int lr = idx / CPR, c = idx % CPR;
-        const int row = m0 + lr, col = n0 + c * 8;
-        if (row >= p.M || col >= p.N) continue;
-        const int head = col / hd, d0 = col - head * hd;
-        bf16* base;
-        int hidx, nh;
-        if (head < nq) { base = p.sq; hidx = head; nh = nq; }
-        else if (head < nq + nkv) { base = p.sk; hidx = head - nq; nh = nkv; }
-        else { base = p.sv; hidx = head - nq - nkv; nh = nkv; }
-        const int b = row / S, s = row - b * S;
-        bf16* drow = base + (((int64_t)b * nh + hidx) * S + s) * hdp;
-        bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
-        if (p.rcos && head < nq + nkv) {
-            const bool first = d0 < hh;
-            const int pc = first ? c * 8 + hh : c * 8 - hh;   // the rotate_half partner, same head, same tile
-            const bf16x8 pv = *(const bf16x8*)(smem + lr * rs + pc * 2);
-            const int i = first ? d0 : d0 - hh;
-            const f32x4 c0 = *(const f32x4*)(p.rcos + (int64_t)s * hh + i), c1 = *(const f32x4*)(p.rcos + (int64_t)s * hh + i + 4);
-            const f32x4 s0 = *(const f32x4*)(p.rsin + (int64_t)s * hh + i), s1 = *(const f32x4*)(p.rsin + (int64_t)s * hh + i + 4);
+    const int c = tid % CPR, lr0 = tid / CPR;
+    const int col = n0 + c * 8;
+    if (col >= p.N) return;
+    const int head = col / hd, d0 = col - head * hd;
+    bf16* base;
+    int hidx, nh;
+    if (head < nq) { base = p.sq; hidx = head; nh = nq; }
+    else if (head < nq + nkv) { base = p.sk; hidx = head - nq; nh = nkv; }
+    else { base = p.sv; hidx = head - nq - nkv; nh = nkv; }
+    const bool rope = p.rcos && head < nq + nkv;
+    const bool first = d0 < hh;
+    const int pc = first ? c * 8 + hh : c * 8 - hh;   // the rotate_half partner, same head, same tile
+    const int ri = first ? d0 : d0 - hh;
+    const bool last = d0 + 8 == hd;
+#pragma unroll 1
+    for (int g0 = 0; g0 < PER; g0 += G) {
+        f32x4 c0[G], c1[G], s0[G], s1[G];
+        int bq[G], sq[G];   // (batch, position) of the row (clamped to M - 1)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float cs = e < 4 ? c0[e] : c1[e - 4], sn = e < 4 ? s0[e] : s1[e - 4];
-                const float x = (float)v[e], y = (float)pv[e];
-                v[e] = (bf16)(first ? rope_first(x, y, cs, sn) : rope_second(x, y, cs, sn));
+        for (int u = 0; u < G; ++u) {   // unconditional loads (rows clamped), as in epi_flush_g
+            const int row = min(m0 + lr0 + (g0 + u) * RSTEP, p.M - 1);
+            const int b = row / S, sr = row - b * S;
+            bq[u] = b;
+            sq[u] = sr;
+            if (p.rcos) {
+                const float* cp = p.rcos + (int64_t)sr * hh + ri;
+                const float* sp = p.rsin + (int64_t)sr * hh + ri;
+                c0[u] = *(const f32x4*)cp; c1[u] = *(const f32x4*)(cp + 4);
+                s0[u] = *(const f32x4*)sp; s1[u] = *(const f32x4*)(sp + 4);
             }
         }
-        *(bf16x8*)(drow + d0) = v;
-        if (d0 + 8 == hd)
-            for (int d = hd; d < hdp; d += 8) *(bf16x8*)(drow + d) = (bf16x8){};
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int lr = lr0 + (g0 + u) * RSTEP;
+            if (m0 + lr >= p.M) continue;
+            bf16* drow = base + (((int64_t)bq[u] * nh + hidx) * S + sq[u]) * hdp;
+            bf16x8 v = *(const bf16x8*)(smem + lr * rs + c * 16);
+            if (rope) {
+                const bf16x8 pv = *(const bf16x8*)(smem + lr * rs + pc * 2);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float cs = e < 4 ? c0[u][e] : c1[u][e - 4], sn = e < 4 ? s0[u][e] : s1[u][e - 4];
+                    const float x = (float)v[e], y = (float)pv[e];
+                    v[e] = (bf16)(first ? rope_first(x, y, cs, sn) : rope_second(x, y, cs, sn));
+                }
+            }
+            *(bf16x8*)(drow + d0) = v;
+            if (last)
+                for (int d = hd; d < hdp; d += 8) *(bf16x8*)(drow + d) = (bf16x8){};
+        }
     }
 }
 

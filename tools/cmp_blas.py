@@ -38,6 +38,7 @@ def timeit(f, it=10):
 
 for r in rows:
     kind, shp = r["shape"].split(":")[:2]
+    kind = kind.replace("_swiglu", "").replace("_dact", "")   # timed as the plain GEMM of that layout
     M, N, K = (int(x) for x in shp.split("x"))
     f32 = ":f32" in r["shape"]
     if kind == "gemm_kk":
