@@ -1,7 +1,8 @@
 """Fit gemm.hip:plan_gemm's cost model to a tune_gemm.py sweep and report how close the
 model's picks come to the measured best, weighted by each shape's launches per step.
     python tools/fit_plan.py gemm_tune.jsonl [step_shapes.json]
-Model (microseconds): waves x (k-steps per split x step[v,c] + fixed[v,c]) + split traffic / BW,
+Model (microseconds): waves x (k-steps per split x step[v,c] + fixed[v,c]) + split traffic / BW
+(+ a fixed cost of the split's reduce launch),
 v = kernel/tile (v3 256x256, 256x128, 128x256, v8), c = operand class (K-major x K-major, other)."""
 import json
 import math
@@ -45,17 +46,18 @@ for r in rows:
 def pred(x, shape, v, S):
     c, waves, kcs, traffic = feats(shape, v, S)
     step, fixed = x[2 * (NV * c + v)], x[2 * (NV * c + v) + 1]
-    return waves * (kcs * step + fixed) + traffic / (x[4 * NV] * 1e6)
+    return waves * (kcs * step + fixed) + traffic / (x[4 * NV] * 1e6) + (x[4 * NV + 1] if S > 1 else 0.0)
 
 
 def resid(x):
     return [math.log(max(pred(x, s, v, S), 1e-3)) - math.log(t) for s, v, S, t in data]
 
 
-x0 = np.array([0.8, 4.0] * (2 * NV) + [6.0])
-fit = least_squares(resid, x0, bounds=([0.05, 0.0] * (2 * NV) + [1.0], [5.0, 50.0] * (2 * NV) + [20.0]))
+x0 = np.array([0.8, 4.0] * (2 * NV) + [6.0, 2.0])
+fit = least_squares(resid, x0, bounds=([0.05, 0.0] * (2 * NV) + [1.0, 0.0], [5.0, 50.0] * (2 * NV) + [20.0, 50.0]))
 x = fit.x
-print("step/fixed per class (kk, mn) x variant (v3 256x256, 256x128, 128x256, v8, v9); BW TB/s", round(x[4 * NV], 3))
+print("step/fixed per class (kk, mn) x variant (v3 256x256, 256x128, 128x256, v8, v9); BW TB/s", round(x[4 * NV], 3),
+      "; split launch us", round(x[4 * NV + 1], 3))
 for c in range(2):
     print(" ", ["kk", "mn"][c], [(round(x[2 * (NV * c + v)], 4), round(x[2 * (NV * c + v) + 1], 3)) for v in range(NV)])
 tot_best = tot_pick = 0.0
