@@ -1,0 +1,51 @@
+"""kd_gemm_plan (gemm.hip plan_gemm) through the C ABI on the CPU: the cost model's picks on
+the step's shapes that its round-3 refit was measured on (profiles/r03/gemm_tune.jsonl).
+No kernel is launched; the plan only reads the descriptor's shape / layout / dtypes."""
+import ctypes as C
+
+import pytest
+
+from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import _native as NV
+from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
+
+
+def _plan(M, N, K, lay="kk", f32=False, acc=False, ws=None):
+    d = NV.KdGemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.a_layout = NV.KD_LAYOUT_K_MAJOR if lay[0] == "k" else NV.KD_LAYOUT_MN_MAJOR
+    d.b_layout = NV.KD_LAYOUT_K_MAJOR if lay[1] == "k" else NV.KD_LAYOUT_MN_MAJOR
+    d.A = d.B = d.C = d.workspace = 0x10000   # never dereferenced by the plan
+    d.workspace_bytes = ops.GEMM_SPLITK_WS if ws is None else ws
+    d.lda = K if lay[0] == "k" else M
+    d.ldb = K if lay[1] == "k" else N
+    d.ldc = N
+    d.c_dtype = NV.KD_DTYPE_F32 if f32 else NV.KD_DTYPE_BF16
+    d.accumulate = int(acc)
+    d.alpha = 1.0
+    v, s, dp = C.c_int32(), C.c_int32(), C.c_int32()
+    assert NV.lib().kd_gemm_plan(C.byref(d), C.byref(v), C.byref(s), C.byref(dp)) == 0
+    return v.value, s.value, dp.value
+
+
+def test_teacher_down_proj_hybrid():
+    # 336 tiles of 256x256: one whole wave unsplit, the 80-tile tail split 3 ways
+    assert _plan(6144, 3584, 18944) == (16, 3, 256)
+
+
+def test_siglip_qkv_not_split():
+    # 5832x3456x1152: the round-2 model chose a hybrid split here (69 us measured vs 60 unsplit)
+    v, s, dp = _plan(5832, 3456, 1152)
+    assert s == 1 and dp == 0 and v in (2, 3, 4, 16)
+
+
+def test_big_forward_is_v8_unsplit():
+    assert _plan(6144, 37888, 3584) == (16, 1, 0)
+    assert _plan(6144, 152064, 3584) == (16, 1, 0)
+
+
+@pytest.mark.parametrize("shape", [(6144, 896, 9728, "kn"), (9728, 896, 6144, "nn", True, True),
+                                   (1152, 1152, 5832, "nn", True, True), (6144, 896, 4864, "kk", True)])
+def test_split_needs_workspace(shape):
+    # without a workspace no plan may split
+    v, s, dp = _plan(*shape, ws=0)
+    assert s == 1 and dp == 0
