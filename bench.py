@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4] [--no-cpu-baseline] [--cpu-extrapolate]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+`--gpus N` with N > 1 outside a torch.distributed launcher starts the N ranks itself (one
+process per GPU, `torch.distributed.run` as a child process, before this process touches the
+GPU); under a launcher WORLD_SIZE must equal N.  `--dry` replaces the model step by a gloo
+all-reduce on the CPU (tests of the launcher and of the max-over-ranks timing).
+
 A step = one `training_step(batch)` + `loss.backward()` + `optimizer.step()` +
 `zero_grad()` of the drop-in KD module: 7B RGB teacher forward, 0.5B depth student
 forward, fused KD-loss forward+backward, student backward, bucketed RCCL gradient
@@ -61,15 +66,16 @@ def step_tflops_per_sample(kind: str, phase: int) -> float:
     return (teacher + s_fwd + s_bwd) / 1e12
 
 
-def build(cfg, dev, teacher_fp8=False):
+def build(cfg, dev, teacher_fp8=False, grad_comm_dtype=None):
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
     S, T = "llava-hf/llava-onevision-qwen2-0.5b-ov-hf", "llava-hf/llava-onevision-qwen2-7b-ov-hf"
+    kw = dict(teacher_fp8=teacher_fp8, grad_comm_dtype=grad_comm_dtype)
     if cfg["kind"] == "lb":
-        m = K.LogitBasedKD(S, T, teacher_fp8=teacher_fp8)
+        m = K.LogitBasedKD(S, T, **kw)
     elif cfg["kind"] == "fb":
-        m = K.FeatureBasedKD(S, T, teacher_fp8=teacher_fp8)
+        m = K.FeatureBasedKD(S, T, **kw)
     else:
-        m = K.OnlineKnowledgeDistillationLLavaOneVision(S, T, phase=cfg["phase"], teacher_fp8=teacher_fp8)
+        m = K.OnlineKnowledgeDistillationLLavaOneVision(S, T, phase=cfg["phase"], **kw)
         if cfg["phase"] == 2:
             m.freeze_student_vision_layers()
         if cfg["phase"] == 1:
@@ -268,9 +274,112 @@ def fp8_teacher_delta(m, batch):
                           "cosine >= 0.98")
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str], dry: bool) -> int:
+    """`bench.py --gpus N` without a launcher: run N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code.  Nothing here touches
+    the GPU (torch.cuda.device_count() does not initialise it), so no process that holds a
+    GPU context is ever replaced."""
+    import subprocess
+    if not dry:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(json.dumps({"error": f"--gpus {n} but only {have} GPU(s) visible", "n_gpus": n}), flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL across processes)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_main(a, world: int, rank: int):
+    """--dry: the launcher / timing / reporting skeleton without the model (gloo, CPU): a
+    'step' is an all-reduce of a small CPU tensor."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world
+    x = torch.ones(1 << 16)
+
+    def step():
+        if world > 1:
+            dist.all_reduce(x)
+        time.sleep(0.01)
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    per_rank = [dt]
+    if world > 1:
+        g = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(g, torch.tensor([dt], dtype=torch.float64))
+        per_rank = [float(v) for v in g]
+    dt = max(per_rank)
+    if rank == 0:
+        print(json.dumps({"metric": "dry launcher check", "value": round(world * a.steps / dt, 4), "unit": "steps/s",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "dry": True,
+                          "per_rank_ms_per_step": [round(v / a.steps * 1e3, 3) for v in per_rank]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def allreduce_cost(m, dist, dev, world):
+    """The DP exchange of one optimizer step: the buckets GradSync launched in the last
+    reducing backward (count, bytes, dtype), and the same all-reduces timed alone on a
+    scratch buffer (serialized, after the timed region; in the step they overlap the rest
+    of the backward and the next teacher forward)."""
+    import torch
+    gs = m._gsync
+    if gs is None or not gs.last_buckets:
+        return None
+    dt_ = gs.comm_dtype or torch.float32
+    n = sum(gs.last_buckets)
+    buf = torch.zeros(n, dtype=dt_, device=dev)
+    op = dist.ReduceOp.AVG
+    for _ in range(2):   # the first round warms the communicator's channels
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        off = 0
+        for c in gs.last_buckets:
+            dist.all_reduce(buf[off:off + c], op=op)
+            off += c
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+    t = torch.tensor([ms], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item())
+    nbytes = n * buf.element_size()
+    del buf
+    return dict(buckets=len(gs.last_buckets), bytes=nbytes, dtype=str(dt_).replace("torch.", ""),
+                standalone_ms=round(ms, 3),
+                ring_bus_GBps=round(2 * (world - 1) / world * nbytes / (ms * 1e-3) / 1e9, 1),
+                measured="the last reducing backward's buckets all-reduced (AVG) alone, after the timed region, "
+                         "max over ranks; in the step they overlap the backward and the next teacher forward")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
+    ap.add_argument("--dry", action="store_true", help="launcher check without the model (gloo on the CPU)")
+    ap.add_argument("--grad-comm-dtype", default="fp32", choices=("fp32", "bf16"),
+                    help="dtype of the DP gradient all-reduce buckets (dp.GradSync)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
@@ -292,21 +401,33 @@ def main():
                          "roofline kernel's rocprof average)")
     a = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (a.gpus or 1) > 1:
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:], a.dry))
+    world = int(env_world or 1)
+    if a.gpus is not None and a.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry:
+        return dry_main(a, world, rank)
+
+    import torch
+    import torch.distributed as dist
+    if local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
     cfg = CONFIGS[a.config]
     B = a.batch or cfg["batch"]
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
     teacher_fp8 = False if a.teacher_bf16 else (a.fp8_families or cfg.get("teacher_fp8") or False)
-    m, opt = build(cfg, dev, teacher_fp8=teacher_fp8)
+    comm_dtype = torch.bfloat16 if a.grad_comm_dtype == "bf16" else None
+    m, opt = build(cfg, dev, teacher_fp8=teacher_fp8, grad_comm_dtype=comm_dtype)
     m.concurrent_student = not a.serial
     m.student_model.wlane.serial = a.serial   # --serial: one stream for everything (profiling)
     # two synthetic batches, alternated, so every step's teacher forward is a fresh one
@@ -333,20 +454,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    c0 = time.thread_time()
     for i in range(a.steps):
         loss = step(a.warmup + i)
     host_dt = time.perf_counter() - t0   # host enqueue time of the K steps
-    host_cpu = time.thread_time() - c0   # CPU time of the enqueueing thread (not the time it sat blocked)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    per_rank = [dt]
+    if world > 1:   # every rank's time; the job's time is the slowest rank's
+        g = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(g, torch.tensor([dt], dtype=torch.float64, device=dev))
+        per_rank = [float(v.item()) for v in g]
+        dt = max(per_rank)
+    comm = allreduce_cost(m, dist, dev, world) if world > 1 else None
     loss_v = float(loss.item())
     # host cost of enqueueing ONE step onto an idle GPU (in the timed loop the HIP queue is
     # full and every launch waits for a slot, so host_enqueue tracks the GPU time)
@@ -436,9 +558,10 @@ def main():
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": 1536, "image": "336x336 (2 tiles, 1485 tokens)",
                    "parallelism": f"dp{world}"},
         "mfu": round(value * tf_sample / world / PEAK_BF16_TFLOPS, 4),
+        "per_rank_ms_per_step": [round(v / a.steps * 1e3, 2) for v in per_rank],
+        "grad_allreduce": comm,
         "host_enqueue_ms_per_step": round(host_dt * 1e3 / a.steps, 2),
         "host_enqueue_ms_idle_step": round(host_idle_ms, 2),
-        "host_cpu_ms_per_step": round(host_cpu * 1e3 / a.steps, 2),
         "tflop_per_sample": round(tf_sample, 2),
         "loss": round(loss_v, 5),
         "teacher_fwd": tfwd,
@@ -451,18 +574,20 @@ def main():
         out["dtype"] = f"bf16 (student, loss) + fp8 e4m3 teacher linears ({m.teacher_fp8})"
         if rank == 0:
             out["fp8_teacher_delta"] = fp8_teacher_delta(m, batches[0])
-    if rank == 0 and not a.no_delta:
+    if not a.no_delta:
         # one more step with its logits kept: the fused loss kernel's terms vs the CPU oracle
-        # on the same (bf16) logits
-        m.keep_logits = True
+        # on the same (bf16) logits.  Every rank takes the step (its backward all-reduces);
+        # rank 0 compares.
+        m.keep_logits = rank == 0
         step(a.warmup + a.steps + 2)
         torch.cuda.synchronize()
         m.keep_logits = False
         variant, T = m._loss_spec()[:2]
-        try:
-            out["kd_loss_delta"] = kd_loss_delta(m, batches[(a.warmup + a.steps + 2) % 2], (variant, T))
-        except Exception as e:  # report, never hide
-            out["kd_loss_delta"] = {"error": repr(e)}
+        if rank == 0:
+            try:
+                out["kd_loss_delta"] = kd_loss_delta(m, batches[(a.warmup + a.steps + 2) % 2], (variant, T))
+            except Exception as e:  # report, never hide
+                out["kd_loss_delta"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = host_cpu_info()[0]
         try:

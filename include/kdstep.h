@@ -178,7 +178,12 @@ typedef struct {
                                  21 stream-K on 16 (256 workgroups take equal runs of the tiles' k-steps,
                                  shared tiles folded from fp32 partial planes; needs workspace);
                                  22 16 with register staging instead of LDS-DMA (K-major operands;
-                                 measured slower, kept for A/B: tools/ab_gemm_rs.py) */
+                                 measured slower, kept for A/B: tools/ab_gemm_rs.py);
+                                 23 the 256x256 4-wave tiles on 32x32x16 MFMAs (v11, K-major x K-major;
+                                 other layouts run 16); 24 = 16 forced even where the default is v11 / v12;
+                                 25 diagnostic build of 16 (whole-line DMA rows, WRONG results: timing only);
+                                 26 16 with whole-cache-line staging of K-major operands (v12, stage pairs;
+                                 K-major x K-major, other layouts run 16; bit-identical to 16) */
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;

@@ -43,12 +43,15 @@ class GradSync:
         self.unsynced = False    # local grads accumulated since the last reduction
         self.world = dist.get_world_size()
         self.avg_in_collective = dist.get_backend() == "nccl"   # RCCL AVG; gloo has no AVG
+        self.last_buckets = []   # element counts of the buckets of the last reducing backward
+        self._cur_buckets = []
 
     # -------------------------------------------------------------- backward ----
     def begin(self, sync: bool):
         self.wait()              # nothing in flight while this backward accumulates into grad
         self.active = bool(sync)
         self.hi = None
+        self._cur_buckets = []
 
     def layer_done(self, first: int, before_launch=None):
         """Everything from flat offset `first` to the high-water mark is final."""
@@ -69,6 +72,7 @@ class GradSync:
             if top > lo:
                 self._launch(lo, top)
             self.unsynced = False
+            self.last_buckets = list(self._cur_buckets)
         else:
             self.unsynced = True
         self.active = False
@@ -88,8 +92,12 @@ class GradSync:
             w.wait()
             if buf is not None:   # bf16 bucket back into the fp32 buffer
                 if g.is_cuda:
+                    import torch
                     from . import ops
                     ops.cast_bf16_f32(buf, g)
+                    # the bucket was allocated on the backward's stream; this cast runs on the
+                    # awaiting one (the optimizer's): keep the block until the cast has read it
+                    buf.record_stream(torch.cuda.current_stream())
                 else:
                     g.copy_(buf)
             if not self.avg_in_collective:
@@ -109,5 +117,6 @@ class GradSync:
             else:
                 buf.copy_(g)
         t = g if buf is None else buf
+        self._cur_buckets.append(int(g.numel()))
         op = d.ReduceOp.AVG if self.avg_in_collective else d.ReduceOp.SUM
         self.works.append((d.all_reduce(t, op=op, async_op=True), g, buf))

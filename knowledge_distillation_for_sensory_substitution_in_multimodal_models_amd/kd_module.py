@@ -33,7 +33,8 @@ import torch.nn as nn
 
 from . import ops
 from .dp import GradSync
-from .modeling import (STREAM_PRIORITY_HIGH, STUDENT_05B, TEACHER_7B, LlavaOnevisionModel, tiny_config)
+from .modeling import (STREAM_PRIORITY_HIGH, STUDENT_05B, TEACHER_7B, LlavaOnevisionModel, real_width_config,
+                       tiny_config)
 
 try:  # the reference's base class when installed; otherwise a minimal stand-in
     import pytorch_lightning as _pl  # noqa: F401
@@ -53,7 +54,12 @@ MODEL_CONFIGS = {
     "llava-hf/llava-onevision-qwen2-7b-ov-hf": TEACHER_7B,
     "tiny-student": tiny_config(teacher=False),
     "tiny-teacher": tiny_config(teacher=True),
+    # the real widths at 2 layers per tower (model-level parity fixtures, tests/golden/model_real_*)
+    "real2-student": real_width_config(teacher=False, layers=2),
+    "real2-teacher": real_width_config(teacher=True, layers=2),
 }
+# the public checkpoints' names: weights too large for the CPU RNG (device RNG instead)
+_HUB_NAMES = ("llava-hf/llava-onevision-qwen2-0.5b-ov-hf", "llava-hf/llava-onevision-qwen2-7b-ov-hf")
 
 
 def _device():
@@ -77,8 +83,25 @@ class _KDStepFn(torch.autograd.Function):
         return None, None, None
 
 
+_FP16_MSG = ("the MI355X KD step trains in bf16 with fp32 master weights (no loss scaling); the reference's "
+             "fp16 autocast + GradScaler mode (Trainer precision=\"16\", DT1T:147) is not supported: use "
+             "precision=\"bf16-true\" (INTEGRATION.md)")
+
+
+def check_trainer_precision(precision) -> None:
+    """Reject the fp16 modes (precision "16", "16-mixed", "16-true"): a GradScaler would scale
+    the loss and then look for torch .grad tensors the fused optimizer never creates."""
+    p = str(precision if precision is not None else "").strip().lower()
+    if p == "16" or p.startswith("16-") or p in ("fp16", "half"):
+        raise ValueError(_FP16_MSG)
+
+
 class FusedAdamW(torch.optim.Optimizer):
     """torch.optim.AdamW semantics (DT:198-201) as one kernel over the trainable range."""
+
+    # GradScaler.step hands itself to a step() that takes `grad_scaler`: the fp16 path is
+    # then refused here with a clear error instead of an assertion inside the scaler
+    _step_supports_amp_scaling = True
 
     def __init__(self, module, lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         super().__init__([module._anchor], dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -86,7 +109,10 @@ class FusedAdamW(torch.optim.Optimizer):
         self.step_count = 0
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, grad_scaler=None):
+        # GradScaler passes itself (torch 2.x), or sets grad_scale / found_inf (announced)
+        if grad_scaler is not None or getattr(self, "grad_scale", None) is not None:
+            raise RuntimeError(_FP16_MSG)
         loss = closure() if closure is not None else None
         m = self.module
         g = self.param_groups[0]
@@ -235,7 +261,9 @@ class _KDBase(_Base):
         # Trainer's value (the reference sets it there, DT1T:70, :155), else 1
         self.accumulate_grad_batches = None if accumulate_grad_batches is None else int(accumulate_grad_batches)
         dev = _device()
-        small = model_name_student.startswith("tiny")
+        # test models draw their weights from the CPU RNG in spec order (bitwise what the
+        # reference's fixtures were generated with); the full-size ones from the device RNG
+        small = model_name_student not in _HUB_NAMES
         self.student_model = LlavaOnevisionModel(MODEL_CONFIGS[model_name_student], dev, trainable=True,
                                                  seed=seed_student, cpu_rng=small)
         self.teacher_model = None
@@ -326,8 +354,15 @@ class _KDBase(_Base):
     def unfreeze_student_vision_layers(self):            # DT:516-523
         self.student_model.train_vision = True
 
+    def _trainer_precision(self):
+        try:
+            tr = self.trainer   # LightningModule.trainer raises when no Trainer is attached
+        except Exception:
+            tr = None
+        return getattr(tr, "precision", None) if tr is not None else None
+
     def setup(self, stage=None):                         # DT:88-91
-        pass
+        check_trainer_precision(self._trainer_precision())
 
     # --------------------------------------------------------------- losses ----
     def _loss_spec(self):
@@ -335,6 +370,7 @@ class _KDBase(_Base):
         raise NotImplementedError
 
     def configure_optimizers(self):                      # DT:198-201
+        check_trainer_precision(self._trainer_precision())
         opt = FusedAdamW(self, lr=self.learning_rate)
         sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
         return [opt], [sched]
@@ -561,6 +597,17 @@ class _KDBase(_Base):
             if getattr(self.teacher_model, "fp8", False):
                 self.teacher_model.enable_fp8(self.teacher_model.fp8_families)   # re-quantise the new weights
 
+    def load_hf_weights(self, student: dict | None = None, teacher: dict | None = None, strict: bool = True):
+        """The weights `from_pretrained(model_name_*)` would load (DT:33-48), given as
+        LlavaOnevisionForConditionalGeneration state_dicts in the transformers-4.45 or 5.x
+        key layout (e.g. read from the hub's safetensors files with safetensors.torch.load_file)."""
+        if student is not None:
+            self.student_model.load_hf_state_dict(student, strict=strict)
+        if teacher is not None:
+            if self.teacher_model is None:
+                raise ValueError(f"{type(self).__name__} has no teacher")
+            self.teacher_model.load_hf_state_dict(teacher, strict=strict)
+
     def _hparams(self):
         # everything that changes the objective or the update is saved, so load_from_checkpoint
         # resumes the same run (loss grouping changes the loss: test_loss_group_size_*)
@@ -660,6 +707,7 @@ class FeatureBasedKD(_KDBase):
         return "kl_logtarget", self.T, self.soft_target_loss_weight, self.ce_loss_weight, 1.0
 
     def configure_optimizers(self):        # FB:233-234 (no scheduler)
+        check_trainer_precision(self._trainer_precision())
         return FusedAdamW(self, lr=self.learning_rate)
 
 
@@ -681,4 +729,5 @@ class LlavaOnevisionModule(_KDBase):
         return "none", 1.0, 0.0, 1.0, None
 
     def configure_optimizers(self):        # BD:137-138
+        check_trainer_precision(self._trainer_precision())
         return FusedAdamW(self, lr=self.learning_rate)

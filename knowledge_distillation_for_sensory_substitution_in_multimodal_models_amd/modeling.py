@@ -102,6 +102,15 @@ def tiny_config(teacher: bool = False) -> LlavaConfig:
     return LlavaConfig(v, t)
 
 
+def real_width_config(teacher: bool = False, layers: int = 2) -> LlavaConfig:
+    """The REAL architectures (SigLIP 1152/4304, 16 x hd 72; Qwen2-7B 3584/18944, 28q/4kv
+    hd 128; Qwen2-0.5B 896/4864, 14q/2kv hd 64; real vocabularies) cut to `layers` layers
+    per tower: model-level parity at the real kernel shapes (tests/golden/model_real_*.npz)."""
+    from dataclasses import replace
+    base = TEACHER_7B if teacher else STUDENT_05B
+    return replace(base, vision=replace(base.vision, layers=layers), text=replace(base.text, layers=layers))
+
+
 # -------------------------------------------------------------- param specs ----
 @dataclass
 class Spec:
@@ -286,6 +295,44 @@ class ParamStore:
         return seen
 
 
+# ------------------------------------------------------- hub key layouts ----
+def hub_key_to_445(k: str) -> str:
+    """A LlavaOnevisionForConditionalGeneration state_dict key in either transformers layout
+    -> the transformers-4.45 name the reference's checkpoints and this build use.
+
+    4.45 (the reference's pin, and the hub's llava-onevision-qwen2-*-ov-hf safetensors):
+    `vision_tower.vision_model.*`, `multi_modal_projector.*`, `image_newline`,
+    `language_model.model.*`, `language_model.lm_head.weight` -- returned unchanged.
+    5.x (installed here): `model.vision_tower.*`, `model.multi_modal_projector.*`,
+    `model.image_newline`, `model.language_model.*`, `lm_head.weight`."""
+    if k.startswith("model.vision_tower.vision_model."):      # 4.5x intermediate layout
+        return "vision_tower.vision_model." + k[len("model.vision_tower.vision_model."):]
+    if k.startswith("model.vision_tower."):
+        return "vision_tower.vision_model." + k[len("model.vision_tower."):]
+    if k.startswith("model.multi_modal_projector."):
+        return k[len("model."):]
+    if k == "model.image_newline":
+        return "image_newline"
+    if k.startswith("model.language_model.model."):
+        return "language_model.model." + k[len("model.language_model.model."):]
+    if k.startswith("model.language_model."):
+        return "language_model.model." + k[len("model.language_model."):]
+    if k == "lm_head.weight":
+        return "language_model.lm_head.weight"
+    return k
+
+
+def hf_state_dict_to_445(sd: dict) -> dict:
+    """Rename a whole state_dict (either layout) to the 4.45 names (hub_key_to_445)."""
+    out = {}
+    for k, v in sd.items():
+        k4 = hub_key_to_445(k)
+        if k4 in out:
+            raise KeyError(f"{k} and another key both map to {k4}")
+        out[k4] = v
+    return out
+
+
 # ------------------------------------------------------------------ helpers ----
 def rope_tables(seq: int, hd: int, theta: float, device):
     """cos/sin [seq, hd/2] fp32 as HF's Qwen2RotaryEmbedding (inv_freq in fp32)."""
@@ -453,6 +500,16 @@ class LlavaOnevisionModel:
             self._maps[key] = (torch.from_numpy(arr).to(self.device), torch.from_numpy(lens).to(self.device))
         maps, lens = self._maps[key]
         return ops.image_src_map(input_ids, self.cfg.image_token_id, maps, lens, self.err)
+
+    # -- weights from a hub / transformers state_dict
+    def load_hf_state_dict(self, sd: dict, strict: bool = True):
+        """Load `LlavaOnevisionForConditionalGeneration.state_dict()` weights in the
+        transformers-4.45 or 5.x key layout (hub_key_to_445) into the flat buffer (bf16; the
+        fp32 master of a trainable model too); a frozen fp8 model is re-quantised."""
+        seen = self.P.load_state_dict(hf_state_dict_to_445(sd), strict=strict)
+        if self.fp8:
+            self.enable_fp8(self.fp8_families)
+        return seen
 
     # -- fp8 teacher (BASELINE config c4)
     def enable_fp8(self, families="all"):

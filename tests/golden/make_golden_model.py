@@ -1,6 +1,6 @@
 """End-to-end golden fixtures from the REFERENCE's forward() (dev container only).
 
-    python tests/golden/make_golden_model.py [all | bench | geometry]
+    python tests/golden/make_golden_model.py [all | bench | geometry | real [name ...]]
 
 Tiny-width LLaVA-OneVision teacher/student (real vocab 152064/151936, real 336x336 token
 layout: 2 tiles, 1485 image tokens, L=1536) with seeded weights drawn by the build's own
@@ -8,6 +8,10 @@ ParamStore (CPU RNG, spec order) are loaded into transformers' model; the refere
 DT / LB / FB / BD module code (forward, compute_*_loss, contrastive_loss, hooks) runs the
 step, autograd gives the student gradients.  Only outputs are committed
 (tests/golden/model_*.npz).  Weights and inputs are regenerated from seeds in the tests.
+
+`real`: the same with the REAL widths cut to 2 layers per tower (model_real_*.npz, bs 1):
+SigLIP 1152/4304 with 16 heads of hd 72, Qwen2-7B 3584/18944 with 28q/4kv heads of hd 128,
+Qwen2-0.5B 896/4864 with 14q/2kv heads of hd 64, the real vocabularies.
 """
 from __future__ import annotations
 
@@ -26,7 +30,11 @@ sys.path.insert(0, str(HERE))
 import make_golden as MG  # noqa: E402
 from oracle.model import hf5_key  # noqa: E402
 from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import (  # noqa: E402
-    ParamStore, tiny_config)
+    ParamStore, real_width_config, tiny_config)
+from model_fixtures import GRAD_SAMPLE, grad_sample_index  # noqa: E402
+
+CONFIGS = {"tiny": (tiny_config(True), tiny_config(False)),
+           "real2": (real_width_config(True, 2), real_width_config(False, 2))}
 from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import (  # noqa: E402
     synthetic_batch, synthetic_batch_mixed)
 
@@ -34,8 +42,8 @@ SEED_T, SEED_S, SEED_DATA = 1, 2, 0
 B, L = 2, 1536
 
 
-def tiny_state(teacher: bool, seed: int):
-    P = ParamStore(tiny_config(teacher), "cpu")
+def tiny_state(teacher: bool, seed: int, cfg=None):
+    P = ParamStore(cfg or tiny_config(teacher), "cpu")
     P.init_(seed, cpu_rng=True)
     return {k: v.float().clone() for k, v in P.state_dict().items()}
 
@@ -60,11 +68,11 @@ def hf_model(cfg, sd):
     return m
 
 
-def batch_cpu(sizes=None):
+def batch_cpu(sizes=None, bs=B):
     """The 336x336 bench layout (B = 2, L = 1536), or with `sizes` a SUNRGBD-geometry batch
     (data.synthetic_batch_mixed: one image per sample at its own size, right padding)."""
     if sizes is None:
-        b = synthetic_batch(B, "cpu", L=L, seed=SEED_DATA, pixel_dtype=torch.bfloat16, cpu_rng=True)
+        b = synthetic_batch(bs, "cpu", L=L, seed=SEED_DATA, pixel_dtype=torch.bfloat16, cpu_rng=True)
     else:
         b = synthetic_batch_mixed(sizes, "cpu", seed=SEED_DATA, pixel_dtype=torch.bfloat16, cpu_rng=True)
     for k in ("rgb_pixel_values", "depth_pixel_values"):
@@ -130,17 +138,27 @@ def logit_stats(logits, rows=LOGIT_ROWS):
             x[:, list(rows), ::LOGIT_COL_STRIDE].float().numpy())
 
 
-def run(kind, phase, teacher_sd, student_sd, out_name, sizes=None):
+_REF = {}
+
+
+def _ref_classes():
+    if not _REF:
+        MG._install_stub()
+        _REF.update(DT=MG._load("ref_dt", MG.DT_PATH), LB=MG._load("ref_lb", MG.LB_PATH),
+                    FB=MG._load("ref_fb", MG.FB_PATH), BD=MG._load_bd())
+    return _REF["DT"], _REF["LB"], _REF["FB"], _REF["BD"]
+
+
+def run(kind, phase, teacher_sd, student_sd, out_name, sizes=None, model="tiny", bs=B):
+    """model: "tiny" (tiny widths, 2 layers) or "real2" (the real widths, 2 layers per tower:
+    modeling.real_width_config); the latter also records every parameter's gradient at
+    GRAD_SAMPLE seeded positions (model_fixtures.grad_sample_index) for per-parameter cosines."""
     from transformers import LlavaOnevisionForConditionalGeneration  # noqa: F401
-    MG._install_stub()
-    DT = MG._load("ref_dt", MG.DT_PATH)
-    LB = MG._load("ref_lb", MG.LB_PATH)
-    FB = MG._load("ref_fb", MG.FB_PATH)
-    BD = MG._load_bd()
-    tcfg, scfg = tiny_config(True), tiny_config(False)
+    DT, LB, FB, BD = _ref_classes()
+    tcfg, scfg = CONFIGS[model]
     student = hf_model(scfg, student_sd)
     teacher = hf_model(tcfg, teacher_sd) if kind != "bd" else None
-    batch = batch_cpu(sizes)
+    batch = batch_cpu(sizes, bs)
     Bb, Lb = batch["depth_input_ids"].shape
     rows = LOGIT_ROWS if sizes is None else (0, 23, 24, Lb // 2, Lb - 28, Lb - 27, Lb - 2, Lb - 1)
     rec = _Recorder()
@@ -208,7 +226,14 @@ def run(kind, phase, teacher_sd, student_sd, out_name, sizes=None):
     out["grad_heads"] = np.stack([grads[n].reshape(-1)[:16].float().numpy() for n in names]) if names else np.zeros((0, 16))
     tot = sum(float(grads[n].pow(2).sum()) for n in names)
     out["grad_total_norm"] = np.float64(math_sqrt(tot))
-    meta = dict(kind=kind, phase=phase, B=Bb, L=Lb, seed_t=SEED_T, seed_s=SEED_S, seed_data=SEED_DATA)
+    if model != "tiny":
+        # [n_params, GRAD_SAMPLE], NaN past a small parameter's last element
+        gs = np.full((len(names), GRAD_SAMPLE), np.nan, dtype=np.float32)
+        for i, n in enumerate(names):
+            v = grads[n].reshape(-1)[grad_sample_index(n, grads[n].numel())].float().numpy()
+            gs[i, :v.size] = v
+        out["grad_samples"] = gs
+    meta = dict(kind=kind, phase=phase, B=Bb, L=Lb, seed_t=SEED_T, seed_s=SEED_S, seed_data=SEED_DATA, model=model)
     if sizes is not None:
         meta["sizes"] = [list(hw) for hw in sizes]
     np.savez_compressed(HERE / f"model_{out_name}.npz", meta=json.dumps(meta), **out)
@@ -236,12 +261,29 @@ GEOMETRY = (
 )
 
 
+# the real widths at 2 layers per tower, bs 1, 336x336 (L = 1536): SigLIP hd 72, the teacher's
+# hd 128 with GQA 28/4 at width 3584, the student's 14/2 at 896, the real MLP widths
+REAL = (("lb", 0, "real_lb"), ("dt", 1, "real_dt1"), ("dt", 2, "real_dt2"), ("fb", 0, "real_fb"))
+
+
+def main_real(names):
+    ssd = tiny_state(False, SEED_S, CONFIGS["real2"][1])
+    tsd = tiny_state(True, SEED_T, CONFIGS["real2"][0])
+    STUDENT_KEYS.extend(ssd.keys())
+    for kind, phase, name in REAL:
+        if names and name not in names:
+            continue
+        run(kind, phase, tsd, ssd, name, model="real2", bs=1)
+
+
 def main():
     torch.set_num_threads(os.cpu_count())
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which == "real":
+        return main_real(sys.argv[2:])
     ssd = tiny_state(False, SEED_S)
     tsd = tiny_state(True, SEED_T)
     STUDENT_KEYS.extend(ssd.keys())
-    which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "bench"):
         for kind, phase, name in (("lb", 0, "lb"), ("dt", 1, "dt1"), ("dt", 2, "dt2"), ("dt", 3, "dt3"),
                                   ("fb", 0, "fb"), ("bd", 0, "bd")):

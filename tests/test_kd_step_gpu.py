@@ -1,12 +1,17 @@
-"""End-to-end KD training_step on the HIP path vs the reference (tiny models, real vocab).
+"""End-to-end KD training_step on the HIP path vs the reference (real vocab).
 
 Fixtures (tests/golden/model_*.npz): the reference's own forward()/training_step driving
-transformers with the same seeded weights — the 336x336 bench layout (2 tiles, 1,485 image
-tokens, L = 1,536, bs 2) for every module kind, and real SUNRGBD geometry (SURVEY KAT 9):
-480x640 (5 tiles, 2,929 image tokens, L = 2,980) at bs 1 for LoCa / DT phase 1, and a mixed,
-right-padded [336x336, 480x640] batch (-100 labels on the pads, NT-Xent over the 7 real
-tiles) for BD / FB / DT phase 1.  The HIP path stores bf16 with fp32 accumulation and fp32
-residual streams; the reference runs fp32, so:
+transformers with the same seeded weights —
+  * tiny widths (2 layers): the 336x336 bench layout (2 tiles, 1,485 image tokens, L = 1,536,
+    bs 2) for every module kind, and real SUNRGBD geometry (SURVEY KAT 9): 480x640 (5
+    tiles, 2,929 image tokens, L = 2,980) at bs 1 for LoCa / DT phase 1, and a mixed,
+    right-padded [336x336, 480x640] batch (-100 labels on the pads, NT-Xent over the 7 real
+    tiles) for BD / FB / DT phase 1;
+  * the REAL widths at 2 layers per tower (real_*: bs 1, 336x336): SigLIP 1152/4304 with 16
+    heads of hd 72, the 7B's Qwen2 3584/18944 with GQA 28/4 at hd 128, the 0.5B's 896/4864
+    with 14/2 at hd 64 — the shapes every kernel of the full-size step runs at.
+The HIP path stores bf16 with fp32 accumulation and fp32 residual streams; the reference
+runs fp32, so:
   every loss term   |d| <= 1e-4 + 1e-3 |ref| (north_star): total, KD term, student CE,
                     teacher CE — each against the reference's own value.  NT-Xent (and the
                     total it enters): |d| <= 1e-4 + 3e-3 |ref|: its logits are feature dot
@@ -22,69 +27,41 @@ residual streams; the reference runs fp32, so:
                     others (ViT training through NT-Xent of near-identical pooled tile
                     features, dt1 / fb / mix_*: ill-conditioned on random weights)
                     |d| <= 1e-3 |ref| + |d_bf16|, the bf16 floor's own miss
-  per-param grads   336x336 kinds: cosine(HIP, fp32 oracle) >= 0.99 and norm within 5 % for
-                    every parameter whose grad norm is >= 1e-3 x the largest; SUNRGBD kinds:
-                    norm within 5 % of the reference's recorded per-parameter norms
+  per-param grads   EVERY parameter (step_parity.param_report): norm within max(1e-3, 1.5x
+                    the bf16 floor's miss) of the reference's norm, cosine to the reference
+                    gradient >= the bf16 floor's cosine - 1e-3
 """
-import json
 import math
-from pathlib import Path
 
 import numpy as np
 import pytest
 import torch
 
-from model_fixtures import ALL_KINDS, GEOMETRY_KINDS, batch, frozen, load, oracle_grads
+from model_fixtures import ALL_KINDS, EVERY_KIND, batch, frozen, load
+from step_parity import FLOOR, logit_report, module, param_report, run_step
 
 ATOL, RTOL = 1e-4, 1e-3   # north_star
 NTX_RTOL = 3e-3           # the NT-Xent term (1 / tau = 14.3 amplification of the feature error)
-FLOOR = json.loads((Path(__file__).resolve().parent / "golden" / "bf16_floor.json").read_text())
-# kinds whose gradient total norm meets the north-star 1e-3 (profiles/r03/parity.json)
-GRAD_NORTH_STAR = {"lb", "dt2", "dt3", "bd", "fb", "sun_lb", "mix_fb"}
-
-
-def _grad(P, name):
-    """The HIP gradient of `name` in the reference's shape (the conv weight's pad columns dropped)."""
-    g = P.grad_view(name)
-    spec = next(s for s in P.specs if s.name == name)
-    if spec.ckpt_shape is not None:
-        g = g[:, :math.prod(spec.ckpt_shape[1:])]
-    return g
+# kinds whose gradient total norm meets the north-star 1e-3 (profiles/r04/parity.json)
+GRAD_NORTH_STAR = {"lb", "dt2", "dt3", "bd", "fb", "sun_lb", "mix_bd", "mix_fb", "mix_dt1", "real_lb", "real_dt1", "real_dt2",
+                   "real_fb"}
 
 
 def _near(got, ref, what, rtol=RTOL):
     assert abs(got - ref) <= ATOL + rtol * abs(ref), f"{what}: {got!r} vs reference {ref!r}"
 
+
 pytestmark = pytest.mark.gpu
 
 
 def _module(kind, phase):
-    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
-    if kind == "lb":
-        return K.LogitBasedKD("tiny-student", "tiny-teacher")
-    if kind == "dt":
-        m = K.OnlineKnowledgeDistillationLLavaOneVision("tiny-student", "tiny-teacher", phase=phase)
-        if phase == 1:
-            m.freeze_student_language_layers()
-        if phase == 2:
-            m.freeze_student_vision_layers()
-        return m
-    if kind == "fb":
-        return K.FeatureBasedKD("tiny-student", "tiny-teacher")
-    return K.LlavaOnevisionModule("tiny-student")
+    return module(kind, phase)
 
 
-@pytest.mark.parametrize("name", list(ALL_KINDS))
+@pytest.mark.parametrize("name", list(EVERY_KIND))
 def test_training_step_matches_reference(name, dev):
-    meta, exp = load(name)
-    kind, phase = ALL_KINDS[name]
-    m = _module(kind, phase)
-    m.keep_logits = True
-    b = batch(meta, dev)
-    loss = m.training_step(b, 0)
-    assert loss.requires_grad and loss.dim() == 0
-    loss.backward()
-    torch.cuda.synchronize()
+    m, meta, exp, loss = run_step(name, dev)
+    kind, phase = EVERY_KIND[name]
     assert int(m.student_model.err.item()) == 0
     # every loss term vs the reference's own forward
     kd, ce, tce, _ = m.last_terms.tolist()
@@ -98,47 +75,21 @@ def test_training_step_matches_reference(name, dev):
     if has_ntx:
         _near(float(m.last_ntxent[1]), float(exp["ntxent"]), "NT-Xent", NTX_RTOL)
     # student logits
-    s3, _ = m.last_logits
-    lse = torch.logsumexp(s3.double(), -1).reshape(-1).cpu().numpy()
-    ref_lse = exp["s_logit_lse"]
-    assert bool((np.abs(lse - ref_lse) <= ATOL + RTOL * np.abs(ref_lse)).all()), \
-        f"logit lse: max |d| {np.abs(lse - ref_lse).max():.3e}"
-    got_rows = s3[:, exp["logit_rows"].tolist(), ::int(exp["logit_col_stride"])].float().cpu().numpy()
-    ref_rows = exp["s_logit_rows"]
-    err = np.abs(got_rows - ref_rows)
-    frac = float((err <= ATOL + RTOL * np.abs(ref_rows)).mean())
-    fl = FLOOR[name]
-    assert frac >= fl["logit_frac_within_north_star"] - 0.01, (frac, fl)
-    assert float(err.max()) <= 1.5 * fl["logit_max_abs"], (float(err.max()), fl)
+    lr = logit_report(m, exp)
     m.last_logits = None
-    P = m.student_model.P
-    # the gradient's total norm (over the reference's parameters; the conv weight's padded tail excluded)
-    names = [str(n) for n in exp["grad_names"]]
-    gn = math.sqrt(sum(float(_grad(P, n).double().pow(2).sum()) for n in names))
-    ref_gn = float(exp["grad_total_norm"])
-    d_bf16 = abs(fl["grad_total_norm"] - ref_gn)
-    bound = RTOL * ref_gn + (0.0 if name in GRAD_NORTH_STAR else d_bf16)
-    assert abs(gn - ref_gn) <= bound, f"grad total norm {gn:.6g} vs reference {ref_gn:.6g} (bf16 floor off by {d_bf16:.4g})"
-    if name in GEOMETRY_KINDS:
-        gmax = float(np.max(exp["grad_norms"]))
-        for n, rn in zip(names, exp["grad_norms"]):
-            if rn < 1e-3 * gmax:
-                continue
-            got = float(_grad(P, n).double().norm())
-            assert abs(got / float(rn) - 1) <= 5e-2, f"{n}: norm {got:.4g} vs {float(rn):.4g}"
-    else:
-        _, ograds = oracle_grads(name)
-        gmax = max(float(g.norm()) for g in ograds.values())
-        for n in names:
-            ref = ograds[n].double().reshape(-1)
-            got = _grad(P, n).double().cpu().reshape(-1)
-            rn = float(ref.norm())
-            if rn < 1e-3 * gmax:
-                continue
-            cos = float((got @ ref) / (got.norm() * ref.norm() + 1e-30))
-            assert cos >= 0.99, f"{n}: cosine {cos:.4f}"
-            assert abs(float(got.norm()) / rn - 1) <= 5e-2, f"{n}: norm {float(got.norm()):.4g} vs {rn:.4g}"
+    fl = FLOOR[name]
+    assert lr["lse_ok"], f"logit lse: max |d| {lr['lse_max_abs']:.3e}"
+    assert lr["rows_frac_within_north_star"] >= fl["logit_frac_within_north_star"] - 0.01, (lr, fl)
+    assert lr["rows_max_abs"] <= 1.5 * fl["logit_max_abs"], (lr, fl)
+    # the gradient: total norm, then every parameter against the reference and the bf16 floor
+    per, tot = param_report(name, m, exp)
+    bound = RTOL + (0.0 if name in GRAD_NORTH_STAR else abs(tot["floor_rel"]))
+    assert abs(tot["rel"]) <= bound, f"grad total norm {tot}"
+    bad = {n: r for n, r in per.items() if not r["ok"]}
+    assert not bad, f"{len(bad)} of {len(per)} parameters outside the bound: " + "; ".join(
+        f"{n}: {r}" for n, r in list(bad.items())[:8])
     # frozen regions received no gradient
+    P = m.student_model.P
     tv, tp, tl = frozen(kind, phase)
     lo_l = P.regions["language"][0]
     if not tl:

@@ -5,7 +5,8 @@ reference's own forward (tests/golden/model_*.npz), as measured deltas.
 
 For each module kind: KD term, student CE, teacher CE, NT-Xent, total (|Δ|, rel Δ and
 whether |Δ| <= 1e-4 + 1e-3 |ref|, the north-star tolerance); student logits per-row
-logsumexp and sampled rows; the student gradient's total norm.  GPU only.
+logsumexp and sampled rows; the student gradient's total norm and every parameter's norm /
+cosine against the reference next to the bf16 floor (tests/step_parity.py).  GPU only.
 """
 from __future__ import annotations
 
@@ -31,16 +32,8 @@ def _d(got, ref):
 def measure(name, dev):
     import numpy as np
     import torch
-    from model_fixtures import ALL_KINDS, batch, load
-    from test_kd_step_gpu import _module
-    meta, exp = load(name)
-    kind, phase = ALL_KINDS[name]
-    m = _module(kind, phase)
-    m.keep_logits = True
-    b = batch(meta, dev)
-    loss = m.training_step(b, 0)
-    loss.backward()
-    torch.cuda.synchronize()
+    from step_parity import logit_report, param_report, run_step
+    m, meta, exp, loss = run_step(name, dev)
     kd, ce, tce, tot = m.last_terms.tolist()
     out = {"total": _d(loss.item(), float(exp["total"])), "student_ce": _d(ce, float(exp["student_ce"]))}
     if not math.isnan(float(exp["teacher_ce"])):
@@ -49,41 +42,29 @@ def measure(name, dev):
         out["kd_term"] = _d(kd, float(exp["kd_term"]))
     if not math.isnan(float(exp["ntxent"])):
         out["ntxent"] = _d(float(m.last_ntxent[1]), float(exp["ntxent"]))
-    s3, _ = m.last_logits
-    lse = torch.logsumexp(s3.double(), -1).reshape(-1).cpu().numpy()
-    dl = np.abs(lse - exp["s_logit_lse"])
-    out["s_logit_lse"] = dict(max_abs=float(dl.max()), max_rel=float((dl / np.abs(exp["s_logit_lse"])).max()),
-                              ok=bool((dl <= ATOL + RTOL * np.abs(exp["s_logit_lse"])).all()))
-    rows = exp["logit_rows"].tolist()
-    st = int(exp["logit_col_stride"])
-    got = s3[:, rows, ::st].float().cpu().numpy()
-    ref = exp["s_logit_rows"]
-    err = np.abs(got - ref)
-    out["s_logit_rows"] = dict(max_abs=float(err.max()), rms_ref=float(np.sqrt((ref ** 2).mean())),
-                               max_rel_to_rms=float(err.max() / np.sqrt((ref ** 2).mean())),
-                               frac_within_north_star=float((err <= ATOL + RTOL * np.abs(ref)).mean()))
-    P = m.student_model.P
-    names = [str(n) for n in exp["grad_names"]]
-    hip = {}
-    for n in names:
-        g = P.grad_view(n)
-        spec = next(s for s in P.specs if s.name == n)
-        if spec.ckpt_shape is not None:
-            g = g[:, :int(np.prod(spec.ckpt_shape[1:]))]
-        hip[n] = g.double().cpu().reshape(-1)
-    tot2 = sum(float(g.pow(2).sum()) for g in hip.values())
-    out["grad_total_norm"] = _d(math.sqrt(tot2), float(exp["grad_total_norm"]))
-    # the yardstick: the same oracle (pinned fp32 restatement) run in bf16 on the CPU
-    from model_fixtures import grad_total_norm, oracle_grads
-    _, bgr, blog = oracle_grads(name, torch.bfloat16, with_logits=True)
-    out["grad_total_norm"]["bf16_oracle"] = _d(grad_total_norm(bgr), float(exp["grad_total_norm"]))
-    berr = np.abs(blog[:, rows, ::st].float().numpy() - ref)
-    out["s_logit_rows"]["bf16_oracle_frac_within_north_star"] = float((berr <= ATOL + RTOL * np.abs(ref)).mean())
-    out["s_logit_rows"]["bf16_oracle_max_abs"] = float(berr.max())
-    # per parameter group: where the total-norm difference comes from
-    _, fgr = oracle_grads(name)
-    out["grad_groups"] = groups(hip, {k: v.double().reshape(-1) for k, v in fgr.items()},
-                                {k: v.double().reshape(-1) for k, v in bgr.items()})
+    from step_parity import FLOOR
+    fl = FLOOR[name]
+    lr = logit_report(m, exp)
+    lr.update(bf16_floor_frac_within_north_star=fl["logit_frac_within_north_star"],
+              bf16_floor_max_abs=fl["logit_max_abs"])
+    out["s_logits"] = lr
+    m.last_logits = None
+    per, totn = param_report(name, m, exp)
+    out["grad_total_norm"] = totn
+    out["grad_params"] = per
+    out["grad_params_ok"] = f"{sum(r['ok'] for r in per.values())}/{len(per)}"
+    # per parameter group: where the total-norm difference comes from (tiny fixtures: full vectors)
+    if "grad_samples" not in exp:
+        from model_fixtures import oracle_grads
+        from step_parity import hip_grad
+        P = m.student_model.P
+        hip = {str(n): hip_grad(P, str(n)).double().cpu().reshape(-1) for n in exp["grad_names"]}
+        _, bgr = oracle_grads(name, torch.bfloat16)
+        _, fgr = oracle_grads(name)
+        out["grad_groups"] = groups(hip, {k: v.double().reshape(-1) for k, v in fgr.items()},
+                                    {k: v.double().reshape(-1) for k, v in bgr.items()})
+    del m
+    torch.cuda.empty_cache()
     return out
 
 
@@ -120,10 +101,10 @@ def main():
     ap.add_argument("kinds", nargs="*")
     a = ap.parse_args()
     import torch
-    from model_fixtures import KINDS
+    from model_fixtures import EVERY_KIND
     dev = torch.device("cuda:0")
     rep = {"tolerance": f"|d| <= {ATOL} + {RTOL} |ref| (north_star)"}
-    for name in (a.kinds or KINDS):
+    for name in (a.kinds or EVERY_KIND):
         rep[name] = measure(name, dev)
         print(name, json.dumps(rep[name]), flush=True)
     if a.out:
