@@ -422,18 +422,26 @@ __device__ __forceinline__ int acc_col(int lane) { return (lane >> 4) * 4; }
 // and dominated the v8 tile time); the accumulators are only read (so v8's stay in the
 // AGPR file), one 16x16 tile at a time, into an LDS image that is then written out in
 // 16-B row chunks: pre = alpha*acc + bias -> [aux <- pre] -> C <- act(pre) (+ resid, + C).
-template <int ACT, int TM, int TN, int MT, int NT, bool F32>
+// L32: the accumulators of v11's 32x32x16 MFMAs (C^T blocks, MFMA operands swapped) viewed as
+// f32x4 [MT = 4 row blocks of 32][NT = 16]: j = 4 bj + g holds C[32 i + (l & 31)][32 bj + 8 g +
+// 4 (l >> 5) + 0..3] -- again four consecutive columns of one row per lane and group.
+template <bool L32>
+__device__ __forceinline__ int acc_col_of(int j, int lane) {
+    return L32 ? (j >> 2) * 32 + 8 * (j & 3) + 4 * (lane >> 5) : j * 16 + acc_col(lane);
+}
+
+template <int ACT, int TM, int TN, int MT, int NT, bool F32, bool L32 = false>
 __device__ __forceinline__ void epi_to_lds(const f32x4 (&acc)[MT][NT], char* smem, int rs, float alpha,
                                            const f32x4 (&bcol)[NT], int wm, int wn, int lane, int r_lo, int r_hi) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-        const int lr0 = wm * TM + i * 16;
+        const int lr0 = wm * TM + i * (L32 ? 32 : 16);
         if (lr0 < r_lo || lr0 >= r_hi) continue;
-        const int lr = lr0 - r_lo + acc_row(lane);
+        const int lr = lr0 - r_lo + (L32 ? (lane & 31) : acc_row(lane));
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const f32x4 a = acc[i][j];
-            const int lc = wn * TN + j * 16 + acc_col(lane);
+            const int lc = wn * TN + acc_col_of<L32>(j, lane);
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = apply_act(a[r] * alpha + bcol[j][r], ACT);
@@ -443,14 +451,14 @@ __device__ __forceinline__ void epi_to_lds(const f32x4 (&acc)[MT][NT], char* sme
     }
 }
 
-template <int TM, int TN, int MT, int NT, bool F32>
+template <int TM, int TN, int MT, int NT, bool F32, bool L32 = false>
 __device__ __forceinline__ void epi_to_lds_act(int act, const f32x4 (&acc)[MT][NT], char* smem, int rs, float alpha,
                                                const f32x4 (&bcol)[NT], int wm, int wn, int lane, int r_lo, int r_hi) {
     switch (act) {
-        case KD_ACT_GELU_TANH: epi_to_lds<KD_ACT_GELU_TANH, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
-        case KD_ACT_GELU_ERF: epi_to_lds<KD_ACT_GELU_ERF, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
-        case KD_ACT_SILU: epi_to_lds<KD_ACT_SILU, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
-        default: epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, F32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+        case KD_ACT_GELU_TANH: epi_to_lds<KD_ACT_GELU_TANH, TM, TN, MT, NT, F32, L32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+        case KD_ACT_GELU_ERF: epi_to_lds<KD_ACT_GELU_ERF, TM, TN, MT, NT, F32, L32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+        case KD_ACT_SILU: epi_to_lds<KD_ACT_SILU, TM, TN, MT, NT, F32, L32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
+        default: epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, F32, L32>(acc, smem, rs, alpha, bcol, wm, wn, lane, r_lo, r_hi); break;
     }
 }
 
@@ -789,7 +797,7 @@ __device__ __forceinline__ void epi_row_stats(const GemmP& p, const char* smem, 
 // HAS_ACT: the activation epilogue is instantiated for the forward (K-major x K-major) kernels
 // only; the launcher rejects an activation with MN-major operands or an fp32 output.
 template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2, bool HAS_ACT = true,
-          bool RST = false>
+          bool RST = false, bool L32 = false>
 __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int n0, int wm,
                                           int wn, int lane, int tid) {
     const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
@@ -801,39 +809,39 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
     if (p.bias) {
         int cols[NT];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) cols[j] = min(n0 + wn * TN + j * 16 + acc_col(lane), p.N - 4);
+        for (int j = 0; j < NT; ++j) cols[j] = min(n0 + wn * TN + acc_col_of<L32>(j, lane), p.N - 4);
         load_bias4<NT>(p, cols, bcol);
     }
     constexpr int RS16 = BN * 2 + 16, RS32 = BN * 4 + 16;
     if (HAS_ACT && p.sq) {   // q|k|v scatter (+RoPE) straight from the bf16 tile
-        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
         epi_flush_qkv<BM, BN, NTHR>(p, smem, RS16, m0, n0, tid);
         return;
     }
     if (p.act == KD_ACT_DGELU_TANH || p.act == KD_ACT_DSWIGLU) {   // aux is READ (the forward pre-activation)
-        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
         epi_flush_dact<BM, BN, NTHR>(p, smem, RS16, m0, n0, tid, full);
         return;
     }
     if (p.aux) {   // pre-activation (bf16) for the backward
-        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
         epi_flush<BM, BN, NTHR, false, false, false>(p, smem, RS16, p.aux, p.ld_aux, m0, n0, tid, full);
         __syncthreads();
     }
     const bool res = p.resid != nullptr, accum = p.accumulate != 0;
     if (!p.c_f32) {
-        if (HAS_ACT) epi_to_lds_act<TM, TN, MT, NT, false>(p.act, acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
-        else epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        if (HAS_ACT) epi_to_lds_act<TM, TN, MT, NT, false, L32>(p.act, acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
+        else epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
         epi_flush_sel<BM, BN, NTHR, false>(p, smem, RS16, p.C, p.ldc, m0, n0, tid, full, res, accum);
         if constexpr (RST) epi_row_stats(p, smem, RS16, m0, n0, tid);
     } else {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {   // fp32: two half tiles of BM/2 rows
-            epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, true>(acc, smem, RS32, alpha, bcol, wm, wn, lane, h * BM / 2, (h + 1) * BM / 2);
+            epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, true, L32>(acc, smem, RS32, alpha, bcol, wm, wn, lane, h * BM / 2, (h + 1) * BM / 2);
             __syncthreads();
             epi_flush_sel<BM / 2, BN, NTHR, true>(p, smem, RS32, p.C, p.ldc, m0 + h * BM / 2, n0, tid, full, res, accum);
             __syncthreads();
@@ -847,7 +855,7 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
 // second pass over HBM: pre-activations are staged once as bf16 in LDS (the rounding the
 // unfused GEMM output had), optionally written to aux ([M, 2I] gate | up, for the
 // backward), then combined in fp32 exactly as k_swiglu_fwd does.
-template <int TM, int TN, int MT, int NT, int NTHR>
+template <int TM, int TN, int MT, int NT, int NTHR, bool L32 = false>
 __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int nb, int wm,
                                              int wn, int lane, int tid) {
     float alpha = p.alpha;
@@ -856,7 +864,7 @@ __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[
 #pragma unroll
     for (int j = 0; j < NT; ++j) bcol[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     constexpr int RS = 256 * 2 + 16;
-    epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false>(acc, smem, RS, alpha, bcol, wm, wn, lane, 0, 256);
+    epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS, alpha, bcol, wm, wn, lane, 0, 256);
     __syncthreads();
     const int I = p.glu;
     const bool full = m0 + 256 <= p.M;
@@ -1073,6 +1081,10 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     // lm_head GEMMs of the KD step): a build of its own, so the plain forward kernel carries none
     // of that code and the lm_head launches are their own line in a kernel trace
     constexpr bool RSTATS = (EXP & 32) && !A_MN && !B_MN;
+    // bit 7 (diagnostic, forced variant 25, WRONG results): each K-major DMA instruction reads
+    // 8 rows x 128 B (whole cache lines) instead of 16 rows x 64 B -- the same instructions and
+    // bytes, half the cache lines per instruction: isolates the cost of half-line row segments
+    constexpr bool WIDE = (EXP & 128) && !A_MN && !B_MN;
 
     uint32_t* stamps = nullptr;
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
@@ -1102,12 +1114,26 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
             const int wrow = row < 128 ? nb + row : p.glu + nb + row - 128;
             vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
         }
+        if (WIDE) {
+            const int row = 8 * (wid * 4 + u) + (lane >> 3);
+            va[u] = (uint32_t)((int64_t)row * p.lda * 2 + (lane & 7) * 16);
+            const int wrow = glu ? (row < 128 ? nb + row : p.glu + nb + row - 128) : row;
+            vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + (lane & 7) * 16);
+        }
     }
     // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl;
     // FULL: the stage lies wholly inside K (no per-lane tail masking)
     auto dma = [&](int st, int sl, int u, auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
         if (NODMA) return;
+        if (WIDE) {
+            const bool isA = u < 4;
+            char* dst = smem + sl * SS + (isA ? 0 : SA) + (wid * 4 + (u & 3)) * 1024;
+            const int soff = st * BK2 * 2 < K * 2 ? st * BK2 * 2 : 0;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, isA ? va[u & 3] : vb[u & 3],
+                                                     soff, 0, 0);
+            return;
+        }
         const bool isA = u < 4;
         const bool mn = isA ? A_MN : B_MN;
         const int i = wid * 4 + (u & 3);
@@ -1278,6 +1304,378 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
             o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
         }
     }
+}
+
+// =============================================================================
+// v11: v8's tile, ring, DMA and barriers (256x256, four waves of 128x128, the 4-slot BK = 32
+// LDS-DMA ring, three stages in flight) on 32x32x16 MFMAs, K-major x K-major operands (every
+// forward GEMM of the step).  Why: with one wave per SIMD a 16x16x32 MFMA holds the SIMD's
+// vector issue for 8 of its 16 cycles, so a k-step's 64 MFMAs leave 512 issue cycles for its
+// 8 LDS-DMA pieces (~60 cycles each among MFMAs) and 16 fragment reads, and v8's step measures
+// ~1,240 cycles against 1,024 of MFMA; a 32x32x16 MFMA holds issue for 8 of its 32 cycles, so
+// the same step (32 MFMAs of 32 cycles) has 768 free issue cycles.  Per step and wave: 8 units
+// of 4 MFMAs (unit q: k-half h = q >> 2, row block bi = q & 3, column blocks 0..3), each unit
+// carrying one DMA piece of stage t+4 and two fragment reads of stage t+1 (A block q >> 1,
+// k-half q & 1, and the same for B).  Fragments: lane l reads row (l & 31), 16-B chunk
+// 2h + (l >> 5) of the [rows][32 k] image (v8's swizzle f4 is conflict-free for this read:
+// every 16-lane ds_read_b128 group covers the 16 (row & 3, chunk) slots once).  Accumulators:
+// f32x16 [4][4] in AGPRs (C^T blocks), viewed as f32x4 [4][16] by the L32 epilogue.
+// =============================================================================
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ void mfma32_agpr(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// the tile's last MFMA with its result-latency drain in the same asm statement (mfma_agpr_last;
+// 64 wait states >= the 32x32x16's 16-pass latency with margin)
+__device__ __forceinline__ void mfma32_agpr_last(f32x16& acc, const bf16x8& a, const bf16x8& b, int last) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0\n\t"
+                 "s_cmp_eq_u32 %3, 0\n\t"
+                 "s_cbranch_scc1 .Lkd_mfma32_nodrain%=\n\t"
+                 "s_nop 15\n\t"
+                 "s_nop 15\n\t"
+                 "s_nop 15\n\t"
+                 "s_nop 15\n"
+                 ".Lkd_mfma32_nodrain%=:"
+                 : "+a"(acc) : "v"(a), "v"(b), "s"(__builtin_amdgcn_readfirstlane(last)) : "scc");
+}
+
+// 32x32x16 operand fragment (K-major [rows][32 k] stage image): rows rb..rb+31, k-half h
+__device__ __forceinline__ bf16x8 frag32(const char* tile, int rb, int h, int lane) {
+    const int r = rb + (lane & 31);
+    const int c = 2 * h + (lane >> 5);
+    return *(const bf16x8*)(tile + r * 64 + ((c ^ f4(r)) << 4));
+}
+
+// EXP bits as v8: 4 = the fused SwiGLU build, 32 = the lm_head row-statistics build
+template <int EXP>
+__device__ __forceinline__ void g11_tile(GemmP p, int tm, int tn, char* smem) {
+    constexpr bool RSTATS = EXP & 32;
+    constexpr bool glu = EXP & 4;
+    constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int K = p.K;
+    const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
+    const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
+    const int nb = tn * 128;
+    const __amdgpu_buffer_rsrc_t rsBk = glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
+                                            : make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
+    uint32_t va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        va[u] = voff8<false>(wid * 4 + u, lane, p.lda, m0, p.M);
+        vb[u] = voff8<false>(wid * 4 + u, lane, p.ldb, n0, p.N);
+        if (glu) {   // tile row r -> weight row (r < 128 ? nb + r : I + nb + r - 128); same LDS swizzle
+            const int row = 16 * (wid * 4 + u) + (lane >> 2);
+            const int gc = (lane & 3) ^ f4(row);
+            const int wrow = row < 128 ? nb + row : p.glu + nb + row - 128;
+            vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
+        }
+    }
+    // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl
+    auto dma = [&](int st, int sl, int u, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        const bool isA = u < 4;
+        const int i = wid * 4 + (u & 3);
+        char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
+        uint32_t v = isA ? va[u & 3] : vb[u & 3];
+        int soff = st * BK2 * 2;
+        if (!FULL) {
+            const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
+            if (kleft < BK2) {                // zero the chunks at k >= K
+                const int row = 16 * i + (lane >> 2);
+                const int gc = (lane & 3) ^ f4(row);
+                if (gc * 8 >= kleft) v = OOB;
+                if (kleft <= 0) soff = 0;
+            }
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, v, soff, 0, 0);
+    };
+    using FullT = std::integral_constant<bool, true>;
+    using PartT = std::integral_constant<bool, false>;
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){};
+    const int ra = wm * 128, cb = wn * 128;
+#pragma unroll
+    for (int st = 0; st < NS8; ++st)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dma(st, st, u, PartT{});
+    wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
+    __builtin_amdgcn_s_barrier();
+    // fragment sets: index 2 * block + k-half
+    bf16x8 xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        xa[q] = frag32(smem, ra + (q >> 1) * 32, q & 1, lane);
+        xb[q] = frag32(smem + SA, cb + (q >> 1) * 32, q & 1, lane);
+    }
+#define KD_G11_SYNC()                                      \
+    {                                                      \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        wait_vm<16>();                                     \
+        __builtin_amdgcn_s_barrier();                      \
+    }
+    KD_G11_SYNC()
+    __builtin_amdgcn_sched_barrier(0);
+#define KD_SB __builtin_amdgcn_sched_barrier(0);
+#define KD_G11_STEP(SL, CA, CB, NA, NB, FT)                                                                  \
+    {                                                                                                         \
+        const int t_ = t + (SL);                                                                              \
+        const char* na_ = smem + (((SL) + 1) % NS8) * SS;                                                     \
+        _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                       \
+            const int h_ = q >> 2, bi_ = q & 3;                                                               \
+            mfma32_agpr(acc[bi_][0], CB[0 + h_], CA[2 * bi_ + h_]); KD_SB                                     \
+            dma(t_ + NS8, (SL), q, FT{});                                                                     \
+            KD_SB                                                                                             \
+            mfma32_agpr(acc[bi_][1], CB[2 + h_], CA[2 * bi_ + h_]); KD_SB                                     \
+            NA[q] = frag32(na_, ra + (q >> 1) * 32, q & 1, lane);                                             \
+            KD_SB                                                                                             \
+            mfma32_agpr(acc[bi_][2], CB[4 + h_], CA[2 * bi_ + h_]); KD_SB                                     \
+            NB[q] = frag32(na_ + SA, cb + (q >> 1) * 32, q & 1, lane);                                        \
+            if (q == 7) KD_G11_SYNC()                                                                         \
+            KD_SB                                                                                             \
+            if (q == 7) mfma32_agpr_last(acc[bi_][3], CB[6 + h_], CA[2 * bi_ + h_], t_ + 1 == nk);            \
+            else mfma32_agpr(acc[bi_][3], CB[6 + h_], CA[2 * bi_ + h_]);                                      \
+            KD_SB                                                                                             \
+        }                                                                                                     \
+    }
+    int t = 0;
+    for (; t + 2 * NS8 <= nk_full; t += NS8) {   // every DMA of these steps lies inside K
+        KD_G11_STEP(0, xa, xb, ya, yb, FullT)
+        KD_G11_STEP(1, ya, yb, xa, xb, FullT)
+        KD_G11_STEP(2, xa, xb, ya, yb, FullT)
+        KD_G11_STEP(3, ya, yb, xa, xb, FullT)
+    }
+    for (; t + NS8 <= nk; t += NS8) {
+        KD_G11_STEP(0, xa, xb, ya, yb, PartT)
+        KD_G11_STEP(1, ya, yb, xa, xb, PartT)
+        KD_G11_STEP(2, xa, xb, ya, yb, PartT)
+        KD_G11_STEP(3, ya, yb, xa, xb, PartT)
+    }
+    const int rem = nk - t;
+    if (rem > 0) KD_G11_STEP(0, xa, xb, ya, yb, PartT)
+    if (rem > 1) KD_G11_STEP(1, ya, yb, xa, xb, PartT)
+    if (rem > 2) KD_G11_STEP(2, xa, xb, ya, yb, PartT)
+#undef KD_G11_STEP
+#undef KD_G11_SYNC
+#undef KD_SB
+    // drain the ring (out-of-range DMAs still write LDS) and the MFMA pipe before the
+    // accumulators are read back (asm MFMAs are invisible to the hazard recognizer)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    const f32x4 (&acc4)[4][16] = *reinterpret_cast<const f32x4(*)[4][16]>(&acc);
+    if (glu) epilogue_glu<128, 128, 4, 16, NTH8, true>(p, acc4, smem, m0, nb, wm, wn, lane, tid);
+    else epilogue2<256, 256, 2, 2, 128, 128, 4, 16, NTH8, true, RSTATS, true>(p, acc4, smem, m0, n0, wm, wn, lane, tid);
+}
+
+template <int EXP = 0>
+__global__ void __launch_bounds__(NTH8, 1) k_gemm11(GemmP p_) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tiles_m = (p_.M + 255) / 256, tiles_n = (p_.N + 255) / 256;
+    GemmP p = p_;
+    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += k0;
+        p.B += k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    int tm, tn;
+    tile_of(p.gx, tiles_m, tiles_n, tm, tn, p.tile0, p.gm);
+    g11_tile<EXP>(p, tm, tn, smem);
+}
+
+// =============================================================================
+// v12: v8 (256x256 tile, four waves of 128x128 on 16x16x32 MFMAs, AGPR accumulators, the same
+// 128 KiB of ring) with WHOLE-CACHE-LINE staging of K-major operands.  v8's K-major DMA
+// instruction covers 16 rows x 64 B (one BK = 32 stage), half of a 128-B line per row; the
+// diagnostic build that reads 8 rows x 128 B per instruction instead (same instructions and
+// bytes, forced variant 25) ran 8-10 % faster on the big forward shapes (profiles/r04, the
+// hipBLASLt kernel stages BK = 64 for the same reason).  Here the ring holds two PAIRS of
+// stages (stages 2q, 2q+1 = 64 k): a pair image is [256 rows][128 B] per operand (k 0..63 of
+// each row, 16-B chunk c at physical chunk c ^ swp(row), swp(r) = (r >> 1) & 7: every
+// 16-lane group of a ds_read_b128 fragment read covers the 16 (row & 1, chunk) bank slots once),
+// filled by instructions of 8 rows x 128 B (lane l: row 8i + (l >> 3), logical chunk
+// (l & 7) ^ swp(row) -> lane-linear LDS position).  Compute stays per BK = 32 stage (64 MFMAs
+// per step, fragments of stage t+1 read during step t).  Pair q (in pair slot q % 2) can only be
+// refilled once stage 2q-3 is in registers, so pair q is issued in the odd step 2q-3, 16 DMA
+// instructions per wave (two per unit), and must land by the end of step 2q-2: step ends wait
+// vmcnt(0) after even steps and vmcnt(16) after odd ones.
+// =============================================================================
+__device__ __forceinline__ int swp(int r) { return (r >> 1) & 7; }
+
+// 16x16x32 operand fragment of stage half h (k 32h..32h+31) from a pair image [rows][128 B]
+__device__ __forceinline__ bf16x8 frag_pair(const char* img, int rb, int h, int lane) {
+    const int r = rb + (lane & 15);
+    const int c = 4 * h + (lane >> 4);
+    return *(const bf16x8*)(img + r * 128 + ((c ^ swp(r)) << 4));
+}
+
+template <int EXP>
+__device__ __forceinline__ void g12_tile(GemmP p, int tm, int tn, char* smem) {
+    constexpr bool RSTATS = EXP & 32;
+    constexpr bool glu = EXP & 4;
+    constexpr int PA = 256 * 128;       // one operand's pair image (32 KiB)
+    constexpr int PS = 2 * PA;          // a pair slot (64 KiB); two of them
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int K = p.K;
+    const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
+    const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
+    const int nb = tn * 128;
+    const __amdgpu_buffer_rsrc_t rsB = glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
+                                           : make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
+    // wave w fills rows 64w .. 64w + 63 of each operand: instruction j (0..7) rows 64w + 8j + (l >> 3);
+    // the lane's swizzled chunk depends on j only through j & 1, the row step goes to soffset
+    const int rlo = 64 * wid + (lane >> 3);
+    const int brow = glu ? (wid < 2 ? nb : p.glu + nb - 128) : 0;   // weight row of tile row 0 of this wave's half
+    uint32_t va[2], vb[2];
+    int gcl[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int gc = (lane & 7) ^ swp(rlo + 8 * e);
+        gcl[e] = gc;
+        va[e] = (uint32_t)((int64_t)rlo * p.lda * 2 + gc * 16);
+        vb[e] = (uint32_t)((int64_t)(brow + rlo) * p.ldb * 2 + gc * 16);
+    }
+    // instruction j of operand (isA) of pair q into pair slot ps
+    auto dma = [&](int q, int ps, int j, bool isA, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        char* dst = smem + ps * PS + (isA ? 0 : PA) + (wid * 8 + j) * 1024;
+        uint32_t v = isA ? va[j & 1] : vb[j & 1];
+        const int64_t ld = isA ? p.lda : p.ldb;
+        int kq = q * 64;
+        if (!FULL) {
+            const int kleft = K - kq;     // valid k of this pair (<= 0: past the end)
+            if (gcl[j & 1] * 8 >= kleft) v = OOB;
+            if (kleft <= 0) kq = 0;
+        }
+        const int soff = __builtin_amdgcn_readfirstlane((int)(8 * j * ld * 2 + kq * 2));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsB, (lds_void_t*)dst, 16, v, soff, 0, 0);
+    };
+    using FullT = std::integral_constant<bool, true>;
+    using PartT = std::integral_constant<bool, false>;
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int ra = wm * 128, cb = wn * 128;
+    // prologue: pairs 0 and 1 (stages 0..3) into pair slots 0 and 1; pair 0 landed
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dma(q, q, j, true, PartT{});
+            dma(q, q, j, false, PartT{});
+        }
+    wait_vm<16>();
+    __builtin_amdgcn_s_barrier();
+    bf16x8 xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        xa[u] = frag_pair(smem, ra + u * 16, 0, lane);
+        xb[u] = frag_pair(smem + PA, cb + u * 16, 0, lane);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#define KD_G12_SYNC(ODD)                                   \
+    {                                                      \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        if (ODD) wait_vm<16>();                            \
+        else wait_vm<0>();                                 \
+        __builtin_amdgcn_s_barrier();                      \
+    }
+#define KD_SB __builtin_amdgcn_sched_barrier(0);
+    // step t + SL (SL = 0..3 of a group of four; t % 4 == 0): stage t+SL is in registers (CA, CB);
+    // stage t+SL+1 is read from pair slot ((SL+1) >> 1) & 1, half (SL+1) & 1; odd SL issue pair
+    // (t+SL+3)/2 into pair slot ((SL+3) >> 1) & 1
+#define KD_G12_STEP(SL, CA, CB, NA, NB, FT)                                                                  \
+    {                                                                                                         \
+        const int t_ = t + (SL);                                                                              \
+        const char* na_ = smem + ((((SL) + 1) >> 1) & 1) * PS;                                                \
+        constexpr int nh_ = ((SL) + 1) & 1;                                                                   \
+        constexpr bool odd_ = (SL) & 1;                                                                       \
+        const int q_ = (t_ + 3) >> 1;                                                                         \
+        constexpr int qs_ = (((SL) + 3) >> 1) & 1;                                                            \
+        _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
+            mfma_agpr(acc[u][0], CB[0], CA[u]); KD_SB                                                         \
+            if (odd_) dma(q_, qs_, u, true, FT{});                                                            \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][1], CB[1], CA[u]); KD_SB                                                         \
+            if (u < 4) NA[2 * u] = frag_pair(na_, ra + 2 * u * 16, nh_, lane);                                \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][2], CB[2], CA[u]); mfma_agpr(acc[u][3], CB[3], CA[u]); KD_SB                     \
+            if (u < 4) NB[2 * u] = frag_pair(na_ + PA, cb + 2 * u * 16, nh_, lane);                           \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][4], CB[4], CA[u]); KD_SB                                                         \
+            if (odd_) dma(q_, qs_, u, false, FT{});                                                           \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][5], CB[5], CA[u]); KD_SB                                                         \
+            if (u < 4) NA[2 * u + 1] = frag_pair(na_, ra + (2 * u + 1) * 16, nh_, lane);                      \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][6], CB[6], CA[u]); KD_SB                                                         \
+            if (u < 4) NB[2 * u + 1] = frag_pair(na_ + PA, cb + (2 * u + 1) * 16, nh_, lane);                 \
+            if (u == 7) KD_G12_SYNC(odd_)                                                                     \
+            KD_SB                                                                                             \
+            if (u == 7) mfma_agpr_last(acc[u][7], CB[7], CA[u], t_ + 1 == nk);                                \
+            else mfma_agpr(acc[u][7], CB[7], CA[u]);                                                          \
+            KD_SB                                                                                             \
+        }                                                                                                     \
+    }
+    int t = 0;
+    for (; t + 8 <= nk_full; t += 4) {   // every pair these steps issue (up to stage t + 7) lies inside K
+        KD_G12_STEP(0, xa, xb, ya, yb, FullT)
+        KD_G12_STEP(1, ya, yb, xa, xb, FullT)
+        KD_G12_STEP(2, xa, xb, ya, yb, FullT)
+        KD_G12_STEP(3, ya, yb, xa, xb, FullT)
+    }
+    for (; t + 4 <= nk; t += 4) {
+        KD_G12_STEP(0, xa, xb, ya, yb, PartT)
+        KD_G12_STEP(1, ya, yb, xa, xb, PartT)
+        KD_G12_STEP(2, xa, xb, ya, yb, PartT)
+        KD_G12_STEP(3, ya, yb, xa, xb, PartT)
+    }
+    const int rem = nk - t;
+    if (rem > 0) KD_G12_STEP(0, xa, xb, ya, yb, PartT)
+    if (rem > 1) KD_G12_STEP(1, ya, yb, xa, xb, PartT)
+    if (rem > 2) KD_G12_STEP(2, xa, xb, ya, yb, PartT)
+#undef KD_G12_STEP
+#undef KD_G12_SYNC
+#undef KD_SB
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (glu) epilogue_glu<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
+    else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, true, RSTATS>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+template <int EXP = 0>
+__global__ void __launch_bounds__(NTH8, 1) k_gemm12(GemmP p_) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tiles_m = (p_.M + 255) / 256, tiles_n = (p_.N + 255) / 256;
+    GemmP p = p_;
+    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += k0;
+        p.B += k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    int tm, tn;
+    tile_of(p.gx, tiles_m, tiles_n, tm, tn, p.tile0, p.gm);
+    g12_tile<EXP>(p, tm, tn, smem);
 }
 
 template <bool A_MN, bool B_MN, int EXP = 0>
@@ -1998,6 +2396,24 @@ int launch_quant_rows_f8(const void* x, int64_t ldx, int R, int K, void* q, int6
 }
 
 
+// v11 (32x32x16 MFMAs) in place of v8 for K-major x K-major tiles: forced variant 23 (24 forces
+// v8 for A/B), else the library default (KD_GEMM_V11=0 turns it off)
+static bool use_v11(int variant) {
+    if (variant == 23) return true;
+    if (variant != 0 && variant != 16) return false;
+    static const int env = [] { const char* e = std::getenv("KD_GEMM_V11"); return e ? std::atoi(e) : -1; }();
+    return env == 1;
+}
+
+// v12 (whole-line staging of K-major operands) in place of v8 for K-major x K-major tiles:
+// forced variant 26, else the library default (KD_GEMM_V12=0 turns it off); 24 forces v8
+static bool use_v12(int variant) {
+    if (variant == 26) return true;
+    if (variant != 0 && variant != 16) return false;
+    static const int env = [] { const char* e = std::getenv("KD_GEMM_V12"); return e ? std::atoi(e) : 0; }();
+    return env == 1;
+}
+
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d != nullptr, "gemm: null descriptor");
     KD_CHECK_ARG(d->A && d->B && (d->C || d->qkv), "gemm: null operand");
@@ -2021,7 +2437,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldc >= w && d->ld_aux >= w && d->ldc % 8 == 0 && d->ld_aux % 8 == 0 &&
                        (uintptr_t)d->aux % 16 == 0, "gemm backward activation: ldc / ld_aux >= N (2N for dswiglu), 16-B rows");
     }
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 22), "gemm: unknown variant");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 26), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     KD_CHECK_SHAPE(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
@@ -2124,8 +2540,12 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
         pk.gx = (int)grid.x; pk.gy = 1;
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
+        else if (use_v11(d->variant)) hipLaunchKernelGGL((k_gemm11<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (use_v12(d->variant)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 22)
             hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (d->variant == 25)
+            hipLaunchKernelGGL((k_gemm8<false, false, 132>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
         return KD_OK;
@@ -2182,11 +2602,20 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, q);         \
         else L8(0)                                                                                              \
     }
+                if (!amn && !bmn && use_v11(force)) {   // v11: the same tiles on 32x32x16 MFMAs
+                    hipLaunchKernelGGL((k_gemm11<0>), grid, dim3(NTH8), lds, st, q);
+                    return;
+                }
+                if (!amn && !bmn && use_v12(force)) {   // v12: the same tiles, whole-line K-major staging
+                    hipLaunchKernelGGL((k_gemm12<0>), grid, dim3(NTH8), lds, st, q);
+                    return;
+                }
                 switch (force) {   // the diagnostic builds exist for the forward (K-major x K-major) layout only
                     case 17: L8K(1) break;
                     case 18: L8K(2) break;
                     case 19: L8K(64) break;
                     case 22: L8K(8) break;
+                    case 25: L8K(128) break;
                     default: L8(0) break;
                 }
 #undef L8K
