@@ -378,6 +378,12 @@ __device__ __forceinline__ float half_max(float v) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// s_waitcnt lgkmcnt(N) that names the 8 asm-read registers it retires ("+v": the compiler can
+// neither read them before the wait nor place a copy of them above it)
+template <int N> __device__ __forceinline__ void wait_lgkm_def8(u32x2 (&r)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(%8)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7]) : "i"(N) : "memory");
+}
 __device__ __forceinline__ float half_sum(float v) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -522,7 +528,9 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
                 asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ka[kk]) : "v"(koff[kk]), "i"(BUF * 2 * TILE));
 #pragma unroll
             for (int kk = 0; kk < KS; ++kk) {
-                asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(KS - 1) : "memory");
+                // the counted wait names the register it retires (ka[kk], the oldest read in
+                // flight), so no compiler copy of it can be placed before the wait
+                asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ka[kk]) : "i"(KS - 1) : "memory");
                 __builtin_amdgcn_sched_barrier(0);
                 sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ka[kk]), qf[kk], sc[0], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
@@ -530,7 +538,7 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
             }
 #pragma unroll
             for (int kk = 0; kk < KS; ++kk) {
-                asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(KS - 1 - kk) : "memory");
+                asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(kb[kk]) : "i"(KS - 1 - kk) : "memory");
                 __builtin_amdgcn_sched_barrier(0);
                 sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kb[kk]), qf[kk], sc[1], 0, 0, 0);
             }
@@ -592,23 +600,24 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
         const bf16x8 vf = cat4(__builtin_bit_cast(bf16x4, vr[SET][2 * s]), __builtin_bit_cast(bf16x4, vr[SET][2 * s + 1])); \
         o[D] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], o[D], 0, 0, 0);                                 \
     }
-#define KD_F32_WAIT(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory"); __builtin_amdgcn_sched_barrier(0);
+// the counted wait retires the 8 reads of vr[SET] (the older set in flight) and names them
+#define KD_F32_WAIT(N, SET) wait_lgkm_def8<N>(vr[SET]); __builtin_amdgcn_sched_barrier(0);
             KD_F32_RD(0, 0)
             KD_F32_RD(1, 1)
-            KD_F32_WAIT(8)
+            KD_F32_WAIT(8, 0)
             KD_F32_MM(0, 0)
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (ND > 2) { KD_F32_RD(2, 0) KD_F32_WAIT(8) }
-            else { KD_F32_WAIT(0) }
+            if constexpr (ND > 2) { KD_F32_RD(2, 0) KD_F32_WAIT(8, 1) }
+            else { KD_F32_WAIT(0, 1) }
             KD_F32_MM(1, 1)
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (ND > 2) {
-                if constexpr (ND > 3) { KD_F32_RD(3, 1) KD_F32_WAIT(8) }
-                else { KD_F32_WAIT(0) }
+                if constexpr (ND > 3) { KD_F32_RD(3, 1) KD_F32_WAIT(8, 0) }
+                else { KD_F32_WAIT(0, 0) }
                 KD_F32_MM(2, 0)
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (ND > 3) {
-                    KD_F32_WAIT(0)
+                    KD_F32_WAIT(0, 1)
                     KD_F32_MM(3, 1)
                 }
             }

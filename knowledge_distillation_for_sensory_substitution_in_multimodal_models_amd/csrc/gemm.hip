@@ -2405,13 +2405,18 @@ static bool use_v11(int variant) {
     return env == 1;
 }
 
-// v12 (whole-line staging of K-major operands) in place of v8 for K-major x K-major tiles:
-// forced variant 26, else the library default (KD_GEMM_V12=0 turns it off); 24 forces v8
-static bool use_v12(int variant) {
+// v12 (whole-line staging of K-major operands, bit-identical to v8) in place of v8 for K-major x
+// K-major tiles: forced variant 26; 24 forces v8; otherwise where it measured faster
+// (profiles/r04/ab_v12_vs_v8.txt, interleaved on one box): N <= 10240 and K <= 4096 -- student
+// gate|up+SwiGLU 116.3 -> 108.2 us, teacher q|k|v 161.2 -> 157.7, o_proj 153.2 -> 151.1, SigLIP
+// fc2 109.0 -> 102.4 -- and not on the wide-N shapes (teacher gate|up +2 %, lm_heads +3 / +11 %:
+// its stage pairs halve the prefetch depth, see g12_tile).  KD_GEMM_V12=0 / 1: never / always.
+static bool use_v12(int variant, int64_t N = 0, int64_t K = 0) {
     if (variant == 26) return true;
     if (variant != 0 && variant != 16) return false;
-    static const int env = [] { const char* e = std::getenv("KD_GEMM_V12"); return e ? std::atoi(e) : 0; }();
-    return env == 1;
+    static const int env = [] { const char* e = std::getenv("KD_GEMM_V12"); return e ? std::atoi(e) : -1; }();
+    if (env >= 0) return env == 1;
+    return N > 0 && N <= 10240 && K <= 4096;
 }
 
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
@@ -2440,6 +2445,8 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 26), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
+    // the tiled epilogues load a lane's 4 bias columns as one f32x4 / bf16x4 vector (load_bias4)
+    KD_CHECK_ALIGN(d->bias, d->bias_dtype == KD_DTYPE_F32 ? 16 : 8, "gemm: bias must be 16-B (fp32) / 8-B (bf16) aligned");
     KD_CHECK_SHAPE(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
     if (d->a_layout == KD_LAYOUT_K_MAJOR) {
         KD_CHECK_SHAPE(d->K % 8 == 0 && d->lda >= d->K, "gemm: K-major A needs K % 8 == 0, lda >= K");
@@ -2541,7 +2548,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         pk.gx = (int)grid.x; pk.gy = 1;
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
         else if (use_v11(d->variant)) hipLaunchKernelGGL((k_gemm11<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
-        else if (use_v12(d->variant)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (use_v12(d->variant, d->N, d->K)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 22)
             hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 25)
@@ -2606,7 +2613,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                     hipLaunchKernelGGL((k_gemm11<0>), grid, dim3(NTH8), lds, st, q);
                     return;
                 }
-                if (!amn && !bmn && use_v12(force)) {   // v12: the same tiles, whole-line K-major staging
+                if (!amn && !bmn && use_v12(force, d->N, q.K)) {   // v12: the same tiles, whole-line K-major staging
                     hipLaunchKernelGGL((k_gemm12<0>), grid, dim3(NTH8), lds, st, q);
                     return;
                 }

@@ -594,7 +594,13 @@ class LlavaOnevisionModel:
             raise RuntimeError(f"pixel_values has {P} tiles per sample; image_sizes need {max(counts)}")
         px = pixel_values.reshape(B * P, *pixel_values.shape[2:])
         if any(n != P for n in counts):
-            idx = torch.tensor([b * P + t for b in range(B) for t in range(counts[b])], device=px.device)
+            # the compact-tile index, cached per (tile counts, P) like the anyres maps: no
+            # pageable host-to-device copy on every forward of a mixed batch
+            key = ("tiles", tuple(counts), P)
+            idx = self._maps.get(key)
+            if idx is None:
+                idx = torch.tensor([b * P + t for b in range(B) for t in range(counts[b])], device=px.device)
+                self._maps[key] = idx
             px = px.index_select(0, idx)
         px = px.contiguous()
         tiles = int(sum(counts))   # vision tiles of the batch
