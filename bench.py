@@ -506,13 +506,17 @@ def main():
     if a.shapes and rank == 0:
         with open(a.shapes, "w") as f:
             json.dump(ops.TIMER.by_shape(top=200), f, indent=1)
-    # the roofline kernel: the fused gate|up + SwiGLU GEMM (k_gemm8<K-major,K-major> SwiGLU build,
-    # one launch per call, 28 + 24 calls per step) -- a kernel of its own, so the rocprofv3
-    # kernel trace's average for it is directly comparable
-    fwd = ops.TIMER.summary("gemm_kk_swiglu")
+    # the roofline kernel: the fused gate|up + SwiGLU GEMM of the teacher MLPs, k_gemm8<false, false, 4>
+    # (one launch per call, 28 per step, the largest GEMM family of the step) -- a kernel build of its
+    # own, so the rocprofv3 kernel trace's average for it is directly comparable.  Since round 4 the
+    # student's gate|up (N = 9728, K = 896) runs on the v12 build k_gemm12<4> (the library's use_v12:
+    # N <= 10240 and K <= 4096), reported beside it.
+    v8_shape = lambda M, N, K: N > 10240 or K > 4096
+    fwd = ops.TIMER.summary("gemm_kk_swiglu", where=v8_shape)
+    fwd12 = ops.TIMER.summary("gemm_kk_swiglu", where=lambda M, N, K: not v8_shape(M, N, K))
     fwd8 = ops.TIMER.summary("gemm_f8_swiglu")
     traffic = None   # PMC HBM bytes per launch of that kernel (tools/pmc_bench.sh -> profiles/)
-    for rd in ("r03", "r02", "r01"):
+    for rd in ("r04", "r03", "r02", "r01"):
         tpath = REPO / "profiles" / rd / "pmc_traffic.json"
         if tpath.exists():
             fg = json.load(open(tpath)).get("roofline_kernel")
@@ -521,15 +525,18 @@ def main():
                 break
     if fwd:
         ach = fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12
-        roof = dict(bound="mfma", kernel="k_gemm8<false, false, 4> (fused gate|up GEMM + SwiGLU epilogue of every "
-                                           "teacher and student MLP, bf16)",
+        roof = dict(bound="mfma", kernel="k_gemm8<false, false, 4> (fused gate|up GEMM + SwiGLU epilogue of the "
+                                           "teacher MLPs, bf16)",
                     achieved=round(ach, 1), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s", frac=round(ach / PEAK_BF16_TFLOPS, 4),
                     traffic=traffic, traffic_unit="bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                    "profiles/*/pmc_traffic.json)",
                     flops_per_launch=round(fwd["flops_per_launch"] / 1e9, 2),
                     avg_launch_us=round(fwd["avg_ms"] * 1e3, 2),
                     measured="HIP events on the launch stream over 2 serialized steps after the timed region "
-                             "(bench.py --serial under rocprofv3 gives the matching kernel trace)")
+                             "(bench.py --serial under rocprofv3 gives the matching kernel trace)",
+                    student_swiglu_v12=None if not fwd12 else dict(
+                        kernel="k_gemm12<4>", launches=fwd12["launches"], avg_launch_us=round(fwd12["avg_ms"] * 1e3, 2),
+                        tflops=round(fwd12["flops"] / (fwd12["total_ms"] * 1e-3) / 1e12, 1)))
     if fwd8:   # c4: the fp8 teacher's fused gate|up GEMM is the dominant kernel
         ach = fwd8["flops"] / (fwd8["total_ms"] * 1e-3) / 1e12
         roof = dict(bound="mfma", kernel="k_gemm8f8<4, 0> (fp8 e4m3 fused gate|up GEMM + SwiGLU epilogue of the teacher "

@@ -1523,6 +1523,12 @@ template <int EXP>
 __device__ __forceinline__ void g12_tile(GemmP p, int tm, int tn, char* smem) {
     constexpr bool RSTATS = EXP & 32;
     constexpr bool glu = EXP & 4;
+    // EXP & 256 (forced variant 27): no barrier at the end of odd steps.  The only cross-wave
+    // hazards are per PAIR: RAW (pair q, issued in step 2q-3, is first read in step 2q-1: every
+    // wave's vmcnt(0) + the barrier at the end of EVEN step 2q-2) and WAR (pair q+2 overwrites
+    // pair q's slot in odd step 2q+1, after every wave's last read of pair q in step 2q: the
+    // lgkmcnt(0) + barrier at the end of even step 2q); the odd-step barrier guards nothing.
+    constexpr bool NOB = EXP & 256;
     constexpr int PA = 256 * 128;       // one operand's pair image (32 KiB)
     constexpr int PS = 2 * PA;          // a pair slot (64 KiB); two of them
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1591,7 +1597,7 @@ __device__ __forceinline__ void g12_tile(GemmP p, int tm, int tn, char* smem) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 #define KD_G12_SYNC(ODD)                                   \
-    {                                                      \
+    if (!(NOB && (ODD))) {                                 \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
         if (ODD) wait_vm<16>();                            \
         else wait_vm<0>();                                 \
@@ -2442,7 +2448,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldc >= w && d->ld_aux >= w && d->ldc % 8 == 0 && d->ld_aux % 8 == 0 &&
                        (uintptr_t)d->aux % 16 == 0, "gemm backward activation: ldc / ld_aux >= N (2N for dswiglu), 16-B rows");
     }
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 26), "gemm: unknown variant");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 27), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     // the tiled epilogues load a lane's 4 bias columns as one f32x4 / bf16x4 vector (load_bias4)
@@ -2548,6 +2554,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         pk.gx = (int)grid.x; pk.gy = 1;
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
         else if (use_v11(d->variant)) hipLaunchKernelGGL((k_gemm11<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (d->variant == 27) hipLaunchKernelGGL((k_gemm12<4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (use_v12(d->variant, d->N, d->K)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 22)
             hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
@@ -2611,6 +2618,10 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     }
                 if (!amn && !bmn && use_v11(force)) {   // v11: the same tiles on 32x32x16 MFMAs
                     hipLaunchKernelGGL((k_gemm11<0>), grid, dim3(NTH8), lds, st, q);
+                    return;
+                }
+                if (!amn && !bmn && force == 27) {   // v12 without the odd-step barriers (A/B)
+                    hipLaunchKernelGGL((k_gemm12<256>), grid, dim3(NTH8), lds, st, q);
                     return;
                 }
                 if (!amn && !bmn && use_v12(force, d->N, q.K)) {   // v12: the same tiles, whole-line K-major staging

@@ -58,8 +58,11 @@ struct RowStats {
 static_assert(sizeof(RowStats) == 64, "RowStats layout");
 
 struct Layout {
-    size_t stats, lab_last, klo_last, mask, ovr, part_kl, err, total;
+    size_t stats, lab_last, klo_last, mask, ovr, part_kl, gran, err, total;
 };
+
+constexpr int RR_SLICE_CHUNKS = 512 * 5;   // = RR_SLICE below (k_loss_grad_loca_rr)
+inline int rr_nsl(int V) { const int nch = V / 8; return (nch + RR_SLICE_CHUNKS - 1) / RR_SLICE_CHUNKS; }
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
@@ -74,6 +77,7 @@ inline Layout make_layout(int B, int L, int V) {
     lo.mask = off;     off = align16(off + (size_t)((V + 63) / 64) * 8);
     lo.ovr = off;      off = align16(off + (size_t)V * 8);   // q [V], then log2 q [V]
     lo.part_kl = off;  off = align16(off + rows * 4);
+    lo.gran = off;     off = align16(off + rows * (size_t)rr_nsl(V) * 16);   // k_loss_grad_loca_rr hand-off granules
     lo.total = off;
     return lo;
 }
@@ -633,6 +637,226 @@ k_loss_grad_loca(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restri
     }
 }
 
+// Register-resident LoCa (round 4): k_loss_grad_loca reads every row twice (pass A for S,
+// pass B for dlogits) and the second read missed the caches (rocprofv3 FETCH_SIZE 2.08x the two
+// logit tensors: a row is 608 KB, far above a CU's share of its XCD's 4 MB L2).  Here a row is
+// cut into nsl column slices of <= RR_NT * RR_C 16-B chunks per tensor, one per workgroup, and
+// each lane keeps its RR_C chunks of the teacher and of the student row in REGISTERS between
+// the passes, so HBM sees one read of each logit tensor and one write of dlogits (two 512-thread
+// workgroups per CU, 160 KB of loads in flight; holding the next row in a second register set
+// instead leaves one workgroup per CU and measured 2.0x slower: too few waves for the VALU).  The slices
+// of a row exchange their pass-A partials (KD term, S) through 8-B granules {tag, value} stored
+// write-through at agent scope (cdna_hip_programming.md §6 G16 R2: no fence, no flag); every
+// slice sums the nsl partials in slice order, so all of a row's workgroups use the same S.
+// All of a row's slices must be resident together: the grid is nsl x (resident workgroups /
+// nsl) persistent workgroups (row groups stride the rows), and every poll is bounded in time
+// (the timeout sets bit 4 of the error words: KD_ERR_LAUNCH from kd_loss_check, AdamW skips).
+// Same per-element arithmetic as k_loss_grad_loca; the row sums differ in fp32 order only.
+constexpr int RR_NT = 512, RR_NW = RR_NT / 64;
+constexpr int RR_C = 5;                                   // 16-B chunks of each tensor per lane per row
+constexpr int RR_SLICE = RR_NT * RR_C;                    // max chunks per slice
+static_assert(RR_SLICE == RR_SLICE_CHUNKS, "slice size");
+constexpr int RR_MAX_SL = 16;                             // slices per row (V <= 327,680)
+constexpr int RR_MASK_W = RR_SLICE * 8 / 64 + 2;          // mask words a slice spans
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ void gran_store(unsigned long long* p, float v) {
+    __hip_atomic_store((gu64*)p, (1ull << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long gran_load(const unsigned long long* p) {
+    return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <bool T1>
+__global__ void __launch_bounds__(RR_NT, 4)
+k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
+                    int V, int rows, float invT, float clamp_min, const RowStats* __restrict__ stats,
+                    const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g,
+                    const float* __restrict__ coefs, bf16* __restrict__ D_, int64_t ld_d,
+                    float* __restrict__ part_kl, int nsl, int cps, int n_rg,
+                    unsigned long long* __restrict__ gran, int* __restrict__ err, int* __restrict__ err_ext) {
+    __shared__ unsigned long long smask[RR_MASK_W];
+    __shared__ float red[2 * RR_NW];
+    __shared__ float row_sums[2];
+    const float ce_coef = coefs[1], kd_coef = coefs[2];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int sl = (int)(blockIdx.x % (unsigned)nsl), rg = (int)(blockIdx.x / (unsigned)nsl);
+    const int c_lo = sl * cps, c_hi = min(V >> 3, c_lo + cps);   // this workgroup's chunks [c_lo, c_hi)
+    const int w_lo = (c_lo * 8) >> 6;
+    const uint32_t vo = (uint32_t)tid * 16;
+    // the slice through buffer descriptors (SGPRs) and ONE lane offset: out-of-slice chunks read
+    // zeros (never used); 64-bit per-chunk addresses hoisted out of the row loop spilled
+    const uint32_t nb = (uint32_t)(c_hi - c_lo) * 16;
+    for (int i = tid; i < RR_MASK_W; i += RR_NT) {
+        const int w = w_lo + i;
+        smask[i] = w < ((V + 63) >> 6) ? mask_g[w] : 0ull;
+    }
+    __syncthreads();
+    // the override mask is one table for the whole launch and the slice is fixed per
+    // workgroup: a lane's RR_C mask bytes, once
+    uint64_t mb = 0;
+#pragma unroll
+    for (int j = 0; j < RR_C; ++j) {
+        const int c = c_lo + tid + j * RR_NT;
+        if (c < c_hi) mb |= ((smask[((c * 8) >> 6) - w_lo] >> ((c * 8) & 63)) & 0xffull) << (8 * j);
+    }
+    LocaRow R;
+    R.a = invT * KD_LOG2E;
+    R.lcl = log2f(clamp_min);
+    R.kd_coef = kd_coef;
+    const float lk = kd_coef > 0.f ? log2f(kd_coef) : -INFINITY;
+    typedef __attribute__((ext_vector_type(2))) float f32x2;
+    typedef bf16x8 Set[RR_C];
+    auto load = [&](Set& xt, Set& xs, int r) {
+        const __amdgpu_buffer_rsrc_t rT = slice_rsrc(T_ + (int64_t)r * ld_t + c_lo * 8, nb);
+        const __amdgpu_buffer_rsrc_t rS = slice_rsrc(S_ + (int64_t)r * ld_s + c_lo * 8, nb);
+#pragma unroll
+        for (int j = 0; j < RR_C; ++j) {
+            xt[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rT, vo, j * RR_NT * 16, 0));
+            xs[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rS, vo, j * RR_NT * 16, 0));
+        }
+    };
+    // row r from registers (xt, xs)
+    auto row = [&](Set& xt, Set& xs, int r) {
+        const RowStats st = stats[r];
+        R.cq = (st.mt * invT + logf(st.zt)) * KD_LOG2E;
+        R.cs = (st.ms * invT + logf(st.zs)) * KD_LOG2E;
+        // ---- pass A (k_loss_grad_loca's arithmetic)
+        const f32x2 a2 = {R.a, R.a}, cq2 = {R.cq, R.cq}, cs2 = {R.cs, R.cs};
+        f32x2 term2 = {0.f, 0.f}, sacc2 = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < RR_C; ++j) {
+            const int c = c_lo + tid + j * RR_NT;
+            if (c >= c_hi) break;
+            const int v = c * 8;
+            float t[8], sv[8], lq[8], q[8], lps[8];
+            bf16x8_to_f32(xt[j], t);
+            bf16x8_to_f32(xs[j], sv);
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+                const f32x2 lq2 = f32x2{t[k], t[k + 1]} * a2 - cq2;
+                const f32x2 lp2 = f32x2{sv[k], sv[k + 1]} * a2 - cs2;
+                lq[k] = lq2.x; lq[k + 1] = lq2.y;
+                lps[k] = lp2.x; lps[k + 1] = lp2.y;
+                q[k] = ex2(lq[k]);
+                q[k + 1] = ex2(lq[k + 1]);
+            }
+            if ((mb >> (8 * j)) & 0xffu) {
+                const f32x4 o0 = *(const f32x4*)(ovr + v), o1 = *(const f32x4*)(ovr + v + 4);
+                const f32x4 l0 = *(const f32x4*)(ovr + V + v), l1 = *(const f32x4*)(ovr + V + v + 4);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float o = k < 4 ? o0[k] : o1[k - 4];
+                    const bool on = o == o;
+                    q[k] = on ? o : q[k];
+                    lq[k] = on ? (k < 4 ? l0[k] : l1[k - 4]) : lq[k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+                const f32x2 qq = {q[k], q[k + 1]};
+                const f32x2 lc2 = {fmaxf(lps[k], R.lcl), fmaxf(lps[k + 1], R.lcl)};
+                term2 = qq * (f32x2{lq[k], lq[k + 1]} - lc2) + term2;
+                sacc2 += f32x2{lps[k] >= R.lcl ? q[k] : 0.f, lps[k + 1] >= R.lcl ? q[k + 1] : 0.f};
+            }
+        }
+        // slice partials: the block's two sums in one LDS round
+        const float tw = wave_sum(term2.x + term2.y), sw = wave_sum(sacc2.x + sacc2.y);
+        if (lane == 0) { red[wid] = tw; red[RR_NW + wid] = sw; }
+        __syncthreads();
+        if (wid == 0) {
+            float tp = 0.f, sp = 0.f;
+#pragma unroll
+            for (int i = 0; i < RR_NW; ++i) { tp += red[i]; sp += red[RR_NW + i]; }
+            if (nsl > 1) {
+                unsigned long long* g = gran + (int64_t)r * nsl * 2;
+                if (lane == 0) { gran_store(g + 2 * sl, tp); gran_store(g + 2 * sl + 1, sp); }
+                // poll the row's 2 nsl granules (this slice's own included: its store is visible
+                // to its own loads once written), bounded by ~1 s of the 100 MHz real-time clock.
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                unsigned long long x = 1ull << 32;
+                for (;;) {
+                    x = lane < 2 * nsl ? gran_load(g + lane) : (1ull << 32);
+                    if (__all((unsigned)(x >> 32) == 1u)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+                        if (lane == 0) {
+                            atomicOr(err, 4);
+                            if (err_ext != nullptr) atomicOr(err_ext, 4);
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                const float xv = __uint_as_float((unsigned)x);
+                tp = 0.f; sp = 0.f;
+                for (int s2 = 0; s2 < nsl; ++s2) {   // slice order: every slice of the row gets the same sums
+                    tp += __shfl(xv, 2 * s2, 64);
+                    sp += __shfl(xv, 2 * s2 + 1, 64);
+                }
+            }
+            if (lane == 0) {
+                row_sums[0] = tp; row_sums[1] = sp;
+                if (sl == 0) part_kl[r] = tp * KD_LN2;
+            }
+        }
+        __syncthreads();
+        const float Ssum = row_sums[1];
+        if (D_ == nullptr) return;
+        // ---- pass B from the registers
+        R.cec = st.valid ? ce_coef : 0.f;
+        R.K = kd_coef * Ssum + (T1 ? R.cec : 0.f);
+        R.cqk = R.cq - lk;
+        R.c1 = (st.ms + logf(st.zs1)) * KD_LOG2E;
+        bf16* drow = D_ + (int64_t)r * ld_d;
+        const __amdgpu_buffer_rsrc_t rD = slice_rsrc(drow + c_lo * 8, nb);
+#pragma unroll
+        for (int j = 0; j < RR_C; ++j) {
+            const int c = c_lo + tid + j * RR_NT;
+            if (c >= c_hi) break;
+            const int v = c * 8;
+            float t[8], sv[8], qk[8];
+            bf16x8_to_f32(xt[j], t);
+            bf16x8_to_f32(xs[j], sv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) qk[k] = ex2(fmaf(t[k], R.a, -R.cqk));
+            if ((mb >> (8 * j)) & 0xffu) {
+                const f32x4 o0 = *(const f32x4*)(ovr + v), o1 = *(const f32x4*)(ovr + v + 4);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float o = k < 4 ? o0[k] : o1[k - 4];
+                    qk[k] = o == o ? o * kd_coef : qk[k];
+                }
+            }
+            bf16x8 out;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) out[k] = (bf16)loca_grad<T1>(R, qk[k], sv[k]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out), rD, vo, j * RR_NT * 16, 0);
+        }
+        // the CE one-hot: the lane that wrote labn's chunk rewrites that element (program order)
+        const int labn = st.lab_next;
+        if (st.valid) {
+            const int c = labn >> 3;
+            if (c >= c_lo && c < c_hi && (c - c_lo) % RR_NT == tid) {
+                const bf16* trow = T_ + (int64_t)r * ld_t;
+                const bf16* srow = S_ + (int64_t)r * ld_s;
+                float qk = ex2(fmaf((float)trow[labn], R.a, -R.cqk));
+                if ((smask[(labn >> 6) - w_lo] >> (labn & 63)) & 1ull) qk = ovr[labn] * kd_coef;
+                const float g = loca_grad<T1>(R, qk, (float)srow[labn]);
+                drow[labn] = (bf16)(g - R.cec);
+            }
+        }
+    };
+    for (int r = rg; r < rows; r += n_rg) {
+        Set xt, xs;
+        load(xt, xs, r);
+        row(xt, xs, r);
+    }
+}
+
 __global__ void k_finalize(const RowStats* __restrict__ stats, const float* __restrict__ part_kl,
                            int rows, double kl_scale, float kd_weight, float ce_weight,
                            float out_scale, int out_acc, float* __restrict__ out) {
@@ -711,6 +935,29 @@ k_loss_grad(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ 
     const float ce_coef = coefs[1], kd_coef = coefs[2];
     loss_grad_body<VARIANT>(T_, ld_t, S_, ld_s, V, rows, invT, clamp_min, stats, ovr,
                             mask_g, kd_coef, ce_coef, D_, ld_d, part_kl, smask, red);
+}
+
+// resident k_loss_grad_loca_rr workgroups on the current device (cached per device): CUs x
+// min(occupancy answer, 2) -- two 512-thread workgroups per CU is what __launch_bounds__(512, 4)
+// reserves registers for, and the occupancy API can answer one block high (MI355X_MICROARCH)
+int rr_resident() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cache[dev] == 0) {
+        int cus = 0, nb = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_loss_grad_loca_rr<true>, RR_NT, 0) != hipSuccess)
+            cus = nb = 0;
+        cache[dev] = cus * std::min(nb, 2) > 0 ? cus * std::min(nb, 2) : -1;
+    }
+    return cache[dev] > 0 ? cache[dev] : 0;
+}
+
+// KD_LOSS_RR=0: the two-read k_loss_grad_loca (A/B; read at every call, so a test can switch)
+bool rr_enabled() {
+    const char* e = std::getenv("KD_LOSS_RR");
+    return e == nullptr || std::atoi(e) != 0;
 }
 
 }  // namespace
@@ -795,7 +1042,25 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, \
                        V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl)
     const bool loca_fast = variant == KD_LOSS_LOCA && kd_coef >= 0.f && T_ != nullptr;
-    if (loca_fast && invT == 1.f) {
+    const int nsl = rr_nsl(V_s);
+    const int resident = rr_resident();
+    if (loca_fast && rr_enabled() && nsl <= RR_MAX_SL && resident >= 2 * nsl) {
+        // register-resident slices (k_loss_grad_loca_rr): resident / nsl row groups of nsl
+        // workgroups, every one of them resident at once
+        const int cps = (V_s / 8 + nsl - 1) / nsl;
+        const int n_rg = std::min(resident / nsl, rows);
+        unsigned long long* gran = (unsigned long long*)(w + lo.gran);
+        if (nsl > 1 && hipMemsetAsync(gran, 0, (size_t)rows * nsl * 16, stream) != hipSuccess)
+            return fail(KD_ERR_LAUNCH, "kd_loss: memset granules");
+        if (invT == 1.f)
+            hipLaunchKernelGGL(k_loss_grad_loca_rr<true>, dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s,
+                               V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg,
+                               gran, err, p.err_out);
+        else
+            hipLaunchKernelGGL(k_loss_grad_loca_rr<false>, dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s,
+                               V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg,
+                               gran, err, p.err_out);
+    } else if (loca_fast && invT == 1.f) {
         hipLaunchKernelGGL(k_loss_grad_loca<true>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, V_s,
                            rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl);
     } else if (loca_fast) {
@@ -823,6 +1088,8 @@ int kd_loss_check_impl(const void* ws_, void* stream_) {
     KD_CHECK_ARG(ws_ != nullptr, "kd_loss_check: null workspace");
     if (hipStreamSynchronize(as_stream(stream_)) != hipSuccess) return fail(KD_ERR_LAUNCH, "kd_loss_check: sync");
     if (hipMemcpy(&h, ws_, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(KD_ERR_LAUNCH, "kd_loss_check: copy");
+    if (h & 4) return fail(KD_ERR_LAUNCH, "kd_loss: a row's slice hand-off timed out (k_loss_grad_loca_rr: "
+                                          "its workgroups were not resident together)");
     if (h) return fail(KD_ERR_LABEL_RANGE, "kd_loss: label outside [0, V) (LoCa gathers at every label; "
                                             "CE targets must be -100 or in range)");
     return KD_OK;

@@ -230,6 +230,9 @@ class _ErrorWatch:
         if bits & 2:
             raise RuntimeError(f"student CE: target {lab} is out of bounds (not -100 and not in [0, {V})) "
                                f"at batch {row // L}, position {row % L}")
+        if bits & 4:
+            raise RuntimeError("kd_loss: a row's slice hand-off timed out (the loss kernel's workgroups were "
+                               "not resident together); this step's gradient was not applied")
         for who, e in (("student", serr), ("teacher", terr)):
             if e & 1:
                 raise RuntimeError(f"{who} embed_tokens: input id outside the vocabulary")

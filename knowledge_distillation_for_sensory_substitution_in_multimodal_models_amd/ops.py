@@ -43,8 +43,11 @@ class KernelTimer:
             out.append((key.value.decode(), fl.value, ms.value))
         return out
 
-    def summary(self, kind):
+    def summary(self, kind, where=None):
+        """Totals of one kind; where(M, N, K) selects shapes (None: all)."""
         recs = [r for r in self.records() if r[0].split(":", 1)[0] == kind]
+        if where is not None:
+            recs = [r for r in recs if where(*map(int, r[0].split(":")[1].split("x")))]
         if not recs:
             return None
         ms = [r[2] for r in recs]

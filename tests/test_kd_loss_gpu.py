@@ -202,3 +202,31 @@ def test_loss_with_gemm_row_stats(variant, T, dev):
     assert torch.allclose(a, b, rtol=2e-6, atol=1e-9), (a, b)
     dd = (d0.float() - d1.float()).abs()
     assert bool((dd <= 2.0 ** -7 * d0.float().abs() + 1e-9).all()), dd.max().item()
+
+
+@pytest.mark.parametrize("B,L,V,T,ovr", [(2, 384, 151936, 1.0, True), (2, 384, 151936, 0.8, True),
+                                         (1, 200, 20480, 1.0, False), (3, 7, 24, 1.0, True)])
+def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev, monkeypatch):
+    """k_loss_grad_loca_rr (row slices held in registers, partials handed between the slices'
+    workgroups) == k_loss_grad_loca (KD_LOSS_RR=0, two reads of every row) up to the fp32 order
+    of the row sums: terms within 2e-6 relative, dlogits within one bf16 ulp.  Cases: the real
+    vocab at T = 1 and 0.8 (8 slices), one slice (V = 20480), a vocab of 3 chunks; labels drawn
+    from a few ids so the LoCa override columns (DT:184-185) fall into several slices."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(5)
+    s = (torch.randn(B, L, V, generator=g) * 2).to(dev, torch.bfloat16)
+    t = (torch.randn(B, L, V + 128, generator=g) * 2).to(dev, torch.bfloat16)
+    hi = min(V, 4000) if ovr else V
+    labels = torch.randint(0, hi, (B, L), generator=g)
+    labels[:, ::3] = torch.randint(0, V, labels[:, ::3].shape, generator=g)
+    labels = labels.to(dev)
+    out = []
+    for rr in ("0", "1"):
+        monkeypatch.setenv("KD_LOSS_RR", rr)
+        out.append(ops.kd_loss_fwd_bwd(s, t, labels, "loca", temperature=T, check=True))
+    torch.cuda.synchronize()
+    (l0, d0), (l1, d1) = out
+    a, b = l0.cpu().double(), l1.cpu().double()
+    assert torch.allclose(a, b, rtol=2e-6, atol=1e-9), (a, b)
+    dd = (d0.float() - d1.float()).abs()
+    assert bool((dd <= 2.0 ** -7 * d0.float().abs() + 1e-12).all()), dd.max().item()

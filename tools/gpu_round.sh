@@ -1,5 +1,6 @@
 # Round-end style GPU pass (run under gpurun):
 #   STEPS="tests parity bench prof pmc" ROUND=r02 bash tools/gpu_round.sh
+# smoke  : __graft_entry__.smoke()
 # tests  : pytest -m gpu (every parity test); gemm: only the GEMM / fp8 GEMM tests
 # c2, c4 : bench.py --config c2 / c4 (the other single-GPU BASELINE configs) -> gpurun_out/bench_c*.log
 # parity : tools/parity_report.py -> gpurun_out/parity.json (per-term deltas vs the reference)
@@ -18,6 +19,8 @@ BENCH_ARGS=${BENCH_ARGS:-""}
 for s in $STEPS; do
   echo "== $s $(date +%T)"
   case $s in
+    smoke)  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
+            tail -1 gpurun_out/smoke.log ;;
     tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
             tail -2 gpurun_out/pytest_gpu.log ;;
     parity) timeout -k 10 600 python -u tools/parity_report.py --out gpurun_out/parity.json $PARITY_KINDS > gpurun_out/parity.log 2>&1 || { echo "parity failed"; tail -20 gpurun_out/parity.log; exit 1; } ;;
