@@ -1005,7 +1005,12 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
             hipMemsetAsync(klo_last, 0xff, (size_t)V_s * 4, stream) != hipSuccess)
             return fail(KD_ERR_LAUNCH, "kd_loss: memset tables");
     }
-    const int grid = rows < 2048 ? rows : 2048;
+    // k_row_stats: one workgroup per row (the dispatcher balances them); a grid of 2048 row-strided
+    // workgroups left 512 of them (3 rows each) on a third of the CUs after the first 1536 (six
+    // per CU) finished.  KD_RS_GRID=n: a grid of n row-strided workgroups (A/B).
+    const char* rs_env = std::getenv("KD_RS_GRID");
+    const int rs_cap = rs_env ? std::max(1, std::atoi(rs_env)) : 1 << 30;
+    const int grid = std::min(rows, rs_cap);
     const bool part = p.s_row_stats != nullptr;
     if (part) {
         KD_CHECK_ARG(!T_ || p.t_row_stats, "kd_loss: s_row_stats without t_row_stats");
