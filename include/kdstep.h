@@ -83,7 +83,10 @@ typedef struct {
     int32_t out_accumulate; /* 1: loss_out += out_scale * value (loss groups, §8e)      */
     int32_t* err_out;       /* optional device int32[4], caller-zeroed, never reset here:
                                [0] |= 1 LoCa gather label outside [0, V_s) (DT:166),
-                                      2 CE target outside {-100} u [0, V_s);
+                                      2 CE target outside {-100} u [0, V_s),
+                                      4 the LoCa kernel's row-slice hand-off timed out
+                                        (its workgroups were not resident together; the
+                                        loss / dlogits of this call are invalid);
                                [1] first offending label, [2] its row + row_base,
                                [3] claim flag                                          */
     int32_t row_base;       /* added to the row reported in err_out[2]                   */
@@ -121,7 +124,8 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t,
                     float* loss_out, void* dlogits, int64_t ld_d,
                     void* workspace, size_t workspace_bytes, void* stream);
 /* Synchronises `stream` and reports a device-side error recorded in `workspace` by the
- * last kd_loss_fwd_bwd (KD_ERR_LABEL_RANGE), else KD_OK. */
+ * last kd_loss_fwd_bwd (KD_ERR_LABEL_RANGE; KD_ERR_LAUNCH for a timed-out row-slice
+ * hand-off of the register-resident LoCa kernel), else KD_OK. */
 int kd_loss_check(const void* workspace, void* stream);
 
 /* ------------------------------------------------------------------ GEMM ---- */
