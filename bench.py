@@ -506,12 +506,13 @@ def main():
     if a.shapes and rank == 0:
         with open(a.shapes, "w") as f:
             json.dump(ops.TIMER.by_shape(top=200), f, indent=1)
-    # the roofline kernel: the fused gate|up + SwiGLU GEMM of the teacher MLPs, k_gemm8<false, false, 4>
-    # (one launch per call, 28 per step, the largest GEMM family of the step) -- a kernel build of its
-    # own, so the rocprofv3 kernel trace's average for it is directly comparable.  Since round 4 the
-    # student's gate|up (N = 9728, K = 896) runs on the v12 build k_gemm12<4> (the library's use_v12:
-    # N <= 10240 and K <= 4096), reported beside it.
-    v8_shape = lambda M, N, K: N > 10240 or K > 4096
+    # the roofline kernel: the fused gate|up + SwiGLU GEMM, k_gemm8<false, false, 4> (one launch per
+    # call: the 28 teacher + 24 student MLP gate|up GEMMs of a step, the largest GEMM family) -- a
+    # kernel build of its own, so the rocprofv3 kernel trace's average for it is directly comparable.
+    # With KD_GEMM_V12=1 the library runs the student's (N <= 10240, K <= 4096) on the v12 build
+    # k_gemm12<4> instead, reported beside it.
+    v12_on = os.environ.get("KD_GEMM_V12") == "1"
+    v8_shape = (lambda M, N, K: N > 10240 or K > 4096) if v12_on else (lambda M, N, K: True)
     fwd = ops.TIMER.summary("gemm_kk_swiglu", where=v8_shape)
     fwd12 = ops.TIMER.summary("gemm_kk_swiglu", where=lambda M, N, K: not v8_shape(M, N, K))
     fwd8 = ops.TIMER.summary("gemm_f8_swiglu")
@@ -526,7 +527,7 @@ def main():
     if fwd:
         ach = fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12
         roof = dict(bound="mfma", kernel="k_gemm8<false, false, 4> (fused gate|up GEMM + SwiGLU epilogue of the "
-                                           "teacher MLPs, bf16)",
+                                           + ("teacher MLPs, bf16)" if v12_on else "teacher and student MLPs, bf16)"),
                     achieved=round(ach, 1), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s", frac=round(ach / PEAK_BF16_TFLOPS, 4),
                     traffic=traffic, traffic_unit="bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                    "profiles/*/pmc_traffic.json)",

@@ -431,8 +431,14 @@ template <int HDP> struct Stage {
 // (prologue, tile compute, end-of-tile wait + barrier, epilogue, whole wave, tiles computed)
 // written as uint32 over the wave's own first Q row after its Q fragments are loaded (the
 // tool passes a scratch Q; nothing else reads that row: Q rows belong to one workgroup)
-template <int HDP, bool CAUSAL, bool RS, bool ST = false>
-__global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
+// NW waves per workgroup (query block of 32 NW rows; NW = 6 forced variant 36 / the host's choice
+// where it balances the grid better: SigLIP's 729 queries are 4 blocks of 192 (512 workgroups, one
+// round on 256 CUs x 2) instead of 6 blocks of 128 (768: a second, half-empty round).  Waves 4 and 5
+// stage nothing (the K/V DMA stays on waves 0-3); three waves per SIMD: <= 168 VGPRs.
+template <int HDP, bool CAUSAL, bool RS, bool ST = false, int NW = 4>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 3) k_attn_fwd32(AttnP p) {
+    static_assert(NW == 4 || (NW == 6 && !RS && !ST), "k_attn_fwd32: 6 waves only for the LDS-DMA build");
+    constexpr int QB = 32 * NW;   // query rows per workgroup
     uint64_t st_t0 = 0, st_pro = 0, st_cmp = 0, st_bar = 0, st_prev = 0;
     int st_n = 0;
     uint64_t st_r0 = 0;
@@ -445,13 +451,14 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r32 = lane & 31, hf = lane >> 5;
-    const int nqb = (p.S + 127) / 128;
+    const int nqb = (p.S + QB - 1) / QB;
     const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
     const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const int q0 = qb * 128 + wid * 32;   // the wave's first query (uniform)
+    const int q0 = qb * QB + wid * 32;   // the wave's first query (uniform)
+    const bool stager = NW == 4 || wid < 4;   // the waves that issue the K/V LDS-DMA
     const int myq = q0 + r32;
 
     bf16x8 qf[KS];
@@ -466,7 +473,7 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
     float m = -INFINITY, l = 0.f;
 
     const int nkv_all = (p.S + 63) / 64;
-    const int nkv = CAUSAL ? min((qb + 1) * 2, nkv_all) : nkv_all;
+    const int nkv = CAUSAL ? min(((qb + 1) * QB + 63) / 64, nkv_all) : nkv_all;
     const int nkv_w = CAUSAL ? min(nkv, (q0 + 31) / 64 + 1) : nkv;   // tiles with a key <= the wave's last query
     Stage<HDP> stg;
     u32x4 stk[Stage<HDP>::NL], stv[Stage<HDP>::NL];
@@ -476,7 +483,7 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
         stg.load(stv, V, 0, p.S, wid);
         stg.write_k(smem, stk);
         stg.write_v(smem + TILE, stv);
-    } else {
+    } else if (stager) {
         stage_kv32<HDP, false>(smem, K, 0, p.S, wid, lane);
         stage_kv32<HDP, true>(smem + TILE, V, 0, p.S, wid, lane);
     }
@@ -506,7 +513,7 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32(AttnP p) {
                         // every wave passed the barrier that ended tile t - 1, its last reader)
                 stg.load(stk, K, (t + 1) * 64, p.S, wid);
                 stg.load(stv, V, (t + 1) * 64, p.S, wid);
-            } else {
+            } else if (stager) {
                 char* nb = smem + (BUF ^ 1) * 2 * TILE;
                 stage_kv32<HDP, false>(nb, K, (t + 1) * 64, p.S, wid, lane);
                 stage_kv32<HDP, true>(nb + TILE, V, (t + 1) * 64, p.S, wid, lane);
@@ -1630,6 +1637,22 @@ __global__ void k_attn_delta(const bf16* __restrict__ O, const bf16* __restrict_
 
 }  // namespace
 
+// the six-wave forward by default: not yet (A/B with forced variant 36 first); head dim 128
+// needs more than the 168 VGPRs of three waves per SIMD (it spilled), so it keeps four waves
+static bool fwd_nw6(const kd_attn_desc* d) {
+    (void)d;
+    return false;
+}
+template <int HD, bool C>
+void launch_fwd_nw6(dim3 grid, size_t smem, hipStream_t st, const AttnP& p) {
+    if constexpr (HD == 128) {
+        grid.z = (p.S + 127) / 128;
+        hipLaunchKernelGGL((k_attn_fwd32<HD, C, false>), grid, dim3(256), smem, st, p);
+    } else {
+        hipLaunchKernelGGL((k_attn_fwd32<HD, C, false, false, 6>), grid, dim3(384), smem, st, p);
+    }
+}
+
 int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     KD_CHECK_ARG(d && d->q && d->k && d->v && d->o, "attn_fwd: null pointer");
     KD_CHECK_SHAPE(d->B > 0 && d->S > 0 && d->H > 0 && d->HKV > 0 && d->H % d->HKV == 0, "attn_fwd: heads");
@@ -1647,13 +1670,17 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     const char* fve = std::getenv("KD_ATTN_FWD_V");
     const int fv = fve ? std::atoi(fve) : 0;
     const bool v16 = fv == 16;
-    dim3 grid(d->H, d->B, v16 ? (d->S + 64 * nq - 1) / (64 * nq) : (d->S + 127) / 128);
+    // six-wave workgroups (192 query rows) where they fill the GPU in fewer rounds: forced variant 36,
+    // or (unforced) the shapes measured faster (fwd_nw6 below)
+    const bool nw6 = fv == 36 || (fv == 0 && fwd_nw6(d));
+    dim3 grid(d->H, d->B, v16 ? (d->S + 64 * nq - 1) / (64 * nq) : (d->S + (nw6 ? 191 : 127)) / (nw6 ? 192 : 128));
     hipStream_t st = as_stream(stream_);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem = 2 * 2 * 64 * rb;
 #define LAUNCH(HD, C)                                                                                \
     do {                                                                                             \
-        if (fv == 0 || fv == 32) hipLaunchKernelGGL((k_attn_fwd32<HD, C, false>), grid, dim3(256), smem, st, p); \
+        if (nw6) launch_fwd_nw6<HD, C>(grid, smem, st, p);                                           \
+        else if (fv == 0 || fv == 32) hipLaunchKernelGGL((k_attn_fwd32<HD, C, false>), grid, dim3(256), smem, st, p); \
         else if (fv == 35) hipLaunchKernelGGL((k_attn_fwd32<HD, C, true>), grid, dim3(256), smem, st, p); \
         else if (fv == 33) hipLaunchKernelGGL((k_attn_fwd32p<HD, C>), grid, dim3(256), smem, st, p); \
         else if (fv == 34) hipLaunchKernelGGL((k_attn_fwd32<HD, C, false, true>), grid, dim3(256), smem, st, p); \

@@ -2411,18 +2411,20 @@ static bool use_v11(int variant) {
     return env == 1;
 }
 
-// v12 (whole-line staging of K-major operands, bit-identical to v8) in place of v8 for K-major x
-// K-major tiles: forced variant 26; 24 forces v8; otherwise where it measured faster
-// (profiles/r04/ab_v12_vs_v8.txt, interleaved on one box): N <= 10240 and K <= 4096 -- student
-// gate|up+SwiGLU 116.3 -> 108.2 us, teacher q|k|v 161.2 -> 157.7, o_proj 153.2 -> 151.1, SigLIP
-// fc2 109.0 -> 102.4 -- and not on the wide-N shapes (teacher gate|up +2 %, lm_heads +3 / +11 %:
-// its stage pairs halve the prefetch depth, see g12_tile).  KD_GEMM_V12=0 / 1: never / always.
+// v12 (whole-line staging of K-major operands, bit-identical to v8): forced variant 26 (24 forces
+// v8); KD_GEMM_V12=1 runs it wherever v8 would run.  Not the default: it measured faster than v8
+// only with the weights warm in the Infinity Cache (back-to-back calls, profiles/r04/ab_v12_vs_v8.txt:
+// student gate|up 112.0 -> 103.8 us, teacher q|k|v 161.4 -> 156.9); in the step's cache state --
+// every weight read cold, a whole step after its last use -- v12 is slower than v8 on every shape
+// (profiles/r04/ab_cold.txt, tools/ab_cold.py: teacher q|k|v scatter 225.6 -> 244.3 us, o_proj
+// 180.2 -> 184.9, student down 96.0 -> 108.5, SigLIP o_proj 53.8 -> 58.3): its stage pairs halve
+// the prefetch depth, which an HBM-latency read stream exposes (g12_tile).
 static bool use_v12(int variant, int64_t N = 0, int64_t K = 0) {
+    (void)N; (void)K;
     if (variant == 26) return true;
     if (variant != 0 && variant != 16) return false;
     static const int env = [] { const char* e = std::getenv("KD_GEMM_V12"); return e ? std::atoi(e) : -1; }();
-    if (env >= 0) return env == 1;
-    return N > 0 && N <= 10240 && K <= 4096;
+    return env == 1;
 }
 
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {

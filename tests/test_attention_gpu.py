@@ -147,3 +147,22 @@ def test_attn_bwd_dkdv_variants_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
     (dq0, dk0, dv0), (dq1, dk1, dv1) = outs
     sl = (Ellipsis, slice(0, hd))   # the head-dim padding [hd, hdp) is not an output
     assert torch.equal(dk0[sl], dk1[sl]) and torch.equal(dv0[sl], dv1[sl]) and torch.equal(dq0[sl], dq1[sl])
+
+
+@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
+def test_attn_fwd_six_waves_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
+    """Forced variant 36: workgroups of six waves (192 query rows; only waves 0-3 stage K/V) ==
+    the four-wave kernel bit for bit: every wave walks its own queries over the same K/V tiles
+    in the same order (causal: the same per-wave tile count).  Head dim 128 keeps four waves."""
+    import os
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=3)
+    outs = []
+    try:
+        for var in ("32", "36"):
+            os.environ["KD_ATTN_FWD_V"] = var
+            outs.append(ops.attn_fwd(q, k, v, hd, causal))
+    finally:
+        os.environ.pop("KD_ATTN_FWD_V", None)
+    (o0, l0), (o1, l1) = outs
+    assert torch.equal(o0, o1) and torch.equal(l0, l1)
