@@ -2264,12 +2264,24 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
                               (int64_t)ceil_div(d->M, 128) * ceil_div(d->N, 256), t256, t256};
     const bool kk = d->a_layout == KD_LAYOUT_K_MAJOR && d->b_layout == KD_LAYOUT_K_MAJOR;
     // per variant (v3 256x256, 256x128, 128x256; v8; v9): {K-major x K-major, MN-major operand}
-    // refitted in round 3 (profiles/r03/gemm_tune.jsonl: the step's 42 shapes after the epilogue
-    // and attention changes), with the split's reduce launch as a constant of its own
-    static const double step_c[2][5] = {{0.7524, 0.5218, 0.5092, 0.6844, 0.7183}, {0.7375, 0.5501, 0.5469, 0.6022, 0.6876}};
-    static const double fixed_c[2][5] = {{5.253, 3.402, 3.414, 8.478, 5.888}, {5.885, 3.479, 3.398, 8.695, 8.442}};
-    constexpr double kBW = 7.711e6;        // partial-plane bytes per microsecond
-    constexpr double kSplitLaunch = 5.623;  // the reduce kernel (us); a hybrid plan launches two more kernels
+    // refitted in round 4 to the step's CACHE STATE (profiles/r04/gemm_tune_cold.jsonl,
+    // tools/tune_gemm_cold.py: every candidate timed with operand B cold -- the step reads each
+    // weight / saved activation a whole step after its last use -- and operand A just written);
+    // the round-3 constants came from warm back-to-back calls, which favour shallow prefetch and
+    // unsplit tails ({{0.7524, 0.5218, 0.5092, 0.6844, 0.7183}, {0.7375, 0.5501, 0.5469, 0.6022,
+    // 0.6876}}, {{5.253, 3.402, 3.414, 8.478, 5.888}, {5.885, 3.479, 3.398, 8.695, 8.442}}, 7.711e6,
+    // 5.623).  v9 keeps its round-3 constants (not in the automatic choice).
+    // KD_PLAN_SET=3 selects the round-3 constants (A/B); KD_GEMM_HYBRID=0 drops the hybrid plans.
+    static const double step_c4[2][5] = {{0.8167, 0.5676, 0.5775, 0.7550, 0.7183}, {0.8016, 0.6139, 0.6026, 0.6942, 0.6876}};
+    static const double fixed_c4[2][5] = {{8.830, 5.440, 5.343, 11.954, 5.888}, {9.291, 5.201, 5.162, 12.159, 8.442}};
+    static const double step_c3[2][5] = {{0.7524, 0.5218, 0.5092, 0.6844, 0.7183}, {0.7375, 0.5501, 0.5469, 0.6022, 0.6876}};
+    static const double fixed_c3[2][5] = {{5.253, 3.402, 3.414, 8.478, 5.888}, {5.885, 3.479, 3.398, 8.695, 8.442}};
+    static const bool set3 = [] { const char* e = std::getenv("KD_PLAN_SET"); return e && std::atoi(e) == 3; }();
+    static const bool hybrid_on = [] { const char* e = std::getenv("KD_GEMM_HYBRID"); return !e || std::atoi(e) != 0; }();
+    const double (&step_c)[2][5] = set3 ? step_c3 : step_c4;
+    const double (&fixed_c)[2][5] = set3 ? fixed_c3 : fixed_c4;
+    const double kBW = set3 ? 7.711e6 : 9.109e6;          // partial-plane bytes per microsecond
+    const double kSplitLaunch = set3 ? 5.623 : 6.499;     // the reduce kernel (us); a hybrid plan launches two more kernels
     constexpr bool kV9Auto = false;   // v9 enters the model's choice once its constants are fitted
     const double* step = step_c[kk ? 0 : 1];
     const double* fixed = fixed_c[kk ? 0 : 1];
@@ -2301,7 +2313,7 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
             if (t < bt) { bt = t; best = GemmPlan{vcode[v], S, kcs * BK2, 0}; }
             // hybrid: whole waves unsplit, the tail tiles split S ways (model's choice only)
             const int64_t dp = (tiles[v] / 256) * 256, tail = tiles[v] - dp;
-            if (S > 1 && d->split_k <= 0 && dp > 0 && tail > 0) {
+            if (hybrid_on && S > 1 && d->split_k <= 0 && dp > 0 && tail > 0) {
                 const double tb = (double)tbm[v] * tbn[v];
                 double th = (double)(dp / 256) * ((double)nk * step[v] + fixed[v]) +
                             (double)((tail * S + 255) / 256) * ((double)kcs * step[v] + fixed[v]) +
