@@ -211,7 +211,20 @@ typedef struct {
     int32_t row_stats_vs;      /* column bound of [2..7] (the student vocab V_s); <= 0: N */
     float row_stats_inv_t;     /* 1 / T of [3] */
     int32_t row_stats_top2;
+    /* optional: B is PRE-TILED (kd_gemm_pretile below) instead of a [N][K] matrix: every DMA of the
+       256x256 kernel then reads one contiguous KiB (whole cache lines). K-major bf16 operands, the
+       256x256 v8 kernel (variant 0 / 16 / 24), no split-K or row_stats; bit-identical results. For
+       frozen weights (the teacher): tile once, multiply many times. ldb is ignored. */
+    int32_t b_pretiled;
 } kd_gemm_desc;
+
+/* Pre-tiled B for kd_gemm_desc.b_pretiled: W [N][K] (row stride ldw, K % 8 == 0) rewritten as
+ * [ceil(N / 256) tiles][ceil(K / 32) stages][256 rows][32 k] -- each stage the exact LDS image the
+ * 256x256 kernel stages (16-B chunks swizzled per row), zero past N and K.  glu = 1: the layout of
+ * the fused SwiGLU GEMM (act KD_ACT_SWIGLU, N = 2I, I % 128 == 0): tile t holds gate rows
+ * [128 t, 128 t + 128) then up rows [I + 128 t, I + 128 t + 128).  Enqueued on `stream`. */
+size_t kd_gemm_pretile_size(int N, int K, int glu);
+int kd_gemm_pretile(const void* W, int64_t ldw, int N, int K, int glu, void* out, void* stream);
 /* q|k|v scatter epilogue of a fused projection GEMM (the attention input of SigLIP / Qwen2:
  * HF5 siglip :250-270, qwen2 :80-110 view / transpose / apply_rotary_pos_emb): the output tile,
  * bias added and rounded to bf16 as the plain GEMM's C, is written straight to head-major

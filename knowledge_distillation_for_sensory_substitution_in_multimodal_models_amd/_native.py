@@ -78,6 +78,7 @@ class KdGemmDesc(C.Structure):
         ("qkv", C.c_void_p),
         ("row_stats", C.c_void_p), ("row_stats_vs", C.c_int32), ("row_stats_inv_t", C.c_float),
         ("row_stats_top2", C.c_int32),
+        ("b_pretiled", C.c_int32),
     ]
 
 
@@ -131,6 +132,8 @@ SIGNATURES = {
                                _vp, _vp, _i64, _vp, _sz, _vp]),
     "kd_loss_check": (_i32, [_vp, _vp]),
     "kd_gemm": (_i32, [C.POINTER(KdGemmDesc), _vp]),
+    "kd_gemm_pretile_size": (_sz, [_i32, _i32, _i32]),
+    "kd_gemm_pretile": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp]),
     "kd_attn_fwd": (_i32, [C.POINTER(KdAttnDesc), _vp]),
     "kd_attn_bwd": (_i32, [C.POINTER(KdAttnBwdDesc), _vp]),
     "kd_attn_bwd_workspace_size": (C.c_size_t, [C.POINTER(KdAttnBwdDesc)]),

@@ -41,6 +41,10 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t, const voi
 int kd_loss_check(const void* workspace, void* stream) { return kd::kd_loss_check_impl(workspace, stream); }
 
 int kd_gemm(const kd_gemm_desc* desc, void* stream) { return kd::gemm_timed(desc, stream); }
+size_t kd_gemm_pretile_size(int N, int K, int glu) { return kd::gemm_pretile_size(N, K, glu); }
+int kd_gemm_pretile(const void* W, int64_t ldw, int N, int K, int glu, void* out, void* stream) {
+    return kd::launch_gemm_pretile(W, ldw, N, K, glu, out, stream);
+}
 size_t kd_gemm_workspace_size(const kd_gemm_desc* desc) { return kd::gemm_workspace_size(desc); }
 int kd_gemm_plan(const kd_gemm_desc* desc, int32_t* variant, int32_t* split_k, int32_t* dp_tiles) {
     return kd::gemm_plan_query(desc, variant, split_k, dp_tiles);

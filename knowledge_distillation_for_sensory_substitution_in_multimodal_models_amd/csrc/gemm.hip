@@ -1085,6 +1085,13 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     // 8 rows x 128 B (whole cache lines) instead of 16 rows x 64 B -- the same instructions and
     // bytes, half the cache lines per instruction: isolates the cost of half-line row segments
     constexpr bool WIDE = (EXP & 128) && !A_MN && !B_MN;
+    // bit 8: B PRE-TILED (kd_gemm_desc.b_pretiled, kd_gemm_pretile): the K-major B operand is stored
+    // as each 256-row tile's stages, [tile][stage][256 rows][64 B] with the LDS chunk swizzle (and, for
+    // the SwiGLU build, the gate|up row gather) already applied, zero-padded past N and K, so every
+    // DMA instruction reads ONE contiguous KiB (8 whole cache lines) instead of 16 half-lines, and
+    // lands the same LDS image (bit-identical results)
+    constexpr bool TB = (EXP & 256) && !B_MN && !WIDE && !RS;
+    const int nkt = (p.K + BK2 - 1) / BK2;   // stages per pre-tiled tile
 
     uint32_t* stamps = nullptr;
     if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
@@ -1101,19 +1108,21 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     constexpr bool glu = !B_MN && (EXP & 4);   // gate rows [nb, nb+128) and up rows [I+nb, I+nb+128)
     const int nb = tn * 128;
     const __amdgpu_buffer_rsrc_t rsBk =
-        glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
-            : make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
+        TB ? make_rsrc(p.B + (int64_t)tn * nkt * (256 * BK2), (uint32_t)nkt * (256 * BK2 * 2))
+           : glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
+                 : make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
     uint32_t va[4], vb[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         va[u] = voff8<A_MN>(wid * 4 + u, lane, p.lda, m0, p.M);
         vb[u] = voff8<B_MN>(wid * 4 + u, lane, p.ldb, n0, p.N);
-        if (glu) {   // tile row r -> weight row (r < 128 ? nb + r : I + nb + r - 128); same LDS swizzle
+        if (glu && !TB) {   // tile row r -> weight row (r < 128 ? nb + r : I + nb + r - 128); same LDS swizzle
             const int row = 16 * (wid * 4 + u) + (lane >> 2);
             const int gc = (lane & 3) ^ f4(row);
             const int wrow = row < 128 ? nb + row : p.glu + nb + row - 128;
             vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
         }
+        if (TB) vb[u] = (uint32_t)((wid * 4 + u) * 1024 + lane * 16);   // lane-linear KiB of the stage image
         if (WIDE) {
             const int row = 8 * (wid * 4 + u) + (lane >> 3);
             va[u] = (uint32_t)((int64_t)row * p.lda * 2 + (lane & 7) * 16);
@@ -1139,6 +1148,12 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         const int i = wid * 4 + (u & 3);
         char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
         uint32_t v = isA ? va[u & 3] : vb[u & 3];
+        if (TB && !isA) {   // one contiguous KiB of stage st (zero-padded past K); past the last stage: zeros
+            int soff = st * (256 * BK2 * 2);
+            if (!FULL && st >= nkt) { v = OOB; soff = 0; }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsBk, (lds_void_t*)dst, 16, v, soff, 0, 0);
+            return;
+        }
         if (!mn) {
             int soff = HOT ? 0 : st * BK2 * 2;
             if (!FULL) {
@@ -2414,6 +2429,46 @@ int launch_quant_rows_f8(const void* x, int64_t ldx, int R, int K, void* q, int6
 }
 
 
+// kd_gemm_pretile: W [N][K] (row stride ldw) -> the v8 K-major stage images of B, tile by tile:
+// [ceil(N / 256) tiles][ceil(K / 32) stages][256 rows][4 chunks of 8], position (row r, chunk pc)
+// holding logical chunk pc ^ f4(r) (the ring's swizzle), zeros past N and K; glu_I > 0 (the SwiGLU
+// build, N = 2 glu_I): tile t's rows [0, 128) are gate rows 128 t + r, rows [128, 256) up rows
+// glu_I + 128 t + r - 128.  One thread per 16-B chunk.
+__global__ void k_pretile_b(const bf16* __restrict__ W, int64_t ldw, int N, int K, int glu_I, int nkt, int64_t total,
+                            bf16* __restrict__ out) {
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int pc = (int)(idx & 3), r = (int)((idx >> 2) & 255);
+        const int64_t ts = idx >> 10;
+        const int st = (int)(ts % nkt), t = (int)(ts / nkt);
+        const int wrow = glu_I > 0 ? (r < 128 ? 128 * t + r : glu_I + 128 * t + r - 128) : 256 * t + r;
+        const int k = st * BK2 + 8 * (pc ^ f4(r));
+        bf16x8 v = (bf16x8){};
+        if (wrow < N && k < K) v = *(const bf16x8*)(W + (int64_t)wrow * ldw + k);
+        *(bf16x8*)(out + idx * 8) = v;
+    }
+}
+
+size_t gemm_pretile_size(int N, int K, int glu) {
+    if (N <= 0 || K <= 0) return 0;
+    const int64_t tiles = glu ? (N / 256) : ceil_div(N, 256);
+    return (size_t)tiles * ceil_div(K, BK2) * 256 * BK2 * 2;
+}
+
+int launch_gemm_pretile(const void* W, int64_t ldw, int N, int K, int glu, void* out, void* stream) {
+    KD_CHECK_ARG(W && out, "gemm_pretile: null pointer");
+    KD_CHECK_SHAPE(N > 0 && K > 0 && K % 8 == 0 && ldw >= K && ldw % 8 == 0, "gemm_pretile: K % 8 == 0, ldw >= K");
+    KD_CHECK_SHAPE(!glu || N % 256 == 0, "gemm_pretile: the SwiGLU layout needs N = 2I with I % 128 == 0");
+    KD_CHECK_ALIGN(W, 16, "gemm_pretile: W must be 16-B aligned");
+    KD_CHECK_ALIGN(out, 16, "gemm_pretile: out must be 16-B aligned");
+    const int nkt = ceil_div(K, BK2);
+    const int64_t total = (int64_t)(gemm_pretile_size(N, K, glu) / 16);
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_pretile_b, dim3(grid), dim3(256), 0, as_stream(stream), (const bf16*)W, ldw, N, K,
+                       glu ? N / 2 : 0, nkt, total, (bf16*)out);
+    KD_LAUNCH_CHECK("k_pretile_b");
+    return KD_OK;
+}
+
 // v11 (32x32x16 MFMAs) in place of v8 for K-major x K-major tiles: forced variant 23 (24 forces
 // v8 for A/B), else the library default (KD_GEMM_V11=0 turns it off)
 static bool use_v11(int variant) {
@@ -2448,6 +2503,10 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d->c_dtype == KD_DTYPE_BF16 || d->c_dtype == KD_DTYPE_F32, "gemm: c_dtype");
     KD_CHECK_ARG(d->ab_dtype == KD_DTYPE_BF16 || d->ab_dtype == KD_DTYPE_FP8_E4M3, "gemm: ab_dtype");
     KD_CHECK_ARG(!d->qkv || d->ab_dtype == KD_DTYPE_BF16, "gemm qkv: bf16 operands only");
+    KD_CHECK_ARG(!d->b_pretiled || (d->ab_dtype == KD_DTYPE_BF16 && d->a_layout == KD_LAYOUT_K_MAJOR &&
+                                    d->b_layout == KD_LAYOUT_K_MAJOR && !d->row_stats && d->split_k <= 1 &&
+                                    (d->variant == 0 || d->variant == 16 || d->variant == 24)),
+                 "gemm b_pretiled: K-major bf16 operands on the 256x256 v8 kernel, no split-K / row_stats");
     if (d->ab_dtype == KD_DTYPE_FP8_E4M3) return launch_gemm_f8(d, stream_);
     KD_CHECK_ARG(d->act >= KD_ACT_NONE && d->act <= KD_ACT_DSWIGLU, "gemm: act");
     const bool dact = d->act == KD_ACT_DGELU_TANH || d->act == KD_ACT_DSWIGLU;
@@ -2567,15 +2626,26 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
         pk.gx = (int)grid.x; pk.gy = 1;
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
-        else if (use_v11(d->variant)) hipLaunchKernelGGL((k_gemm11<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (!d->b_pretiled && use_v11(d->variant)) hipLaunchKernelGGL((k_gemm11<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 27) hipLaunchKernelGGL((k_gemm12<4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
-        else if (use_v12(d->variant, d->N, d->K)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (!d->b_pretiled && use_v12(d->variant, d->N, d->K)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 22)
             hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 25)
             hipLaunchKernelGGL((k_gemm8<false, false, 132>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (d->b_pretiled) hipLaunchKernelGGL((k_gemm8<false, false, 4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
+        return KD_OK;
+    }
+    if (d->b_pretiled) {   // the v8 kernel over every tile, unsplit (the pre-tiled layout is per 256-row tile)
+        KD_CHECK_ARG(d->N % 8 == 0 && c_ok16, "gemm b_pretiled: N % 8 == 0 and 16-B aligned C / residual rows");
+        GemmP q = p;
+        q.gm = pick_gm(ceil_div(d->M, 256), ceil_div(d->N, 256));
+        const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 256), 1);
+        q.gx = (int)grid.x; q.gy = 1; q.tile0 = 0;
+        hipLaunchKernelGGL((k_gemm8<false, false, 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, q);
+        KD_LAUNCH_CHECK("k_gemm8 (b_pretiled)");
         return KD_OK;
     }
     const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,

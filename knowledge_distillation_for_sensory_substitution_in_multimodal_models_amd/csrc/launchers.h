@@ -12,6 +12,8 @@ size_t kd_loss_ws(int B, int L, int V);
 int kd_loss_check_impl(const void* ws, void* stream);
 int launch_gemm(const kd_gemm_desc* d, void* stream);
 size_t gemm_workspace_size(const kd_gemm_desc* d);
+size_t gemm_pretile_size(int N, int K, int glu);
+int launch_gemm_pretile(const void* W, int64_t ldw, int N, int K, int glu, void* out, void* stream);
 int gemm_plan_query(const kd_gemm_desc* d, int32_t* var, int32_t* split, int32_t* dp);
 int launch_attn_fwd(const kd_attn_desc* d, void* stream);
 int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream);

@@ -238,7 +238,7 @@ def _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate
 
 
 def gemm_qkv(x: torch.Tensor, w: torch.Tensor, bias, q, k, v, S: int, nq: int, nkv: int, hd: int, hdp: int,
-             cos=None, sin=None, variant: int = 0):
+             cos=None, sin=None, variant: int = 0, b_pretiled: torch.Tensor | None = None):
     """Fused q|k|v projection: x [M, K] @ w[N, K]^T + bias written straight to head-major q
     [B, nq, S, hdp], k / v [B, nkv, S, hdp] (+ RoPE with cos / sin [S, hd/2] fp32), the
     padding zeroed (include/kdstep.h kd_qkv_scatter) — equal to gemm() + qkv_split()."""
@@ -252,6 +252,8 @@ def gemm_qkv(x: torch.Tensor, w: torch.Tensor, bias, q, k, v, S: int, nq: int, n
                                        torch.bfloat16, 0, variant, 1)
     d.C, d.ldc = None, 0
     d.qkv = C.cast(C.pointer(sc), C.c_void_p)
+    if b_pretiled is not None:
+        _set_pretiled(d, b_pretiled, N, K, False)
     NV.call("kd_gemm", C.byref(d), _stream())
     return q, k, v
 
@@ -286,8 +288,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
          residual=None, aux=None, alpha: float = 1.0, alpha_dev=None, accumulate: bool = False,
          out_dtype=torch.bfloat16, residual_row_mod: int = 0, variant: int = 0, split_k: int = 0,
          row_stats: torch.Tensor | None = None, row_stats_vs: int = 0, row_stats_inv_t: float = 1.0,
-         row_stats_top2: bool = False) -> torch.Tensor:
+         row_stats_top2: bool = False, b_pretiled: torch.Tensor | None = None) -> torch.Tensor:
     """out[M, N] = epilogue(alpha * a[M, K] @ b[N, K]^T).
+
+    b_pretiled: pretile_b(b, glu=act == "swiglu") -- the kernel reads B from it (every DMA one
+    contiguous KiB); `b` still gives the shape (kd_gemm_desc.b_pretiled).
 
     split_k: 0 = library cost model (bounded by the cached GEMM_SPLITK_WS workspace),
     1 = never split, >1 = forced number of K splits (tests).
@@ -313,7 +318,31 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, *, b
         d.row_stats_vs = int(row_stats_vs)
         d.row_stats_inv_t = float(row_stats_inv_t)
         d.row_stats_top2 = 1 if row_stats_top2 else 0
+    if b_pretiled is not None:
+        _set_pretiled(d, b_pretiled, N, K, act == "swiglu")
     NV.call("kd_gemm", C.byref(d), _stream())
+    return out
+
+
+def _set_pretiled(d, bt, N, K, glu):
+    need = NV.lib().kd_gemm_pretile_size(N, K, 1 if glu else 0)
+    if not bt.is_contiguous() or bt.numel() * bt.element_size() != need:
+        raise RuntimeError(f"b_pretiled: expected a contiguous pretile_b() buffer of {need} bytes")
+    d.B = bt.data_ptr()
+    d.b_pretiled = 1
+
+
+def pretile_b(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
+    """w [N, K] bf16 (K contiguous) -> the pre-tiled B of kd_gemm_desc.b_pretiled (kd_gemm_pretile):
+    each 256-row tile's 32-k stages as the exact LDS images the 256x256 kernel stages; glu: the
+    fused SwiGLU GEMM's gate|up row gather (w = [gate; up])."""
+    _require(w, torch.bfloat16, "pretile_b.w")
+    N, K = w.shape
+    if w.stride(1) != 1:
+        raise RuntimeError("pretile_b: rows must be K-contiguous")
+    n = NV.lib().kd_gemm_pretile_size(N, K, 1 if glu else 0)
+    out = torch.empty(n // 2, dtype=torch.bfloat16, device=w.device)
+    NV.call("kd_gemm_pretile", w.data_ptr(), w.stride(0), N, K, 1 if glu else 0, out.data_ptr(), _stream())
     return out
 
 
