@@ -352,6 +352,9 @@ int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
  * torch.optim.Optimizer.zero_grad(set_to_none=False) that Lightning calls after each step). */
 int kd_zero(void* ptr, uint64_t bytes, void* stream);
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* Read `bytes` at `ptr` once (16-B loads; grid workgroups of 256 threads, <= 0: automatic) so that
+ * the next kernel finds them in the Infinity Cache / L2 (weights read cold a step after their last use). */
+int kd_prefetch(const void* ptr, uint64_t bytes, int grid, void* stream);
 /* y (fp32) = x (bf16), n elements (the bf16 gradient all-reduce buckets, dp.GradSync). */
 int kd_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);
 /* fp8 row quantisation (the fp8 GEMM's operands): per row r of x (bf16 [R][K], K % 16 == 0)

@@ -161,6 +161,7 @@ SIGNATURES = {
     "kd_sumsq": (_i32, [_vp, _i64, _vp, _vp]),
     "kd_zero": (_i32, [_vp, C.c_uint64, _vp]),
     "kd_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
+    "kd_prefetch": (_i32, [_vp, C.c_uint64, _i32, _vp]),
     "kd_cast_bf16_f32": (_i32, [_vp, _vp, _i64, _vp]),
     "kd_quant_rows_fp8": (_i32, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp]),
     "kd_depth_to_3ch_workspace_size": (_sz, [_i32, _i32, _i32]),

@@ -125,6 +125,7 @@ int kd_image_src_map(const int64_t* ids, int B, int L, int64_t tok, const int32_
     return kd::launch_image_src_map(ids, B, L, tok, map, ld, len, src, err, s);
 }
 int kd_cast_f32_bf16(const float* x, void* y, int64_t n, void* s) { return kd::launch_cast_f32_bf16(x, y, n, s); }
+int kd_prefetch(const void* ptr, uint64_t bytes, int grid, void* s) { return kd::launch_prefetch(ptr, bytes, grid, s); }
 int kd_cast_bf16_f32(const void* x, float* y, int64_t n, void* s) { return kd::launch_cast_bf16_f32(x, y, n, s); }
 int kd_quant_rows_fp8(const void* x, int64_t ldx, int R, int K, void* q, int64_t ldq, float* scale, void* s) {
     return kd::launch_quant_rows_f8(x, ldx, R, K, q, ldq, scale, s);

@@ -50,6 +50,7 @@ int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, 
                          const int* map_len, int* src, int* err, void* stream);
 int launch_quant_rows_f8(const void* x, int64_t ldx, int R, int K, void* q, int64_t ldq, float* scale, void* stream);
 int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+int launch_prefetch(const void* ptr, uint64_t bytes, int grid, void* stream);
 int launch_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);
 size_t depth3_ws(int B, int H, int W);
 size_t image_resize_ws(int H, int W, int oh, int ow);

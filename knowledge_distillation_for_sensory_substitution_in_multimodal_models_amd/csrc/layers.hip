@@ -1031,6 +1031,27 @@ int launch_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream) {
     return KD_OK;
 }
 
+// Read `bytes` once (16-B loads, grid-strided) so they sit in the Infinity Cache / L2 for the next
+// kernel (kd_prefetch): the step reads each weight a whole step after its last use, and a GEMM that
+// meets cold weights stalls on them tile by tile; a streaming read moves them at full HBM rate.
+__global__ void k_prefetch(const u32x4* __restrict__ p, int64_t n16) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+        const u32x4 v = p[i];
+        asm volatile("" ::"v"(v));   // keep the load
+    }
+}
+
+int launch_prefetch(const void* ptr, uint64_t bytes, int grid, void* stream) {
+    KD_CHECK_ARG(ptr != nullptr, "prefetch: null pointer");
+    KD_CHECK_ALIGN(ptr, 16, "prefetch: 16-B aligned");
+    const int64_t n16 = (int64_t)(bytes / 16);
+    if (n16 == 0) return KD_OK;
+    const int g = grid > 0 ? grid : (int)std::min<int64_t>((n16 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_prefetch, dim3(g), dim3(256), 0, as_stream(stream), (const u32x4*)ptr, n16);
+    KD_LAUNCH_CHECK("k_prefetch");
+    return KD_OK;
+}
+
 int launch_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream) {
     KD_CHECK_ARG(x && y, "cast: null pointer");
     hipLaunchKernelGGL(k_cast_f32_bf16, dim3(grid_for(n, 256, 16384)), dim3(256), 0, as_stream(stream), x, (bf16*)y, n);

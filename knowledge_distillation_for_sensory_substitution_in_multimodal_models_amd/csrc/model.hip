@@ -505,9 +505,21 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int n_tiles, int save, voi
 // One nn.Linear of the forward: the bf16 MFMA GEMM, or on the fp8 path (weights bound by
 // kd_model_set_fp8) the activation rows quantised to e4m3 with a per-row scale and the fp8
 // GEMM against the e4m3 weight rows and their per-channel scales (kdstep.h, fp8 path).
+// KD_PREFETCH_W=1 (A/B): a streaming read of a forward linear's weights (kd_prefetch) right before
+// its GEMM -- every weight is read a whole step after its last use, and a GEMM that meets cold
+// weights stalls on them tile by tile (tools/ab_cold.py --prefetch)
+static const int g_prefetch_w = [] {
+    const char* e = std::getenv("KD_PREFETCH_W");
+    return e ? std::atoi(e) : 0;
+}();
+
 int lin(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int N, int K, const bf16* x, int64_t ldx, int widx,
         void* out, int64_t ldo, const GemmArgs& g) {
-    if (!m->f8q || m->soff[widx] < 0 || !(m->fam[widx] & m->f8_families) || g.row_stats)
+    const bool f8 = m->f8q && m->soff[widx] >= 0 && (m->fam[widx] & m->f8_families) && !g.row_stats;
+    if (g_prefetch_w)
+        KD_TRY(launch_prefetch(f8 ? (const void*)(m->f8q + m->off(widx)) : (const void*)m->W(widx),
+                               (uint64_t)N * K * (f8 ? 1 : 2), 0, s));
+    if (!f8)
         return gemm(s, P.splitk, M, N, K, km(x, ldx), km(m->W(widx), K), out, ldo, g);
     KD_TRY(launch_quant_rows_f8(x, ldx, M, K, P.qa, K, P.sa, s));
     kd_gemm_desc d;
@@ -546,6 +558,7 @@ int qkv_proj(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int K, const b
         kd_qkv_scatter sc{q, k, v, cs, sn, S, nq, nkv, hd, hdp};
         g.qkv = &sc;
         g.split_k = 1;
+        if (g_prefetch_w) KD_TRY(launch_prefetch(m->W(widx), (uint64_t)N * K * 2, 0, s));
         return gemm(s, P.splitk, M, N, K, km(x, K), km(m->W(widx), K), nullptr, 0, g);
     }
     KD_TRY(lin(m, P, s, M, N, K, x, K, widx, qkv, N, g));

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--variants", default="0,24,26")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--prefetch", action="store_true",
+                    help="also time kd_prefetch(weights) + the GEMM together (the plan's build), residual re-written too")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     vs = [int(v) for v in a.variants.split(",")]
@@ -47,6 +49,7 @@ def main():
         x = torch.randn(M, K, generator=g, device=dev).bfloat16()
         w = (torch.randn(N, K, generator=g, device=dev) * K ** -0.5).bfloat16()
         extra = {}
+        res = None
         if kind.startswith("qkv"):
             B, S, nq, nkv, hd, hdp, rope = (int(t) for t in kind.split(":")[1].split(","))
             bias = torch.randn(N, generator=g, device=dev).bfloat16()
@@ -81,6 +84,28 @@ def main():
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             call = lambda var: ops.gemm(x, w, out=out, variant=var)
         res_t = {}
+        warm_extra = [res] if isinstance(res, torch.Tensor) else []
+        if a.prefetch:
+            from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import _native as NV
+            for mode in ("cold", "prefetch"):
+                ts = []
+                for i in range(a.iters):
+                    junk.fill_(1.0)
+                    x.mul_(1.0)
+                    for t_ in warm_extra:
+                        t_.mul_(1.0)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    if mode == "prefetch":
+                        NV.call("kd_prefetch", w.data_ptr(), w.numel() * 2, 0, ops._stream())
+                    call(0)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1) * 1e3)
+                ts.sort()
+                res_t[f"{mode}_us"] = round(ts[len(ts) // 2], 1)
+            print(name, f"M={M} N={N} K={K} W={w.numel() * 2 / 1e6:.1f}MB", json.dumps(res_t), flush=True)
+            continue
         for var in vs:
             try:
                 call(var)
