@@ -61,8 +61,9 @@ struct Layout {
     size_t stats, lab_last, klo_last, mask, ovr, part_kl, gran, err, total;
 };
 
-constexpr int RR_SLICE_CHUNKS = 512 * 5;   // = RR_SLICE below (k_loss_grad_loca_rr)
-inline int rr_nsl(int V) { const int nch = V / 8; return (nch + RR_SLICE_CHUNKS - 1) / RR_SLICE_CHUNKS; }
+// k_loss_grad_loca_rr: RC 16-B chunks per lane and tensor (5: two 512-thread workgroups per CU, the
+// default; 3: three, KD_LOSS_RR_C=3), so a slice is <= 512 RC chunks; granules sized for RC = 3
+inline int rr_nsl(int V, int rc = 5) { const int nch = V / 8, sc = 512 * rc; return (nch + sc - 1) / sc; }
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
@@ -77,7 +78,7 @@ inline Layout make_layout(int B, int L, int V) {
     lo.mask = off;     off = align16(off + (size_t)((V + 63) / 64) * 8);
     lo.ovr = off;      off = align16(off + (size_t)V * 8);   // q [V], then log2 q [V]
     lo.part_kl = off;  off = align16(off + rows * 4);
-    lo.gran = off;     off = align16(off + rows * (size_t)rr_nsl(V) * 16);   // k_loss_grad_loca_rr hand-off granules
+    lo.gran = off;     off = align16(off + rows * (size_t)rr_nsl(V, 3) * 16);   // k_loss_grad_loca_rr hand-off granules
     lo.total = off;
     return lo;
 }
@@ -653,9 +654,8 @@ k_loss_grad_loca(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restri
 // (the timeout sets bit 4 of the error words: KD_ERR_LAUNCH from kd_loss_check, AdamW skips).
 // Same per-element arithmetic as k_loss_grad_loca; the row sums differ in fp32 order only.
 constexpr int RR_NT = 512, RR_NW = RR_NT / 64;
-constexpr int RR_C = 5;                                   // 16-B chunks of each tensor per lane per row
+constexpr int RR_C = 5;                                   // 16-B chunks of each tensor per lane per row (max)
 constexpr int RR_SLICE = RR_NT * RR_C;                    // max chunks per slice
-static_assert(RR_SLICE == RR_SLICE_CHUNKS, "slice size");
 constexpr int RR_MAX_SL = 16;                             // slices per row (V <= 327,680)
 constexpr int RR_MASK_W = RR_SLICE * 8 / 64 + 2;          // mask words a slice spans
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -671,8 +671,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, u
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <bool T1>
-__global__ void __launch_bounds__(RR_NT, 4)
+template <bool T1, int RC>
+__global__ void __launch_bounds__(RR_NT, RC >= 5 ? 4 : 6)
 k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
                     int V, int rows, float invT, float clamp_min, const RowStats* __restrict__ stats,
                     const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g,
@@ -697,10 +697,10 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
     }
     __syncthreads();
     // the override mask is one table for the whole launch and the slice is fixed per
-    // workgroup: a lane's RR_C mask bytes, once
+    // workgroup: a lane's RC mask bytes, once
     uint64_t mb = 0;
 #pragma unroll
-    for (int j = 0; j < RR_C; ++j) {
+    for (int j = 0; j < RC; ++j) {
         const int c = c_lo + tid + j * RR_NT;
         if (c < c_hi) mb |= ((smask[((c * 8) >> 6) - w_lo] >> ((c * 8) & 63)) & 0xffull) << (8 * j);
     }
@@ -710,12 +710,12 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
     R.kd_coef = kd_coef;
     const float lk = kd_coef > 0.f ? log2f(kd_coef) : -INFINITY;
     typedef __attribute__((ext_vector_type(2))) float f32x2;
-    typedef bf16x8 Set[RR_C];
+    typedef bf16x8 Set[RC];
     auto load = [&](Set& xt, Set& xs, int r) {
         const __amdgpu_buffer_rsrc_t rT = slice_rsrc(T_ + (int64_t)r * ld_t + c_lo * 8, nb);
         const __amdgpu_buffer_rsrc_t rS = slice_rsrc(S_ + (int64_t)r * ld_s + c_lo * 8, nb);
 #pragma unroll
-        for (int j = 0; j < RR_C; ++j) {
+        for (int j = 0; j < RC; ++j) {
             xt[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rT, vo, j * RR_NT * 16, 0));
             xs[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rS, vo, j * RR_NT * 16, 0));
         }
@@ -729,7 +729,7 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         const f32x2 a2 = {R.a, R.a}, cq2 = {R.cq, R.cq}, cs2 = {R.cs, R.cs};
         f32x2 term2 = {0.f, 0.f}, sacc2 = {0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < RR_C; ++j) {
+        for (int j = 0; j < RC; ++j) {
             const int c = c_lo + tid + j * RR_NT;
             if (c >= c_hi) break;
             const int v = c * 8;
@@ -814,7 +814,7 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         bf16* drow = D_ + (int64_t)r * ld_d;
         const __amdgpu_buffer_rsrc_t rD = slice_rsrc(drow + c_lo * 8, nb);
 #pragma unroll
-        for (int j = 0; j < RR_C; ++j) {
+        for (int j = 0; j < RC; ++j) {
             const int c = c_lo + tid + j * RR_NT;
             if (c >= c_hi) break;
             const int v = c * 8;
@@ -937,21 +937,29 @@ k_loss_grad(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ 
                             mask_g, kd_coef, ce_coef, D_, ld_d, part_kl, smask, red);
 }
 
-// resident k_loss_grad_loca_rr workgroups on the current device (cached per device): CUs x
-// min(occupancy answer, 2) -- two 512-thread workgroups per CU is what __launch_bounds__(512, 4)
-// reserves registers for, and the occupancy API can answer one block high (MI355X_MICROARCH)
-int rr_resident() {
-    static int cache[64] = {0};
+// resident k_loss_grad_loca_rr<., rc> workgroups on the current device (cached per device and rc):
+// CUs x min(occupancy answer, the workgroups per CU its __launch_bounds__ reserves registers for:
+// 2 at rc = 5, 3 at rc = 3) -- the occupancy API can answer one block high (MI355X_MICROARCH)
+int rr_resident(int rc) {
+    static int cache[64][2] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (cache[dev] == 0) {
+    const int k = rc >= 5 ? 0 : 1, cap = rc >= 5 ? 2 : 3;
+    if (cache[dev][k] == 0) {
         int cus = 0, nb = 0;
+        const void* fn = rc >= 5 ? (const void*)k_loss_grad_loca_rr<true, 5> : (const void*)k_loss_grad_loca_rr<true, 3>;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_loss_grad_loca_rr<true>, RR_NT, 0) != hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, RR_NT, 0) != hipSuccess)
             cus = nb = 0;
-        cache[dev] = cus * std::min(nb, 2) > 0 ? cus * std::min(nb, 2) : -1;
+        cache[dev][k] = cus * std::min(nb, cap) > 0 ? cus * std::min(nb, cap) : -1;
     }
-    return cache[dev] > 0 ? cache[dev] : 0;
+    return cache[dev][k] > 0 ? cache[dev][k] : 0;
+}
+
+// chunks per lane of the register-resident kernel: 5 (default) or KD_LOSS_RR_C=3 (read per call)
+int rr_chunks() {
+    const char* e = std::getenv("KD_LOSS_RR_C");
+    return (e && std::atoi(e) == 3) ? 3 : 5;
 }
 
 // KD_LOSS_RR=0: the two-read k_loss_grad_loca (A/B; read at every call, so a test can switch)
@@ -1047,8 +1055,9 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     hipLaunchKernelGGL(k_loss_grad<VAR>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, \
                        V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl)
     const bool loca_fast = variant == KD_LOSS_LOCA && kd_coef >= 0.f && T_ != nullptr;
-    const int nsl = rr_nsl(V_s);
-    const int resident = rr_resident();
+    const int rc = rr_chunks();
+    const int nsl = rr_nsl(V_s, rc);
+    const int resident = rr_resident(rc);
     if (loca_fast && rr_enabled() && nsl <= RR_MAX_SL && resident >= 2 * nsl) {
         // register-resident slices (k_loss_grad_loca_rr): resident / nsl row groups of nsl
         // workgroups, every one of them resident at once
@@ -1057,14 +1066,13 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
         unsigned long long* gran = (unsigned long long*)(w + lo.gran);
         if (nsl > 1 && hipMemsetAsync(gran, 0, (size_t)rows * nsl * 16, stream) != hipSuccess)
             return fail(KD_ERR_LAUNCH, "kd_loss: memset granules");
-        if (invT == 1.f)
-            hipLaunchKernelGGL(k_loss_grad_loca_rr<true>, dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s,
-                               V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg,
-                               gran, err, p.err_out);
-        else
-            hipLaunchKernelGGL(k_loss_grad_loca_rr<false>, dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s,
-                               V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg,
-                               gran, err, p.err_out);
+#define KD_LAUNCH_RR(T1v, RCv)                                                                                   \
+    hipLaunchKernelGGL((k_loss_grad_loca_rr<T1v, RCv>), dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s, \
+                       V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg, gran,   \
+                       err, p.err_out)
+        if (rc == 5) { if (invT == 1.f) KD_LAUNCH_RR(true, 5); else KD_LAUNCH_RR(false, 5); }
+        else { if (invT == 1.f) KD_LAUNCH_RR(true, 3); else KD_LAUNCH_RR(false, 3); }
+#undef KD_LAUNCH_RR
     } else if (loca_fast && invT == 1.f) {
         hipLaunchKernelGGL(k_loss_grad_loca<true>, dim3(lg_grid), dim3(LG_NT), smem, stream, T_, ld_t, S_, ld_s, V_s,
                            rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl);
