@@ -187,7 +187,9 @@ typedef struct {
                                  other layouts run 16); 24 = 16 forced even where the default is v11 / v12;
                                  25 diagnostic build of 16 (whole-line DMA rows, WRONG results: timing only);
                                  26 16 with whole-cache-line staging of K-major operands (v12, stage pairs;
-                                 K-major x K-major, other layouts run 16; bit-identical to 16) */
+                                 K-major x K-major, other layouts run 16; bit-identical to 16);
+                                 27 26 without the odd-step barriers (A/B); 28 SwiGLU only: the stamp build
+                                 of 16 (per-wave cycle totals into the workspace, tools/stamp_glu.py) */
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;

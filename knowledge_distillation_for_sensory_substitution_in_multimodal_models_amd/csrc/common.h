@@ -46,7 +46,10 @@ typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 // SiLU / sigmoid with v_exp_f32 + v_rcp_f32 instead of an IEEE fp32 division (~10 instructions
 // each). Every SiLU of the build (GEMM epilogues, k_swiglu_fwd / bwd, the decode GEMV) uses these
 // forms, so the fused and unfused paths stay bit-identical.
-__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+// exp(-x) as v_exp_f32 (2^y) of y = x * -log2(e), written out: the packed SwiGLU epilogue
+// (gemm.hip silu_mul_pair) repeats exactly these operations two elements at a time
+#define KD_SILU_LOG2E 1.4426950408889634f
+__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -KD_SILU_LOG2E)); }
 __device__ __forceinline__ float silu_fast(float x) { return x * sigmoid_fast(x); }
 // SwiGLU backward of one element: d = dL/dh, h = silu(g) * u -> (dL/dg, dL/du); shared by
 // k_swiglu_bwd and the fused dgrad epilogue (KD_ACT_DSWIGLU), so both agree bit for bit

@@ -849,14 +849,114 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
     }
 }
 
+// the accumulators as bf16 into the LDS image, unscaled (alpha == 1, no bias: a * 1 + 0 == a for
+// every accumulator -- they start at +0, so none is -0 -- and the FMA of epi_to_lds is skipped)
+template <int TM, int TN, int MT, int NT, bool L32>
+__device__ __forceinline__ void epi_to_lds_raw(const f32x4 (&acc)[MT][NT], char* smem, int rs, int wm, int wn, int lane) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int lr = wm * TM + i * (L32 ? 32 : 16) + (L32 ? (lane & 31) : acc_row(lane));
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const f32x4 a = acc[i][j];
+            const int lc = wn * TN + acc_col_of<L32>(j, lane);
+            *(bf16x4*)(smem + lr * rs + lc * 2) = (bf16x4){(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+        }
+    }
+}
+
+// this lane's index in its wave, recomputed (v_mbcnt) instead of read from a register the k-loop
+// spilled: an epilogue that reloads it from scratch waits a memory round trip first
+__device__ __forceinline__ int lane_now() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// silu(g) * u of two bf16 pairs (words: element 2k in the low half), in the arithmetic of
+// silu_fast / k_swiglu_fwd (common.h) as packed fp32 operations: the same IEEE operations in the
+// same order, two elements per v_pk_mul / v_pk_add, so the result is bit-identical
+__device__ __forceinline__ uint32_t silu_mul_pair(uint32_t gw, uint32_t uw) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    const f2 g = {__uint_as_float(gw << 16), __uint_as_float(gw & 0xffff0000u)};
+    const f2 u = {__uint_as_float(uw << 16), __uint_as_float(uw & 0xffff0000u)};
+    const f2 t = g * (f2){-KD_SILU_LOG2E, -KD_SILU_LOG2E};
+    f2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+    e = e + (f2){1.f, 1.f};
+    const f2 r = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+    const f2 o = (g * r) * u;
+    const bf16 lo = (bf16)o.x, hi = (bf16)o.y;
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+}
+
 // SwiGLU epilogue (KD_ACT_SWIGLU, v8 only): the 256-column tile holds gate features
 // [nb, nb+128) in columns 0-127 and the matching up features in columns 128-255 (the B
 // rows are gathered that way by the DMA), so C[:, nb + c] = silu(gate) * up needs no
 // second pass over HBM: pre-activations are staged once as bf16 in LDS (the rounding the
-// unfused GEMM output had), optionally written to aux ([M, 2I] gate | up, for the
-// backward), then combined in fp32 exactly as k_swiglu_fwd does.
-template <int TM, int TN, int MT, int NT, int NTHR, bool L32 = false>
+// unfused GEMM output had), then one pass per 8-column chunk reads its gate and up chunks,
+// writes them to aux ([M, 2I] gate | up, for the backward) when asked, and combines them in
+// fp32 exactly as k_swiglu_fwd does. Stores are buffer stores on one descriptor per output
+// (rows past M fall outside its range and are dropped: no per-row test), a lane's column offset
+// in a VGPR and the row step in the scalar offset.
+// ST (diagnostic, forced variant 28): mk[0] = s_memtime after the LDS staging (incl. its barrier),
+// mk[1] = after the combined pass behind a vmcnt(0) drain.
+template <int TM, int TN, int MT, int NT, int NTHR, bool L32 = false, bool ST = false>
 __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int nb, int wm,
+                                             int wn, int lane, int tid, uint64_t* mk = nullptr) {
+    float alpha = p.alpha;
+    if (p.alpha_dev) alpha *= *p.alpha_dev;
+    constexpr int RS = 256 * 2 + 16;
+    const int ln = lane_now();
+    if (alpha == 1.f) {
+        epi_to_lds_raw<TM, TN, MT, NT, L32>(acc, smem, RS, wm, wn, ln);
+    } else {
+        f32x4 bcol[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bcol[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS, alpha, bcol, wm, wn, ln, 0, 256);
+    }
+    __syncthreads();
+    if (ST) mk[0] = __builtin_amdgcn_s_memtime();
+    constexpr int RSTEP = NTHR / 16, PER = 256 / RSTEP;
+    const int t = (wm * (256 / TN) + wn) * 64 + ln;   // == tid, from wave-uniform values and v_mbcnt
+    const int c = t & 15, lr0 = t >> 4;
+    const int rows = min(256, p.M - m0);
+    const int I = p.glu;
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc((const bf16*)p.C + (int64_t)m0 * p.ldc + nb, rec_bytes(rows, p.ldc));
+    const uint32_t vc = (uint32_t)((lr0 * p.ldc + c * 8) * 2);
+    const int sc = RSTEP * (int)p.ldc * 2;
+    const char* src = smem + lr0 * RS + c * 16;
+    if (p.aux) {
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.aux + (int64_t)m0 * p.ld_aux, rec_bytes(rows, p.ld_aux));
+        const uint32_t vg = (uint32_t)((lr0 * p.ld_aux + nb + c * 8) * 2), vu = vg + (uint32_t)(I * 2);
+        const int sa = RSTEP * (int)p.ld_aux * 2;
+#pragma unroll 4
+        for (int it = 0; it < PER; ++it) {
+            const u32x4 g = *(const u32x4*)(src + it * RSTEP * RS);
+            const u32x4 u = *(const u32x4*)(src + it * RSTEP * RS + 256);
+            __builtin_amdgcn_raw_buffer_store_b128(g, ra, vg, it * sa, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(u, ra, vu, it * sa, 0);
+            const u32x4 o = {silu_mul_pair(g[0], u[0]), silu_mul_pair(g[1], u[1]), silu_mul_pair(g[2], u[2]),
+                             silu_mul_pair(g[3], u[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, rc, vc, it * sc, 0);
+        }
+    } else {
+#pragma unroll 4
+        for (int it = 0; it < PER; ++it) {
+            const u32x4 g = *(const u32x4*)(src + it * RSTEP * RS);
+            const u32x4 u = *(const u32x4*)(src + it * RSTEP * RS + 256);
+            const u32x4 o = {silu_mul_pair(g[0], u[0]), silu_mul_pair(g[1], u[1]), silu_mul_pair(g[2], u[2]),
+                             silu_mul_pair(g[3], u[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, rc, vc, it * sc, 0);
+        }
+    }
+    (void)lane; (void)tid;
+    if (ST) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); mk[1] = __builtin_amdgcn_s_memtime(); }
+}
+
+// the round-4 SwiGLU epilogue before the packed rewrite (EXP bit 512 / KD_GLU_EPI_V0=1: A/B only)
+template <int TM, int TN, int MT, int NT, int NTHR, bool L32 = false>
+__device__ __forceinline__ void epilogue_glu_v0(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int nb, int wm,
                                              int wn, int lane, int tid) {
     float alpha = p.alpha;
     if (p.alpha_dev) alpha *= *p.alpha_dev;
@@ -1094,7 +1194,12 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     const int nkt = (p.K + BK2 - 1) / BK2;   // stages per pre-tiled tile
 
     uint32_t* stamps = nullptr;
-    if (STAMP) { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
+    // the SwiGLU stamp build (variant 28) keeps its aux output: stamps go to the workspace (p.sk_ws)
+    if (STAMP) {
+        if ((EXP & 4) && !B_MN) stamps = (uint32_t*)p.sk_ws;
+        else { stamps = (uint32_t*)p.aux; p.aux = nullptr; }
+    }
+    uint64_t mk[2] = {0, 0};
     uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
     if (STAMP) ts0 = __builtin_amdgcn_s_memtime();
     constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
@@ -1308,14 +1413,18 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     uint64_t te0 = 0;
     if (STAMP) { te0 = __builtin_amdgcn_s_memtime(); s_units += te0 - tprev; }
     __syncthreads();
-    if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
+    if constexpr (!A_MN && !B_MN && (EXP & 512)) epilogue_glu_v0<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
+    else if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8, false, STAMP>(p, acc, smem, m0, nb, wm, wn, lane, tid, mk);
     else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN, RSTATS>(p, acc, smem, m0, n0, wm, wn, lane, tid);
     if (STAMP) {
+        if (glu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         s_epi = te1 - te0;
         if (lane == 0) {
             uint32_t* o = stamps + ((int64_t)(blockIdx.y * p.gx + blockIdx.x) * 4 + wid) * 8;
-            o[0] = (uint32_t)s_pro; o[1] = 0; o[2] = 0; o[3] = (uint32_t)s_bar;
+            // glu: o[1] = LDS staging (incl. the barrier), o[2] = the aux + silu * up pass
+            o[0] = (uint32_t)s_pro; o[1] = glu ? (uint32_t)(mk[0] - te0) : 0; o[2] = glu ? (uint32_t)(mk[1] - mk[0]) : 0;
+            o[3] = (uint32_t)s_bar;
             o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
         }
     }
@@ -2272,6 +2381,12 @@ inline int sk_max_pieces(int64_t tiles, int64_t nk, int G) {
     return (int)((nk - 1) / per + 2);
 }
 
+// KD_GLU_EPI_V0=1: the SwiGLU GEMM with the previous (unpacked) epilogue, for A/B (read per call)
+bool glu_epi_v0() {
+    const char* e = std::getenv("KD_GLU_EPI_V0");
+    return e && std::atoi(e) != 0;
+}
+
 GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t M = d->M, N = d->N;
     const int64_t t256 = (int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 256);
@@ -2521,7 +2636,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldc >= w && d->ld_aux >= w && d->ldc % 8 == 0 && d->ld_aux % 8 == 0 &&
                        (uintptr_t)d->aux % 16 == 0, "gemm backward activation: ldc / ld_aux >= N (2N for dswiglu), 16-B rows");
     }
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 27), "gemm: unknown variant");
+    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 28), "gemm: unknown variant");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     // the tiled epilogues load a lane's 4 bias columns as one f32x4 / bf16x4 vector (load_bias4)
@@ -2631,9 +2746,15 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         else if (!d->b_pretiled && use_v12(d->variant, d->N, d->K)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 22)
             hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (d->variant == 28) {   // stamp build: per-wave cycle totals to the workspace (tools/stamp_glu.py)
+            KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)grid.x * 4 * 8 * 4, "gemm swiglu stamps: workspace");
+            pk.sk_ws = (float*)d->workspace;
+            hipLaunchKernelGGL((k_gemm8<false, false, 5>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        }
         else if (d->variant == 25)
             hipLaunchKernelGGL((k_gemm8<false, false, 132>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->b_pretiled) hipLaunchKernelGGL((k_gemm8<false, false, 4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (glu_epi_v0()) hipLaunchKernelGGL((k_gemm8<false, false, 4 | 512>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
         return KD_OK;

@@ -301,6 +301,9 @@ def test_swiglu_epilogue_bitexact(M, I, K, dev):
     assert torch.equal(aux, gu_ref)
     assert torch.equal(a, a_ref)
     assert torch.equal(ops.gemm(h, w, act="swiglu"), a_ref)
+    # alpha != 1 takes the scaled staging path of the epilogue (alpha == 1 skips the multiply)
+    half = ops.gemm(h, w, alpha=0.5, variant=16, split_k=1)
+    assert torch.equal(ops.gemm(h, w, act="swiglu", alpha=0.5), ops.swiglu_fwd(half, I))
     g = gu_ref.float()
     _check(a, torch.nn.functional.silu(g[:, :I]) * g[:, I:])
 

@@ -1,0 +1,8 @@
+# round-4 GPU pass T: where the fused gate|up + SwiGLU GEMM's epilogue cycles go (stamp build 28)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+echo "== stamps $(date +%T)"
+timeout -k 10 200 python -u tools/stamp_glu.py 6144 37888 3584 2>&1 | grep -v amdgpu.ids || exit 1
+timeout -k 10 200 python -u tools/stamp_glu.py 6144 9728 896 --aux 2>&1 | grep -v amdgpu.ids || exit 1
+echo "done $(date +%T)"
