@@ -1201,7 +1201,8 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     }
     uint64_t mk[2] = {0, 0};
     uint64_t s_pro = 0, s_bar = 0, s_units = 0, s_epi = 0, ts0 = 0;
-    if (STAMP) ts0 = __builtin_amdgcn_s_memtime();
+    uint64_t rt0 = 0;
+    if (STAMP) { ts0 = __builtin_amdgcn_s_memtime(); rt0 = __builtin_amdgcn_s_memrealtime(); }
     constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: LDS-DMA bases in SGPRs
@@ -1426,6 +1427,13 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
             o[0] = (uint32_t)s_pro; o[1] = glu ? (uint32_t)(mk[0] - te0) : 0; o[2] = glu ? (uint32_t)(mk[1] - mk[0]) : 0;
             o[3] = (uint32_t)s_bar;
             o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
+            if (glu && wid == 0) {   // placement record per workgroup, past the per-wave block:
+                // real-time start / end (100 MHz), HW_ID (CU / SE of this workgroup), XCC_ID
+                uint32_t* w = stamps + (int64_t)p.gx * 4 * 8 + (int64_t)blockIdx.x * 4;
+                w[0] = (uint32_t)rt0; w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                w[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+                w[3] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+            }
         }
     }
 }
@@ -2747,7 +2755,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         else if (d->variant == 22)
             hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 28) {   // stamp build: per-wave cycle totals to the workspace (tools/stamp_glu.py)
-            KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)grid.x * 4 * 8 * 4, "gemm swiglu stamps: workspace");
+            KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)grid.x * (4 * 8 + 4) * 4, "gemm swiglu stamps: workspace");
             pk.sk_ws = (float*)d->workspace;
             hipLaunchKernelGGL((k_gemm8<false, false, 5>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         }

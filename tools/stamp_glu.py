@@ -38,3 +38,30 @@ print(f"{M}x{N}x{K} swiglu{' +aux' if want_aux else ''}: {blocks} tiles, {int(st
 for n, col in rows:
     print(f"  {n:18s} mean {col.mean().item():10.0f}  ({100 * col.mean().item() / tot:5.1f}%)  p10 {col.quantile(0.1).item():9.0f}"
           f"  p90 {col.quantile(0.9).item():9.0f}")
+
+# per-CU placement (wave 0 of each workgroup): start / end on the 100 MHz real-time clock, HW_ID, XCC_ID;
+# the gap between one workgroup's end and the next one's start on the same CU is time no stamp above sees
+pl = ws[blocks * 4 * 8 * 4: blocks * (4 * 8 + 4) * 4].view(torch.int32).view(blocks, 4).cpu().numpy().astype("int64")
+import collections
+import numpy as np
+start, end = pl[:, 0] & 0xFFFFFFFF, pl[:, 1] & 0xFFFFFFFF
+hw, xcc = pl[:, 2], pl[:, 3] & 0xF
+cu = (hw >> 8) & 0xF
+se = (hw >> 13) & 0x7
+key = xcc * 1000 + se * 100 + cu
+per = collections.defaultdict(list)
+for k, s0, e0 in zip(key, start, end):
+    per[k].append((s0, e0))
+gaps, lens, counts = [], [], []
+for k, v in per.items():
+    v.sort()
+    counts.append(len(v))
+    lens += [e - s for s, e in v]
+    gaps += [v[i + 1][0] - v[i][1] for i in range(len(v) - 1)]
+t0, t1 = start.min(), end.max()
+g = np.array(gaps) * 10.0   # ns
+ln = np.array(lens) * 10.0
+print(f"  placement: {len(per)} CUs used, workgroups per CU min {min(counts)} max {max(counts)}; launch span {(t1 - t0) / 100:.1f} us")
+print(f"  workgroup life mean {ln.mean() / 1e3:.2f} us; gap to the CU's next workgroup mean {g.mean() / 1e3:.2f} us "
+      f"p10 {np.quantile(g, 0.1) / 1e3:.2f} p90 {np.quantile(g, 0.9) / 1e3:.2f}  ({100 * g.sum() / (g.sum() + ln.sum()):.1f}% of CU time)")
+print(f"  in-kernel clock: {st[:, 6].mean().item() / (ln.mean() / 1e3):.0f} MHz (mean wave cycles / mean workgroup life)")
