@@ -2842,7 +2842,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                     return;
                 }
                 switch (force) {   // the diagnostic builds exist for the forward (K-major x K-major) layout only
-                    case 17: L8K(1) break;
+                    case 17: L8(1) break;   // stamps: every layout
                     case 18: L8K(2) break;
                     case 19: L8K(64) break;
                     case 22: L8K(8) break;
