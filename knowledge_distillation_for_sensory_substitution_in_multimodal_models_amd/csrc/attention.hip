@@ -678,6 +678,223 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 3) k_attn_fwd32(AttnP p
     }
 }
 
+// k_attn_fwd64: k_attn_fwd32's arithmetic with TWO 32-row query blocks per wave (workgroup = 4 waves
+// x 64 rows = 256 query rows), one wave per SIMD (up to 512 registers: O of both blocks, 2 x ND x 16,
+// beside their scores). Every K fragment (ds_read_b128) and every V^T fragment (ds_read_b64_tr_b16)
+// read from LDS feeds both blocks' MFMAs, so LDS reads and their issue slots per MFMA halve -- at one
+// block per wave a tile's ~4.5 softmax VALU + 1.5 LDS reads per MFMA exceed the ~5 fillers a 32x32x16
+// MFMA gap hides (MI355X_MICROARCH constants). Per query row the operations and their order are
+// k_attn_fwd32's (same max, lazy rescale, exps, sum chains, PV MFMA order), so O and lse are
+// bit-identical to it. Causal: a wave's two blocks end on the same 64-key tile (its first row is a
+// multiple of 64), so neither computes a tile the other skips. Forced variant 64 (KD_ATTN_FWD_V=64).
+template <int HDP, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1) k_attn_fwd64(AttnP p) {
+    constexpr int QB = 256;
+    constexpr int RB = Geo<HDP>::RB;
+    constexpr int TILE = 64 * RB;
+    constexpr int KS = HDP == 96 ? 5 : HDP / 16;
+    constexpr int ND = HDP == 64 ? 2 : (HDP == 96 ? 3 : 4);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r32 = lane & 31, hf = lane >> 5;
+    const int nqb = (p.S + QB - 1) / QB;
+    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
+    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
+    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
+    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const int q0 = qb * QB + wid * 64;   // block j: rows q0 + 32 j + [0, 32)
+    bf16x8 qf[2][KS];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int myq = q0 + 32 * j + r32;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+            qf[j][kk] = myq < p.S ? *(const bf16x8*)(Q + (int64_t)myq * HDP + kk * 16 + 8 * hf) : (bf16x8){};
+    }
+    f32x16 o[2][ND];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[j][d][i] = 0.f;
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    const int nkv_all = (p.S + 63) / 64;
+    const int nkv = CAUSAL ? min(((qb + 1) * QB + 63) / 64, nkv_all) : nkv_all;
+    const int nkv_w = CAUSAL ? min(nkv, (q0 + 63) / 64 + 1) : nkv;   // both blocks: the same last tile
+    stage_kv32<HDP, false>(smem, K, 0, p.S, wid, lane);
+    stage_kv32<HDP, true>(smem + TILE, V, 0, p.S, wid, lane);
+    uint32_t koff[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+        koff[kk] = (uint32_t)(uintptr_t)smem + r32 * RB + (((2 * kk + hf) ^ swK<RB>(r32)) << 4);
+    uint32_t vaddr[ND];
+    {
+        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+        const int row = 4 * hf + ((lane >> 2) & 3);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            const int col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            vaddr[d] = sbase + TILE + row * RB + ((((col >> 3) ^ swV32<RB>(row))) << 4) + ((col & 4) << 1);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    auto tile = [&](const int t, auto buf_c) {
+        constexpr int BUF = decltype(buf_c)::value;
+        if (t + 1 < nkv) {
+            char* nb = smem + (BUF ^ 1) * 2 * TILE;
+            stage_kv32<HDP, false>(nb, K, (t + 1) * 64, p.S, wid, lane);
+            stage_kv32<HDP, true>(nb + TILE, V, (t + 1) * 64, p.S, wid, lane);
+        }
+        if (t < nkv_w) {
+            f32x16 sc[2][2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) sc[j][kt][i] = 0.f;
+            // S^T = K Q^T for both blocks: each K fragment feeds two MFMAs
+            u32x4 ka[KS], kb[KS];
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk)
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ka[kk]) : "v"(koff[kk]), "i"(BUF * 2 * TILE));
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ka[kk]) : "i"(KS - 1) : "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                sc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ka[kk]), qf[0][kk], sc[0][0], 0, 0, 0);
+                sc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ka[kk]), qf[1][kk], sc[1][0], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kb[kk]) : "v"(koff[kk]), "i"(BUF * 2 * TILE + 32 * RB));
+            }
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(kb[kk]) : "i"(KS - 1 - kk) : "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                sc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kb[kk]), qf[0][kk], sc[0][1], 0, 0, 0);
+                sc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kb[kk]), qf[1][kk], sc[1][1], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            bf16x8 pf[2][4];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int qj = q0 + 32 * j, myq = qj + r32;
+                if (t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qj)) {
+#pragma unroll
+                    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const int key = t * 64 + 32 * kt + 8 * (i >> 2) + 4 * hf + (i & 3);
+                            if (key >= p.S || (CAUSAL && key > myq)) sc[j][kt][i] = -INFINITY;
+                        }
+                }
+                float mt = -INFINITY;
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sc[j][kt][i]);
+                mt = half_max(mt);
+                const float mts = mt * p.scale_log2;
+                const bool move = mts > m[j] + 8.f;
+                if (__ballot(move)) {
+                    const float mn = move ? mts : m[j];
+                    const float alpha = __builtin_amdgcn_exp2f(m[j] - mn);
+                    l[j] *= alpha;
+#pragma unroll
+                    for (int d = 0; d < ND; ++d) o[j][d] *= alpha;
+                    m[j] = mn;
+                }
+                const float mref = (m[j] == -INFINITY) ? 0.f : m[j];
+                float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][kt][i], p.scale_log2, -mref));
+                        sc[j][kt][i] = e;
+                        ls[i & 3] += e;
+                    }
+                l[j] += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) pf[j][s4][e] = (bf16)sc[j][s4 >> 1][8 * (s4 & 1) + e];
+            }
+            // O^T += V^T P^T for both blocks: each V^T fragment feeds two MFMAs
+            u32x2 vr[2][8];
+#define KD_F64_RD(D, SET)                                                                                        \
+    _Pragma("unroll") for (int s4 = 0; s4 < 4; ++s4) {                                                           \
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[SET][2 * s4]) : "v"(vaddr[D]), "i"(BUF * 2 * TILE + (16 * s4) * RB));     \
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[SET][2 * s4 + 1]) : "v"(vaddr[D]), "i"(BUF * 2 * TILE + (16 * s4 + 8) * RB)); \
+    }
+#define KD_F64_MM(D, SET)                                                                                        \
+    _Pragma("unroll") for (int s4 = 0; s4 < 4; ++s4) {                                                           \
+        const bf16x8 vf = cat4(__builtin_bit_cast(bf16x4, vr[SET][2 * s4]), __builtin_bit_cast(bf16x4, vr[SET][2 * s4 + 1])); \
+        o[0][D] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][s4], o[0][D], 0, 0, 0);                       \
+        o[1][D] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1][s4], o[1][D], 0, 0, 0);                       \
+    }
+#define KD_F64_WAIT(N, SET) wait_lgkm_def8<N>(vr[SET]); __builtin_amdgcn_sched_barrier(0);
+            KD_F64_RD(0, 0)
+            KD_F64_RD(1, 1)
+            KD_F64_WAIT(8, 0)
+            KD_F64_MM(0, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ND > 2) { KD_F64_RD(2, 0) KD_F64_WAIT(8, 1) }
+            else { KD_F64_WAIT(0, 1) }
+            KD_F64_MM(1, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ND > 2) {
+                if constexpr (ND > 3) { KD_F64_RD(3, 1) KD_F64_WAIT(8, 0) }
+                else { KD_F64_WAIT(0, 0) }
+                KD_F64_MM(2, 0)
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (ND > 3) {
+                    KD_F64_WAIT(0, 1)
+                    KD_F64_MM(3, 1)
+                }
+            }
+#undef KD_F64_RD
+#undef KD_F64_MM
+#undef KD_F64_WAIT
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    int t = 0;
+    for (; t + 1 < nkv; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        tile(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const float lj = half_sum(l[j]);
+        const int myq = q0 + 32 * j + r32;
+        if (myq < p.S) {
+            const float inv = 1.f / lj;
+            bf16* orow = p.o + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int dd = 32 * d + 8 * g + 4 * hf;
+                    if (dd < p.hd) {
+                        bf16x4 w;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[j][d][4 * g + r] * inv);
+                        *(bf16x4*)(orow + dd) = w;
+                    }
+                }
+            if (hf == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq] = (m[j] + log2f(lj)) * 0.6931471805599453f;
+        }
+    }
+}
+
 // k_attn_fwd32 software-pipelined at 32-key sub-tile granularity. In k_attn_fwd32 every step
 // of a tile waits on the previous one (QK^T -> max -> exp -> PV), and with two waves per SIMD
 // the waves spent ~half their lifetime stalled on those dependencies (SQ_WAIT_INST_ANY), the
@@ -1663,7 +1880,8 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
             d->B, d->H, d->HKV, d->S, d->hd, (float)(1.4426950408889634 / std::sqrt((double)d->hd))};
     // NQ query sub-tiles per wave (KD_ATTN_FWD_NQ=1 restores one, for A/B)
     static const int nq = [] { const char* e = std::getenv("KD_ATTN_FWD_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
-    // KD_ATTN_FWD_V (A/B and diagnostics): unset / 32 = k_attn_fwd32 (LDS-DMA staging), 35 = its
+    // KD_ATTN_FWD_V (A/B and diagnostics): unset / 32 = k_attn_fwd32 (LDS-DMA staging), 64 = k_attn_fwd64
+    // (two query blocks per wave), 35 = its
     // register-staged build, 33 = the sub-tile-pipelined k_attn_fwd32p, 34 = the stamp build,
     // 16 = the 16x16x32 k_attn_fwd
     // (read per call, so a test can switch variants inside one process)
@@ -1673,13 +1891,16 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     // six-wave workgroups (192 query rows) where they fill the GPU in fewer rounds: forced variant 36,
     // or (unforced) the shapes measured faster (fwd_nw6 below)
     const bool nw6 = fv == 36 || (fv == 0 && fwd_nw6(d));
-    dim3 grid(d->H, d->B, v16 ? (d->S + 64 * nq - 1) / (64 * nq) : (d->S + (nw6 ? 191 : 127)) / (nw6 ? 192 : 128));
+    const bool w64 = fv == 64;   // two query blocks per wave (k_attn_fwd64), 256 rows per workgroup
+    dim3 grid(d->H, d->B, v16 ? (d->S + 64 * nq - 1) / (64 * nq)
+                              : (w64 ? (d->S + 255) / 256 : (d->S + (nw6 ? 191 : 127)) / (nw6 ? 192 : 128)));
     hipStream_t st = as_stream(stream_);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem = 2 * 2 * 64 * rb;
 #define LAUNCH(HD, C)                                                                                \
     do {                                                                                             \
         if (nw6) launch_fwd_nw6<HD, C>(grid, smem, st, p);                                           \
+        else if (w64) hipLaunchKernelGGL((k_attn_fwd64<HD, C>), grid, dim3(256), smem, st, p);       \
         else if (fv == 0 || fv == 32) hipLaunchKernelGGL((k_attn_fwd32<HD, C, false>), grid, dim3(256), smem, st, p); \
         else if (fv == 35) hipLaunchKernelGGL((k_attn_fwd32<HD, C, true>), grid, dim3(256), smem, st, p); \
         else if (fv == 33) hipLaunchKernelGGL((k_attn_fwd32p<HD, C>), grid, dim3(256), smem, st, p); \

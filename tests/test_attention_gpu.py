@@ -166,3 +166,21 @@ def test_attn_fwd_six_waves_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
         os.environ.pop("KD_ATTN_FWD_V", None)
     (o0, l0), (o1, l1) = outs
     assert torch.equal(o0, o1) and torch.equal(l0, l1)
+
+@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
+def test_attn_fwd_two_blocks_per_wave_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
+    """Forced variant 64 (k_attn_fwd64): two 32-row query blocks per wave sharing every K / V^T
+    fragment read, 256 query rows per workgroup == the four-wave k_attn_fwd32 bit for bit (per
+    query row the same operations in the same order; a wave's two causal blocks end on one tile)."""
+    import os
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=4)
+    outs = []
+    try:
+        for var in ("32", "64"):
+            os.environ["KD_ATTN_FWD_V"] = var
+            outs.append(ops.attn_fwd(q, k, v, hd, causal))
+    finally:
+        os.environ.pop("KD_ATTN_FWD_V", None)
+    (o0, l0), (o1, l1) = outs
+    assert torch.equal(o0, o1) and torch.equal(l0, l1)
