@@ -127,6 +127,74 @@ template <> struct XChunk<float> {
     __device__ __forceinline__ float get(int j) const { return j < 4 ? a[j] : b[j - 4]; }
 };
 
+// k_norm_fwd with every load of the row issued first: IT = ceil(D / 512) chunks per lane, the chunk index
+// clamped into the row so no load sits under a lane-dependent branch (k_norm_fwd's conditional loads were
+// each followed by their own vmcnt(0): seven serial memory round trips per 3584-wide row), the weight /
+// bias chunks loaded beside x. The arithmetic and its order are k_norm_fwd's (bit-identical).
+template <bool RMS, int IT, typename XT>
+__global__ void __launch_bounds__(NT) k_norm_fwd2(const XT* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
+                                                  const bf16* __restrict__ bias, bf16* __restrict__ y, int64_t ldy,
+                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                  int R, int D, float eps) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= R) return;
+    const XT* xr = x + (int64_t)row * ldx;
+    const int nch = D / 8;
+    XChunk<XT> xc[IT];
+    bf16x8 wc[IT], bc[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int c = min(lane + it * 64, nch - 1);
+        xc[it].load(xr + c * 8);
+        wc[it] = *(const bf16x8*)(w + c * 8);
+        if (!RMS) bc[it] = *(const bf16x8*)(bias + c * 8);
+    }
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        if (lane + it * 64 < nch) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { const float f = xc[it].get(j); s += f; ss += f * f; }
+        }
+    }
+    s = wave_sum(s);
+    const float mean = RMS ? 0.f : s / D;
+    float var;
+    if (RMS) {
+        var = wave_sum(ss) / D;
+    } else {
+        float v2 = 0.f;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            if (lane + it * 64 < nch)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { const float dd = xc[it].get(j) - mean; v2 += dd * dd; }
+        }
+        var = wave_sum(v2) / D;
+    }
+    const float rstd = rsqrtf(var + eps);
+    bf16* yr = y + (int64_t)row * ldy;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int c = lane + it * 64;
+        if (c < nch) {
+            float o[8];
+            if (!RMS) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = (xc[it].get(j) - mean) * rstd * (float)wc[it][j] + (float)bc[it][j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = xc[it].get(j) * rstd * (float)wc[it][j];
+            }
+            store8(yr + c * 8, o);
+        }
+    }
+    if (lane == 0) {
+        if (mean_out) mean_out[row] = mean;
+        if (rstd_out) rstd_out[row] = rstd;
+    }
+}
+
 template <bool RMS, int IT, typename XT>
 __global__ void __launch_bounds__(NT) k_norm_bwd(const XT* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
                                                  const bf16* __restrict__ dy, int64_t lddy,
@@ -805,6 +873,38 @@ int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const vo
     KD_CHECK_SHAPE(D % 8 == 0 && D <= 4096 && ldx % 8 == 0 && ldy % 8 == 0, "norm_fwd: D must be a multiple of 8, <= 4096");
     const dim3 grid((R + 3) / 4);
     hipStream_t st = as_stream(stream);
+    // KD_NORM_FWD_V=1 (read per call): the previous kernel, for A/B
+    const char* ve = std::getenv("KD_NORM_FWD_V");
+    if (!(ve && std::atoi(ve) == 1)) {
+        const int it = (D / 8 + 63) / 64;
+#define KD_NF2(ITV)                                                                                                   \
+    do {                                                                                                               \
+        if (x_f32) {                                                                                                   \
+            if (rms) hipLaunchKernelGGL((k_norm_fwd2<true, ITV, float>), grid, dim3(NT), 0, st, (const float*)x, ldx,   \
+                                        (const bf16*)w, nullptr, (bf16*)y, ldy, mean, rstd, R, D, eps);                \
+            else hipLaunchKernelGGL((k_norm_fwd2<false, ITV, float>), grid, dim3(NT), 0, st, (const float*)x, ldx,      \
+                                    (const bf16*)w, (const bf16*)b, (bf16*)y, ldy, mean, rstd, R, D, eps);             \
+        } else {                                                                                                       \
+            if (rms) hipLaunchKernelGGL((k_norm_fwd2<true, ITV, bf16>), grid, dim3(NT), 0, st, (const bf16*)x, ldx,     \
+                                        (const bf16*)w, nullptr, (bf16*)y, ldy, mean, rstd, R, D, eps);                \
+            else hipLaunchKernelGGL((k_norm_fwd2<false, ITV, bf16>), grid, dim3(NT), 0, st, (const bf16*)x, ldx,        \
+                                    (const bf16*)w, (const bf16*)b, (bf16*)y, ldy, mean, rstd, R, D, eps);             \
+        }                                                                                                              \
+    } while (0)
+        switch (it) {
+            case 1: KD_NF2(1); break;
+            case 2: KD_NF2(2); break;
+            case 3: KD_NF2(3); break;
+            case 4: KD_NF2(4); break;
+            case 5: KD_NF2(5); break;
+            case 6: KD_NF2(6); break;
+            case 7: KD_NF2(7); break;
+            default: KD_NF2(8); break;
+        }
+#undef KD_NF2
+        KD_LAUNCH_CHECK("k_norm_fwd2");
+        return KD_OK;
+    }
     if (x_f32) {
         if (rms) hipLaunchKernelGGL((k_norm_fwd<true, float>), grid, dim3(NT), 0, st, (const float*)x, ldx, (const bf16*)w,
                                     nullptr, (bf16*)y, ldy, mean, rstd, R, D, eps);
