@@ -1173,7 +1173,16 @@ struct AttnBwdP {
     float* dkp; float* dvp;                         // GQA partials [B, H, S, HDP] fp32 (grp > 1)
     int B, H, HKV, S, hd;
     float scale, scale_log2;
+    // optional token-major [B*S, (H + 2 HKV) hd] bf16 output (kd_qkv_merge's layout, no RoPE; MHA):
+    // dq | dk | dv written there directly instead of dq / dk / dv
+    bf16* dqkv; int64_t ld_qkv;
 };
+
+// this lane's 4 consecutive columns [dd, dd + 4) of head `head` at token (b, s) in the merged
+// dqkv row (columns past hd are head-dim padding: not written)
+__device__ __forceinline__ void put_qkv4(const AttnBwdP& p, int b, int s, int head, int dd, const bf16x4& w) {
+    if (dd < p.hd) *(bf16x4*)(p.dqkv + ((int64_t)b * p.S + s) * p.ld_qkv + (int64_t)head * p.hd + dd) = w;
+}
 
 // 64 rows x ncols of a row-strided matrix (token-major dO) -> swK LDS image [64][RB];
 // columns >= ncols and rows >= S land as zeros (out-of-range buffer offsets)
@@ -1409,8 +1418,13 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv(AttnBwdP p) {
                 bf16x4 wk, wv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(dk[d][r] * p.scale); wv[r] = (bf16)dv[d][r]; }
-                *(bf16x4*)(dKr + dd) = wk;
-                *(bf16x4*)(dVr + dd) = wv;
+                if (p.dqkv) {
+                    put_qkv4(p, b, mykey, p.H + kvh, dd, wk);
+                    put_qkv4(p, b, mykey, p.H + p.HKV + kvh, dd, wv);
+                } else {
+                    *(bf16x4*)(dKr + dd) = wk;
+                    *(bf16x4*)(dVr + dd) = wv;
+                }
             }
         } else {
             float* dKr = p.dkp + ((int64_t)(b * p.H + h) * p.S + mykey) * HDP;
@@ -1625,8 +1639,13 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv2(AttnBwdP p) {
                 bf16x4 wk, wv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(dk[c][d][r] * p.scale); wv[r] = (bf16)dv[c][d][r]; }
-                *(bf16x4*)(dKr + dd) = wk;
-                *(bf16x4*)(dVr + dd) = wv;
+                if (p.dqkv) {
+                    put_qkv4(p, b, mykey[c], p.H + kvh, dd, wk);
+                    put_qkv4(p, b, mykey[c], p.H + p.HKV + kvh, dd, wv);
+                } else {
+                    *(bf16x4*)(dKr + dd) = wk;
+                    *(bf16x4*)(dVr + dd) = wv;
+                }
             }
         } else {
             float* dKr = p.dkp + ((int64_t)(b * p.H + h) * p.S + mykey[c]) * HDP;
@@ -1827,9 +1846,17 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 #pragma unroll
     for (int j = 0; j < NQ; ++j)
         if (qok[j]) {
-            float* dQr = p.dq + ((int64_t)(b * p.H + h) * p.S + myq[j]) * HDP;
+            if (p.dqkv) {   // the merged row: (bf16) of the scaled fp32 value, as kd_qkv_merge rounds it
 #pragma unroll
-            for (int d = 0; d < DT; ++d) *(f32x4*)(dQr + d * 16 + 4 * g) = acc[j][d] * p.scale;
+                for (int d = 0; d < DT; ++d) {
+                    const f32x4 v = acc[j][d] * p.scale;
+                    put_qkv4(p, b, myq[j], h, d * 16 + 4 * g, (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]});
+                }
+            } else {
+                float* dQr = p.dq + ((int64_t)(b * p.H + h) * p.S + myq[j]) * HDP;
+#pragma unroll
+                for (int d = 0; d < DT; ++d) *(f32x4*)(dQr + d * 16 + 4 * g) = acc[j][d] * p.scale;
+            }
         }
 }
 
@@ -1936,8 +1963,11 @@ size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d) {
 }
 
 int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
-    KD_CHECK_ARG(d && d->q && d->k && d->v && d->o && d->dO && d->lse && d->delta && d->dq && d->dk && d->dv,
+    KD_CHECK_ARG(d && d->q && d->k && d->v && d->o && d->dO && d->lse && d->delta && (d->dqkv || (d->dq && d->dk && d->dv)),
                  "attn_bwd: null pointer");
+    KD_CHECK_ARG(!d->dqkv || (d->H == d->HKV && d->ld_qkv >= (int64_t)3 * d->H * d->hd && d->ld_qkv % 4 == 0 &&
+                              (uintptr_t)d->dqkv % 8 == 0),
+                 "attn_bwd: dqkv needs H == HKV, ld_qkv >= 3 H hd (multiple of 4) and an 8-B aligned base");
     KD_CHECK_SHAPE(d->B > 0 && d->S > 0 && d->HKV > 0 && d->H % d->HKV == 0 && d->hd % 4 == 0 && d->hd <= d->hdp,
                    "attn_bwd: shape");
     KD_CHECK_SHAPE(d->hdp == 64 || d->hdp == 96 || d->hdp == 128, "attn_bwd: padded head dim must be 64/96/128");
@@ -1958,7 +1988,7 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     float* dvp = need ? dkp + (size_t)d->B * d->H * d->S * d->hdp : nullptr;
     AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, d->lse, d->delta,
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
-               (float)(sc * 1.4426950408889634)};
+               (float)(sc * 1.4426950408889634), (bf16*)d->dqkv, d->ld_qkv};
     // dK / dV: two 16-key sub-tiles per wave by default; KD_ATTN_BWD_V=16 selects the one-sub-tile
     // kernel (A/B; read per call)
     const char* bve = std::getenv("KD_ATTN_BWD_V");

@@ -684,8 +684,9 @@ int lm_forward(kd_model* m, const FwdPlan& P, const float* cs, const float* sn, 
 struct BwdPlan {
     bf16 *dx, *da, *dgu, *dh2, *do_, *dk, *dv, *dqkv, *dh, *demb;   // language model
     float *dq, *delta;
-    bf16 *dfeats, *dz, *dxv, *du, *dh2v, *dov, *dkv, *dvv, *dqkvv, *dhv;   // projector / vision
-    float *dqv, *deltav;
+    bf16 *dfeats, *dz, *dxv, *du, *dh2v, *dov, *dqkvv, *dhv;   // projector / vision (attention writes dqkvv directly)
+    float *deltav;
+    float* dqv = nullptr; bf16 *dkv = nullptr, *dvv = nullptr;   // KD_ATTN_DQKV=0 (A/B): head-major + kd_qkv_merge
     void *attn_ws, *attn_ws_v, *norm_ws;
     size_t attn_ws_bytes, attn_ws_v_bytes, norm_ws_bytes;
     void *splitk_main, *splitk_lane;
@@ -736,10 +737,12 @@ BwdPlan plan_backward(const kd_model* m, int B, int L, int n_tiles, void* base) 
     P.du = A.take<bf16>(NT * Iv);
     P.dh2v = A.take<bf16>(NT * D);
     P.dov = A.take<bf16>(NT * D);
-    P.dqv = A.take<float>((int64_t)NI * c.v_heads * np * hdp);
-    P.dkv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
-    P.dvv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
     P.deltav = A.take<float>((int64_t)NI * c.v_heads * np);
+    if (const char* e = std::getenv("KD_ATTN_DQKV"); e && std::atoi(e) == 0) {
+        P.dqv = A.take<float>((int64_t)NI * c.v_heads * np * hdp);
+        P.dkv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+        P.dvv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
+    }
     P.dqkvv = A.take<bf16>(NT * 3 * D);
     P.dhv = A.take<bf16>(NT * D);
     kd_attn_bwd_desc vd = vis_attn_desc(m, NI);
@@ -879,11 +882,15 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
         {
             kd_attn_bwd_desc d = vis_attn_desc(m, NI);
             d.q = b.q; d.k = b.k; d.v = b.v; d.o = b.o; d.dO = P.dov; d.lse = b.lse; d.delta = P.deltav;
-            d.dq = P.dqv; d.dk = P.dkv; d.dv = P.dvv; d.workspace = P.attn_ws_v; d.workspace_bytes = P.attn_ws_v_bytes;
+            d.workspace = P.attn_ws_v; d.workspace_bytes = P.attn_ws_v_bytes;
+            // MHA, no RoPE: dq | dk | dv straight into the fused q|k|v gradient (no kd_qkv_merge pass)
+            if (P.dqv) { d.dq = P.dqv; d.dk = P.dkv; d.dv = P.dvv; }
+            else { d.dqkv = P.dqkvv; d.ld_qkv = 3 * D; }
             KD_TRY(launch_attn_bwd(&d, s));
         }
-        KD_TRY(launch_qkv_merge(P.dqv, P.dkv, P.dvv, P.dqkvv, 3 * D, nullptr, nullptr, NI, np, c.v_heads, c.v_heads, hd,
-                                hdp, s));
+        if (P.dqv)
+            KD_TRY(launch_qkv_merge(P.dqv, P.dkv, P.dvv, P.dqkvv, 3 * D, nullptr, nullptr, NI, np, c.v_heads, c.v_heads,
+                                    hd, hdp, s));
         KD_TRY(gemm(s, P.splitk_main, NT, D, 3 * D, km(P.dqkvv, 3 * D), mn(m->W(m->vis(i, VQW)), D), P.dhv, D, g0));
         if (gw) {
             lane.begin();

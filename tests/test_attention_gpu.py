@@ -184,3 +184,27 @@ def test_attn_fwd_two_blocks_per_wave_bitexact(B, H, HKV, S, hd, hdp, causal, de
         os.environ.pop("KD_ATTN_FWD_V", None)
     (o0, l0), (o1, l1) = outs
     assert torch.equal(o0, o1) and torch.equal(l0, l1)
+
+
+@pytest.mark.parametrize("B,H,S,hd,hdp", [(2, 2, 729, 72, 96), (1, 16, 729, 72, 96), (1, 3, 100, 64, 64), (2, 4, 200, 128, 128)])
+@pytest.mark.parametrize("bwd_v", ["0", "16"])
+def test_attn_bwd_direct_dqkv_bitexact(B, H, S, hd, hdp, bwd_v, dev):
+    """kd_attn_bwd_desc.dqkv (MHA): dq | dk | dv written straight into the token-major fused q|k|v
+    gradient == kd_attn_bwd + kd_qkv_merge (no RoPE) bit for bit, for both dK/dV kernels; the
+    columns outside [0, 3 H hd) of a wider row are left untouched."""
+    import os
+    ops = _ops()
+    q, k, v = _inputs(B, H, H, S, hd, hdp, dev, seed=5)
+    g = torch.Generator(device=dev).manual_seed(6)
+    o, lse = ops.attn_fwd(q, k, v, hd, False)
+    do = torch.randn(B, S, H, hd, device=dev, generator=g).bfloat16()
+    try:
+        os.environ["KD_ATTN_BWD_V"] = bwd_v
+        dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, hd, False)
+        ref = ops.qkv_merge(dq, dk, dv, B, S, H, H, hd, hdp)
+        wide = torch.full((B * S, 3 * H * hd + 8), 7.0, dtype=torch.bfloat16, device=dev)
+        ops.attn_bwd(q, k, v, o, do, lse, hd, False, dqkv=wide[:, : 3 * H * hd + 8])
+    finally:
+        os.environ.pop("KD_ATTN_BWD_V", None)
+    assert torch.equal(wide[:, : 3 * H * hd], ref)
+    assert torch.all(wide[:, 3 * H * hd:] == 7.0)
