@@ -282,11 +282,14 @@ typedef struct {
     const float* lse; float* delta; float* dq; void* dk; void* dv;
     int32_t B, H, HKV, S, hd, hdp, causal;
     void* workspace; uint64_t workspace_bytes;
-    /* optional (H == HKV): the token-major bf16 [B*S, ld_qkv] gradient of a fused q|k|v projection,
-     * columns [0, H hd) dq | [H hd, 2 H hd) dk | [2 H hd, 3 H hd) dv -- kd_qkv_merge's layout without
-     * RoPE, bit-identical to kd_attn_bwd + kd_qkv_merge -- written directly; dq / dk / dv are then
-     * not written (may be NULL). NULL: the head-major dq / dk / dv above. */
+    /* optional: the token-major bf16 [B*S, ld_qkv] gradient of a fused q|k|v projection, columns
+     * [0, H hd) dq | [H hd, (H + HKV) hd) dk | [(H + HKV) hd, (H + 2 HKV) hd) dv -- kd_qkv_merge's layout,
+     * bit-identical to kd_attn_bwd + kd_qkv_merge -- written directly; dq / dk / dv are then not
+     * written (may be NULL). NULL: the head-major dq / dk / dv above. */
     void* dqkv; int64_t ld_qkv;
+    /* with dqkv and GQA: RoPE tables [S, hd/2] fp32 (kd_qkv_split's); dq and dk are rotated back as
+     * kd_qkv_merge does (hd == hdp, hd % 32 == 0). NULL: no rotation. */
+    const float* cos_t; const float* sin_t;
 } kd_attn_bwd_desc;
 size_t kd_attn_bwd_workspace_size(const kd_attn_bwd_desc* desc);
 int kd_attn_bwd(const kd_attn_bwd_desc* desc, void* stream);

@@ -99,7 +99,7 @@ class KdAttnBwdDesc(C.Structure):
                 ("dv", C.c_void_p),
                 ("B", C.c_int32), ("H", C.c_int32), ("HKV", C.c_int32), ("S", C.c_int32), ("hd", C.c_int32),
                 ("hdp", C.c_int32), ("causal", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64),
-                ("dqkv", C.c_void_p), ("ld_qkv", C.c_int64)]
+                ("dqkv", C.c_void_p), ("ld_qkv", C.c_int64), ("cos_t", C.c_void_p), ("sin_t", C.c_void_p)]
 
 
 class KdModelConfig(C.Structure):

@@ -1176,6 +1176,7 @@ struct AttnBwdP {
     // optional token-major [B*S, (H + 2 HKV) hd] bf16 output (kd_qkv_merge's layout, no RoPE; MHA):
     // dq | dk | dv written there directly instead of dq / dk / dv
     bf16* dqkv; int64_t ld_qkv;
+    const float *rcos, *rsin;   // with dqkv: RoPE tables [S, hd/2] -> dq and dk rotated back (k_qkv_merge's transpose)
 };
 
 // this lane's 4 consecutive columns [dd, dd + 4) of head `head` at token (b, s) in the merged
@@ -1660,6 +1661,53 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv2(AttnBwdP p) {
     }
 }
 
+// The GQA group sum written straight into the fused q|k|v gradient row (kd_attn_bwd_desc.dqkv): one
+// thread per 4-column chunk pair (c, c + hd/2) of a (b, kvh, s) row, dk and dv rounded to bf16 exactly
+// as k_attn_group_sum does, then dk rotated back (RoPE tables; k_qkv_merge's arithmetic on those bf16
+// values) -- bit-identical to k_attn_group_sum + k_qkv_merge.
+__global__ void k_attn_group_sum_qkv(const float* __restrict__ dkp, const float* __restrict__ dvp, bf16* __restrict__ dqkv,
+                                     int64_t ld, const float* __restrict__ rcos, const float* __restrict__ rsin, int B,
+                                     int H, int HKV, int S, int hd, int hdp, float scale) {
+    const int grp = H / HKV, hh = hd / 2, c4 = hh / 4;
+    const int64_t total = (int64_t)B * HKV * S * c4;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(idx % c4) * 4;
+        const int64_t rs = idx / c4;               // (b, kvh, s)
+        const int s = (int)(rs % S);
+        const int64_t bk = rs / S;
+        const int kvh = (int)(bk % HKV), b = (int)(bk / HKV);
+        f32x4 ak1 = (f32x4){0.f, 0.f, 0.f, 0.f}, av1 = ak1, ak2 = ak1, av2 = ak1;
+        for (int j = 0; j < grp; ++j) {
+            const int64_t off = (((int64_t)b * H + kvh * grp + j) * S + s) * hdp + c;
+            ak1 += *(const f32x4*)(dkp + off);
+            av1 += *(const f32x4*)(dvp + off);
+            ak2 += *(const f32x4*)(dkp + off + hh);
+            av2 += *(const f32x4*)(dvp + off + hh);
+        }
+        bf16x4 k1, k2, v1, v2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            k1[r] = (bf16)(ak1[r] * scale); k2[r] = (bf16)(ak2[r] * scale);
+            v1[r] = (bf16)av1[r]; v2[r] = (bf16)av2[r];
+        }
+        if (rcos) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float y1, y2;
+                rope_t((float)k1[r], (float)k2[r], rcos[(int64_t)s * hh + c + r], rsin[(int64_t)s * hh + c + r], y1, y2);
+                k1[r] = (bf16)y1; k2[r] = (bf16)y2;
+            }
+        }
+        bf16* row = dqkv + ((int64_t)b * S + s) * ld;
+        bf16* kr = row + (int64_t)(H + kvh) * hd;
+        bf16* vr = row + (int64_t)(H + HKV + kvh) * hd;
+        *(bf16x4*)(kr + c) = k1;
+        *(bf16x4*)(kr + c + hh) = k2;
+        *(bf16x4*)(vr + c) = v1;
+        *(bf16x4*)(vr + c + hh) = v2;
+    }
+}
+
 // dK[b,kvh] = scale * sum_{h in group} dKp[b,h], dV likewise (d < 16*DT columns)
 __global__ void k_attn_group_sum(const float* __restrict__ dkp, const float* __restrict__ dvp, bf16* __restrict__ dk,
                                  bf16* __restrict__ dv, int B, int H, int HKV, int S, int hdp, int dcols, float scale) {
@@ -1847,11 +1895,28 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     for (int j = 0; j < NQ; ++j)
         if (qok[j]) {
             if (p.dqkv) {   // the merged row: (bf16) of the scaled fp32 value, as kd_qkv_merge rounds it
+                f32x4 v[DT];
 #pragma unroll
-                for (int d = 0; d < DT; ++d) {
-                    const f32x4 v = acc[j][d] * p.scale;
-                    put_qkv4(p, b, myq[j], h, d * 16 + 4 * g, (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]});
+                for (int d = 0; d < DT; ++d) v[d] = acc[j][d] * p.scale;
+                if (p.rcos) {   // RoPE transpose: columns c and c + hd/2 (d-tiles d and d + hd/32) sit in this lane
+                    const int hh = p.hd / 2, dh = hh / 16;
+                    const float* cr = p.rcos + (int64_t)myq[j] * hh;
+                    const float* sr = p.rsin + (int64_t)myq[j] * hh;
+#pragma unroll
+                    for (int d = 0; d < DT; ++d) {
+                        if (d >= dh || d + dh >= DT) continue;
+                        const int i = d * 16 + 4 * g;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float y1, y2;
+                            rope_t(v[d][r], v[d + dh][r], cr[i + r], sr[i + r], y1, y2);
+                            v[d][r] = y1; v[d + dh][r] = y2;
+                        }
+                    }
                 }
+#pragma unroll
+                for (int d = 0; d < DT; ++d)
+                    put_qkv4(p, b, myq[j], h, d * 16 + 4 * g, (bf16x4){(bf16)v[d][0], (bf16)v[d][1], (bf16)v[d][2], (bf16)v[d][3]});
             } else {
                 float* dQr = p.dq + ((int64_t)(b * p.H + h) * p.S + myq[j]) * HDP;
 #pragma unroll
@@ -1965,9 +2030,13 @@ size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d) {
 int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     KD_CHECK_ARG(d && d->q && d->k && d->v && d->o && d->dO && d->lse && d->delta && (d->dqkv || (d->dq && d->dk && d->dv)),
                  "attn_bwd: null pointer");
-    KD_CHECK_ARG(!d->dqkv || (d->H == d->HKV && d->ld_qkv >= (int64_t)3 * d->H * d->hd && d->ld_qkv % 4 == 0 &&
+    KD_CHECK_ARG(!d->dqkv || (d->ld_qkv >= (int64_t)(d->H + 2 * d->HKV) * d->hd && d->ld_qkv % 4 == 0 &&
                               (uintptr_t)d->dqkv % 8 == 0),
-                 "attn_bwd: dqkv needs H == HKV, ld_qkv >= 3 H hd (multiple of 4) and an 8-B aligned base");
+                 "attn_bwd: dqkv needs ld_qkv >= (H + 2 HKV) hd (a multiple of 4) and an 8-B aligned base");
+    KD_CHECK_ARG(!d->cos_t == !d->sin_t && (!d->cos_t || (d->dqkv && d->H != d->HKV && d->hd == d->hdp && d->hd % 32 == 0)),
+                 "attn_bwd: RoPE tables only with dqkv, GQA (H > HKV) and hd == hdp, hd % 32 == 0");
+    KD_CHECK_ARG(!d->dqkv || d->H == d->HKV || (d->hd % 8 == 0),
+                 "attn_bwd: dqkv with GQA needs hd % 8 == 0");
     KD_CHECK_SHAPE(d->B > 0 && d->S > 0 && d->HKV > 0 && d->H % d->HKV == 0 && d->hd % 4 == 0 && d->hd <= d->hdp,
                    "attn_bwd: shape");
     KD_CHECK_SHAPE(d->hdp == 64 || d->hdp == 96 || d->hdp == 128, "attn_bwd: padded head dim must be 64/96/128");
@@ -1988,7 +2057,7 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     float* dvp = need ? dkp + (size_t)d->B * d->H * d->S * d->hdp : nullptr;
     AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, d->lse, d->delta,
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
-               (float)(sc * 1.4426950408889634), (bf16*)d->dqkv, d->ld_qkv};
+               (float)(sc * 1.4426950408889634), (bf16*)d->dqkv, d->ld_qkv, d->cos_t, d->sin_t};
     // dK / dV: two 16-key sub-tiles per wave by default; KD_ATTN_BWD_V=16 selects the one-sub-tile
     // kernel (A/B; read per call)
     const char* bve = std::getenv("KD_ATTN_BWD_V");
@@ -2014,8 +2083,15 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     if (need) {
         const int dcols = 16 * (d->hdp == 64 ? 4 : (d->hdp == 96 ? 5 : 8));
         const int64_t work = (int64_t)d->B * d->HKV * d->S * dcols / 4;
-        hipLaunchKernelGGL(k_attn_group_sum, dim3((unsigned)std::min<int64_t>((work + 255) / 256, 8192)), dim3(256), 0, st,
-                           dkp, dvp, (bf16*)d->dk, (bf16*)d->dv, d->B, d->H, d->HKV, d->S, d->hdp, dcols, (float)sc);
+        if (d->dqkv) {
+            const int64_t work2 = (int64_t)d->B * d->HKV * d->S * (d->hd / 8);
+            hipLaunchKernelGGL(k_attn_group_sum_qkv, dim3((unsigned)std::min<int64_t>((work2 + 255) / 256, 8192)), dim3(256), 0,
+                               st, dkp, dvp, (bf16*)d->dqkv, d->ld_qkv, d->cos_t, d->sin_t, d->B, d->H, d->HKV, d->S, d->hd,
+                               d->hdp, (float)sc);
+        } else {
+            hipLaunchKernelGGL(k_attn_group_sum, dim3((unsigned)std::min<int64_t>((work + 255) / 256, 8192)), dim3(256), 0, st,
+                               dkp, dvp, (bf16*)d->dk, (bf16*)d->dv, d->B, d->H, d->HKV, d->S, d->hdp, dcols, (float)sc);
+        }
         KD_LAUNCH_CHECK("k_attn_group_sum");
     }
     return KD_OK;

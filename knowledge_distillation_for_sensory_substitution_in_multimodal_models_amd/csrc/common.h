@@ -51,6 +51,13 @@ typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 #define KD_SILU_LOG2E 1.4426950408889634f
 __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -KD_SILU_LOG2E)); }
 __device__ __forceinline__ float silu_fast(float x) { return x * sigmoid_fast(x); }
+// transpose of the RoPE rotation of a (first-half, second-half) element pair (HF5 qwen2
+// apply_rotary_pos_emb, backward): k_qkv_merge and the attention backward's fused-gradient
+// epilogues share it, so both produce the same bits
+__device__ __forceinline__ void rope_t(float g1, float g2, float c, float sn, float& y1, float& y2) {
+    y1 = g1 * c + g2 * sn;
+    y2 = g2 * c - g1 * sn;
+}
 // SwiGLU backward of one element: d = dL/dh, h = silu(g) * u -> (dL/dg, dL/du); shared by
 // k_swiglu_bwd and the fused dgrad epilogue (KD_ACT_DSWIGLU), so both agree bit for bit
 __device__ __forceinline__ void swiglu_grad(float d, float g, float u, float& dg, float& du) {

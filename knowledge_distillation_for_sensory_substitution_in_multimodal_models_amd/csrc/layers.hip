@@ -415,7 +415,8 @@ __global__ void k_qkv_merge(const float* __restrict__ dq, const bf16* __restrict
 #pragma unroll
             for (int e = 0; e < VEC; ++e) {
                 const float c = cr[e], sn = sr[e];
-                const float y1 = g1[e] * c + g2[e] * sn, y2 = g2[e] * c - g1[e] * sn;
+                float y1, y2;
+                rope_t(g1[e], g2[e], c, sn, y1, y2);
                 g1[e] = y1; g2[e] = y2;
             }
         }

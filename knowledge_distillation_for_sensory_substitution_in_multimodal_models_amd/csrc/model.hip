@@ -721,9 +721,12 @@ BwdPlan plan_backward(const kd_model* m, int B, int L, int n_tiles, void* base) 
     P.dgu = A.take<bf16>(M * 2 * TI);
     P.dh2 = A.take<bf16>(M * H);
     P.do_ = A.take<bf16>(M * qd);
-    P.dq = A.take<float>(M * qd);
-    P.dk = A.take<bf16>(M * kvd);
-    P.dv = A.take<bf16>(M * kvd);
+    // the attention backward writes the fused q|k|v gradient directly (kd_attn_bwd_desc.dqkv); the
+    // head-major dq / dk / dv + kd_qkv_merge path only with KD_ATTN_DQKV=0 (A/B)
+    const bool merge_ab = [] { const char* e = std::getenv("KD_ATTN_DQKV"); return e && std::atoi(e) == 0; }();
+    P.dq = merge_ab ? A.take<float>(M * qd) : nullptr;
+    P.dk = merge_ab ? A.take<bf16>(M * kvd) : nullptr;
+    P.dv = merge_ab ? A.take<bf16>(M * kvd) : nullptr;
     P.delta = A.take<float>((int64_t)B * c.t_heads * L);
     P.dqkv = A.take<bf16>(M * (qd + 2 * kvd));
     P.dh = A.take<bf16>(M * H);
@@ -807,10 +810,13 @@ int lm_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, const float* cs
         {
             kd_attn_bwd_desc d = lm_attn_desc(m, B, L);
             d.q = b.q; d.k = b.k; d.v = b.v; d.o = b.o; d.dO = P.do_; d.lse = b.lse; d.delta = P.delta;
-            d.dq = P.dq; d.dk = P.dk; d.dv = P.dv; d.workspace = P.attn_ws; d.workspace_bytes = P.attn_ws_bytes;
+            d.workspace = P.attn_ws; d.workspace_bytes = P.attn_ws_bytes;
+            if (P.dq) { d.dq = P.dq; d.dk = P.dk; d.dv = P.dv; }
+            else { d.dqkv = P.dqkv; d.ld_qkv = qd + 2 * kvd; d.cos_t = cs; d.sin_t = sn; }   // RoPE rotated back in-kernel
             KD_TRY(launch_attn_bwd(&d, s));
         }
-        KD_TRY(launch_qkv_merge(P.dq, P.dk, P.dv, P.dqkv, qd + 2 * kvd, cs, sn, B, L, c.t_heads, c.t_kv_heads, hd, hd, s));
+        if (P.dq)
+            KD_TRY(launch_qkv_merge(P.dq, P.dk, P.dv, P.dqkv, qd + 2 * kvd, cs, sn, B, L, c.t_heads, c.t_kv_heads, hd, hd, s));
         KD_TRY(gemm(s, P.splitk_main, M, H, qd + 2 * kvd, km(P.dqkv, qd + 2 * kvd), mn(m->W(m->lm(i, LQW)), H), P.dh, H,
                     g0));
         if (gw) {

@@ -405,10 +405,11 @@ def attn_fwd(q, k, v, hd: int, causal: bool, want_lse: bool = True):
     return o, lse
 
 
-def attn_bwd(q, k, v, o, do, lse, hd: int, causal: bool, dqkv=None):
-    """Returns (dq fp32 [B,H,S,hdp] scaled, dk, dv bf16 [B,HKV,S,hdp]); with `dqkv` (MHA only: a
-    token-major bf16 [B*S, >= 3*H*hd] tensor) the three land there directly in qkv_merge's layout
-    (no RoPE) and that tensor is returned instead."""
+def attn_bwd(q, k, v, o, do, lse, hd: int, causal: bool, dqkv=None, cos=None, sin=None):
+    """Returns (dq fp32 [B,H,S,hdp] scaled, dk, dv bf16 [B,HKV,S,hdp]); with `dqkv` (a token-major
+    bf16 [B*S, >= (H+2*HKV)*hd] tensor) the three land there directly in qkv_merge's layout (dq and
+    dk rotated back with the RoPE tables cos / sin [S, hd/2] when given: GQA, hd == hdp) and that
+    tensor is returned instead."""
     B, H, S, hdp = q.shape
     HKV = k.shape[1]
     dev = q.device
@@ -416,8 +417,8 @@ def attn_bwd(q, k, v, o, do, lse, hd: int, causal: bool, dqkv=None):
     delta = _workspace("attn_delta", B * H * S * 4, dev)
     if dqkv is not None:
         _require(dqkv, torch.bfloat16, "attn_bwd.dqkv")
-        if dqkv.dim() != 2 or dqkv.stride(1) != 1 or dqkv.shape[0] != B * S or dqkv.shape[1] < 3 * H * hd:
-            raise RuntimeError("attn_bwd.dqkv: expected a row-major [B*S, >= 3*H*hd] view")
+        if dqkv.dim() != 2 or dqkv.stride(1) != 1 or dqkv.shape[0] != B * S or dqkv.shape[1] < (H + 2 * HKV) * hd:
+            raise RuntimeError("attn_bwd.dqkv: expected a row-major [B*S, >= (H+2*HKV)*hd] view")
         dq = dk = dv = None
     else:
         dq = torch.empty((B, H, S, hdp), dtype=torch.float32, device=dev)
@@ -425,7 +426,7 @@ def attn_bwd(q, k, v, o, do, lse, hd: int, causal: bool, dqkv=None):
         dv = torch.empty_like(v)
     d = NV.KdAttnBwdDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(),
                          delta.data_ptr(), _ptr(dq), _ptr(dk), _ptr(dv), B, H, HKV, S, hd, hdp,
-                         int(causal), None, 0, _ptr(dqkv), 0 if dqkv is None else dqkv.stride(0))
+                         int(causal), None, 0, _ptr(dqkv), 0 if dqkv is None else dqkv.stride(0), _ptr(cos), _ptr(sin))
     need = NV.lib().kd_attn_bwd_workspace_size(C.byref(d))
     if need:
         ws = _workspace("attn_bwd_partials", need, dev)

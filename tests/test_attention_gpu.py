@@ -208,3 +208,24 @@ def test_attn_bwd_direct_dqkv_bitexact(B, H, S, hd, hdp, bwd_v, dev):
         os.environ.pop("KD_ATTN_BWD_V", None)
     assert torch.equal(wide[:, : 3 * H * hd], ref)
     assert torch.all(wide[:, 3 * H * hd:] == 7.0)
+
+
+@pytest.mark.parametrize("B,H,HKV,S,hd", [(2, 14, 2, 200, 64), (1, 14, 2, 1536, 64), (1, 4, 1, 130, 128), (2, 4, 2, 97, 64)])
+@pytest.mark.parametrize("rope", [True, False])
+def test_attn_bwd_direct_dqkv_gqa_bitexact(B, H, HKV, S, hd, rope, dev):
+    """GQA: the dK/dV group sum and dQ written straight into the fused q|k|v gradient, dq and dk
+    rotated back with the RoPE tables in-kernel == kd_attn_bwd + kd_qkv_merge(cos, sin) bit for bit."""
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hd, dev, seed=7)
+    g = torch.Generator(device=dev).manual_seed(8)
+    o, lse = ops.attn_fwd(q, k, v, hd, True)
+    do = torch.randn(B, S, H, hd, device=dev, generator=g).bfloat16()
+    cos = sin = None
+    if rope:
+        ang = torch.rand(S, hd // 2, device=dev, generator=g) * 6.0
+        cos, sin = torch.cos(ang).contiguous(), torch.sin(ang).contiguous()
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, hd, True)
+    ref = ops.qkv_merge(dq, dk, dv, B, S, H, HKV, hd, hd, cos=cos, sin=sin)
+    out = torch.full_like(ref, 3.0)
+    ops.attn_bwd(q, k, v, o, do, lse, hd, True, dqkv=out, cos=cos, sin=sin)
+    assert torch.equal(out, ref)
