@@ -53,10 +53,11 @@ __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn
 __device__ __forceinline__ float silu_fast(float x) { return x * sigmoid_fast(x); }
 // transpose of the RoPE rotation of a (first-half, second-half) element pair (HF5 qwen2
 // apply_rotary_pos_emb, backward): k_qkv_merge and the attention backward's fused-gradient
-// epilogues share it, so both produce the same bits
+// epilogues share it, so both produce the same bits -- the fused multiply-adds written out: left to
+// -ffp-contract the two call sites contracted differently (1 ulp apart on 5 of 358 k elements)
 __device__ __forceinline__ void rope_t(float g1, float g2, float c, float sn, float& y1, float& y2) {
-    y1 = g1 * c + g2 * sn;
-    y2 = g2 * c - g1 * sn;
+    y1 = __builtin_fmaf(g1, c, g2 * sn);
+    y2 = __builtin_fmaf(g2, c, -(g1 * sn));
 }
 // SwiGLU backward of one element: d = dL/dh, h = silu(g) * u -> (dL/dg, dL/du); shared by
 // k_swiglu_bwd and the fused dgrad epilogue (KD_ACT_DSWIGLU), so both agree bit for bit
