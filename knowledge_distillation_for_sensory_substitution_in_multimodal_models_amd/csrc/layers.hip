@@ -206,12 +206,13 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const XT* __restrict__ x, int64
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nch = D / 8;
     float pw[IT][8], pb[IT][8], wr[IT][8];
+    // the weight chunks: unconditional loads (chunk index clamped; a chunk past the row is never
+    // used), all in flight at once -- a load under the lane-dependent test waited for itself
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-        const int c = lane + it * 64;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { pw[it][j] = 0.f; pb[it][j] = 0.f; wr[it][j] = 0.f; }
-        if (c < nch) load8(w + c * 8, wr[it]);
+        for (int j = 0; j < 8; ++j) { pw[it][j] = 0.f; pb[it][j] = 0.f; }
+        load8(w + min(lane + it * 64, nch - 1) * 8, wr[it]);
     }
     const int r_begin = blockIdx.x * rows_per_block;
     const int r_end = min(R, r_begin + rows_per_block);
