@@ -1928,6 +1928,28 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 // delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]: one thread per (b, q, h) row, 16-B loads
 // (hd % 8 == 0; every row load of both tensors in flight at once). One wave per row with
 // a 2-B load per lane spent 38 us per call on 11 MB.
+// k_attn_delta with the row's NC = hd / 8 chunk pairs all loaded before the sum (the generic loop
+// waited for each pair in turn: 8-9 serial memory round trips per row); the same products summed in
+// the same order, so delta is bit-identical
+template <int NC>
+__global__ void k_attn_delta_n(const bf16* __restrict__ O, const bf16* __restrict__ dO, float* __restrict__ delta, int B,
+                               int H, int S) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= B * S * H) return;
+    const int h = row % H, bq = row / H, q = bq % S, b = bq / S;
+    const bf16* o = O + (int64_t)row * (NC * 8);
+    const bf16* d = dO + (int64_t)row * (NC * 8);
+    bf16x8 a[NC], g[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { a[c] = *(const bf16x8*)(o + 8 * c); g[c] = *(const bf16x8*)(d + 8 * c); }
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += (float)a[c][e] * (float)g[c][e];
+    delta[((int64_t)b * H + h) * S + q] = acc;
+}
+
 __global__ void k_attn_delta(const bf16* __restrict__ O, const bf16* __restrict__ dO, float* __restrict__ delta,
                              int B, int H, int S, int hd) {
     const int row = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2048,8 +2070,15 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     hipStream_t st = as_stream(stream_);
     {
         const int rows = d->B * d->S * d->H;
-        hipLaunchKernelGGL(k_attn_delta, dim3((rows + 255) / 256), dim3(256), 0, st, (const bf16*)d->o,
-                           (const bf16*)d->dO, d->delta, d->B, d->H, d->S, d->hd);
+        // KD_ATTN_DELTA_V=1 (read per call): the generic loop, for A/B
+        const char* dve = std::getenv("KD_ATTN_DELTA_V");
+        const int nc = (dve && std::atoi(dve) == 1) ? 0 : d->hd / 8;
+        const dim3 g((rows + 255) / 256);
+        if (nc == 8) hipLaunchKernelGGL(k_attn_delta_n<8>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
+        else if (nc == 9) hipLaunchKernelGGL(k_attn_delta_n<9>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
+        else if (nc == 16) hipLaunchKernelGGL(k_attn_delta_n<16>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
+        else hipLaunchKernelGGL(k_attn_delta, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H,
+                                d->S, d->hd);
         KD_LAUNCH_CHECK("k_attn_delta");
     }
     const double sc = 1.0 / std::sqrt((double)d->hd);
