@@ -1929,8 +1929,9 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 // (hd % 8 == 0; every row load of both tensors in flight at once). One wave per row with
 // a 2-B load per lane spent 38 us per call on 11 MB.
 // k_attn_delta with the row's NC = hd / 8 chunk pairs all loaded before the sum (the generic loop
-// waited for each pair in turn: 8-9 serial memory round trips per row); the same products summed in
-// the same order, so delta is bit-identical
+// waited for each pair in turn: 8-9 serial memory round trips per row); the same fma chain in the
+// same order, so delta is bit-identical (the fmas are written out: left to the compiler, the two
+// kernels' sums were contracted / paired differently)
 template <int NC>
 __global__ void k_attn_delta_n(const bf16* __restrict__ O, const bf16* __restrict__ dO, float* __restrict__ delta, int B,
                                int H, int S) {
@@ -1946,7 +1947,7 @@ __global__ void k_attn_delta_n(const bf16* __restrict__ O, const bf16* __restric
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc += (float)a[c][e] * (float)g[c][e];
+        for (int e = 0; e < 8; ++e) acc = __builtin_fmaf((float)a[c][e], (float)g[c][e], acc);
     delta[((int64_t)b * H + h) * S + q] = acc;
 }
 
@@ -1961,7 +1962,7 @@ __global__ void k_attn_delta(const bf16* __restrict__ O, const bf16* __restrict_
     for (int c = 0; c < hd; c += 8) {
         const bf16x8 a = *(const bf16x8*)(o + c), g = *(const bf16x8*)(d + c);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc += (float)a[e] * (float)g[e];
+        for (int e = 0; e < 8; ++e) acc = __builtin_fmaf((float)a[e], (float)g[e], acc);   // one fma chain in both kernels
     }
     delta[((int64_t)b * H + h) * S + q] = acc;
 }
