@@ -66,10 +66,10 @@ def step_tflops_per_sample(kind: str, phase: int) -> float:
     return (teacher + s_fwd + s_bwd) / 1e12
 
 
-def build(cfg, dev, teacher_fp8=False, grad_comm_dtype=None):
+def build(cfg, dev, teacher_fp8=False, grad_comm_dtype=None, teacher_residual_f32=False):
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
     S, T = "llava-hf/llava-onevision-qwen2-0.5b-ov-hf", "llava-hf/llava-onevision-qwen2-7b-ov-hf"
-    kw = dict(teacher_fp8=teacher_fp8, grad_comm_dtype=grad_comm_dtype)
+    kw = dict(teacher_fp8=teacher_fp8, grad_comm_dtype=grad_comm_dtype, teacher_residual_f32=teacher_residual_f32)
     if cfg["kind"] == "lb":
         m = K.LogitBasedKD(S, T, **kw)
     elif cfg["kind"] == "fb":
@@ -281,16 +281,43 @@ def _free_port() -> int:
         return so.getsockname()[1]
 
 
+def visible_gpu_count(kfd_root: str = "/sys/class/kfd/kfd/topology/nodes") -> int | None:
+    """GPUs this process may use, counted WITHOUT starting the HIP runtime: the KFD topology's
+    GPU nodes (gfx_target_version != 0; CPU nodes report 0), capped by HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set.  None when the topology is not
+    readable (then each rank checks its own device)."""
+    n = None
+    try:
+        n = 0
+        for node in sorted(os.listdir(kfd_root)):
+            try:
+                props = open(os.path.join(kfd_root, node, "properties")).read().split("\n")
+            except OSError:
+                continue
+            for line in props:
+                k, _, v = line.partition(" ")
+                if k == "gfx_target_version" and v.strip() not in ("", "0"):
+                    n += 1
+                    break
+    except OSError:
+        n = None
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            k = len([x for x in v.split(",") if x.strip() != ""])
+            n = k if n is None else min(n, k)
+    return n
+
+
 def launch_ranks(n: int, argv: list[str], dry: bool) -> int:
     """`bench.py --gpus N` without a launcher: run N ranks (one process per GPU) under
     torch.distributed.run as a CHILD process and return its exit code.  Nothing here touches
-    the GPU (torch.cuda.device_count() does not initialise it), so no process that holds a
-    GPU context is ever replaced."""
+    the GPU: the devices are counted from the KFD topology in sysfs (visible_gpu_count), not
+    through torch.cuda / HIP, so the parent never holds a GPU context and none is ever replaced."""
     import subprocess
     if not dry:
-        import torch
-        have = torch.cuda.device_count()
-        if have < n:
+        have = visible_gpu_count()
+        if have is not None and have < n:
             print(json.dumps({"error": f"--gpus {n} but only {have} GPU(s) visible", "n_gpus": n}), flush=True)
             return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -342,7 +369,7 @@ def allreduce_cost(m, dist, dev, world):
     """The DP exchange of one optimizer step: the buckets GradSync launched in the last
     reducing backward (count, bytes, dtype), and the same all-reduces timed alone on a
     scratch buffer (serialized, after the timed region; in the step they overlap the rest
-    of the backward and the next teacher forward)."""
+    of the backward and the next teacher forward).  `dev` may be the CPU (gloo tests)."""
     import torch
     gs = m._gsync
     if gs is None or not gs.last_buckets:
@@ -350,16 +377,19 @@ def allreduce_cost(m, dist, dev, world):
     dt_ = gs.comm_dtype or torch.float32
     n = sum(gs.last_buckets)
     buf = torch.zeros(n, dtype=dt_, device=dev)
-    op = dist.ReduceOp.AVG
+    gpu = torch.device(dev).type == "cuda"
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
+    # gloo has no AVG: SUM (same bytes on the wire; the value is scratch)
+    op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else dist.ReduceOp.SUM
     for _ in range(2):   # the first round warms the communicator's channels
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
         t0 = time.perf_counter()
         off = 0
         for c in gs.last_buckets:
             dist.all_reduce(buf[off:off + c], op=op)
             off += c
-        torch.cuda.synchronize()
+        sync()
         ms = (time.perf_counter() - t0) * 1e3
     t = torch.tensor([ms], device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -394,6 +424,8 @@ def main():
                     help="one stream: student forward and the weight gradients on the main stream (profiling)")
     ap.add_argument("--shapes", default=None, help="write the per-shape GEMM timing table (JSON) to this path")
     ap.add_argument("--teacher-bf16", action="store_true", help="c4 with the bf16 teacher instead of fp8")
+    ap.add_argument("--teacher-residual-f32", action="store_true",
+                    help="the teacher's Qwen2 residual stream in fp32 (default bf16; DESIGN §4)")
     ap.add_argument("--fp8-families", default=None,
                     help="c4: which teacher linear families run fp8 (modeling.FP8_FAMILIES: all, lm, lm_body, lm_mlp)")
     ap.add_argument("--no-teacher-rate", action="store_true",
@@ -427,7 +459,8 @@ def main():
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
     teacher_fp8 = False if a.teacher_bf16 else (a.fp8_families or cfg.get("teacher_fp8") or False)
     comm_dtype = torch.bfloat16 if a.grad_comm_dtype == "bf16" else None
-    m, opt = build(cfg, dev, teacher_fp8=teacher_fp8, grad_comm_dtype=comm_dtype)
+    m, opt = build(cfg, dev, teacher_fp8=teacher_fp8, grad_comm_dtype=comm_dtype,
+                   teacher_residual_f32=a.teacher_residual_f32)
     m.concurrent_student = not a.serial
     m.student_model.wlane.serial = a.serial   # --serial: one stream for everything (profiling)
     # two synthetic batches, alternated, so every step's teacher forward is a fresh one
@@ -564,7 +597,8 @@ def main():
         "data": "synthetic (random 336x336 pixels, random token ids; random-init weights of the real architectures)",
         "config": {"workload": f"{a.config}: {cfg['desc']}", "model": "llava-onevision-qwen2-7b (teacher) -> 0.5b (student)",
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": 1536, "image": "336x336 (2 tiles, 1485 tokens)",
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "teacher_lm_stream": "fp32" if a.teacher_residual_f32 else "bf16"},
         "mfu": round(value * tf_sample / world / PEAK_BF16_TFLOPS, 4),
         "per_rank_ms_per_step": [round(v / a.steps * 1e3, 2) for v in per_rank],
         "grad_allreduce": comm,

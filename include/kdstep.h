@@ -19,6 +19,13 @@
  *    stream-ordered: no hidden device synchronisation.
  *  - bf16 tensors are raw 16-bit storage (uint16_t / __bf16); fp32 is float.
  *  - Leading dimensions (ld*) are in ELEMENTS.
+ *  - Descriptor structs (kd_gemm_desc, kd_attn_desc, kd_attn_bwd_desc, kd_loss_params, ...) grow
+ *    by appending fields; every release that appends one bumps KD_ABI_VERSION.  Callers MUST
+ *    zero-initialise a descriptor (`kd_gemm_desc d = {0};` / memset) before filling it, so a
+ *    field they do not know is 0 = "off", and should check kd_abi_version() == KD_ABI_VERSION
+ *    at load time (the Python binding refuses a mismatched library).
+ *    ABI 6 -> 7: kd_gemm diagnostic variants (17-20, 22, 23, 25-28) are no longer accepted by
+ *    the product library (A/B builds only); kd_loss err bit 4 is no longer set.
  */
 #ifndef KDSTEP_H
 #define KDSTEP_H
@@ -47,7 +54,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 6
+#define KD_ABI_VERSION 7
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -84,9 +91,7 @@ typedef struct {
     int32_t* err_out;       /* optional device int32[4], caller-zeroed, never reset here:
                                [0] |= 1 LoCa gather label outside [0, V_s) (DT:166),
                                       2 CE target outside {-100} u [0, V_s),
-                                      4 the LoCa kernel's row-slice hand-off timed out
-                                        (its workgroups were not resident together; the
-                                        loss / dlogits of this call are invalid);
+                                      (4: reserved; unused since ABI 7);
                                [1] first offending label, [2] its row + row_base,
                                [3] claim flag                                          */
     int32_t row_base;       /* added to the row reported in err_out[2]                   */
@@ -124,8 +129,7 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t,
                     float* loss_out, void* dlogits, int64_t ld_d,
                     void* workspace, size_t workspace_bytes, void* stream);
 /* Synchronises `stream` and reports a device-side error recorded in `workspace` by the
- * last kd_loss_fwd_bwd (KD_ERR_LABEL_RANGE; KD_ERR_LAUNCH for a timed-out row-slice
- * hand-off of the register-resident LoCa kernel), else KD_OK. */
+ * last kd_loss_fwd_bwd (KD_ERR_LABEL_RANGE), else KD_OK. */
 int kd_loss_check(const void* workspace, void* stream);
 
 /* ------------------------------------------------------------------ GEMM ---- */
@@ -356,6 +360,9 @@ int kd_adamw(float* param, void* param_bf16, const float* grad, float* exp_avg, 
 /* out[i] = a[i] * b[i], i < n (device scalars: e.g. the upstream gradient times the
  * dlogits scale of kd_loss_params.dscale, for kd_gemm's alpha_dev). */
 int kd_scalar_mul(const float* a, const float* b, float* out, int n, void* stream);
+/* y[i] = x[i] * (*s_dev), i < n (s_dev NULL: a copy; y may alias x): e.g. the NT-Xent feature gradient
+ * times the upstream gradient, the hook gradient kd_model_backward takes. */
+int kd_scale_f32(const float* x, const float* s_dev, float* y, int64_t n, void* stream);
 /* out[0] += sum x^2 (gradient norm). */
 int kd_sumsq(const float* x, int64_t n, float* out, void* stream);
 /* bytes zero bytes at ptr, stream-ordered (optimizer.zero_grad() on the flat gradient:
@@ -542,7 +549,10 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
                      void* const* kv_k, void* const* kv_v, int32_t* err, void* stream);
 
 /* Backward of a save = 1 forward (fwd_workspace) from dhn (bf16 [B*L, t_hidden], grad of
- * hn) and dpost (optional bf16 grad of post_ln) into the grad buffer (+=).  Weight
+ * hn) and dpost (optional, fp32 [n_tiles, v_hidden]: the gradient w.r.t. each tile's MEAN post_ln
+ * feature, the hook's pooling DT:243-244; spread as dpost / np over the tile's np rows in fp32,
+ * never rounded to bf16 -- since ABI 7, was a bf16 [n_tiles*np, v_hidden] row gradient) into the
+ * grad buffer (+=).  Weight
  * gradients run on wgrad_stream beside the dgrad chain on `stream`; `stream` waits for
  * all of it before returning.  Work already queued on wgrad_stream (e.g. the caller's
  * lm_head wgrad into a tied embedding) is ordered before the embedding backward.

@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("KDSTEP_LIB", _PKG / "libkdstep.so"))
 HEADER = _PKG.parent / "include" / "kdstep.h"
 
 KD_OK = 0
-ABI_VERSION = 6
+ABI_VERSION = 7
 STATUS_NAMES = {
     0: "KD_OK", 1: "KD_ERR_SHAPE", 2: "KD_ERR_DTYPE", 3: "KD_ERR_ALIGN", 4: "KD_ERR_ARCH",
     5: "KD_ERR_LABEL_RANGE", 6: "KD_ERR_LAUNCH", 7: "KD_ERR_ARG", 8: "KD_ERR_WORKSPACE",
@@ -159,6 +159,7 @@ SIGNATURES = {
     "kd_ntxent": (_i32, [_vp, _vp, _i32, _i32, _f32, _f32, _vp, _vp, _f32, _vp]),
     "kd_adamw": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp, _i32, _vp]),
     "kd_scalar_mul": (_i32, [_vp, _vp, _vp, _i32, _vp]),
+    "kd_scale_f32": (_i32, [_vp, _vp, _vp, C.c_int64, _vp]),
     "kd_sumsq": (_i32, [_vp, _i64, _vp, _vp]),
     "kd_zero": (_i32, [_vp, C.c_uint64, _vp]),
     "kd_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),

@@ -110,6 +110,9 @@ int kd_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t n, 
     return kd::launch_adamw(p, pb, g, m, v, n, lr, b1, b2, eps, wd, step, gscale, skip, n_skip, s);
 }
 int kd_sumsq(const float* x, int64_t n, float* out, void* s) { return kd::launch_sumsq(x, n, out, s); }
+int kd_scale_f32(const float* x, const float* s_dev, float* y, int64_t n, void* s) {
+    return kd::launch_scale_f32(x, s_dev, y, n, s);
+}
 int kd_scalar_mul(const float* a, const float* b, float* out, int n, void* s) {
     return kd::launch_scalar_mul(a, b, out, n, s);
 }

@@ -113,6 +113,7 @@ __device__ __forceinline__ bf16x4 tr_read_off(uint32_t addr) {
     return __builtin_bit_cast(bf16x4, v);
 }
 
+#ifdef KD_AB_BUILD   // the round-2 16x16x32 forward (forced variant 16): the tools' A/B library only
 // NQ query sub-tiles of 16 rows per wave (workgroup = 4 waves x 16·NQ rows): every K
 // fragment (b128) and V^T fragment (tr_b16) read from LDS feeds NQ MFMAs, so LDS bytes
 // per FLOP drop by NQ (at NQ = 1 the kernel was bound by its LDS reads: one 64-key tile =
@@ -322,6 +323,8 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
         }
     }
 }
+
+#endif  // KD_AB_BUILD
 
 // ------------------------------------------------------- forward, 32x32x16 MFMAs ----
 // The 16x16x32 kernel above is bound by VECTOR ISSUE, not by the matrix pipe: a 16x16x32
@@ -678,6 +681,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 3) k_attn_fwd32(AttnP p
     }
 }
 
+#ifdef KD_AB_BUILD   // k_attn_fwd64 / k_attn_fwd32p: measured slower; A/B library only
 // k_attn_fwd64: k_attn_fwd32's arithmetic with TWO 32-row query blocks per wave (workgroup = 4 waves
 // x 64 rows = 256 query rows), one wave per SIMD (up to 512 registers: O of both blocks, 2 x ND x 16,
 // beside their scores). Every K fragment (ds_read_b128) and every V^T fragment (ds_read_b64_tr_b16)
@@ -1162,6 +1166,8 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32p(AttnP p) {
         if (hf == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq] = (m + log2f(l)) * 0.6931471805599453f;
     }
 }
+
+#endif  // KD_AB_BUILD
 
 // ------------------------------------------------------------------ backward ----
 struct AttnBwdP {
@@ -1969,6 +1975,7 @@ __global__ void k_attn_delta(const bf16* __restrict__ O, const bf16* __restrict_
 
 }  // namespace
 
+#ifdef KD_AB_BUILD
 // the six-wave forward by default: not yet (A/B with forced variant 36 first); head dim 128
 // needs more than the 168 VGPRs of three waves per SIMD (it spilled), so it keeps four waves
 static bool fwd_nw6(const kd_attn_desc* d) {
@@ -1985,6 +1992,8 @@ void launch_fwd_nw6(dim3 grid, size_t smem, hipStream_t st, const AttnP& p) {
     }
 }
 
+#endif  // KD_AB_BUILD
+
 int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     KD_CHECK_ARG(d && d->q && d->k && d->v && d->o, "attn_fwd: null pointer");
     KD_CHECK_SHAPE(d->B > 0 && d->S > 0 && d->H > 0 && d->HKV > 0 && d->H % d->HKV == 0, "attn_fwd: heads");
@@ -1993,25 +2002,21 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
     KD_CHECK_SHAPE(!(d->hdp == 96 && d->hd > 80) && !(d->hdp == 64 && d->hd > 64), "attn_fwd: hd exceeds tile cover");
     AttnP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (bf16*)d->o, d->lse,
             d->B, d->H, d->HKV, d->S, d->hd, (float)(1.4426950408889634 / std::sqrt((double)d->hd))};
-    // NQ query sub-tiles per wave (KD_ATTN_FWD_NQ=1 restores one, for A/B)
-    static const int nq = [] { const char* e = std::getenv("KD_ATTN_FWD_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
-    // KD_ATTN_FWD_V (A/B and diagnostics): unset / 32 = k_attn_fwd32 (LDS-DMA staging), 64 = k_attn_fwd64
-    // (two query blocks per wave), 35 = its
-    // register-staged build, 33 = the sub-tile-pipelined k_attn_fwd32p, 34 = the stamp build,
-    // 16 = the 16x16x32 k_attn_fwd
-    // (read per call, so a test can switch variants inside one process)
-    const char* fve = std::getenv("KD_ATTN_FWD_V");
-    const int fv = fve ? std::atoi(fve) : 0;
-    const bool v16 = fv == 16;
-    // six-wave workgroups (192 query rows) where they fill the GPU in fewer rounds: forced variant 36,
-    // or (unforced) the shapes measured faster (fwd_nw6 below)
-    const bool nw6 = fv == 36 || (fv == 0 && fwd_nw6(d));
-    const bool w64 = fv == 64;   // two query blocks per wave (k_attn_fwd64), 256 rows per workgroup
-    dim3 grid(d->H, d->B, v16 ? (d->S + 64 * nq - 1) / (64 * nq)
-                              : (w64 ? (d->S + 255) / 256 : (d->S + (nw6 ? 191 : 127)) / (nw6 ? 192 : 128)));
     hipStream_t st = as_stream(stream_);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem = 2 * 2 * 64 * rb;
+#ifdef KD_AB_BUILD
+    // KD_ATTN_FWD_V (A/B and diagnostics; read per call, so a test can switch variants inside one
+    // process): unset / 32 = k_attn_fwd32 (LDS-DMA staging, the product kernel), 64 = k_attn_fwd64
+    // (two query blocks per wave), 35 = its register-staged build, 33 = the sub-tile-pipelined
+    // k_attn_fwd32p, 34 = the stamp build, 36 = six-wave workgroups, 16 = the 16x16x32 k_attn_fwd
+    // (KD_ATTN_FWD_NQ=1: one query sub-tile per wave)
+    static const int nq = [] { const char* e = std::getenv("KD_ATTN_FWD_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
+    const char* fve = std::getenv("KD_ATTN_FWD_V");
+    const int fv = fve ? std::atoi(fve) : 0;
+    const bool v16 = fv == 16, nw6 = fv == 36, w64 = fv == 64;
+    dim3 grid(d->H, d->B, v16 ? (d->S + 64 * nq - 1) / (64 * nq)
+                              : (w64 ? (d->S + 255) / 256 : (d->S + (nw6 ? 191 : 127)) / (nw6 ? 192 : 128)));
 #define LAUNCH(HD, C)                                                                                \
     do {                                                                                             \
         if (nw6) launch_fwd_nw6<HD, C>(grid, smem, st, p);                                           \
@@ -2023,6 +2028,10 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
         else if (nq == 2) hipLaunchKernelGGL((k_attn_fwd<HD, C, 2>), grid, dim3(256), smem, st, p);  \
         else hipLaunchKernelGGL((k_attn_fwd<HD, C, 1>), grid, dim3(256), smem, st, p);               \
     } while (0)
+#else
+    const dim3 grid(d->H, d->B, (d->S + 127) / 128);
+#define LAUNCH(HD, C) hipLaunchKernelGGL((k_attn_fwd32<HD, C, false>), grid, dim3(256), smem, st, p)
+#endif
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }
     else if (d->hdp == 96) { if (d->causal) LAUNCH(96, true); else LAUNCH(96, false); }
     else { if (d->causal) LAUNCH(128, true); else LAUNCH(128, false); }
@@ -2035,13 +2044,26 @@ int launch_attn_fwd(const kd_attn_desc* d, void* stream_) {
 // accumulator tiles do not fit beside the fragments: the one-sub-tile kernel there; the 7B
 // teacher never runs a backward)
 template <int HD, bool C>
+void launch_dq1(dim3 grid, size_t smem, hipStream_t st, const AttnBwdP& p) {
+#ifdef KD_AB_BUILD
+    hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 1>), grid, dim3(256), smem, st, p);
+#else
+    (void)grid; (void)smem; (void)st; (void)p;
+#endif
+}
+
+template <int HD, bool C>
 void launch_dkdv(bool kv16, dim3 grid, size_t smem, hipStream_t st, const AttnBwdP& p) {
     if constexpr (HD == 128) {
         grid.z = (p.S + 63) / 64;
         hipLaunchKernelGGL((k_attn_bwd_dkdv<HD, C>), grid, dim3(256), smem, st, p);
     } else {
+#ifdef KD_AB_BUILD
         if (kv16) hipLaunchKernelGGL((k_attn_bwd_dkdv<HD, C>), grid, dim3(256), smem, st, p);
-        else hipLaunchKernelGGL((k_attn_bwd_dkdv2<HD, C>), grid, dim3(256), smem, st, p);
+        else
+#endif
+        hipLaunchKernelGGL((k_attn_bwd_dkdv2<HD, C>), grid, dim3(256), smem, st, p);
+        (void)kv16;
     }
 }
 
@@ -2071,9 +2093,13 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     hipStream_t st = as_stream(stream_);
     {
         const int rows = d->B * d->S * d->H;
+#ifdef KD_AB_BUILD
         // KD_ATTN_DELTA_V=1 (read per call): the generic loop, for A/B
         const char* dve = std::getenv("KD_ATTN_DELTA_V");
         const int nc = (dve && std::atoi(dve) == 1) ? 0 : d->hd / 8;
+#else
+        const int nc = d->hd / 8;
+#endif
         const dim3 g((rows + 255) / 256);
         if (nc == 8) hipLaunchKernelGGL(k_attn_delta_n<8>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
         else if (nc == 9) hipLaunchKernelGGL(k_attn_delta_n<9>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
@@ -2088,12 +2114,17 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, d->lse, d->delta,
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
                (float)(sc * 1.4426950408889634), (bf16*)d->dqkv, d->ld_qkv, d->cos_t, d->sin_t};
+#ifdef KD_AB_BUILD
     // dK / dV: two 16-key sub-tiles per wave by default; KD_ATTN_BWD_V=16 selects the one-sub-tile
-    // kernel (A/B; read per call)
+    // kernel, KD_ATTN_DQ_NQ=1 one query sub-tile per dQ wave (A/B; read per call)
     const char* bve = std::getenv("KD_ATTN_BWD_V");
     const bool kv16 = bve && std::atoi(bve) == 16;
-    dim3 grid(d->H, d->B, kv16 ? (d->S + 63) / 64 : (d->S + 127) / 128);
     static const int nq_dq = [] { const char* e = std::getenv("KD_ATTN_DQ_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
+#else
+    constexpr bool kv16 = false;
+    constexpr int nq_dq = 2;
+#endif
+    dim3 grid(d->H, d->B, kv16 ? (d->S + 63) / 64 : (d->S + 127) / 128);
     dim3 grid_q(d->H, d->B, (d->S + 64 * nq_dq - 1) / (64 * nq_dq));
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem_kv = 2 * (2 * 64 * rb + 512);
@@ -2103,7 +2134,7 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
         launch_dkdv<HD, C>(kv16, grid, smem_kv, st, p);                                     \
         KD_LAUNCH_CHECK("k_attn_bwd_dkdv");                                                   \
         if (nq_dq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p); \
-        else hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 1>), grid_q, dim3(256), smem_q, st, p);            \
+        else launch_dq1<HD, C>(grid_q, smem_q, st, p);                                                   \
         KD_LAUNCH_CHECK("k_attn_bwd_dq");                                                     \
     } while (0)
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }

@@ -4,6 +4,12 @@ Each .hip translation unit is compiled to an object in parallel (objects are
 cached by source mtime + header mtimes), then linked into one shared library that
 exports exactly the extern "C" symbols of include/kdstep.h.  No torch headers are
 involved: the library is a plain C-ABI .so loaded with ctypes.
+
+    python csrc/build.py          the product library (package dir)
+    python csrc/build.py --ab     tools/ab/libkdstep_ab.so: the same sources with -DKD_AB_BUILD, i.e.
+                                  also the negative-result / diagnostic kernels and the A/B switches
+                                  (v9, v11, v12, stamp builds, attention variants, ab_knob env vars);
+                                  tools and tools/ab_tests load it with KD_LIBRARY=<path>
 """
 from __future__ import annotations
 
@@ -18,6 +24,8 @@ REPO = HERE.parent.parent
 OUT_DIR = HERE.parent  # the package directory: the .so travels with the snapshot
 LIB = OUT_DIR / "libkdstep.so"
 OBJ_DIR = HERE / "build"
+AB_LIB = REPO / "tools" / "ab" / "libkdstep_ab.so"
+AB_OBJ_DIR = HERE / "build_ab"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
@@ -34,35 +42,39 @@ def _deps_mtime():
     return max(p.stat().st_mtime for p in hdrs)
 
 
-def _compile(src: Path) -> Path:
-    obj = OBJ_DIR / (src.stem + ".o")
+def _compile(src: Path, ab: bool = False) -> Path:
+    obj = (AB_OBJ_DIR if ab else OBJ_DIR) / (src.stem + ".o")
     if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, _deps_mtime()):
         return obj
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *(["-DKD_AB_BUILD"] if ab else []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
     return obj
 
 
-def build(verbose: bool = False, jobs: int | None = None) -> Path:
-    OBJ_DIR.mkdir(exist_ok=True)
+def build(verbose: bool = False, jobs: int | None = None, ab: bool = False) -> Path:
+    lib = AB_LIB if ab else LIB
+    (AB_OBJ_DIR if ab else OBJ_DIR).mkdir(exist_ok=True)
+    lib.parent.mkdir(parents=True, exist_ok=True)
     srcs = _sources()
     jobs = jobs or min(len(srcs), 8)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, srcs))
+        objs = list(ex.map(lambda s_: _compile(s_, ab), srcs))
     newest = max(o.stat().st_mtime for o in objs)
-    if LIB.exists() and LIB.stat().st_mtime > newest:
-        _try_c_host(verbose)
-        return LIB
-    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(LIB)]
+    if lib.exists() and lib.stat().st_mtime > newest:
+        if not ab:
+            _try_c_host(verbose)
+        return lib
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(lib)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     if verbose:
-        print(f"built {LIB}")
-    _try_c_host(verbose)
-    return LIB
+        print(f"built {lib}")
+    if not ab:
+        _try_c_host(verbose)
+    return lib
 
 
 def _try_c_host(verbose: bool) -> None:
@@ -96,5 +108,5 @@ def build_c_host(verbose: bool = False) -> Path:
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    build(verbose=True, ab="--ab" in sys.argv[1:])
     sys.exit(0)

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <string>
 #include <cmath>
+#include <cstdlib>
 
 #include "../../include/kdstep.h"
 
@@ -147,5 +148,18 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // half x2 -> x2 cos + x1 sin (explicit fma: both kernels round identically)
 __device__ __forceinline__ float rope_first(float x1, float x2, float cs, float sn) { return fmaf(x1, cs, -(x2 * sn)); }
 __device__ __forceinline__ float rope_second(float x2, float x1, float cs, float sn) { return fmaf(x2, cs, x1 * sn); }
+
+// A/B and diagnostic switches: read from the environment only in the tools' A/B library
+// (KD_AB_BUILD, `python csrc/build.py --ab`); the product library always takes the default, so
+// no environment variable changes which kernel or plan it runs.
+inline int ab_knob(const char* name, int dflt) {
+#ifdef KD_AB_BUILD
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
+}
 
 }  // namespace kd

@@ -193,7 +193,7 @@ __host__ __device__ inline void tile_grouped(int wg, int tiles_m, int tiles_n, i
 // 1260-1276 us, g = 3 1279-1285, g = 4 1315-1338, g = 8 1341-1358, g = 12 1331, g = 24 1362-1388
 // (profiles/r02/gemm_group_height.txt).
 inline int pick_gm(int tiles_m, int tiles_n) {
-    static const int env = [] { const char* e = std::getenv("KD_GEMM_GM"); return e ? std::atoi(e) : 0; }();
+    static const int env = ab_knob("KD_GEMM_GM", 0);
     if (env > 0) return env;
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     if (nwg % 8 == 0) {
@@ -953,6 +953,7 @@ __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[
     (void)lane; (void)tid;
     if (ST) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); mk[1] = __builtin_amdgcn_s_memtime(); }
 }
+#ifdef KD_AB_BUILD
 
 // the round-4 SwiGLU epilogue before the packed rewrite (EXP bit 512 / KD_GLU_EPI_V0=1: A/B only)
 template <int TM, int TN, int MT, int NT, int NTHR, bool L32 = false>
@@ -992,6 +993,7 @@ __device__ __forceinline__ void epilogue_glu_v0(const GemmP& p, const f32x4 (&ac
         *(bf16x8*)((bf16*)p.C + (int64_t)row * p.ldc + nb + c * 8) = o;
     }
 }
+#endif  // KD_AB_BUILD
 
 // =============================================================================
 // v3: the tiles above and their 4-stage LDS ring, software-pipelined one stage deeper: the
@@ -1181,16 +1183,12 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     // lm_head GEMMs of the KD step): a build of its own, so the plain forward kernel carries none
     // of that code and the lm_head launches are their own line in a kernel trace
     constexpr bool RSTATS = (EXP & 32) && !A_MN && !B_MN;
-    // bit 7 (diagnostic, forced variant 25, WRONG results): each K-major DMA instruction reads
-    // 8 rows x 128 B (whole cache lines) instead of 16 rows x 64 B -- the same instructions and
-    // bytes, half the cache lines per instruction: isolates the cost of half-line row segments
-    constexpr bool WIDE = (EXP & 128) && !A_MN && !B_MN;
     // bit 8: B PRE-TILED (kd_gemm_desc.b_pretiled, kd_gemm_pretile): the K-major B operand is stored
     // as each 256-row tile's stages, [tile][stage][256 rows][64 B] with the LDS chunk swizzle (and, for
     // the SwiGLU build, the gate|up row gather) already applied, zero-padded past N and K, so every
     // DMA instruction reads ONE contiguous KiB (8 whole cache lines) instead of 16 half-lines, and
     // lands the same LDS image (bit-identical results)
-    constexpr bool TB = (EXP & 256) && !B_MN && !WIDE && !RS;
+    constexpr bool TB = (EXP & 256) && !B_MN && !RS;
     const int nkt = (p.K + BK2 - 1) / BK2;   // stages per pre-tiled tile
 
     uint32_t* stamps = nullptr;
@@ -1229,26 +1227,12 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
             vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
         }
         if (TB) vb[u] = (uint32_t)((wid * 4 + u) * 1024 + lane * 16);   // lane-linear KiB of the stage image
-        if (WIDE) {
-            const int row = 8 * (wid * 4 + u) + (lane >> 3);
-            va[u] = (uint32_t)((int64_t)row * p.lda * 2 + (lane & 7) * 16);
-            const int wrow = glu ? (row < 128 ? nb + row : p.glu + nb + row - 128) : row;
-            vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + (lane & 7) * 16);
-        }
     }
     // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl;
     // FULL: the stage lies wholly inside K (no per-lane tail masking)
     auto dma = [&](int st, int sl, int u, auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
         if (NODMA) return;
-        if (WIDE) {
-            const bool isA = u < 4;
-            char* dst = smem + sl * SS + (isA ? 0 : SA) + (wid * 4 + (u & 3)) * 1024;
-            const int soff = st * BK2 * 2 < K * 2 ? st * BK2 * 2 : 0;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, isA ? va[u & 3] : vb[u & 3],
-                                                     soff, 0, 0);
-            return;
-        }
         const bool isA = u < 4;
         const bool mn = isA ? A_MN : B_MN;
         const int i = wid * 4 + (u & 3);
@@ -1414,8 +1398,11 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     uint64_t te0 = 0;
     if (STAMP) { te0 = __builtin_amdgcn_s_memtime(); s_units += te0 - tprev; }
     __syncthreads();
+#ifdef KD_AB_BUILD
     if constexpr (!A_MN && !B_MN && (EXP & 512)) epilogue_glu_v0<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
-    else if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8, false, STAMP>(p, acc, smem, m0, nb, wm, wn, lane, tid, mk);
+    else
+#endif
+    if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8, false, STAMP>(p, acc, smem, m0, nb, wm, wn, lane, tid, mk);
     else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN, RSTATS>(p, acc, smem, m0, n0, wm, wn, lane, tid);
     if (STAMP) {
         if (glu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1438,6 +1425,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     }
 }
 
+#ifdef KD_AB_BUILD   // v11 / v12: measured slower than v8 in the step; tools' A/B library only
 // =============================================================================
 // v11: v8's tile, ring, DMA and barriers (256x256, four waves of 128x128, the 4-slot BK = 32
 // LDS-DMA ring, three stages in flight) on 32x32x16 MFMAs, K-major x K-major operands (every
@@ -1816,6 +1804,8 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm12(GemmP p_) {
     g12_tile<EXP>(p, tm, tn, smem);
 }
 
+#endif  // KD_AB_BUILD
+
 template <bool A_MN, bool B_MN, int EXP = 0>
 __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1860,6 +1850,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     g8_tile<A_MN, B_MN, EXP>(p, tm, tn, smem);
 }
 
+#ifdef KD_AB_BUILD   // v9: equal speed to v8 on the step's shapes, not in the plan; A/B library only
 // =============================================================================
 // v9: 256x256 tile, EIGHT waves in two groups that ping-pong on every SIMD. Group g
 // (waves 4g..4g+3, one per SIMD) owns rows 128g..128g+127; wave 4g+c owns columns
@@ -1989,6 +1980,7 @@ __global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
     if (!A_MN && !B_MN && glu) epilogue_glu<128, 64, 8, 4, NTH9>(p, acc, smem, m0, nb, grp, wc, lane, tid);
     else epilogue2<256, 256, 2, 4, 128, 64, 8, 4, NTH9, !A_MN && !B_MN>(p, acc, smem, m0, n0, grp, wc, lane, tid);
 }
+#endif  // KD_AB_BUILD
 
 
 // =============================================================================
@@ -2389,11 +2381,13 @@ inline int sk_max_pieces(int64_t tiles, int64_t nk, int G) {
     return (int)((nk - 1) / per + 2);
 }
 
+#ifdef KD_AB_BUILD
 // KD_GLU_EPI_V0=1: the SwiGLU GEMM with the previous (unpacked) epilogue, for A/B (read per call)
 bool glu_epi_v0() {
     const char* e = std::getenv("KD_GLU_EPI_V0");
     return e && std::atoi(e) != 0;
 }
+#endif
 
 GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     const int64_t M = d->M, N = d->N;
@@ -2414,8 +2408,8 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     static const double fixed_c4[2][5] = {{8.830, 5.440, 5.343, 11.954, 5.888}, {9.291, 5.201, 5.162, 12.159, 8.442}};
     static const double step_c3[2][5] = {{0.7524, 0.5218, 0.5092, 0.6844, 0.7183}, {0.7375, 0.5501, 0.5469, 0.6022, 0.6876}};
     static const double fixed_c3[2][5] = {{5.253, 3.402, 3.414, 8.478, 5.888}, {5.885, 3.479, 3.398, 8.695, 8.442}};
-    static const bool set3 = [] { const char* e = std::getenv("KD_PLAN_SET"); return e && std::atoi(e) == 3; }();
-    static const bool hybrid_on = [] { const char* e = std::getenv("KD_GEMM_HYBRID"); return !e || std::atoi(e) != 0; }();
+    static const bool set3 = ab_knob("KD_PLAN_SET", 4) == 3;
+    static const bool hybrid_on = ab_knob("KD_GEMM_HYBRID", 1) != 0;
     const double (&step_c)[2][5] = set3 ? step_c3 : step_c4;
     const double (&fixed_c)[2][5] = set3 ? fixed_c3 : fixed_c4;
     const double kBW = set3 ? 7.711e6 : 9.109e6;          // partial-plane bytes per microsecond
@@ -2592,8 +2586,9 @@ int launch_gemm_pretile(const void* W, int64_t ldw, int N, int K, int glu, void*
     return KD_OK;
 }
 
-// v11 (32x32x16 MFMAs) in place of v8 for K-major x K-major tiles: forced variant 23 (24 forces
-// v8 for A/B), else the library default (KD_GEMM_V11=0 turns it off)
+#ifdef KD_AB_BUILD
+// v11 (32x32x16 MFMAs) in place of v8 for K-major x K-major tiles: forced variant 23, or
+// KD_GEMM_V11=1 wherever v8 would run (opt-in; 24 forces v8 for A/B)
 static bool use_v11(int variant) {
     if (variant == 23) return true;
     if (variant != 0 && variant != 16) return false;
@@ -2601,20 +2596,28 @@ static bool use_v11(int variant) {
     return env == 1;
 }
 
-// v12 (whole-line staging of K-major operands, bit-identical to v8): forced variant 26 (24 forces
-// v8); KD_GEMM_V12=1 runs it wherever v8 would run.  Not the default: it measured faster than v8
-// only with the weights warm in the Infinity Cache (back-to-back calls, profiles/r04/ab_v12_vs_v8.txt:
-// student gate|up 112.0 -> 103.8 us, teacher q|k|v 161.4 -> 156.9); in the step's cache state --
-// every weight read cold, a whole step after its last use -- v12 is slower than v8 on every shape
-// (profiles/r04/ab_cold.txt, tools/ab_cold.py: teacher q|k|v scatter 225.6 -> 244.3 us, o_proj
-// 180.2 -> 184.9, student down 96.0 -> 108.5, SigLIP o_proj 53.8 -> 58.3): its stage pairs halve
-// the prefetch depth, which an HBM-latency read stream exposes (g12_tile).
-static bool use_v12(int variant, int64_t N = 0, int64_t K = 0) {
-    (void)N; (void)K;
+// v12 (whole-line staging of K-major operands, bit-identical to v8): forced variant 26, or
+// KD_GEMM_V12=1 wherever v8 would run (opt-in; 24 forces v8).  Measured faster than v8 only with
+// the weights warm in the Infinity Cache (back-to-back calls, profiles/r04/ab_v12_vs_v8.txt); in
+// the step's cache state -- every weight read cold, a whole step after its last use -- slower than
+// v8 on every shape (profiles/r04/ab_cold.txt): its stage pairs halve the prefetch depth.
+static bool use_v12(int variant) {
     if (variant == 26) return true;
     if (variant != 0 && variant != 16) return false;
     static const int env = [] { const char* e = std::getenv("KD_GEMM_V12"); return e ? std::atoi(e) : -1; }();
     return env == 1;
+}
+#endif
+
+// the variants kd_gemm accepts: 0 auto, 1 v1, 2-7 v3 tiles, 16 v8, 21 stream-K, 24 (= 16); the
+// tools' A/B library (KD_AB_BUILD: python csrc/build.py --ab) also the negative-result and
+// diagnostic builds 17-20, 22, 23, 26-28
+static bool variant_known(int v) {
+    if ((v >= 0 && v <= 7) || v == 16 || v == 21 || v == 24) return true;
+#ifdef KD_AB_BUILD
+    if ((v >= 17 && v <= 20) || v == 22 || v == 23 || (v >= 26 && v <= 28)) return true;
+#endif
+    return false;
 }
 
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
@@ -2644,7 +2647,8 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldc >= w && d->ld_aux >= w && d->ldc % 8 == 0 && d->ld_aux % 8 == 0 &&
                        (uintptr_t)d->aux % 16 == 0, "gemm backward activation: ldc / ld_aux >= N (2N for dswiglu), 16-B rows");
     }
-    KD_CHECK_ARG((d->variant >= 0 && d->variant <= 7) || (d->variant >= 16 && d->variant <= 28), "gemm: unknown variant");
+    KD_CHECK_ARG(variant_known(d->variant),
+                 "gemm: unknown variant (the diagnostic / A-B builds 17-20, 22, 23, 26-28 are in the tools' A/B library only)");
     KD_CHECK_ALIGN(d->A, 16, "gemm: A must be 16-B aligned");
     KD_CHECK_ALIGN(d->B, 16, "gemm: B must be 16-B aligned");
     // the tiled epilogues load a lane's 4 bias columns as one f32x4 / bf16x4 vector (load_bias4)
@@ -2748,10 +2752,11 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         pk.gm = pick_gm(ceil_div(d->M, 256), d->N / 256);
         const dim3 grid(ceil_div(d->M, 256) * (d->N / 256), 1);
         pk.gx = (int)grid.x; pk.gy = 1;
+#ifdef KD_AB_BUILD
         if (d->variant == 20) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), (gemm2_lds<256, 256>()), st, pk);
         else if (!d->b_pretiled && use_v11(d->variant)) hipLaunchKernelGGL((k_gemm11<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 27) hipLaunchKernelGGL((k_gemm12<4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
-        else if (!d->b_pretiled && use_v12(d->variant, d->N, d->K)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (!d->b_pretiled && use_v12(d->variant)) hipLaunchKernelGGL((k_gemm12<4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 22)
             hipLaunchKernelGGL((k_gemm8<false, false, 12>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (d->variant == 28) {   // stamp build: per-wave cycle totals to the workspace (tools/stamp_glu.py)
@@ -2759,10 +2764,10 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             pk.sk_ws = (float*)d->workspace;
             hipLaunchKernelGGL((k_gemm8<false, false, 5>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         }
-        else if (d->variant == 25)
-            hipLaunchKernelGGL((k_gemm8<false, false, 132>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
-        else if (d->b_pretiled) hipLaunchKernelGGL((k_gemm8<false, false, 4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else if (glu_epi_v0()) hipLaunchKernelGGL((k_gemm8<false, false, 4 | 512>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else
+#endif
+        if (d->b_pretiled) hipLaunchKernelGGL((k_gemm8<false, false, 4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
         return KD_OK;
@@ -2809,13 +2814,16 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             const dim3 grid((unsigned)nt, gy);
             GemmP q = q0;
             q.gx = nt; q.gy = (int)gy;
+#ifdef KD_AB_BUILD
             if (pl.var == 20) {   // v9
                 const size_t lds = gemm2_lds<256, 256>();
                 if (!amn && !bmn) hipLaunchKernelGGL((k_gemm9<false, false>), grid, dim3(NTH9), lds, st, q);
                 else if (!amn && bmn) hipLaunchKernelGGL((k_gemm9<false, true>), grid, dim3(NTH9), lds, st, q);
                 else if (amn && bmn) hipLaunchKernelGGL((k_gemm9<true, true>), grid, dim3(NTH9), lds, st, q);
                 else hipLaunchKernelGGL((k_gemm9<true, false>), grid, dim3(NTH9), lds, st, q);
-            } else if (pl.var == 16) {   // v8; forced variants 17-19 are its diagnostic builds (EXP bits above)
+            } else
+#endif
+            if (pl.var == 16) {   // v8; forced variants 17-19 are its diagnostic builds (EXP bits above)
                 const size_t lds = gemm2_lds<256, 256>();
 #define L8(E)                                                                                                   \
     {                                                                                                           \
@@ -2829,6 +2837,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, E>), grid, dim3(NTH8), lds, st, q);         \
         else L8(0)                                                                                              \
     }
+#ifdef KD_AB_BUILD
                 if (!amn && !bmn && use_v11(force)) {   // v11: the same tiles on 32x32x16 MFMAs
                     hipLaunchKernelGGL((k_gemm11<0>), grid, dim3(NTH8), lds, st, q);
                     return;
@@ -2837,7 +2846,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                     hipLaunchKernelGGL((k_gemm12<256>), grid, dim3(NTH8), lds, st, q);
                     return;
                 }
-                if (!amn && !bmn && use_v12(force, d->N, q.K)) {   // v12: the same tiles, whole-line K-major staging
+                if (!amn && !bmn && use_v12(force)) {   // v12: the same tiles, whole-line K-major staging
                     hipLaunchKernelGGL((k_gemm12<0>), grid, dim3(NTH8), lds, st, q);
                     return;
                 }
@@ -2846,9 +2855,12 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                     case 18: L8K(2) break;
                     case 19: L8K(64) break;
                     case 22: L8K(8) break;
-                    case 25: L8K(128) break;
                     default: L8(0) break;
                 }
+#else
+                L8(0)
+                (void)force;
+#endif
 #undef L8K
 #undef L8
             } else {

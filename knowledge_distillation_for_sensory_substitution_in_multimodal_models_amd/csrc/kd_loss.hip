@@ -649,9 +649,13 @@ k_loss_grad_loca(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restri
 // of a row exchange their pass-A partials (KD term, S) through 8-B granules {tag, value} stored
 // write-through at agent scope (cdna_hip_programming.md §6 G16 R2: no fence, no flag); every
 // slice sums the nsl partials in slice order, so all of a row's workgroups use the same S.
-// All of a row's slices must be resident together: the grid is nsl x (resident workgroups /
-// nsl) persistent workgroups (row groups stride the rows), and every poll is bounded in time
-// (the timeout sets bit 4 of the error words: KD_ERR_LAUNCH from kd_loss_check, AdamW skips).
+// The grid is nsl x (resident workgroups / nsl) persistent workgroups (row groups stride the rows),
+// so on an idle GPU all of a row's slices run together.  Correctness does not depend on it: a slice
+// polls its partners' granules for a bounded time (rr_poll_ticks) and then computes any absent
+// partial itself -- the same body (pass_a) over the same chunks with the same lane mapping and
+// reduction order, so the same bits the absent slice stores -- and reloads its own chunks.  When
+// other work holds CUs (a concurrent stream, a CU mask) the kernel slows down; it never waits on a
+// workgroup that is not running and never fails.
 // Same per-element arithmetic as k_loss_grad_loca; the row sums differ in fp32 order only.
 constexpr int RR_NT = 512, RR_NW = RR_NT / 64;
 constexpr int RR_C = 5;                                   // 16-B chunks of each tensor per lane per row (max)
@@ -678,19 +682,18 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                     const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g,
                     const float* __restrict__ coefs, bf16* __restrict__ D_, int64_t ld_d,
                     float* __restrict__ part_kl, int nsl, int cps, int n_rg,
-                    unsigned long long* __restrict__ gran, int* __restrict__ err, int* __restrict__ err_ext) {
+                    unsigned long long* __restrict__ gran, uint32_t poll_ticks) {
     __shared__ unsigned long long smask[RR_MASK_W];
     __shared__ float red[2 * RR_NW];
     __shared__ float row_sums[2];
+    __shared__ float gv[2 * RR_MAX_SL];   // the row's slice partials, slice order
+    __shared__ int miss_s;                // slices whose partials did not arrive within poll_ticks
     const float ce_coef = coefs[1], kd_coef = coefs[2];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int sl = (int)(blockIdx.x % (unsigned)nsl), rg = (int)(blockIdx.x / (unsigned)nsl);
     const int c_lo = sl * cps, c_hi = min(V >> 3, c_lo + cps);   // this workgroup's chunks [c_lo, c_hi)
     const int w_lo = (c_lo * 8) >> 6;
     const uint32_t vo = (uint32_t)tid * 16;
-    // the slice through buffer descriptors (SGPRs) and ONE lane offset: out-of-slice chunks read
-    // zeros (never used); 64-bit per-chunk addresses hoisted out of the row loop spilled
-    const uint32_t nb = (uint32_t)(c_hi - c_lo) * 16;
     for (int i = tid; i < RR_MASK_W; i += RR_NT) {
         const int w = w_lo + i;
         smask[i] = w < ((V + 63) >> 6) ? mask_g[w] : 0ull;
@@ -711,27 +714,30 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
     const float lk = kd_coef > 0.f ? log2f(kd_coef) : -INFINITY;
     typedef __attribute__((ext_vector_type(2))) float f32x2;
     typedef bf16x8 Set[RC];
-    auto load = [&](Set& xt, Set& xs, int r) {
-        const __amdgpu_buffer_rsrc_t rT = slice_rsrc(T_ + (int64_t)r * ld_t + c_lo * 8, nb);
-        const __amdgpu_buffer_rsrc_t rS = slice_rsrc(S_ + (int64_t)r * ld_s + c_lo * 8, nb);
+    // chunks [lo, hi) of row r (this lane's: lo + tid + j RR_NT) through buffer descriptors (SGPRs)
+    // and ONE lane offset: out-of-slice chunks read zeros (never used); 64-bit per-chunk addresses
+    // hoisted out of the row loop spilled
+    auto load = [&](Set& xt, Set& xs, int r, int lo, int hi) {
+        const uint32_t nb = (uint32_t)(hi - lo) * 16;
+        const __amdgpu_buffer_rsrc_t rT = slice_rsrc(T_ + (int64_t)r * ld_t + lo * 8, nb);
+        const __amdgpu_buffer_rsrc_t rS = slice_rsrc(S_ + (int64_t)r * ld_s + lo * 8, nb);
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
             xt[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rT, vo, j * RR_NT * 16, 0));
             xs[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rS, vo, j * RR_NT * 16, 0));
         }
     };
-    // row r from registers (xt, xs)
-    auto row = [&](Set& xt, Set& xs, int r) {
-        const RowStats st = stats[r];
-        R.cq = (st.mt * invT + logf(st.zt)) * KD_LOG2E;
-        R.cs = (st.ms * invT + logf(st.zs)) * KD_LOG2E;
-        // ---- pass A (k_loss_grad_loca's arithmetic)
+    // pass A (k_loss_grad_loca's arithmetic) over the chunks [lo, hi) held in (xt, xs), mask bytes mbx:
+    // the lane's KD-term and S partials.  The ONE body both a slice's own partial and a stand-in's
+    // recomputation of it run, so both give the same bits.
+    auto pass_a = [&](const Set& xt, const Set& xs, int lo, int hi, uint64_t mbx, f32x2& term2, f32x2& sacc2) {
         const f32x2 a2 = {R.a, R.a}, cq2 = {R.cq, R.cq}, cs2 = {R.cs, R.cs};
-        f32x2 term2 = {0.f, 0.f}, sacc2 = {0.f, 0.f};
+        term2 = f32x2{0.f, 0.f};
+        sacc2 = f32x2{0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
-            const int c = c_lo + tid + j * RR_NT;
-            if (c >= c_hi) break;
+            const int c = lo + tid + j * RR_NT;
+            if (c >= hi) break;
             const int v = c * 8;
             float t[8], sv[8], lq[8], q[8], lps[8];
             bf16x8_to_f32(xt[j], t);
@@ -745,7 +751,7 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                 q[k] = ex2(lq[k]);
                 q[k + 1] = ex2(lq[k + 1]);
             }
-            if ((mb >> (8 * j)) & 0xffu) {
+            if ((mbx >> (8 * j)) & 0xffu) {
                 const f32x4 o0 = *(const f32x4*)(ovr + v), o1 = *(const f32x4*)(ovr + v + 4);
                 const f32x4 l0 = *(const f32x4*)(ovr + V + v), l1 = *(const f32x4*)(ovr + V + v + 4);
 #pragma unroll
@@ -764,44 +770,82 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                 sacc2 += f32x2{lps[k] >= R.lcl ? q[k] : 0.f, lps[k + 1] >= R.lcl ? q[k + 1] : 0.f};
             }
         }
-        // slice partials: the block's two sums in one LDS round
+    };
+    // the block's two sums of the lanes' partials, in one LDS round; valid in wave 0
+    auto block_sums = [&](f32x2 term2, f32x2 sacc2, float& tp, float& sp) {
         const float tw = wave_sum(term2.x + term2.y), sw = wave_sum(sacc2.x + sacc2.y);
         if (lane == 0) { red[wid] = tw; red[RR_NW + wid] = sw; }
         __syncthreads();
+        tp = 0.f; sp = 0.f;
         if (wid == 0) {
-            float tp = 0.f, sp = 0.f;
 #pragma unroll
             for (int i = 0; i < RR_NW; ++i) { tp += red[i]; sp += red[RR_NW + i]; }
+        }
+    };
+    // row r from registers (xt, xs)
+    auto row = [&](Set& xt, Set& xs, int r) {
+        const RowStats st = stats[r];
+        R.cq = (st.mt * invT + logf(st.zt)) * KD_LOG2E;
+        R.cs = (st.ms * invT + logf(st.zs)) * KD_LOG2E;
+        f32x2 term2, sacc2;
+        pass_a(xt, xs, c_lo, c_hi, mb, term2, sacc2);
+        float tp, sp;
+        block_sums(term2, sacc2, tp, sp);
+        if (wid == 0) {
+            int miss = 0;
             if (nsl > 1) {
+                // hand the slice partials over through the row's 2 nsl granules; poll them for at most
+                // poll_ticks of the 100 MHz real-time clock (the slices of a row run together when
+                // they are co-resident: microseconds apart)
                 unsigned long long* g = gran + (int64_t)r * nsl * 2;
                 if (lane == 0) { gran_store(g + 2 * sl, tp); gran_store(g + 2 * sl + 1, sp); }
-                // poll the row's 2 nsl granules (this slice's own included: its store is visible
-                // to its own loads once written), bounded by ~1 s of the 100 MHz real-time clock.
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 unsigned long long x = 1ull << 32;
                 for (;;) {
                     x = lane < 2 * nsl ? gran_load(g + lane) : (1ull << 32);
                     if (__all((unsigned)(x >> 32) == 1u)) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
-                        if (lane == 0) {
-                            atomicOr(err, 4);
-                            if (err_ext != nullptr) atomicOr(err_ext, 4);
-                        }
-                        break;
-                    }
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > poll_ticks) break;
                     __builtin_amdgcn_s_sleep(2);
                 }
-                const float xv = __uint_as_float((unsigned)x);
-                tp = 0.f; sp = 0.f;
-                for (int s2 = 0; s2 < nsl; ++s2) {   // slice order: every slice of the row gets the same sums
-                    tp += __shfl(xv, 2 * s2, 64);
-                    sp += __shfl(xv, 2 * s2 + 1, 64);
+                const bool have = (unsigned)(x >> 32) == 1u;
+                if (lane < 2 * nsl) gv[lane] = lane == 2 * sl ? tp : (lane == 2 * sl + 1 ? sp : __uint_as_float((unsigned)x));
+                const uint64_t absent = __ballot(!have) & ((2 * nsl < 64 ? (1ull << (2 * nsl)) : 0ull) - 1ull);
+                for (int s2 = 0; s2 < nsl; ++s2) miss |= ((absent >> (2 * s2)) & 3ull) ? (1 << s2) : 0;
+            } else if (lane == 0) {
+                gv[0] = tp; gv[1] = sp;
+            }
+            if (lane == 0) miss_s = miss;
+        }
+        __syncthreads();
+        const int miss = miss_s;
+        if (miss) {
+            // a slice of this row is not running now (its workgroup is not resident beside this one:
+            // other work holds CUs): compute its partials here with the same body and lane mapping, so
+            // they are the bits it stores itself, then restore this slice's chunks.  Progress never
+            // depends on co-residency.
+            for (int s2 = 0; s2 < nsl; ++s2) {
+                if (!((miss >> s2) & 1)) continue;
+                const int lo2 = s2 * cps, hi2 = min(V >> 3, lo2 + cps);
+                uint64_t mb2 = 0;
+#pragma unroll
+                for (int j = 0; j < RC; ++j) {
+                    const int c = lo2 + tid + j * RR_NT;
+                    if (c < hi2) mb2 |= ((mask_g[(c * 8) >> 6] >> ((c * 8) & 63)) & 0xffull) << (8 * j);
                 }
+                load(xt, xs, r, lo2, hi2);
+                pass_a(xt, xs, lo2, hi2, mb2, term2, sacc2);
+                float t2, s3;
+                block_sums(term2, sacc2, t2, s3);
+                if (tid == 0) { gv[2 * s2] = t2; gv[2 * s2 + 1] = s3; }
+                __syncthreads();   // red is reused by the next slice
             }
-            if (lane == 0) {
-                row_sums[0] = tp; row_sums[1] = sp;
-                if (sl == 0) part_kl[r] = tp * KD_LN2;
-            }
+            load(xt, xs, r, c_lo, c_hi);
+        }
+        if (tid == 0) {
+            float a = 0.f, b = 0.f;
+            for (int s2 = 0; s2 < nsl; ++s2) { a += gv[2 * s2]; b += gv[2 * s2 + 1]; }   // slice order
+            row_sums[0] = a; row_sums[1] = b;
+            if (sl == 0) part_kl[r] = a * KD_LN2;
         }
         __syncthreads();
         const float Ssum = row_sums[1];
@@ -812,7 +856,7 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         R.cqk = R.cq - lk;
         R.c1 = (st.ms + logf(st.zs1)) * KD_LOG2E;
         bf16* drow = D_ + (int64_t)r * ld_d;
-        const __amdgpu_buffer_rsrc_t rD = slice_rsrc(drow + c_lo * 8, nb);
+        const __amdgpu_buffer_rsrc_t rD = slice_rsrc(drow + c_lo * 8, (uint32_t)(c_hi - c_lo) * 16);
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
             const int c = c_lo + tid + j * RR_NT;
@@ -852,7 +896,7 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
     };
     for (int r = rg; r < rows; r += n_rg) {
         Set xt, xs;
-        load(xt, xs, r);
+        load(xt, xs, r, c_lo, c_hi);
         row(xt, xs, r);
     }
 }
@@ -958,8 +1002,17 @@ int rr_resident(int rc) {
 
 // chunks per lane of the register-resident kernel: 5 (default) or KD_LOSS_RR_C=3 (read per call)
 int rr_chunks() {
-    const char* e = std::getenv("KD_LOSS_RR_C");
-    return (e && std::atoi(e) == 3) ? 3 : 5;
+    return ab_knob("KD_LOSS_RR_C", 5) == 3 ? 3 : 5;
+}
+
+// poll budget of a slice waiting for its row's other slices, in ticks of the 100 MHz real-time
+// clock: 200 us by default (co-resident slices of a row arrive microseconds apart); after it the
+// slice computes the absent partials itself.  KD_LOSS_RR_POLL_US (read per call; tests: 0 = every
+// slice recomputes every other slice's partials, which must give the same bits)
+uint32_t rr_poll_ticks() {
+    const char* e = std::getenv("KD_LOSS_RR_POLL_US");
+    const long us = e ? std::atol(e) : 200;
+    return (uint32_t)std::min<long>(std::max<long>(us, 0) * 100, 100000000L);
 }
 
 // KD_LOSS_RR=0: the two-read k_loss_grad_loca (A/B; read at every call, so a test can switch)
@@ -1016,8 +1069,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     // k_row_stats: one workgroup per row (the dispatcher balances them); a grid of 2048 row-strided
     // workgroups left 512 of them (3 rows each) on a third of the CUs after the first 1536 (six
     // per CU) finished.  KD_RS_GRID=n: a grid of n row-strided workgroups (A/B).
-    const char* rs_env = std::getenv("KD_RS_GRID");
-    const int rs_cap = rs_env ? std::max(1, std::atoi(rs_env)) : 1 << 30;
+    const int rs_cap = std::max(1, ab_knob("KD_RS_GRID", 1 << 30));
     const int grid = std::min(rows, rs_cap);
     const bool part = p.s_row_stats != nullptr;
     if (part) {
@@ -1059,8 +1111,9 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     const int nsl = rr_nsl(V_s, rc);
     const int resident = rr_resident(rc);
     if (loca_fast && rr_enabled() && nsl <= RR_MAX_SL && resident >= 2 * nsl) {
-        // register-resident slices (k_loss_grad_loca_rr): resident / nsl row groups of nsl
-        // workgroups, every one of them resident at once
+        // register-resident slices (k_loss_grad_loca_rr): resident / nsl row groups of nsl workgroups,
+        // sized so that all of them fit at once on an idle GPU; a slice whose partner is not running
+        // (other work holds CUs) stands in for it after the poll budget, so nothing depends on that
         const int cps = (V_s / 8 + nsl - 1) / nsl;
         const int n_rg = std::min(resident / nsl, rows);
         unsigned long long* gran = (unsigned long long*)(w + lo.gran);
@@ -1069,7 +1122,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
 #define KD_LAUNCH_RR(T1v, RCv)                                                                                   \
     hipLaunchKernelGGL((k_loss_grad_loca_rr<T1v, RCv>), dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s, \
                        V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg, gran,   \
-                       err, p.err_out)
+                       rr_poll_ticks())
         if (rc == 5) { if (invT == 1.f) KD_LAUNCH_RR(true, 5); else KD_LAUNCH_RR(false, 5); }
         else { if (invT == 1.f) KD_LAUNCH_RR(true, 3); else KD_LAUNCH_RR(false, 3); }
 #undef KD_LAUNCH_RR
@@ -1101,8 +1154,6 @@ int kd_loss_check_impl(const void* ws_, void* stream_) {
     KD_CHECK_ARG(ws_ != nullptr, "kd_loss_check: null workspace");
     if (hipStreamSynchronize(as_stream(stream_)) != hipSuccess) return fail(KD_ERR_LAUNCH, "kd_loss_check: sync");
     if (hipMemcpy(&h, ws_, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(KD_ERR_LAUNCH, "kd_loss_check: copy");
-    if (h & 4) return fail(KD_ERR_LAUNCH, "kd_loss: a row's slice hand-off timed out (k_loss_grad_loca_rr: "
-                                          "its workgroups were not resident together)");
     if (h) return fail(KD_ERR_LABEL_RANGE, "kd_loss: label outside [0, V) (LoCa gathers at every label; "
                                             "CE targets must be -100 or in range)");
     return KD_OK;

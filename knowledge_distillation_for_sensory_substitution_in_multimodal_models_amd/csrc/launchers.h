@@ -23,7 +23,7 @@ int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const vo
 size_t norm_bwd_ws(int R, int D);
 int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
                     const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w,
-                    void* ws, size_t ws_bytes, int R, int D, void* stream, int x_f32 = 0);
+                    void* ws, size_t ws_bytes, int R, int D, void* stream, int x_f32 = 0, int dy_group = 0);
 int launch_qkv_split(const void* qkv, int64_t ld, void* q, void* k, void* v, const float* cos_t, const float* sin_t,
                      int B, int S, int nq, int nkv, int hd, int hdp, void* stream);
 int launch_qkv_merge(const float* dq, const void* dk, const void* dv, void* dqkv, int64_t ld, const float* cos_t,
@@ -46,6 +46,7 @@ int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t
                  float eps, float wd, int step, const float* gscale, const int32_t* skip, int n_skip, void* stream);
 int launch_sumsq(const float* x, int64_t n, float* out, void* stream);
 int launch_scalar_mul(const float* a, const float* b, float* out, int n, void* stream);
+int launch_scale_f32(const float* x, const float* s_dev, float* y, int64_t n, void* stream);
 int launch_image_src_map(const int64_t* ids, int B, int L, int64_t image_token, const int* map, int map_ld,
                          const int* map_len, int* src, int* err, void* stream);
 int launch_quant_rows_f8(const void* x, int64_t ldx, int R, int K, void* q, int64_t ldq, float* scale, void* stream);

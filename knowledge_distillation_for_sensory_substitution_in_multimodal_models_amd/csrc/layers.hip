@@ -195,13 +195,28 @@ __global__ void __launch_bounds__(NT) k_norm_fwd2(const XT* __restrict__ x, int6
     }
 }
 
-template <bool RMS, int IT, typename XT>
+// dy chunk of 8 elements: bf16 per row, or (GDY) fp32 per row GROUP -- the post_layernorm hook's
+// gradient, d(pooled tile feature) spread as d / np over the tile's np rows (DT:243-244) without
+// rounding it to bf16: a bf16 value repeated over 729 rows is a coherent error, and the two tiles'
+// post_layernorm.bias contributions cancel to ~1e-3 of each (tools/ntx_bias_study.py)
+template <bool GDY> struct DyChunk {
+    bf16x8 v;
+    __device__ __forceinline__ void load(const void* p) { v = *(const bf16x8*)p; }
+    __device__ __forceinline__ float get(int j) const { return (float)v[j]; }
+};
+template <> struct DyChunk<true> {
+    f32x4 a, b;
+    __device__ __forceinline__ void load(const void* p) { a = *(const f32x4*)p; b = *((const f32x4*)p + 1); }
+    __device__ __forceinline__ float get(int j) const { return j < 4 ? a[j] : b[j - 4]; }
+};
+
+template <bool RMS, int IT, typename XT, bool GDY = false>
 __global__ void __launch_bounds__(NT) k_norm_bwd(const XT* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
-                                                 const bf16* __restrict__ dy, int64_t lddy,
+                                                 const void* __restrict__ dy, int64_t lddy,
                                                  const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                  bf16* __restrict__ dx, int64_t lddx, int dx_accum,
                                                  float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                 int R, int D, int rows_per_block) {
+                                                 int R, int D, int rows_per_block, int gP = 1, float gscale = 1.f) {
     extern __shared__ __attribute__((aligned(16))) float sacc[];  // [4 waves][2][D] per workgroup
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nch = D / 8;
@@ -216,20 +231,20 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const XT* __restrict__ x, int64
     }
     const int r_begin = blockIdx.x * rows_per_block;
     const int r_end = min(R, r_begin + rows_per_block);
-    struct Row { XChunk<XT> x[IT]; bf16x8 g[IT], p[IT]; float mean, rstd; };
+    struct Row { XChunk<XT> x[IT]; DyChunk<GDY> g[IT]; bf16x8 p[IT]; float mean, rstd; };
     // every load is unconditional (row and chunk clamped into range, dx read even when not
     // accumulated): with a data-dependent number of loads in flight hipcc can only wait
     // vmcnt(0), which drains the next row's loads and undoes the pipeline
     auto load = [&](Row& t, int row_) {
         const int row = min(row_, R - 1);
         const XT* xr = x + (int64_t)row * ldx;
-        const bf16* gr = dy + (int64_t)row * lddy;
+        const char* gr = (const char*)dy + (GDY ? (int64_t)(row / gP) * lddy * 4 : (int64_t)row * lddy * 2);
         const bf16* pr = dx + (int64_t)row * lddx;
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int c = min(lane + it * 64, nch - 1);
             t.x[it].load(xr + c * 8);
-            t.g[it] = *(const bf16x8*)(gr + c * 8);
+            t.g[it].load(gr + c * 8 * (GDY ? 4 : 2));
             t.p[it] = *(const bf16x8*)(pr + c * 8);
         }
         t.mean = RMS ? 0.f : mean_in[row];
@@ -243,7 +258,7 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const XT* __restrict__ x, int64
             if (lane + it * 64 >= nch) continue;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float xv = t.x[it].get(j), dv = (float)t.g[it][j];
+                const float xv = t.x[it].get(j), dv = GDY ? t.g[it].get(j) * gscale : t.g[it].get(j);
                 const float xh = (xv - mean) * rstd;
                 const float g = dv * wr[it][j];
                 a1 += g;
@@ -263,7 +278,8 @@ __global__ void __launch_bounds__(NT) k_norm_bwd(const XT* __restrict__ x, int64
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float xh = (t.x[it].get(j) - mean) * rstd;
-                    o[j] = rstd * ((float)t.g[it][j] * wr[it][j] - (RMS ? 0.f : a1) - xh * a2);
+                    const float dv = GDY ? t.g[it].get(j) * gscale : t.g[it].get(j);
+                    o[j] = rstd * (dv * wr[it][j] - (RMS ? 0.f : a1) - xh * a2);
                     if (dx_accum) o[j] += (float)t.p[it][j];
                 }
                 store8(dxr + c * 8, o);
@@ -811,6 +827,12 @@ __global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restric
     if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
+// y = x * (*s) (s may be NULL: a copy); y may alias x
+__global__ void k_scale_f32(const float* x, const float* __restrict__ s, float* y, int64_t n) {
+    const float sc = s ? *s : 1.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = x[i] * sc;
+}
+
 __global__ void k_scalar_mul(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ out, int n) {
     const int i = threadIdx.x;
     if (i < n) out[i] = a[i] * b[i];
@@ -876,8 +898,7 @@ int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const vo
     const dim3 grid((R + 3) / 4);
     hipStream_t st = as_stream(stream);
     // KD_NORM_FWD_V=1 (read per call): the previous kernel, for A/B
-    const char* ve = std::getenv("KD_NORM_FWD_V");
-    if (!(ve && std::atoi(ve) == 1)) {
+    if (ab_knob("KD_NORM_FWD_V", 2) != 1) {
         const int it = (D / 8 + 63) / 64;
 #define KD_NF2(ITV)                                                                                                   \
     do {                                                                                                               \
@@ -924,7 +945,7 @@ int launch_norm_fwd(int rms, const void* x, int64_t ldx, const void* w, const vo
 
 // workgroups of k_norm_bwd: ~8 rows each (2 per wave), at most 512 (2 per CU)
 static int norm_bwd_blocks(int R) {
-    static const int cap = [] { const char* e = std::getenv("KD_NORM_BWD_BLOCKS"); return e ? std::atoi(e) : 512; }();
+    static const int cap = ab_knob("KD_NORM_BWD_BLOCKS", 512);
     return std::max(1, std::min(cap, (R + 7) / 8));
 }
 
@@ -934,8 +955,10 @@ size_t norm_bwd_ws(int R, int D) {
 
 int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const void* dy, int64_t lddy, const float* mean,
                     const float* rstd, void* dx, int64_t lddx, int dx_accum, float* dw, float* db, int accum_w,
-                    void* ws, size_t ws_bytes, int R, int D, void* stream, int x_f32) {
+                    void* ws, size_t ws_bytes, int R, int D, void* stream, int x_f32, int dy_group) {
     KD_CHECK_ARG(x && w && dy && rstd && dx && (rms || mean), "norm_bwd: null pointer");
+    KD_CHECK_ARG(dy_group == 0 || (!rms && dy_group > 0 && R % dy_group == 0 && (uintptr_t)dy % 16 == 0 && lddy % 4 == 0),
+                 "norm_bwd: a grouped fp32 dy is for LayerNorm, rows a multiple of the group, 16-B rows");
     KD_CHECK_SHAPE(D % 8 == 0 && D <= 2048, "norm_bwd: D must be a multiple of 8, <= 2048");
     const int nb = norm_bwd_blocks(R);
     const int rows_per = (R + nb - 1) / nb;
@@ -946,13 +969,24 @@ int launch_norm_bwd(int rms, const void* x, int64_t ldx, const void* w, const vo
     const size_t smem = (size_t)NW_NORM * 2 * D * 4;
 #define KD_NB(RMSV, ITV)                                                                                          \
     do {                                                                                                           \
-        if (x_f32)                                                                                                 \
+        if (dy_group && !RMSV) {                                                                                   \
+            if (x_f32)                                                                                             \
+                hipLaunchKernelGGL((k_norm_bwd<false, ITV, float, true>), dim3(nb), dim3(NT), smem, st,              \
+                                   (const float*)x, ldx, (const bf16*)w, dy, lddy, mean, rstd, (bf16*)dx, lddx,       \
+                                   dx_accum, dw ? dwp : nullptr, db ? dbp : nullptr, R, D, rows_per, dy_group,        \
+                                   1.f / dy_group);                                                                 \
+            else                                                                                                   \
+                hipLaunchKernelGGL((k_norm_bwd<false, ITV, bf16, true>), dim3(nb), dim3(NT), smem, st,               \
+                                   (const bf16*)x, ldx, (const bf16*)w, dy, lddy, mean, rstd, (bf16*)dx, lddx,        \
+                                   dx_accum, dw ? dwp : nullptr, db ? dbp : nullptr, R, D, rows_per, dy_group,        \
+                                   1.f / dy_group);                                                                 \
+        } else if (x_f32)                                                                                          \
             hipLaunchKernelGGL((k_norm_bwd<RMSV, ITV, float>), dim3(nb), dim3(NT), smem, st, (const float*)x, ldx,   \
-                               (const bf16*)w, (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum,          \
+                               (const bf16*)w, dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum,                      \
                                dw ? dwp : nullptr, (RMSV || !db) ? nullptr : dbp, R, D, rows_per);                 \
         else                                                                                                       \
             hipLaunchKernelGGL((k_norm_bwd<RMSV, ITV, bf16>), dim3(nb), dim3(NT), smem, st, (const bf16*)x, ldx,     \
-                               (const bf16*)w, (const bf16*)dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum,          \
+                               (const bf16*)w, dy, lddy, mean, rstd, (bf16*)dx, lddx, dx_accum,                      \
                                dw ? dwp : nullptr, (RMSV || !db) ? nullptr : dbp, R, D, rows_per);                 \
     } while (0)
     const int it = (D + 511) / 512;
@@ -1131,7 +1165,7 @@ int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t
     // parameters up to 16384. A small grid leaves CUs to the GEMMs of the concurrent teacher forward
     // (a v8 GEMM workgroup needs a whole CU, so every CU holding AdamW waves is closed to it).
     int grid = grid_for(n, 256, 16384);
-    if (const char* e = std::getenv("KD_ADAMW_GRID"); e && std::atoi(e) > 0) grid = std::min(grid, std::atoi(e));
+    if (const int cap = ab_knob("KD_ADAMW_GRID", 0); cap > 0) grid = std::min(grid, cap);
     hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, as_stream(stream), p, (bf16*)pb, g, m, v, n,
                        lr, b1, b2, eps, wd, bc1, bc2, gscale, skip, n_skip);
     KD_LAUNCH_CHECK("k_adamw");
@@ -1151,6 +1185,16 @@ int launch_sumsq(const float* x, int64_t n, float* out, void* stream) {
     KD_CHECK_ARG(x && out, "sumsq: null pointer");
     hipLaunchKernelGGL(k_sumsq, dim3(grid_for(n, 256, 2048)), dim3(256), 0, as_stream(stream), x, n, out);
     KD_LAUNCH_CHECK("k_sumsq");
+    return KD_OK;
+}
+
+int launch_scale_f32(const float* x, const float* s_dev, float* y, int64_t n, void* stream) {
+    KD_CHECK_ARG(x && y, "scale_f32: null pointer");
+    KD_CHECK_SHAPE(n >= 0, "scale_f32: n < 0");
+    if (n == 0) return KD_OK;
+    hipLaunchKernelGGL(k_scale_f32, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, as_stream(stream),
+                       x, s_dev, y, n);
+    KD_LAUNCH_CHECK("k_scale_f32");
     return KD_OK;
 }
 

@@ -275,10 +275,7 @@ struct GemmArgs {
 };
 
 // split-K default of the runtime's GEMMs (KD_GEMM_SPLIT_K: 0 = the cost model, 1 = never split)
-static const int g_split_default = [] {
-    const char* e = std::getenv("KD_GEMM_SPLIT_K");
-    return e ? std::atoi(e) : 0;
-}();
+static const int g_split_default = ab_knob("KD_GEMM_SPLIT_K", 0);
 
 int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int64_t ldc, const GemmArgs& g) {
     kd_gemm_desc d;
@@ -305,10 +302,7 @@ int gemm(hipStream_t s, void* ws, int M, int N, int K, Op a, Op b, void* C, int6
 
 // the dgrad GEMMs feeding an activation backward run it in their epilogue (KD_ACT_DGELU_TANH /
 // KD_ACT_DSWIGLU) where the tiled GEMM kernels take the shape; KD_FUSE_DACT=0 turns it off (A/B)
-static const bool g_fuse_dact = [] {
-    const char* e = std::getenv("KD_FUSE_DACT");
-    return !(e && e[0] == '0');
-}();
+static const bool g_fuse_dact = ab_knob("KD_FUSE_DACT", 1) != 0;
 static bool fused_dact_ok(int64_t M, int64_t N) {
     return g_fuse_dact && M >= 128 && N >= 128 && N % 8 == 0 && M * N >= (int64_t)1 << 20;
 }
@@ -508,10 +502,7 @@ FwdPlan plan_forward(const kd_model* m, int B, int L, int n_tiles, int save, voi
 // KD_PREFETCH_W=1 (A/B): a streaming read of a forward linear's weights (kd_prefetch) right before
 // its GEMM -- every weight is read a whole step after its last use, and a GEMM that meets cold
 // weights stalls on them tile by tile (tools/ab_cold.py --prefetch)
-static const int g_prefetch_w = [] {
-    const char* e = std::getenv("KD_PREFETCH_W");
-    return e ? std::atoi(e) : 0;
-}();
+static const int g_prefetch_w = ab_knob("KD_PREFETCH_W", 0);
 
 int lin(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int N, int K, const bf16* x, int64_t ldx, int widx,
         void* out, int64_t ldo, const GemmArgs& g) {
@@ -541,10 +532,7 @@ int lin(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int N, int K, const
 // epilogue writes head-major q / k / v (kd_qkv_scatter) where the tiled kernels take the shape
 // and the weight is on the bf16 path; else the GEMM into `qkv` and k_qkv_split (same bits).
 // KD_FUSE_QKV=0 turns the fusion off (A/B).
-static const bool g_fuse_qkv = [] {
-    const char* e = std::getenv("KD_FUSE_QKV");
-    return !(e && e[0] == '0');
-}();
+static const bool g_fuse_qkv = ab_knob("KD_FUSE_QKV", 1) != 0;
 
 int qkv_proj(kd_model* m, const FwdPlan& P, hipStream_t s, int M, int K, const bf16* x, int widx, const void* bias,
              bf16* qkv, void* q, void* k, void* v, const float* cs, const float* sn, int B, int S, int nq, int nkv,
@@ -723,7 +711,7 @@ BwdPlan plan_backward(const kd_model* m, int B, int L, int n_tiles, void* base) 
     P.do_ = A.take<bf16>(M * qd);
     // the attention backward writes the fused q|k|v gradient directly (kd_attn_bwd_desc.dqkv); the
     // head-major dq / dk / dv + kd_qkv_merge path only with KD_ATTN_DQKV=0 (A/B)
-    const bool merge_ab = [] { const char* e = std::getenv("KD_ATTN_DQKV"); return e && std::atoi(e) == 0; }();
+    const bool merge_ab = ab_knob("KD_ATTN_DQKV", 1) == 0;
     P.dq = merge_ab ? A.take<float>(M * qd) : nullptr;
     P.dk = merge_ab ? A.take<bf16>(M * kvd) : nullptr;
     P.dv = merge_ab ? A.take<bf16>(M * kvd) : nullptr;
@@ -741,7 +729,7 @@ BwdPlan plan_backward(const kd_model* m, int B, int L, int n_tiles, void* base) 
     P.dh2v = A.take<bf16>(NT * D);
     P.dov = A.take<bf16>(NT * D);
     P.deltav = A.take<float>((int64_t)NI * c.v_heads * np);
-    if (const char* e = std::getenv("KD_ATTN_DQKV"); e && std::atoi(e) == 0) {
+    if (ab_knob("KD_ATTN_DQKV", 1) == 0) {
         P.dqv = A.take<float>((int64_t)NI * c.v_heads * np * hdp);
         P.dkv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
         P.dvv = A.take<bf16>((int64_t)NI * c.v_heads * np * hdp);
@@ -846,7 +834,7 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
     if (dpost)
         KD_TRY(launch_norm_bwd(0, F.x_vis_last, D, m->W(m->i_post_w), dpost, D, F.pm, F.pr, dx, D, 1,
                                gw ? m->G(m->i_post_w) : nullptr, gw ? m->G(m->i_post_b) : nullptr, 1, P.norm_ws,
-                               P.norm_ws_bytes, NT, D, s, f32));
+                               P.norm_ws_bytes, NT, D, s, f32, np));   // dpost: fp32 per tile, / np per row
     GemmArgs g0;
     for (int i = c.v_layers - 1; i >= 0; --i) {
         const VisLayerBufs& b = F.vl[i];
@@ -1057,8 +1045,7 @@ int kd_model_create(const kd_model_config* cfg, const void* weights, float* grad
     m->g = grad;
     const int on = grad ? 1 : 0;
     m->train_vision = m->train_projector = m->train_language = on;
-    const char* e = std::getenv("KD_WGRAD_SPLIT_K");
-    m->lane_split_k = e ? std::atoi(e) : 0;
+    m->lane_split_k = kd::ab_knob("KD_WGRAD_SPLIT_K", 0);
     m->i_post_w = m->i_vis0 + cfg->v_layers * kd::VNF;
     m->i_post_b = m->i_post_w + 1;
     m->i_p1w = m->i_post_b + 1;

@@ -230,9 +230,6 @@ class _ErrorWatch:
         if bits & 2:
             raise RuntimeError(f"student CE: target {lab} is out of bounds (not -100 and not in [0, {V})) "
                                f"at batch {row // L}, position {row % L}")
-        if bits & 4:
-            raise RuntimeError("kd_loss: a row's slice hand-off timed out (the loss kernel's workgroups were "
-                               "not resident together); this step's gradient was not applied")
         for who, e in (("student", serr), ("teacher", terr)):
             if e & 1:
                 raise RuntimeError(f"{who} embed_tokens: input id outside the vocabulary")
@@ -249,7 +246,7 @@ class _KDBase(_Base):
     def __init__(self, model_name_student, model_name_teacher, processor=None, learning_rate=1e-5, phase=1,
                  seed_teacher: int = 1, seed_student: int = 2, state_dict=None, loss_group_size: int | None = None,
                  accumulate_grad_batches: int | None = None, teacher_fp8: bool | str = False,
-                 grad_comm_dtype=None, **_ignored):
+                 grad_comm_dtype=None, teacher_residual_f32: bool = False, **_ignored):
         super().__init__()
         self.phase = phase
         self.learning_rate = learning_rate
@@ -321,6 +318,11 @@ class _KDBase(_Base):
         # fp8 (e4m3) teacher weights, quantised once after the broadcast (BASELINE config c4;
         # the reference loads the teacher fp16, DT:43-48)
         # teacher_fp8: False, True (= "all") or a modeling.FP8_FAMILIES policy name ("lm", "lm_mlp", ...)
+        # teacher_residual_f32: the teacher's 3584-wide Qwen2 residual stream in fp32 as well (the
+        # c1 reference teacher runs fp32 end to end, LB:29-33; default bf16)
+        self.teacher_residual_f32 = bool(teacher_residual_f32)
+        if self.teacher_residual_f32 and self.teacher_model is not None:
+            self.teacher_model.set_lm_stream_f32(True)
         if teacher_fp8 is True:
             teacher_fp8 = "all"
         self.teacher_fp8 = teacher_fp8 if (teacher_fp8 and self.teacher_model is not None) else False
@@ -520,7 +522,9 @@ class _KDBase(_Base):
         del dl, ctx["dlogits"]
         dpost = None
         if ctx["dps"] is not None and s.train_vision:
-            dpost = ops.row_group_mean_bwd(ctx["dps"], s.cfg.vision.n_patches, scale_dev=gscale)
+            # the gradient of each tile's pooled feature, fp32 (kd_model_backward spreads it over the
+            # tile's rows without a bf16 rounding: tools/ntx_bias_study.py)
+            dpost = ops.scale_f32(ctx["dps"], gscale)
         s.backward(sf, dhn, dpost, on_layer_done=self._on_layer_done if sync else None)
         if self._gsync is not None:
             self._gsync.end(*self._trainable_range())
@@ -619,7 +623,8 @@ class _KDBase(_Base):
 
     def _run_hparams(self):
         return {"loss_group_size": self.loss_group_size, "accumulate_grad_batches": self.accumulate_grad_batches,
-                "teacher_fp8": getattr(self, "teacher_fp8", False)}
+                "teacher_fp8": getattr(self, "teacher_fp8", False),
+                "teacher_residual_f32": getattr(self, "teacher_residual_f32", False)}
 
     def on_train_epoch_end(self):
         """A batch rejected among the last steps of an epoch is reported here (the reference
@@ -657,7 +662,7 @@ class _KDBase(_Base):
             elif name in hp:
                 args[name] = hp[name]
         if var_kw:   # the saved run knobs a subclass forwards to _KDBase through **kw
-            for name in ("loss_group_size", "accumulate_grad_batches", "teacher_fp8"):
+            for name in ("loss_group_size", "accumulate_grad_batches", "teacher_fp8", "teacher_residual_f32"):
                 if name in hp and name not in args and name not in kw:
                     args[name] = hp[name]
         kw.pop("torch_dtype", None)   # the build's weights are bf16 in HBM whatever the caller's dtype

@@ -444,6 +444,7 @@ class LlavaOnevisionModel:
         # rounding after every residual add moved the gradient norm by +0.12 % (tools/grad_bias_study.py)
         self.residual_f32 = (False, False)
         self.fp8_families = 0
+        self.lm_stream_f32 = False
         self.set_residual_f32(*self._default_streams())
 
     def set_residual_f32(self, vision: bool, language: bool):
@@ -546,8 +547,18 @@ class LlavaOnevisionModel:
 
     def _default_streams(self):
         """(vision, language) fp32 residual streams: both for the trainable student, the
-        SigLIP tower only for a frozen teacher."""
-        return True, bool(self.P.trainable)
+        SigLIP tower only for a frozen teacher unless `lm_stream_f32` is set (its 3584-wide
+        Qwen2 stream in fp32 too: the c1 reference teacher's precision, LB:29-33)."""
+        return True, bool(self.P.trainable) or self.lm_stream_f32
+
+    def set_lm_stream_f32(self, on: bool):
+        """Default precision of the Qwen2 residual stream of a frozen model (the teacher):
+        fp32 (on) or bf16.  The fp8 path keeps bf16 where its residual linears run fp8."""
+        self.lm_stream_f32 = bool(on)
+        if self.fp8:
+            self.enable_fp8(self.fp8_families)
+        else:
+            self.set_residual_f32(*self._default_streams())
 
     def _workspace(self, key, nbytes):
         """One cached workspace per call shape: a save=1 forward's workspace holds the

@@ -580,6 +580,15 @@ def sumsq(x, out):
     return out
 
 
+def scale_f32(x, s_dev=None, out=None):
+    """out = x * s_dev (a device fp32 scalar; None: a copy), fp32 (kd_scale_f32)."""
+    _require(x, torch.float32, "scale_f32.x")
+    if out is None:
+        out = torch.empty_like(x)
+    NV.call("kd_scale_f32", x.data_ptr(), _ptr(s_dev), out.data_ptr(), x.numel(), _stream())
+    return out
+
+
 def scalar_mul(a, b, out=None):
     """out = a * b elementwise on device fp32 scalars (kd_scalar_mul)."""
     _require(a, torch.float32, "a")

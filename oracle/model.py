@@ -126,6 +126,7 @@ class OracleLlava:
             x = x + F.linear(F.silu(F.linear(h, w[p + "mlp.gate_proj.weight"])) * F.linear(h, w[p + "mlp.up_proj.weight"]),
                              w[p + "mlp.down_proj.weight"])
         hn = rms(x, w[lp + "norm.weight"])
+        self.last_hn = hn     # the lm_head input (parity tests split the logits' error at it)
         W = w["language_model.lm_head.weight"] if "language_model.lm_head.weight" in w else w[lp + "embed_tokens.weight"]
         return F.linear(hn, W)
 

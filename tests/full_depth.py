@@ -1,0 +1,244 @@
+"""Full-depth model parity of BASELINE config c1 (logit-based KD, LoCa T = 1; LB:29-33,
+:125-169, :208-261): the HIP training_step of the drop-in module with the REAL 7B teacher and
+0.5B student (all 26 + 28 / 26 + 24 layers, L = 1536, one 336x336 sample) against the pinned
+CPU oracle (oracle/model.py, fp32 end to end as the reference's LB teacher and student) run on
+the SAME weights (the device's bf16 flat buffers, copied to the host and widened to fp32) and
+the same batch.  Shared by tests/test_full_depth_parity_gpu.py and tools/parity_report.py
+--full-depth.  GPU only; ~40 GB of host memory for the oracle (weights + activations).
+
+Measured (every value relative to the fp32 oracle, the tolerance of north_star |d| <= 1e-4 +
+1e-3 |ref| where it applies):
+  terms      KD term, student CE, teacher CE, total
+  lse        per-row logsumexp of the student AND the teacher logits (all 1536 rows)
+  logits     sampled rows of the student logits, split at the lm_head: the stored bf16 logits,
+             the same GEMM with an fp32 output (no final rounding), and the floor a single bf16
+             rounding of the reference's own lm_head input leaves
+  grads      the gradient's total norm, per parameter group and per parameter (norm and
+             cosine against the oracle's full fp32 gradient)
+  floor      optionally the same oracle run in plain bf16 (weights and activations bf16), the
+             yardstick where a figure misses the north-star
+"""
+from __future__ import annotations
+
+import gc
+import math
+import time
+
+import torch
+
+S_NAME, T_NAME = "llava-hf/llava-onevision-qwen2-0.5b-ov-hf", "llava-hf/llava-onevision-qwen2-7b-ov-hf"
+ATOL, RTOL = 1e-4, 1e-3
+N_ROWS = 48            # sampled student-logit rows (all 151,936 columns each)
+
+
+def _log(msg):
+    print(f"[full_depth {time.strftime('%H:%M:%S')}] {msg}", flush=True)
+
+
+def _ns(got: float, ref: float) -> dict:
+    d = abs(got - ref)
+    return dict(got=got, ref=ref, abs=d, rel=d / abs(ref) if ref else None, ok=bool(d <= ATOL + RTOL * abs(ref)))
+
+
+def _cmp_vec(got: torch.Tensor, ref: torch.Tensor) -> dict:
+    """Elementwise: max |d|, max rel, fraction within the north-star."""
+    got, ref = got.double().reshape(-1), ref.double().reshape(-1)
+    d = (got - ref).abs()
+    tol = ATOL + RTOL * ref.abs()
+    return dict(max_abs=float(d.max()), max_rel=float((d / ref.abs().clamp_min(1e-30)).max()),
+                frac_within=float((d <= tol).double().mean()), ok=bool((d <= tol).all()),
+                rel_l2=float((got - ref).norm() / ref.norm()))
+
+
+def batch_cpu():
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    return synthetic_batch(1, "cpu", L=1536, seed=0, pixel_dtype=torch.bfloat16, cpu_rng=True)
+
+
+def _to(b, dev):
+    return {k: (v.to(dev) if torch.is_tensor(v) and k != "image_sizes" else v) for k, v in b.items()}
+
+
+def group_of(name: str) -> str:
+    """Parameter group: the per-layer tensors of one kind summed over layers."""
+    for tag in ("embed_tokens", "lm_head", "model.norm.weight", "patch_embedding", "position_embedding",
+                "post_layernorm", "multi_modal_projector", "image_newline"):
+        if tag in name:
+            return name
+    return ".".join(p for p in name.split(".") if not p.isdigit())
+
+
+def row_index(L: int = 1536, n: int = N_ROWS):
+    g = torch.Generator().manual_seed(1234)
+    return torch.randperm(L, generator=g)[:n].sort().values
+
+
+def hip_step(dev, teacher_residual_f32: bool = False, keep_weights: bool = True):
+    """One training_step + backward of LogitBasedKD at full size, bs 1.  Returns (results on
+    the host, teacher state_dict, student state_dict) -- the weights as fp32 host tensors."""
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
+    m = K.LogitBasedKD(S_NAME, T_NAME, teacher_residual_f32=teacher_residual_f32)
+    bc = batch_cpu()
+    b = _to(bc, dev)
+    m.keep_logits = True
+    loss = m.training_step(b, 0)
+    loss.backward()
+    m.check_errors()
+    torch.cuda.synchronize()
+    s3, t3 = m.last_logits
+    kd, ce, tce, tot = m.last_terms.tolist()
+    rows = row_index()
+    res = dict(terms=dict(kd_term=kd, student_ce=ce, teacher_ce=tce, total=float(loss.item())),
+               weights_checksum=[float(m.teacher_model.P.flat[:1 << 22].float().sum()),
+                                 float(m.student_model.P.flat[:1 << 22].float().sum())],
+               s_lse=torch.logsumexp(s3[0].double(), -1).cpu(),
+               t_lse=torch.logsumexp(t3[0].double(), -1).cpu(),
+               s_rows=s3[0, rows.to(dev)].float().cpu(),
+               t_rows=t3[0, rows.to(dev), :s3.shape[-1]].float().cpu())
+    m.last_logits = None
+    del s3, t3
+    # the lm_head again on the same final-norm hidden state with an fp32 output: the logits before
+    # their bf16 rounding (the forward is deterministic and no optimizer step ran)
+    s = m.student_model
+    fwd = s.forward(b["depth_input_ids"], b["depth_pixel_values"], b["image_sizes"])
+    hn = fwd["hn"][rows.to(dev)].contiguous()
+    res["s_rows_f32"] = ops.gemm(hn, s.lm_head_weight(), out_dtype=torch.float32).cpu()
+    res["hn_rows"] = hn.float().cpu()
+    del fwd, hn
+    P = s.P
+    g = P.grad
+    torch.cuda.synchronize()
+    grads = {}
+    for spec in P.specs:
+        v = P.view(spec.name, g)
+        if spec.ckpt_shape is not None:
+            v = v[:, :math.prod(spec.ckpt_shape[1:])].reshape(spec.ckpt_shape)
+        grads[spec.name] = v.cpu().clone()
+    res["grads"] = grads
+    tsd = ssd = None
+    if keep_weights:
+        tsd = {k: v.detach().float().cpu() for k, v in m.teacher_model.P.state_dict().items()}
+        ssd = {k: v.detach().float().cpu() for k, v in P.state_dict().items()
+               if k != "language_model.lm_head.weight"}     # tied: one tensor, as transformers
+    del m, loss, b
+    gc.collect()
+    torch.cuda.empty_cache()
+    return res, tsd, ssd
+
+
+def oracle_step(tsd, ssd, dtype=torch.float32):
+    """The pinned CPU oracle's LB step (compute_loca_loss at T = 1 + the student CE, LB:164-165)
+    on the same weights, in `dtype`; the student gradient by autograd."""
+    from oracle import kd_losses as KL
+    from oracle.model import OracleLlava
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import STUDENT_05B, TEACHER_7B
+    b = batch_cpu()
+    for k in ("rgb_pixel_values", "depth_pixel_values"):
+        b[k] = b[k].to(dtype)
+    tw = {k: v.to(dtype) for k, v in tsd.items()}
+    sw = {k: v.detach().to(dtype).requires_grad_(True) for k, v in ssd.items()}   # leaves (fp32: no copy)
+    teacher, student = OracleLlava(tw, TEACHER_7B), OracleLlava(sw, STUDENT_05B)
+    with torch.no_grad():
+        t_logits, _ = teacher(b["rgb_input_ids"], b["rgb_pixel_values"], b["image_sizes"])
+    del teacher, tw
+    gc.collect()
+    s_logits, _ = student(b["depth_input_ids"], b["depth_pixel_values"], b["image_sizes"])
+    hn = student.last_hn.detach()
+    labels = b["labels"]
+    kd = KL.loca_kd_term(t_logits, s_logits, labels, T=KL.LB_HPARAMS["T"], alpha=KL.LB_HPARAMS["alpha"])
+    ce = KL.causal_lm_ce(s_logits, labels)
+    tce = KL.causal_lm_ce(t_logits, labels)
+    total = kd + ce
+    total.float().backward()
+    rows = row_index()
+    res = dict(terms=dict(kd_term=float(kd.detach()), student_ce=float(ce.detach()), teacher_ce=float(tce),
+                          total=float(total.detach())),
+               s_lse=torch.logsumexp(s_logits[0].detach().double(), -1),
+               t_lse=torch.logsumexp(t_logits[0].double(), -1),
+               s_rows=s_logits[0, rows].detach().float(),
+               t_rows=t_logits[0, rows, :s_logits.shape[-1]].float(),
+               hn_rows=hn[0, rows].float(),
+               grads={k: v.grad for k, v in sw.items() if v.grad is not None})
+    del s_logits, t_logits, kd, ce, tce, total, student
+    gc.collect()
+    return res
+
+
+def compare(hip: dict, ref: dict, W: torch.Tensor | None = None) -> dict:
+    """Every figure of `hip` against `ref` (both from hip_step / oracle_step)."""
+    out = {"terms": {k: _ns(hip["terms"][k], ref["terms"][k]) for k in ref["terms"]}}
+    if "weights_checksum" in hip:
+        out["weights_checksum"] = hip["weights_checksum"]
+    out["s_lse"] = _cmp_vec(hip["s_lse"], ref["s_lse"])
+    out["t_lse"] = _cmp_vec(hip["t_lse"], ref["t_lse"])
+    out["s_logits_rows"] = _cmp_vec(hip["s_rows"], ref["s_rows"])
+    out["t_logits_rows"] = _cmp_vec(hip["t_rows"], ref["t_rows"])
+    if "s_rows_f32" in hip:
+        out["s_logits_rows_f32_out"] = _cmp_vec(hip["s_rows_f32"], ref["s_rows"])
+    if "hn_rows" in hip and "hn_rows" in ref:
+        out["hn_rows_rel_l2"] = float((hip["hn_rows"].double() - ref["hn_rows"].double()).norm()
+                                      / ref["hn_rows"].double().norm())
+    if W is not None and "hn_rows" in ref:
+        # one bf16 rounding of the REFERENCE's own lm_head input, fp64 product: the floor of any
+        # bf16-input lm_head, whatever happened upstream
+        one = ref["hn_rows"].bfloat16().double() @ W.double().t()
+        out["s_logits_rows_floor_bf16_input"] = _cmp_vec(one, ref["s_rows"])
+    # gradients: total norm, per group, per parameter
+    hg, rg = hip["grads"], ref["grads"]
+    names = [n for n in rg]
+    tot_h = math.sqrt(sum(float(hg[n].double().pow(2).sum()) for n in names))
+    tot_r = math.sqrt(sum(float(rg[n].double().pow(2).sum()) for n in names))
+    out["grad_total_norm"] = dict(got=tot_h, ref=tot_r, rel=(tot_h - tot_r) / tot_r,
+                                  ok=bool(abs(tot_h - tot_r) <= RTOL * tot_r))
+    groups = {}
+    per = {}
+    for n in names:
+        a, r = hg[n].double().reshape(-1), rg[n].double().reshape(-1)
+        an, rn = float(a.norm()), float(r.norm())
+        cos = float((a @ r) / (an * rn + 1e-300))
+        err = float((a - r).norm())
+        per[n] = dict(ref_norm=rn, norm_rel=(an / rn - 1) if rn > 0 else an, cos=cos, err_rel=err / rn if rn else err)
+        gr = groups.setdefault(group_of(n), [0.0, 0.0, 0.0])
+        gr[0] += rn * rn
+        gr[1] += an * an
+        gr[2] += err * err
+    out["grad_groups"] = {k: dict(ref_norm=math.sqrt(v[0]), norm_rel=math.sqrt(v[1] / v[0]) - 1 if v[0] else None,
+                                  err_rel=math.sqrt(v[2] / v[0]) if v[0] else None)
+                          for k, v in sorted(groups.items())}
+    out["grad_params"] = per
+    worst = sorted(per.items(), key=lambda kv: -abs(kv[1]["err_rel"]))[:8]
+    out["grad_params_worst"] = {k: v for k, v in worst}
+    out["grad_params_min_cos"] = min(v["cos"] for v in per.values() if v["ref_norm"] > 0)
+    return out
+
+
+def measure(dev, floor: bool = False, teacher_stream_ab: bool = False) -> dict:
+    """The whole report: HIP (default teacher stream) vs the fp32 oracle; optionally the plain
+    bf16 oracle (floor) and the HIP step with the teacher's Qwen2 residual stream in fp32."""
+    t0 = time.time()
+    _log("HIP step (teacher Qwen2 stream bf16, the default)")
+    hip, tsd, ssd = hip_step(dev, teacher_residual_f32=False)
+    W = ssd["language_model.model.embed_tokens.weight"]
+    hip32 = None
+    if teacher_stream_ab:
+        _log("HIP step (teacher Qwen2 stream fp32)")
+        hip32, _, _ = hip_step(dev, teacher_residual_f32=True, keep_weights=False)
+    _log(f"fp32 oracle step on the same weights ({torch.get_num_threads()} threads)")
+    ref = oracle_step(tsd, ssd, torch.float32)
+    rep = {"config": "c1: LogitBasedKD (LoCa T = 1), bs 1, L 1536, 336x336, full depth (SigLIP 26 + Qwen2 28 / 24 layers)",
+           "tolerance": f"|d| <= {ATOL} + {RTOL} |ref| (north_star); gradient total norm rel <= {RTOL}",
+           "reference": "oracle/model.py + oracle/kd_losses.py in fp32 on the device's bf16 weights widened to fp32",
+           "hip": compare(hip, ref, W)}
+    if hip32 is not None:
+        rep["hip_teacher_stream_f32"] = compare(hip32, ref, W)
+        del hip32
+    if floor:
+        _log("bf16 oracle step (the floor)")
+        fl = oracle_step(tsd, ssd, torch.bfloat16)
+        fl["grads"] = {k: v.float() for k, v in fl["grads"].items()}
+        rep["bf16_floor"] = compare(fl, ref, None)
+        del fl
+    rep["seconds"] = round(time.time() - t0, 1)
+    _log(f"done in {rep['seconds']} s")
+    return rep

@@ -4,13 +4,18 @@ gradient against the reference's, each next to the bf16 floor (the pinned oracle
 plain bf16, tests/golden/bf16_floor.json).  Used by tests/test_kd_step_gpu.py and
 tools/parity_report.py.  GPU only.
 
-Per-parameter gradient bound (every parameter the reference differentiates):
-  norm   | |g| / |g_ref| - 1 |  <=  max(1e-3, 1.5 x the bf16 floor's own norm miss,
-                                      0.25 x the bf16 floor's relative error |g_bf16 - g_ref| / |g_ref|)
-  cosine cos(g, g_ref)        >=  the bf16 floor's cosine - 1e-3
+Per-parameter gradient bound (every parameter the reference differentiates), never looser than
+1 % on the norm and 0.99 on the cosine:
+  norm   | |g| / |g_ref| - 1 |  <=  min(1e-2, max(1e-3, 1.5 x the bf16 floor's own norm miss,
+                                      0.25 x the bf16 floor's relative error |g_bf16 - g_ref| / |g_ref|))
+  cosine cos(g, g_ref)        >=  max(0.99, the bf16 floor's cosine - 1e-3)
 The floor's relative error is sqrt(2 (1 - cos_floor)); a quarter of it covers parameters whose
 gradient is so small that bf16 noise decides its norm (the Qwen2 k_proj.bias, ~1e-6 of the
 largest gradient: HIP 0.29 % vs the floor's 0.18 % norm miss, both at cosine 0.99996+).
+Where the bf16 floor itself is noise (floor cosine < 0.99 or floor norm miss > 5 %: gradients that
+are a cancelling sum, e.g. the NT-Xent-only SigLIP post_layernorm.bias, whose two tiles'
+contributions cancel to ~8e-4 of each, tools/ntx_bias_study.py) a parameter outside that bound may
+instead meet an ABSOLUTE one:  |g - g_ref| <= 1e-3 x |the same layer's weight gradient (reference)|.
 g_ref: the fp32 oracle's full gradient for the tiny fixtures (the oracle is pinned to the
 reference's recorded norms and heads, tests/test_oracle_model.py); the reference's own
 gradient at GRAD_SAMPLE seeded positions for the real-width fixtures; |g_ref| is always the
@@ -37,6 +42,8 @@ from model_fixtures import EVERY_KIND, batch, grad_sample_index, load, module_na
 ATOL, RTOL = 1e-4, 1e-3   # north_star
 FLOOR = json.loads((Path(__file__).resolve().parent / "golden" / "bf16_floor.json").read_text())
 NORM_MIN, NORM_FLOOR_X, FLOOR_ERR_X, COS_SLACK = 1e-3, 1.5, 0.25, 1e-3
+NORM_CAP, COS_CAP = 1e-2, 0.99          # no bound looser than 1 % on the norm / 0.99 on the cosine
+NOISE_NORM, ABS_REL = 0.05, 1e-3        # the bf16 floor is noise: absolute criterion vs the layer's weight
 ZERO_REL = 1e-2
 
 
@@ -141,10 +148,20 @@ def param_report(name, m, exp):
             rep[n] = dict(ref_norm=rn, norm=gz, q_bias_ref_norm=qn, ratio=gz / qn, bound_ratio=ZERO_REL,
                           exactly_zero=True, ok=bool(gz <= ZERO_REL * qn))
             continue
-        bn = max(NORM_MIN, NORM_FLOOR_X * f["norm_rel"], FLOOR_ERR_X * math.sqrt(max(0.0, 2 * (1 - f["cos"]))))
-        bc = f["cos"] - COS_SLACK
-        rep[n] = dict(ref_norm=rn, norm_rel=norm_rel, cos=cos, floor_norm_rel=f["norm_rel"], floor_cos=f["cos"],
-                      bound_norm_rel=bn, bound_cos=bc, ok=bool(norm_rel <= bn and cos >= bc))
+        bn = min(NORM_CAP, max(NORM_MIN, NORM_FLOOR_X * f["norm_rel"],
+                               FLOOR_ERR_X * math.sqrt(max(0.0, 2 * (1 - f["cos"])))))
+        bc = max(COS_CAP, f["cos"] - COS_SLACK)
+        r = dict(ref_norm=rn, norm_rel=norm_rel, cos=cos, floor_norm_rel=f["norm_rel"], floor_cos=f["cos"],
+                 bound_norm_rel=bn, bound_cos=bc, ok=bool(norm_rel <= bn and cos >= bc), criterion="relative")
+        noise = f["cos"] < COS_CAP or f["norm_rel"] > NOISE_NORM
+        wname = n[:-len("bias")] + "weight" if n.endswith(".bias") else None
+        if not r["ok"] and noise and wname in ref_norm:
+            # |g - g_ref| over the compared entries, scaled to the whole tensor when they are a sample
+            err = float((a - b).norm()) * math.sqrt(g.numel() / a.numel())
+            bound = ABS_REL * ref_norm[wname]
+            r.update(abs_err=err, abs_bound=bound, weight_ref_norm=ref_norm[wname], ok=bool(err <= bound),
+                     criterion="absolute (bf16 floor is noise)")
+        rep[n] = r
     ref_gn = float(exp["grad_total_norm"])
     gn = math.sqrt(tot)
     return rep, dict(got=gn, ref=ref_gn, rel=(gn - ref_gn) / ref_gn,

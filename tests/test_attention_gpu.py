@@ -83,30 +83,6 @@ def test_attn_fwd(B, H, HKV, S, hd, hdp, causal, dev):
     assert (lse - rlse).abs().max().item() < 1e-3 * rlse.abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize("variant", ["16", "32"])
-@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", [CASES[1], CASES[2], CASES[3], CASES[7], CASES[8]])
-def test_attn_fwd_variants_agree(B, H, HKV, S, hd, hdp, causal, variant, dev):
-    """The pipelined 32x32x16 kernel (default), the unpipelined one (KD_ATTN_FWD_V=32) and the
-    16x16x32 one (=16) compute the same softmax; they differ only in the fp32 summation order
-    of the scores / row sums and the sub-tile width of the lazy rescale (which changes the
-    bf16 rounding of P): outputs within 2^-7 (|o| + P|V|), lse within 1e-5 relative."""
-    import os
-    ops = _ops()
-    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev)
-    outs = []
-    try:
-        for var in ("0", variant):
-            os.environ["KD_ATTN_FWD_V"] = var   # read by the launcher on every call
-            outs.append(ops.attn_fwd(q, k, v, hd, causal))
-    finally:
-        os.environ.pop("KD_ATTN_FWD_V", None)
-    (o0, l0), (o1, l1) = outs
-    d = (o0.float() - o1.float()).abs()
-    pabs = _ref_pabs(q[..., :hd].float(), k[..., :hd].float(), v[..., :hd].float(), causal, hd).permute(0, 2, 1, 3)
-    assert bool((d <= 2.0 ** -7 * (o0.float().abs() + pabs) + 1e-4).all()), d.max().item()
-    assert (l0 - l1).abs().max().item() <= 1e-5 * l0.abs().max().item() + 1e-5
-
-
 @pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
 def test_attn_bwd(B, H, HKV, S, hd, hdp, causal, dev):
     ops = _ops()
@@ -125,87 +101,21 @@ def test_attn_bwd(B, H, HKV, S, hd, hdp, causal, dev):
     _close(dv[..., :hd], vf.grad, 8e-2, 3e-2)
 
 
-@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", [CASES[0], CASES[1], CASES[3], CASES[4], CASES[5], CASES[6]])
-def test_attn_bwd_dkdv_variants_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
-    """dK / dV with two 16-key sub-tiles per wave (default) == the one-sub-tile kernel
-    (KD_ATTN_BWD_V=16) bit for bit: the same MFMA sequence and arithmetic per element; only the
-    sharing of LDS fragments between the sub-tiles differs (and fully masked causal query
-    halves are skipped, which adds exact zeros)."""
-    import os
-    ops = _ops()
-    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=4)
-    o, lse = ops.attn_fwd(q, k, v, hd, causal)
-    g = torch.Generator().manual_seed(5)
-    do = torch.randn(B, S, H, hd, generator=g).to(dev, torch.bfloat16)
-    outs = []
-    try:
-        for var in ("0", "16"):
-            os.environ["KD_ATTN_BWD_V"] = var
-            outs.append(ops.attn_bwd(q, k, v, o, do, lse, hd, causal))
-    finally:
-        os.environ.pop("KD_ATTN_BWD_V", None)
-    (dq0, dk0, dv0), (dq1, dk1, dv1) = outs
-    sl = (Ellipsis, slice(0, hd))   # the head-dim padding [hd, hdp) is not an output
-    assert torch.equal(dk0[sl], dk1[sl]) and torch.equal(dv0[sl], dv1[sl]) and torch.equal(dq0[sl], dq1[sl])
-
-
-@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
-def test_attn_fwd_six_waves_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
-    """Forced variant 36: workgroups of six waves (192 query rows; only waves 0-3 stage K/V) ==
-    the four-wave kernel bit for bit: every wave walks its own queries over the same K/V tiles
-    in the same order (causal: the same per-wave tile count).  Head dim 128 keeps four waves."""
-    import os
-    ops = _ops()
-    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=3)
-    outs = []
-    try:
-        for var in ("32", "36"):
-            os.environ["KD_ATTN_FWD_V"] = var
-            outs.append(ops.attn_fwd(q, k, v, hd, causal))
-    finally:
-        os.environ.pop("KD_ATTN_FWD_V", None)
-    (o0, l0), (o1, l1) = outs
-    assert torch.equal(o0, o1) and torch.equal(l0, l1)
-
-@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", CASES)
-def test_attn_fwd_two_blocks_per_wave_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
-    """Forced variant 64 (k_attn_fwd64): two 32-row query blocks per wave sharing every K / V^T
-    fragment read, 256 query rows per workgroup == the four-wave k_attn_fwd32 bit for bit (per
-    query row the same operations in the same order; a wave's two causal blocks end on one tile)."""
-    import os
-    ops = _ops()
-    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=4)
-    outs = []
-    try:
-        for var in ("32", "64"):
-            os.environ["KD_ATTN_FWD_V"] = var
-            outs.append(ops.attn_fwd(q, k, v, hd, causal))
-    finally:
-        os.environ.pop("KD_ATTN_FWD_V", None)
-    (o0, l0), (o1, l1) = outs
-    assert torch.equal(o0, o1) and torch.equal(l0, l1)
-
-
 @pytest.mark.parametrize("B,H,S,hd,hdp", [(2, 2, 729, 72, 96), (1, 16, 729, 72, 96), (1, 3, 100, 64, 64), (2, 4, 200, 128, 128)])
-@pytest.mark.parametrize("bwd_v", ["0", "16"])
-def test_attn_bwd_direct_dqkv_bitexact(B, H, S, hd, hdp, bwd_v, dev):
+def test_attn_bwd_direct_dqkv_bitexact(B, H, S, hd, hdp, dev):
     """kd_attn_bwd_desc.dqkv (MHA): dq | dk | dv written straight into the token-major fused q|k|v
-    gradient == kd_attn_bwd + kd_qkv_merge (no RoPE) bit for bit, for both dK/dV kernels; the
-    columns outside [0, 3 H hd) of a wider row are left untouched."""
-    import os
+    gradient == kd_attn_bwd + kd_qkv_merge (no RoPE) bit for bit (hd 128: the one-sub-tile dK/dV
+    kernel, else the two-sub-tile one); the columns outside [0, 3 H hd) of a wider row are left
+    untouched."""
     ops = _ops()
     q, k, v = _inputs(B, H, H, S, hd, hdp, dev, seed=5)
     g = torch.Generator(device=dev).manual_seed(6)
     o, lse = ops.attn_fwd(q, k, v, hd, False)
     do = torch.randn(B, S, H, hd, device=dev, generator=g).bfloat16()
-    try:
-        os.environ["KD_ATTN_BWD_V"] = bwd_v
-        dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, hd, False)
-        ref = ops.qkv_merge(dq, dk, dv, B, S, H, H, hd, hdp)
-        wide = torch.full((B * S, 3 * H * hd + 8), 7.0, dtype=torch.bfloat16, device=dev)
-        ops.attn_bwd(q, k, v, o, do, lse, hd, False, dqkv=wide[:, : 3 * H * hd + 8])
-    finally:
-        os.environ.pop("KD_ATTN_BWD_V", None)
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, hd, False)
+    ref = ops.qkv_merge(dq, dk, dv, B, S, H, H, hd, hdp)
+    wide = torch.full((B * S, 3 * H * hd + 8), 7.0, dtype=torch.bfloat16, device=dev)
+    ops.attn_bwd(q, k, v, o, do, lse, hd, False, dqkv=wide[:, : 3 * H * hd + 8])
     assert torch.equal(wide[:, : 3 * H * hd], ref)
     assert torch.all(wide[:, 3 * H * hd:] == 7.0)
 
@@ -229,26 +139,3 @@ def test_attn_bwd_direct_dqkv_gqa_bitexact(B, H, HKV, S, hd, rope, dev):
     out = torch.full_like(ref, 3.0)
     ops.attn_bwd(q, k, v, o, do, lse, hd, True, dqkv=out, cos=cos, sin=sin)
     assert torch.equal(out, ref)
-
-
-@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", [(2, 2, 2, 729, 72, 96, False), (1, 14, 2, 256, 64, 64, True),
-                                                    (1, 4, 1, 130, 128, 128, True), (1, 2, 2, 33, 40, 64, False)])
-def test_attn_delta_unrolled_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
-    """k_attn_delta_n (every chunk pair of a row loaded before the sum; hd 64 / 72 / 128) == the
-    generic k_attn_delta loop (KD_ATTN_DELTA_V=1): dq / dk / dv bit for bit (hd 40: both the loop)."""
-    import os
-    ops = _ops()
-    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=9)
-    g = torch.Generator(device=dev).manual_seed(10)
-    o, lse = ops.attn_fwd(q, k, v, hd, causal)
-    do = torch.randn(B, S, H, hd, device=dev, generator=g).bfloat16()
-    outs = []
-    try:
-        for var in ("1", "2"):
-            os.environ["KD_ATTN_DELTA_V"] = var
-            outs.append([t.clone() for t in ops.attn_bwd(q, k, v, o, do, lse, hd, causal)])
-    finally:
-        os.environ.pop("KD_ATTN_DELTA_V", None)
-    sl = (Ellipsis, slice(0, hd))   # the head-dim padding [hd, hdp) is not an output
-    for a, b_ in zip(*outs):
-        assert torch.equal(a[sl], b_[sl])

@@ -1,0 +1,50 @@
+"""BASELINE config c1 at FULL depth against the pinned fp32 oracle on the same weights
+(tests/full_depth.py): the logit-based KD step (LB:125-169, compute_loca_loss at T = 1,
+LB:208-261) with the real 7B teacher (SigLIP 26 layers, Qwen2-7B 28) and 0.5B student (26 +
+24), L = 1536, one 336x336 sample; the reference's LB teacher and student are fp32 end to end
+(LB:29-33), and so is the oracle here.
+
+Held (north_star: |d| <= 1e-4 + 1e-3 |ref|; measured on MI355X, profiles/r05/full_depth.json):
+  KD term, student CE, teacher CE, total         north_star        (2.2e-5 / 1.1e-5 / 1.0e-4 / 1.1e-5 rel)
+  per-row logsumexp, student and teacher logits  north_star, every row   (max 9.8e-6 / 7.2e-5 rel)
+  gradient total norm                            rel <= 1e-3       (-1.5e-4)
+  every parameter's gradient                     norm within 1 %, cosine >= 0.999 vs the oracle's
+                                                 full fp32 gradient (worst: 0.85 % / 0.99972)
+  SigLIP k_proj.bias (exactly zero in exact arithmetic, tests/step_parity.py)
+                                                 |g| <= 1e-2 |q_proj.bias grad| of the same layer
+  raw student logits (48 sampled rows x 151,936) fraction within north_star >= 0.10 (0.119; plain
+                                                 bf16 oracle 0.044): the bf16 rounding of the
+                                                 lm_head INPUT alone leaves 0.41 (stated, not held)
+"""
+import pytest
+import torch
+
+from full_depth import compare, hip_step, oracle_step
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(1200)
+def test_c1_full_depth_matches_fp32_oracle(dev):
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    hip, tsd, ssd = hip_step(dev)
+    ref = oracle_step(tsd, ssd, torch.float32)
+    r = compare(hip, ref, ssd["language_model.model.embed_tokens.weight"])
+    del tsd, ssd
+    for k, v in r["terms"].items():
+        assert v["ok"], (k, v)
+    assert r["s_lse"]["ok"], r["s_lse"]
+    assert r["t_lse"]["ok"], r["t_lse"]
+    assert r["grad_total_norm"]["ok"], r["grad_total_norm"]
+    per = r["grad_params"]
+    for n, v in per.items():
+        if n.startswith("vision_tower.") and n.endswith("self_attn.k_proj.bias"):
+            qn = float(hip["grads"][n.replace("k_proj.bias", "q_proj.bias")].double().norm())
+            gz = float(hip["grads"][n].double().norm())
+            assert gz <= 1e-2 * qn, (n, gz, qn)
+            continue
+        assert abs(v["norm_rel"]) <= 1e-2 and v["cos"] >= 0.999, (n, v)
+    assert r["s_logits_rows"]["frac_within"] >= 0.10, r["s_logits_rows"]
+    # the fp32-output lm_head on the same hidden state: the bf16 rounding of the stored logits
+    # is not where the raw-logit misses come from
+    assert r["s_logits_rows_f32_out"]["frac_within"] >= r["s_logits_rows"]["frac_within"] - 0.01

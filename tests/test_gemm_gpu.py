@@ -93,7 +93,7 @@ def test_epilogue_bias_act_residual_aux_accumulate(dev):
     assert (out - 0.5 * (a.float() @ w.float().t())).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("variant,split_k", [(1, 1), (5, 1), (6, 1), (7, 1), (16, 1), (20, 1), (16, 3), (0, 0)])
+@pytest.mark.parametrize("variant,split_k", [(1, 1), (5, 1), (6, 1), (7, 1), (16, 1), (16, 3), (0, 0)])
 def test_fp32_residual_stream(variant, split_k, dev):
     """C (fp32) = A B^T + bias + residual (fp32): the fp32 residual stream's epilogue (o_proj /
     fc2 / down_proj with kd_model_set_residual_f32) in every kernel and through the split-K
@@ -115,7 +115,7 @@ def test_fp32_residual_stream(variant, split_k, dev):
         ops.gemm(a, w, residual=res)   # bf16 C with an fp32 residual is rejected
 
 
-VARIANTS = [1, 5, 6, 7, 16, 20]   # 128x128 v1; v3 256x256 / 256x128 / 128x256 (8 waves); v8 256x256 (4 waves, AGPR acc);
+VARIANTS = [1, 5, 6, 7, 16]   # 128x128 v1; v3 256x256 / 256x128 / 128x256 (8 waves); v8 256x256 (4 waves, AGPR acc);
 #                                  v9 256x256 (8 waves, ping-pong)
 
 
@@ -142,7 +142,7 @@ def test_variants_all_layouts(variant, M, N, K, dev):
         _check(ops.gemm(at.t(), w, variant=variant), at.float().t() @ w.float().t())
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 16, 20])
+@pytest.mark.parametrize("variant", [5, 6, 7, 16])
 def test_variant_epilogue(variant, dev):
     ops = _ops()
     M, N, K = 1458, 1152, 192
@@ -162,7 +162,7 @@ def test_variant_epilogue(variant, dev):
 
 
 @pytest.mark.parametrize("split", [2, 3, 7])
-@pytest.mark.parametrize("variant", [0, 6, 7, 16, 20])
+@pytest.mark.parametrize("variant", [0, 6, 7, 16])
 @pytest.mark.parametrize("M,N,K", [(520, 384, 2248), (1152, 1152, 5832)])
 def test_splitk_all_layouts(split, variant, M, N, K, dev):
     """Forced K splits (fp32 partial planes + reduce) in every operand layout; K is not a
@@ -308,26 +308,6 @@ def test_swiglu_epilogue_bitexact(M, I, K, dev):
     _check(a, torch.nn.functional.silu(g[:, :I]) * g[:, I:])
 
 
-@pytest.mark.parametrize("M,N,K", [(6144 // 4, 896, 4864 // 2), (1456, 1152, 1152), (304, 520, 600), (4096, 4096, 4096)])
-def test_v9_bitexact_vs_v8(M, N, K, dev):
-    """v9 (8-wave ping-pong) accumulates every output element over the same k32 MFMA
-    sequence as v8, so the two agree bit for bit in every operand layout, with and without
-    the SwiGLU epilogue."""
-    ops = _ops()
-    a = _rand(M, K, dev=dev, seed=90)
-    w = _rand(N, K, dev=dev, seed=91, scale=0.05)
-    at = _rand(K, M, dev=dev, seed=92)
-    wt = _rand(K, N, dev=dev, seed=93, scale=0.05)
-    for A, B in ((a, w), (a, wt.t()), (at.t(), w), (at.t(), wt.t())):
-        assert torch.equal(ops.gemm(A, B, variant=20, split_k=1), ops.gemm(A, B, variant=16, split_k=1))
-    if N % 256 == 0:
-        g9 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        g8 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        o9 = ops.gemm(a, w, act="swiglu", aux=g9, variant=20)
-        o8 = ops.gemm(a, w, act="swiglu", aux=g8, variant=16)
-        assert torch.equal(o9, o8) and torch.equal(g9, g8)
-
-
 @pytest.mark.parametrize("variant", [0, 5, 6, 7, 16])
 @pytest.mark.parametrize("M, N, K", [(1100, 1040, 392), (6144 // 2, 4864, 896), (5832 // 4, 4304, 1152)])
 def test_fused_backward_activation(variant, M, N, K, dev):
@@ -383,29 +363,4 @@ def test_qkv_scatter_epilogue_equals_gemm_then_split(shape, variant, dev):
     for got, ref, n in ((q, q0, "q"), (k, k0, "k"), (v, v0, "v")):
         assert torch.equal(got, ref), f"{n}: {int((got != ref).sum())} elements differ"
 
-
-@pytest.mark.parametrize("M,N,K", [(6144 // 4, 896, 4864 // 2), (1456, 1152, 1152), (304, 520, 600), (4096, 4096, 4096),
-                                   (5832 // 4, 4304, 1152), (512, 512, 2248), (256, 768, 32), (300, 272, 4304)])
-def test_register_staged_v8_bitexact(M, N, K, dev):
-    """The register-staged v8 build (variant 22: buffer loads to VGPRs + ds_write_b128 instead of
-    LDS-DMA, the same LDS image) accumulates over the same k32 MFMA sequence as v8: bit for bit
-    equal, plain and with the epilogue (bias, gelu, residual, aux) and the SwiGLU build; K tails
-    of every length, partial tiles, K shorter than the prefetch ring."""
-    ops = _ops()
-    a = _rand(M, K, dev=dev, seed=120)
-    w = _rand(N, K, dev=dev, seed=121, scale=0.05)
-    assert torch.equal(ops.gemm(a, w, variant=22, split_k=1), ops.gemm(a, w, variant=16, split_k=1))
-    bias = _rand(N, dev=dev, seed=122)
-    res = _rand(M, N, dev=dev, seed=123)
-    ax16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    ax22 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    o16 = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=res, aux=ax16, variant=16, split_k=1)
-    o22 = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=res, aux=ax22, variant=22, split_k=1)
-    assert torch.equal(o22, o16) and torch.equal(ax22, ax16)
-    if N % 256 == 0:
-        g16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        g22 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        s16 = ops.gemm(a, w, act="swiglu", aux=g16, variant=16)
-        s22 = ops.gemm(a, w, act="swiglu", aux=g22, variant=22)
-        assert torch.equal(s22, s16) and torch.equal(g22, g16)
 

@@ -230,3 +230,25 @@ def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev, mo
     assert torch.allclose(a, b, rtol=2e-6, atol=1e-9), (a, b)
     dd = (d0.float() - d1.float()).abs()
     assert bool((dd <= 2.0 ** -7 * d0.float().abs() + 1e-12).all()), dd.max().item()
+
+
+@pytest.mark.parametrize("B,L,V,T", [(2, 384, 151936, 1.0), (1, 257, 151936, 0.8), (2, 64, 60000, 1.0)])
+def test_register_resident_loca_stand_in_is_bit_identical(B, L, V, T, dev, monkeypatch):
+    """Co-residency is not required by k_loss_grad_loca_rr: a slice whose partner slices have not
+    handed over their pass-A partials within the poll budget computes them itself (same body, same
+    lane mapping, same reduction order).  KD_LOSS_RR_POLL_US=0 forces that stand-in path for every
+    absent partial of every row; the loss terms and dlogits must be the default path's bits, and no
+    error may be raised (the loss must never depend on workgroups being resident)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(11)
+    s = (torch.randn(B, L, V, generator=g) * 2).to(dev, torch.bfloat16)
+    t = (torch.randn(B, L, V + 128, generator=g) * 2).to(dev, torch.bfloat16)
+    labels = torch.randint(0, V, (B, L), generator=g).to(dev)
+    out = []
+    for us in ("200", "0"):
+        monkeypatch.setenv("KD_LOSS_RR_POLL_US", us)
+        out.append(ops.kd_loss_fwd_bwd(s, t, labels, "loca", temperature=T, check=True))
+    torch.cuda.synchronize()
+    (l0, d0), (l1, d1) = out
+    assert torch.equal(l0.cpu(), l1.cpu()), (l0, l1)
+    assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))

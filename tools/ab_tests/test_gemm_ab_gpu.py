@@ -1,0 +1,59 @@
+"""GEMM A/B builds (v9 = variant 20, register staging = variant 22) bit-exact against v8, moved from tests/test_gemm_gpu.py (round 5).
+
+Runs against the tools' A/B library, built with
+    python knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd/csrc/build.py --ab
+    python -m pytest tools/ab_tests -m gpu        (conftest.py points KDSTEP_LIB at tools/ab/libkdstep_ab.so)
+The product library rejects these variants / ignores these switches.
+"""
+import pytest
+import torch
+
+from test_gemm_gpu import _ops, _rand
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,K", [(6144 // 4, 896, 4864 // 2), (1456, 1152, 1152), (304, 520, 600), (4096, 4096, 4096)])
+def test_v9_bitexact_vs_v8(M, N, K, dev):
+    """v9 (8-wave ping-pong) accumulates every output element over the same k32 MFMA
+    sequence as v8, so the two agree bit for bit in every operand layout, with and without
+    the SwiGLU epilogue."""
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=90)
+    w = _rand(N, K, dev=dev, seed=91, scale=0.05)
+    at = _rand(K, M, dev=dev, seed=92)
+    wt = _rand(K, N, dev=dev, seed=93, scale=0.05)
+    for A, B in ((a, w), (a, wt.t()), (at.t(), w), (at.t(), wt.t())):
+        assert torch.equal(ops.gemm(A, B, variant=20, split_k=1), ops.gemm(A, B, variant=16, split_k=1))
+    if N % 256 == 0:
+        g9 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        g8 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        o9 = ops.gemm(a, w, act="swiglu", aux=g9, variant=20)
+        o8 = ops.gemm(a, w, act="swiglu", aux=g8, variant=16)
+        assert torch.equal(o9, o8) and torch.equal(g9, g8)
+
+
+@pytest.mark.parametrize("M,N,K", [(6144 // 4, 896, 4864 // 2), (1456, 1152, 1152), (304, 520, 600), (4096, 4096, 4096),
+                                   (5832 // 4, 4304, 1152), (512, 512, 2248), (256, 768, 32), (300, 272, 4304)])
+def test_register_staged_v8_bitexact(M, N, K, dev):
+    """The register-staged v8 build (variant 22: buffer loads to VGPRs + ds_write_b128 instead of
+    LDS-DMA, the same LDS image) accumulates over the same k32 MFMA sequence as v8: bit for bit
+    equal, plain and with the epilogue (bias, gelu, residual, aux) and the SwiGLU build; K tails
+    of every length, partial tiles, K shorter than the prefetch ring."""
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=120)
+    w = _rand(N, K, dev=dev, seed=121, scale=0.05)
+    assert torch.equal(ops.gemm(a, w, variant=22, split_k=1), ops.gemm(a, w, variant=16, split_k=1))
+    bias = _rand(N, dev=dev, seed=122)
+    res = _rand(M, N, dev=dev, seed=123)
+    ax16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    ax22 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    o16 = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=res, aux=ax16, variant=16, split_k=1)
+    o22 = ops.gemm(a, w, bias=bias, act="gelu_tanh", residual=res, aux=ax22, variant=22, split_k=1)
+    assert torch.equal(o22, o16) and torch.equal(ax22, ax16)
+    if N % 256 == 0:
+        g16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        g22 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        s16 = ops.gemm(a, w, act="swiglu", aux=g16, variant=16)
+        s22 = ops.gemm(a, w, act="swiglu", aux=g22, variant=22)
+        assert torch.equal(s22, s16) and torch.equal(g22, g16)

@@ -1,41 +1,63 @@
-# Round-end style GPU pass (run under gpurun):
-#   STEPS="tests parity bench prof pmc" ROUND=r02 bash tools/gpu_round.sh
-# smoke  : __graft_entry__.smoke()
-# tests  : pytest -m gpu (every parity test); gemm: only the GEMM / fp8 GEMM tests
-# c2, c4 : bench.py --config c2 / c4 (the other single-GPU BASELINE configs) -> gpurun_out/bench_c*.log
-# parity : tools/parity_report.py -> gpurun_out/parity.json (per-term deltas vs the reference)
-# bench  : python bench.py (the driver's default line) -> gpurun_out/bench.log
-# prof   : rocprofv3 --kernel-trace --stats of a serialized bench (its roofline-kernel average
-#          is what bench.py's HIP-event pass measures)
-# step   : kernel trace of the concurrent (default) bench -> gpurun_out/step_breakdown.txt
-# blas   : PMC clock / MFMA-busy of kd_gemm vs hipBLASLt on the two big shapes (tools/pmc_vs_blas.sh)
-# pmc    : HBM traffic per kernel (tools/pmc_bench.sh, two --pmc passes)
-# Every step has its own time limit; the first failure ends the script.
+# The one GPU runner (run under gpurun): a sequence of named steps, each with its own time limit;
+# the first failure ends the script (no retries).  Outputs under gpurun_out/$ROUND/.
+#   STEPS="smoke tests fullparity bench prof" ROUND=r05 bash tools/gpu_round.sh
+# smoke      __graft_entry__.smoke()
+# tests      pytest -m gpu (every parity test; PYTEST_K="expr" narrows it, PYTEST_FILES the files)
+# abtests    pytest tools/ab_tests (the A/B library tools/ab/libkdstep_ab.so: build it locally with
+#            csrc/build.py --ab before the call; it travels with the tree)
+# fullparity c1 at full depth vs the fp32 oracle + the plain-bf16 floor + the teacher-stream A/B
+#            (tools/parity_report.py --full-depth) -> full_depth.json
+# parity     the reduced-depth fixtures' per-term / per-parameter report -> parity.json
+# ntx        tools/ntx_bias_study.py (NT-Xent-only bias gradients) -> ntx_bias.json
+# bench      bench.py (the driver's default line; BENCH_ARGS appended) -> bench.json
+# c2|c3|c4   bench.py --config cN --no-cpu-baseline -> bench_cN.json
+# ab         the c1 bench once per setting in AB_SETS ("|"-separated env settings, read by the A/B
+#            library only when KDSTEP_LIB points at it; bench flags in AB_ARGS) -> ab_<i>.json
+# prof       rocprofv3 --kernel-trace --stats of a serialized bench -> prof/ (kernel_stats.csv)
+# step       kernel trace of the concurrent bench -> step_breakdown.txt
+# pmc        HBM traffic per kernel (tools/pmc_bench.sh: FETCH / WRITE passes)
+# pmcstep    MFMA-busy / wave cycles / clock per kernel family (tools/pmc_bench.sh mfma) -> pmc_step.json
+# blas       PMC clock / MFMA-busy / FETCH of kd_gemm vs hipBLASLt on the big shapes (tools/pmc_vs_blas.sh)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
+ROUND=${ROUND:-r05}
+O=gpurun_out/$ROUND
+mkdir -p $O
 STEPS=${STEPS:-"tests parity bench prof"}
 BENCH_ARGS=${BENCH_ARGS:-""}
+fail() { echo "$1 failed"; tail -${3:-30} "$2"; exit 1; }
 for s in $STEPS; do
   echo "== $s $(date +%T)"
   case $s in
-    smoke)  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
-            tail -1 gpurun_out/smoke.log ;;
-    tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-            tail -2 gpurun_out/pytest_gpu.log ;;
-    parity) timeout -k 10 600 python -u tools/parity_report.py --out gpurun_out/parity.json $PARITY_KINDS > gpurun_out/parity.log 2>&1 || { echo "parity failed"; tail -20 gpurun_out/parity.log; exit 1; } ;;
-    bench)  timeout -k 10 900 python -u bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
-            tail -1 gpurun_out/bench.log ;;
-    c2|c4)  timeout -k 10 600 python -u bench.py --config $s --no-cpu-baseline > gpurun_out/bench_$s.log 2>&1 || { echo "bench $s failed"; tail -30 gpurun_out/bench_$s.log; exit 1; }
-            tail -1 gpurun_out/bench_$s.log | cut -c1-240 ;;
-    gemm)   timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_fp8_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gemm.log 2>&1 || { echo "gemm tests failed"; tail -30 gpurun_out/pytest_gemm.log; exit 1; }
-            tail -1 gpurun_out/pytest_gemm.log ;;
-    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-teacher-rate --no-cpu-baseline --no-delta $BENCH_ARGS > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; } ;;
-    step)   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/profstep -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-delta --no-timer --no-teacher-rate $BENCH_ARGS > gpurun_out/profstep.log 2>&1 || { echo "profstep failed"; tail -20 gpurun_out/profstep.log; exit 1; }
-            python3 tools/step_breakdown.py $(ls gpurun_out/profstep/*/run_results.db gpurun_out/profstep/run_results.db 2>/dev/null | head -1) 40 > gpurun_out/step_breakdown.txt 2>&1; head -45 gpurun_out/step_breakdown.txt ;;
-    blas)   bash tools/pmc_vs_blas.sh > gpurun_out/pmc_blas.log 2>&1 || { echo "pmc_vs_blas failed"; tail -10 gpurun_out/pmc_blas.log; exit 1; }
-            cat gpurun_out/pmc_blas/summary.txt ;;
-    pmc)    bash tools/pmc_bench.sh > gpurun_out/pmc_bench.log 2>&1 || { echo "pmc failed"; tail -10 gpurun_out/pmc_bench.log; exit 1; } ;;
+    smoke)  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+            tail -1 $O/smoke.log ;;
+    tests)  timeout -k 10 1100 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -q --timeout 900 --timeout-method thread \
+                -p no:cacheprovider ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1 || fail pytest $O/pytest_gpu.log 60
+            tail -2 $O/pytest_gpu.log ;;
+    abtests) timeout -k 10 600 python -u -m pytest tools/ab_tests -m gpu -x -q --timeout 300 --timeout-method thread \
+                -p no:cacheprovider > $O/pytest_ab.log 2>&1 || fail abtests $O/pytest_ab.log 40
+            tail -2 $O/pytest_ab.log ;;
+    fullparity) timeout -k 10 900 python -u tools/parity_report.py --full-depth --floor --teacher-stream-ab \
+                --out $O/full_depth.json > $O/full_depth.log 2>&1 || fail fullparity $O/full_depth.log ;;
+    parity) timeout -k 10 600 python -u tools/parity_report.py --out $O/parity.json $PARITY_KINDS > $O/parity.log 2>&1 || fail parity $O/parity.log ;;
+    ntx)    timeout -k 10 300 python -u tools/ntx_bias_study.py > $O/ntx_bias.json 2> $O/ntx_bias.err || fail ntx $O/ntx_bias.err ;;
+    bench)  timeout -k 10 900 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+            tail -1 $O/bench.json | cut -c1-240 ;;
+    c2|c3|c4) timeout -k 10 600 python -u bench.py --config $s --no-cpu-baseline > $O/bench_$s.json 2> $O/bench_$s.err || fail "bench $s" $O/bench_$s.err
+            tail -1 $O/bench_$s.json | cut -c1-240 ;;
+    ab)     IFS='|' read -ra SETS <<< "$AB_SETS"; i=0
+            for v in "${SETS[@]}"; do
+              i=$((i + 1))
+              env $v timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-delta --no-timer $AB_ARGS > $O/ab_$i.json 2> $O/ab_$i.err || fail "ab $i" $O/ab_$i.err
+              python3 -c "import json; d=json.loads(open('$O/ab_$i.json').read().strip().splitlines()[-1]); print('[$v]', d['value'], d['ms_per_step'])"
+            done ;;
+    prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-teacher-rate --no-cpu-baseline --no-delta $BENCH_ARGS > $O/prof.log 2>&1 || fail prof $O/prof.log 20 ;;
+    step)   timeout -k 10 300 rocprofv3 --kernel-trace -d $O/profstep -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-delta --no-timer --no-teacher-rate $BENCH_ARGS > $O/profstep.log 2>&1 || fail profstep $O/profstep.log 20
+            python3 tools/step_breakdown.py $(ls $O/profstep/*/run_results.db $O/profstep/run_results.db 2>/dev/null | head -1) 40 > $O/step_breakdown.txt 2>&1; head -45 $O/step_breakdown.txt ;;
+    blas)   OUT=$O bash tools/pmc_vs_blas.sh > $O/pmc_blas.log 2>&1 || fail pmc_vs_blas $O/pmc_blas.log 10
+            cat $O/pmc_blas/summary.txt ;;
+    pmc)    OUT=$O bash tools/pmc_bench.sh > $O/pmc_bench.log 2>&1 || fail pmc $O/pmc_bench.log 10 ;;
+    pmcstep) OUT=$O bash tools/pmc_bench.sh mfma > $O/pmc_step.log 2>&1 || fail pmcstep $O/pmc_step.log 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

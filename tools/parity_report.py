@@ -98,9 +98,25 @@ def groups(hip, f32, b16):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
+    ap.add_argument("--full-depth", action="store_true",
+                    help="c1 at full depth vs the fp32 oracle on the same weights (tests/full_depth.py)")
+    ap.add_argument("--floor", action="store_true", help="--full-depth: also the plain-bf16 oracle (the floor)")
+    ap.add_argument("--teacher-stream-ab", action="store_true",
+                    help="--full-depth: also the HIP step with the teacher's Qwen2 residual stream in fp32")
     ap.add_argument("kinds", nargs="*")
     a = ap.parse_args()
     import torch
+    if a.full_depth:
+        from full_depth import measure as fd_measure
+        rep = fd_measure(torch.device("cuda:0"), floor=a.floor, teacher_stream_ab=a.teacher_stream_ab)
+        for k in ("hip", "hip_teacher_stream_f32", "bf16_floor"):
+            if k in rep:
+                r = {kk: vv for kk, vv in rep[k].items() if kk != "grad_params"}
+                print(k, json.dumps(r), flush=True)
+        if a.out:
+            Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+            Path(a.out).write_text(json.dumps(rep, indent=1))
+        return
     from model_fixtures import EVERY_KIND
     dev = torch.device("cuda:0")
     rep = {"tolerance": f"|d| <= {ATOL} + {RTOL} |ref| (north_star)"}

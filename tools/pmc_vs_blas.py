@@ -35,7 +35,10 @@ for d in sorted(glob.glob(os.path.join(root, "*_*x*x*"))):
         wave = sum(r.get("SQ_WAVE_CYCLES", 0) for r in rows) / n
         busy = sum(r.get("SQ_BUSY_CYCLES", 0) for r in rows) / n
         clk = grbm / 8 / ns
+        fetch = sum(r.get("FETCH_SIZE", 0) for r in rows) / n * 2048.0   # KB, x2 (gfx950 wide-read correction)
+        write = sum(r.get("WRITE_SIZE", 0) for r in rows) / n * 1024.0
         print(f"{prog:5s} {shape:18s} {name[-44:]:44s} n={n:2d} {ns / 1e3:8.1f} us {flop / ns / 1e3:7.1f} TF/s "
               f"clock {clk:5.3f} GHz  FLOP/cycle {flop / (grbm / 8):9.0f}  MFMA-busy/FLOP {mfma / flop * 1e3:7.4f}e-3  "
               f"MFMA-busy/wall-cycle {mfma / (grbm / 8):8.1f}  SQ_BUSY/wall-cycle {busy / (grbm / 8):6.2f}  "
-              f"wave-cycles/FLOP {wave / flop * 1e3:7.4f}e-3")
+              f"wave-cycles/FLOP {wave / flop * 1e3:7.4f}e-3  FETCH {fetch / 1e9:6.3f} GB  WRITE {write / 1e9:6.3f} GB "
+              f"(A + B once: {(M + N) * K * 2 / 1e9:6.3f} GB)")
