@@ -550,13 +550,22 @@ def main():
     fwd12 = ops.TIMER.summary("gemm_kk_swiglu", where=lambda M, N, K: not v8_shape(M, N, K))
     fwd8 = ops.TIMER.summary("gemm_f8_swiglu")
     traffic = None   # PMC HBM bytes per launch of that kernel (tools/pmc_bench.sh -> profiles/)
-    for rd in ("r04", "r03", "r02", "r01"):
+    for rd in ("r05", "r04", "r03", "r02", "r01"):
         tpath = REPO / "profiles" / rd / "pmc_traffic.json"
         if tpath.exists():
             fg = json.load(open(tpath)).get("roofline_kernel")
             if fg:
                 traffic = round(fg["traffic_bytes"])
                 break
+    # the step-wide MFMA utilisation per kernel family (tools/pmc_step.py over the serialized step)
+    step_pmc = None
+    spath = REPO / "profiles" / "r05" / "pmc_step.json"
+    if spath.exists():
+        sp = json.load(open(spath))
+        step_pmc = dict(source="profiles/r05/pmc_step.json", serialized_step_ms=sp["serialized_step_ms"],
+                        step_mfma_util_vs_peak=sp.get("step_mfma_util_vs_peak"),
+                        families={k: dict(ms=v["ms_per_step"], mfma=v["mfma_util_vs_peak"], hbm_gbs=v["hbm_gbs"])
+                                  for k, v in list(sp["families"].items())[:10]})
     if fwd:
         ach = fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12
         roof = dict(bound="mfma", kernel="k_gemm8<false, false, 4> (fused gate|up GEMM + SwiGLU epilogue of the "
@@ -565,7 +574,7 @@ def main():
                     traffic=traffic, traffic_unit="bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                    "profiles/*/pmc_traffic.json)",
                     flops_per_launch=round(fwd["flops_per_launch"] / 1e9, 2),
-                    avg_launch_us=round(fwd["avg_ms"] * 1e3, 2),
+                    avg_launch_us=round(fwd["avg_ms"] * 1e3, 2), step_pmc=step_pmc,
                     measured="HIP events on the launch stream over 2 serialized steps after the timed region "
                              "(bench.py --serial under rocprofv3 gives the matching kernel trace)",
                     student_swiglu_v12=None if not fwd12 else dict(

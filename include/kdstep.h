@@ -277,9 +277,10 @@ typedef struct {
 } kd_attn_desc;
 int kd_attn_fwd(const kd_attn_desc* desc, void* stream);
 
-/* Backward: dO [B,S,H,hd]; delta workspace [B,H,S] fp32; dq fp32 [B,H,S,hdp] (scaled,
- * overwritten); dk/dv bf16 [B,HKV,S,hdp]. Two kernels (dK/dV per key block and query
- * head; dQ per query block), no atomics. GQA (H > HKV) needs `workspace` of
+/* Backward: dO [B,S,H,hd]; delta workspace [B,H,S] fp32 (rowsum(dO * O), computed by the dQ
+ * kernel and read by the dK/dV kernel); dq fp32 [B,H,S,hdp] (scaled, overwritten); dk/dv bf16
+ * [B,HKV,S,hdp]. Two kernels (dQ per query block, then dK/dV per key block and query head), no
+ * atomics. GQA (H > HKV) needs `workspace` of
  * kd_attn_bwd_workspace_size() bytes for the per-query-head dK/dV partials. */
 typedef struct {
     const void* q; const void* k; const void* v; const void* o; const void* dO;

@@ -58,6 +58,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
+// (h, b, z) of this workgroup in a grid (H, B, NZ) whose z is a query block.  The dispatcher deals
+// workgroup L = x + H (y + B z) to XCD L % 8 (MI355X_MICROARCH: workgroup dispatch), so with the plain
+// mapping the G = H / HKV query heads of one GQA group -- which read the SAME K / V tiles -- land on G
+// different XCDs and every XCD's L2 fetches the group's K / V (rocprofv3 FETCH 4.9x q + k + v on the
+// 7B teacher's causal forward, round 4).  Here the G heads of one (z, b, kv head) group run on one XCD
+// at consecutive dispatch slots there (group grp -> XCD grp % 8), and the groups keep their z order
+// per XCD (z = 0 first: the heaviest causal blocks).  Bijective whenever HKV B NZ % 8 == 0; else, and
+// for MHA (G = 1), the plain mapping.
+__device__ __forceinline__ void gqa_xcd_map(int H, int HKV, int B, int& h, int& b, int& z) {
+    const int G = H / HKV, ngroups = HKV * B * (int)gridDim.z;
+    if (G > 1 && (ngroups & 7) == 0) {
+        const int L = (int)(blockIdx.x + H * (blockIdx.y + B * blockIdx.z));
+        const int xcd = L & 7, slot = L >> 3;
+        const int grp = (slot / G) * 8 + xcd;
+        h = (grp % HKV) * G + slot % G;
+        b = (grp / HKV) % B;
+        z = grp / (HKV * B);
+    } else {
+        h = blockIdx.x; b = blockIdx.y; z = blockIdx.z;
+    }
+}
+
 // 64 rows x HDP of a [S][HDP] head slab -> LDS image [64][RB] with chunk swizzle SW
 template <int HDP, bool VIMG>
 __device__ __forceinline__ void stage_kv(char* lds, const bf16* slab, int row0, int S, int wid, int lane) {
@@ -134,8 +156,10 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
     const int nqb = (p.S + QBLK - 1) / QBLK;
     // grid (H, B, query blocks): every head's longest causal block is dispatched first, the
     // shortest fill the tail
-    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
-    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
+    int h, b, zb;
+    gqa_xcd_map(p.H, p.HKV, p.B, h, b, zb);
+    const int qb = CAUSAL ? (nqb - 1 - zb) : zb;
+    const int kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
@@ -455,8 +479,10 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 3) k_attn_fwd32(AttnP p
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r32 = lane & 31, hf = lane >> 5;
     const int nqb = (p.S + QB - 1) / QB;
-    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
-    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
+    int h, b, zb;
+    gqa_xcd_map(p.H, p.HKV, p.B, h, b, zb);
+    const int qb = CAUSAL ? (nqb - 1 - zb) : zb;
+    const int kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
@@ -1173,7 +1199,8 @@ __global__ void __launch_bounds__(256, 2) k_attn_fwd32p(AttnP p) {
 struct AttnBwdP {
     const bf16* q; const bf16* k; const bf16* v;   // [B, heads, S, HDP]
     const bf16* dO;                                  // [B, S, H, hd]
-    const float* lse; const float* delta;           // [B, H, S]
+    const bf16* o;                                   // [B, S, H, hd] (k_attn_bwd_dq computes delta from it)
+    const float* lse; float* delta;                 // [B, H, S] (delta: written by k_attn_bwd_dq)
     float* dq;                                      // [B, H, S, HDP] fp32 (scaled)
     bf16* dk; bf16* dv;                             // [B, HKV, S, HDP]
     float* dkp; float* dvp;                         // GQA partials [B, H, S, HDP] fp32 (grp > 1)
@@ -1758,8 +1785,10 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     const int nqb = (p.S + QBLK - 1) / QBLK;
     // grid (H, B, query blocks): every head's longest causal block is dispatched first, the
     // shortest fill the tail
-    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
-    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
+    int h, b, zb;
+    gqa_xcd_map(p.H, p.HKV, p.B, h, b, zb);
+    const int qb = CAUSAL ? (nqb - 1 - zb) : zb;
+    const int kvh = h / (p.H / p.HKV);
     const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
     const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
     const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
@@ -1772,20 +1801,35 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
     for (int j = 0; j < NQ; ++j) {
         myq[j] = qb * QBLK + wid * 16 * NQ + j * 16 + li;
         qok[j] = myq[j] < p.S;
-        const bf16* dOr = p.dO + (((int64_t)b * p.S + myq[j]) * p.H + h) * p.hd;
+        const int64_t orow = (((int64_t)b * p.S + myq[j]) * p.H + h) * p.hd;
+        const bf16* dOr = p.dO + orow;
+        const bf16* Or = p.o + orow;
+        // delta = rowsum(dO * O) (the softmax backward's row constant), fused here: the lane's dO
+        // chunks (the dP operand) times the same chunks of O, summed over the 4 lanes of the row
+        float dsum = 0.f;
 #pragma unroll
         for (int kk = 0; kk < KSF; ++kk) {
             const int d0 = kk * 32 + 8 * g;
             qf[j][kk] = qok[j] ? *(const bf16x8*)(Q + (int64_t)myq[j] * HDP + d0) : (bf16x8){};
             df[j][kk] = (qok[j] && d0 < p.hd) ? *(const bf16x8*)(dOr + d0) : (bf16x8){};
+            const bf16x8 of = (qok[j] && d0 < p.hd) ? *(const bf16x8*)(Or + d0) : (bf16x8){};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dsum = __builtin_fmaf((float)df[j][kk][e], (float)of[e], dsum);
         }
         if (HALF) {   // dims 32 KSF + 4g + [0, 4); dO rows hold hd (a multiple of 4) columns
             const int d0 = KSF * 32 + 4 * g;
             qh[j] = qok[j] ? *(const bf16x4*)(Q + (int64_t)myq[j] * HDP + d0) : (bf16x4){};
             dh[j] = (qok[j] && d0 < p.hd) ? *(const bf16x4*)(dOr + d0) : (bf16x4){};
+            const bf16x4 oh = (qok[j] && d0 < p.hd) ? *(const bf16x4*)(Or + d0) : (bf16x4){};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dsum = __builtin_fmaf((float)dh[j][e], (float)oh[e], dsum);
         }
+        dsum += __shfl_xor(dsum, 16, 64);
+        dsum += __shfl_xor(dsum, 32, 64);
+        dl[j] = qok[j] ? dsum : 0.f;
+        // the dK / dV kernel, launched after this one, reads delta
+        if (qok[j] && g == 0) p.delta[((int64_t)b * p.H + h) * p.S + myq[j]] = dsum;
         lse2[j] = qok[j] ? p.lse[((int64_t)b * p.H + h) * p.S + myq[j]] * 1.4426950408889634f : 0.f;
-        dl[j] = qok[j] ? p.delta[((int64_t)b * p.H + h) * p.S + myq[j]] : 0.f;
     }
     f32x4 acc[NQ][DT];
 #pragma unroll
@@ -1931,48 +1975,6 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
         }
 }
 
-// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]: one thread per (b, q, h) row, 16-B loads
-// (hd % 8 == 0; every row load of both tensors in flight at once). One wave per row with
-// a 2-B load per lane spent 38 us per call on 11 MB.
-// k_attn_delta with the row's NC = hd / 8 chunk pairs all loaded before the sum (the generic loop
-// waited for each pair in turn: 8-9 serial memory round trips per row); the same fma chain in the
-// same order, so delta is bit-identical (the fmas are written out: left to the compiler, the two
-// kernels' sums were contracted / paired differently)
-template <int NC>
-__global__ void k_attn_delta_n(const bf16* __restrict__ O, const bf16* __restrict__ dO, float* __restrict__ delta, int B,
-                               int H, int S) {
-    const int row = blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= B * S * H) return;
-    const int h = row % H, bq = row / H, q = bq % S, b = bq / S;
-    const bf16* o = O + (int64_t)row * (NC * 8);
-    const bf16* d = dO + (int64_t)row * (NC * 8);
-    bf16x8 a[NC], g[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) { a[c] = *(const bf16x8*)(o + 8 * c); g[c] = *(const bf16x8*)(d + 8 * c); }
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc = __builtin_fmaf((float)a[c][e], (float)g[c][e], acc);
-    delta[((int64_t)b * H + h) * S + q] = acc;
-}
-
-__global__ void k_attn_delta(const bf16* __restrict__ O, const bf16* __restrict__ dO, float* __restrict__ delta,
-                             int B, int H, int S, int hd) {
-    const int row = blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= B * S * H) return;
-    const int h = row % H, bq = row / H, q = bq % S, b = bq / S;
-    const bf16* o = O + (int64_t)row * hd;
-    const bf16* d = dO + (int64_t)row * hd;
-    float acc = 0.f;
-    for (int c = 0; c < hd; c += 8) {
-        const bf16x8 a = *(const bf16x8*)(o + c), g = *(const bf16x8*)(d + c);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc = __builtin_fmaf((float)a[e], (float)g[e], acc);   // one fma chain in both kernels
-    }
-    delta[((int64_t)b * H + h) * S + q] = acc;
-}
-
 }  // namespace
 
 #ifdef KD_AB_BUILD
@@ -2091,27 +2093,12 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     if (need && (!d->workspace || d->workspace_bytes < need))
         return fail(KD_ERR_WORKSPACE, "attn_bwd: GQA needs kd_attn_bwd_workspace_size() bytes of workspace");
     hipStream_t st = as_stream(stream_);
-    {
-        const int rows = d->B * d->S * d->H;
-#ifdef KD_AB_BUILD
-        // KD_ATTN_DELTA_V=1 (read per call): the generic loop, for A/B
-        const char* dve = std::getenv("KD_ATTN_DELTA_V");
-        const int nc = (dve && std::atoi(dve) == 1) ? 0 : d->hd / 8;
-#else
-        const int nc = d->hd / 8;
-#endif
-        const dim3 g((rows + 255) / 256);
-        if (nc == 8) hipLaunchKernelGGL(k_attn_delta_n<8>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
-        else if (nc == 9) hipLaunchKernelGGL(k_attn_delta_n<9>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
-        else if (nc == 16) hipLaunchKernelGGL(k_attn_delta_n<16>, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H, d->S);
-        else hipLaunchKernelGGL(k_attn_delta, g, dim3(256), 0, st, (const bf16*)d->o, (const bf16*)d->dO, d->delta, d->B, d->H,
-                                d->S, d->hd);
-        KD_LAUNCH_CHECK("k_attn_delta");
-    }
+    // delta = rowsum(dO * O) is computed by the dQ kernel (its lanes hold the dO rows already) and
+    // written for the dK / dV kernel, which therefore runs second
     const double sc = 1.0 / std::sqrt((double)d->hd);
     float* dkp = need ? (float*)d->workspace : nullptr;
     float* dvp = need ? dkp + (size_t)d->B * d->H * d->S * d->hdp : nullptr;
-    AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, d->lse, d->delta,
+    AttnBwdP p{(const bf16*)d->q, (const bf16*)d->k, (const bf16*)d->v, (const bf16*)d->dO, (const bf16*)d->o, d->lse, d->delta,
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
                (float)(sc * 1.4426950408889634), (bf16*)d->dqkv, d->ld_qkv, d->cos_t, d->sin_t};
 #ifdef KD_AB_BUILD
@@ -2131,11 +2118,11 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
     const size_t smem_q = 2 * 2 * 64 * rb;
 #define LAUNCH(HD, C)                                                                         \
     do {                                                                                      \
-        launch_dkdv<HD, C>(kv16, grid, smem_kv, st, p);                                     \
-        KD_LAUNCH_CHECK("k_attn_bwd_dkdv");                                                   \
         if (nq_dq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p); \
         else launch_dq1<HD, C>(grid_q, smem_q, st, p);                                                   \
         KD_LAUNCH_CHECK("k_attn_bwd_dq");                                                     \
+        launch_dkdv<HD, C>(kv16, grid, smem_kv, st, p);                                     \
+        KD_LAUNCH_CHECK("k_attn_bwd_dkdv");                                                   \
     } while (0)
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }
     else if (d->hdp == 96) { if (d->causal) LAUNCH(96, true); else LAUNCH(96, false); }

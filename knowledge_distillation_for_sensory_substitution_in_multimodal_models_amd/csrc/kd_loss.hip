@@ -690,6 +690,11 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
     __shared__ int miss_s;                // slices whose partials did not arrive within poll_ticks
     const float ce_coef = coefs[1], kd_coef = coefs[2];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // the plain mapping: a row group's nsl slices are consecutive workgroups (so, dealt round-robin, on
+    // nsl different XCDs).  Placing them on one XCD (round 5) measured SLOWER: k_loss_grad_loca_rr
+    // 1812 us vs 1508-1536 us at c1 (profiles/r05), with 4 more VGPRs spilled.  A per-slice compacted
+    // LDS copy of the override values costs 25-30 VGPRs in each pass body and spilled 51-65 VGPRs at the
+    // 128-VGPR bound of two 512-thread workgroups per CU; neither is kept.
     const int sl = (int)(blockIdx.x % (unsigned)nsl), rg = (int)(blockIdx.x / (unsigned)nsl);
     const int c_lo = sl * cps, c_hi = min(V >> 3, c_lo + cps);   // this workgroup's chunks [c_lo, c_hi)
     const int w_lo = (c_lo * 8) >> 6;

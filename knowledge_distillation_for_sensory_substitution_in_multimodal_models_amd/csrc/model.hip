@@ -709,9 +709,11 @@ BwdPlan plan_backward(const kd_model* m, int B, int L, int n_tiles, void* base) 
     P.dgu = A.take<bf16>(M * 2 * TI);
     P.dh2 = A.take<bf16>(M * H);
     P.do_ = A.take<bf16>(M * qd);
-    // the attention backward writes the fused q|k|v gradient directly (kd_attn_bwd_desc.dqkv); the
-    // head-major dq / dk / dv + kd_qkv_merge path only with KD_ATTN_DQKV=0 (A/B)
-    const bool merge_ab = ab_knob("KD_ATTN_DQKV", 1) == 0;
+    // the attention backward writes the fused q|k|v gradient directly (kd_attn_bwd_desc.dqkv, RoPE
+    // rotated back in-kernel: grouped-query attention); plain multi-head attention with RoPE
+    // (t_kv_heads == t_heads) and KD_ATTN_DQKV=0 (A/B) take the head-major dq / dk / dv +
+    // kd_qkv_merge path (the MHA dK kernel writes its result unrotated)
+    const bool merge_ab = ab_knob("KD_ATTN_DQKV", 1) == 0 || c.t_kv_heads == c.t_heads;
     P.dq = merge_ab ? A.take<float>(M * qd) : nullptr;
     P.dk = merge_ab ? A.take<bf16>(M * kvd) : nullptr;
     P.dv = merge_ab ? A.take<bf16>(M * kvd) : nullptr;

@@ -97,26 +97,3 @@ def test_attn_fwd_two_blocks_per_wave_bitexact(B, H, HKV, S, hd, hdp, causal, de
         os.environ.pop("KD_ATTN_FWD_V", None)
     (o0, l0), (o1, l1) = outs
     assert torch.equal(o0, o1) and torch.equal(l0, l1)
-
-
-@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", [(2, 2, 2, 729, 72, 96, False), (1, 14, 2, 256, 64, 64, True),
-                                                    (1, 4, 1, 130, 128, 128, True), (1, 2, 2, 33, 40, 64, False)])
-def test_attn_delta_unrolled_bitexact(B, H, HKV, S, hd, hdp, causal, dev):
-    """k_attn_delta_n (every chunk pair of a row loaded before the sum; hd 64 / 72 / 128) == the
-    generic k_attn_delta loop (KD_ATTN_DELTA_V=1): dq / dk / dv bit for bit (hd 40: both the loop)."""
-    import os
-    ops = _ops()
-    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=9)
-    g = torch.Generator(device=dev).manual_seed(10)
-    o, lse = ops.attn_fwd(q, k, v, hd, causal)
-    do = torch.randn(B, S, H, hd, device=dev, generator=g).bfloat16()
-    outs = []
-    try:
-        for var in ("1", "2"):
-            os.environ["KD_ATTN_DELTA_V"] = var
-            outs.append([t.clone() for t in ops.attn_bwd(q, k, v, o, do, lse, hd, causal)])
-    finally:
-        os.environ.pop("KD_ATTN_DELTA_V", None)
-    sl = (Ellipsis, slice(0, hd))   # the head-dim padding [hd, hdp) is not an output
-    for a, b_ in zip(*outs):
-        assert torch.equal(a[sl], b_[sl])

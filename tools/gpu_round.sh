@@ -16,7 +16,8 @@
 # prof       rocprofv3 --kernel-trace --stats of a serialized bench -> prof/ (kernel_stats.csv)
 # step       kernel trace of the concurrent bench -> step_breakdown.txt
 # pmc        HBM traffic per kernel (tools/pmc_bench.sh: FETCH / WRITE passes)
-# pmcstep    MFMA-busy / wave cycles / clock per kernel family (tools/pmc_bench.sh mfma) -> pmc_step.json
+# pmcstep    MFMA-busy / wave cycles / clock per kernel family (tools/pmc_bench.sh mfma; wall times from
+#            the prof step's kernel trace, so list prof first) -> pmc_step.json
 # blas       PMC clock / MFMA-busy / FETCH of kd_gemm vs hipBLASLt on the big shapes (tools/pmc_vs_blas.sh)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

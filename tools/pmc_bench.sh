@@ -20,5 +20,8 @@ done
 python3 tools/pmc_traffic.py $OUT/pmc_bench > $OUT/pmc_traffic.json && head -c 600 $OUT/pmc_traffic.json
 if [ "$1" = mfma ]; then
   timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $OUT/pmc_bench/p3 -o p -- python3 $BENCH > $OUT/pmc_bench_p3.log 2>&1 || { echo "pmc pass 3 failed"; tail -5 $OUT/pmc_bench_p3.log; exit 1; }
-  python3 tools/pmc_step.py $OUT/pmc_bench > $OUT/pmc_step.json && head -c 2000 $OUT/pmc_step.json
+  # the wall times come from the plain kernel trace of the same serialized bench (gpu_round.sh step prof)
+  TRACE=$(ls $OUT/prof/*/run_kernel_trace.csv $OUT/prof/run_kernel_trace.csv 2>/dev/null | head -1)
+  [ -n "$TRACE" ] || { echo "pmcstep needs the prof step's kernel trace first (STEPS=\"prof pmcstep\")"; exit 1; }
+  python3 tools/pmc_step.py $OUT/pmc_bench $TRACE > $OUT/pmc_step.json && head -c 2000 $OUT/pmc_step.json
 fi

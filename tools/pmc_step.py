@@ -1,19 +1,23 @@
-"""Per kernel family of the serialized c1 step: time, MFMA utilisation, clock and HBM traffic, from
-the rocprofv3 --pmc passes of tools/pmc_bench.sh mfma (north_star: "rocprof HBM GB/s and MFMA
-utilisation against gfx950 peak").
+"""Per kernel family of the serialized c1 step: time, MFMA utilisation and HBM traffic (north_star:
+"rocprof HBM GB/s and MFMA utilisation against gfx950 peak").
 
-    python tools/pmc_step.py gpurun_out/r05/pmc_bench > pmc_step.json
+    python tools/pmc_step.py <pmc_bench dir> <kernel_trace.csv> > pmc_step.json
 
-Passes (separate runs of the same serialized bench, bench.py --steps 2 --warmup 1 --serial):
-  p1 FETCH_SIZE, p2 WRITE_SIZE (KB; FETCH_SIZE x2: the gfx950 wide-read correction, MI355X_MICROARCH.md)
-  p3 GRBM_GUI_ACTIVE, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_VALU_MFMA_BUSY_CYCLES
-Per dispatch: wall = End - Start (ns); cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs);
-clock = cycles / wall.  SQ_VALU_MFMA_BUSY_CYCLES counts MFMA pipe cycles summed over the SIMDs
-(32 per 32x32x16 bf16 MFMA, 16 per 16x16x32), so the matrix pipes' utilisation is
-  mfma_util = MFMA_BUSY / (1024 SIMDs x cycles)            (256 CUs x 4 SIMDs)
-and at the clock the chip held it corresponds to mfma_util x clock / 2.4 GHz of the 2.5 PF dense bf16
-peak (the peak is quoted at 2.4 GHz).  A family's figures are sums over its dispatches (ratios of
-sums), per step = / the 3 steps each pass runs.
+Inputs (tools/gpu_round.sh steps prof + pmcstep; every run is `bench.py --serial`, so one kernel at a time):
+  kernel_trace.csv   rocprofv3 --kernel-trace of the bench (no counters): each family's WALL time per step
+  p1 FETCH_SIZE, p2 WRITE_SIZE, p3 GRBM_GUI_ACTIVE + SQ_WAVE_CYCLES + SQ_BUSY_CYCLES +
+  SQ_VALU_MFMA_BUSY_CYCLES   (--pmc passes of a shorter run of the same bench; counters per step)
+A run's step count is its number of k_adamw dispatches (one per optimizer step), so both sources are
+per step.  Counter-collection passes run slower than the plain trace (measured +40-55 % on the big
+GEMMs) and GRBM_GUI_ACTIVE / 8 / wall reads high on short dispatches (MI355X_MICROARCH, DVFS
+give-back), so the wall time and the clock are NOT taken from the counter passes:
+  mfma_util_vs_peak = MFMA_BUSY per step / (1024 SIMDs x 2.4 GHz x traced wall per step)
+      SQ_VALU_MFMA_BUSY_CYCLES counts MFMA pipe cycles summed over the SIMDs (16 per 16x16x32 bf16 MFMA,
+      32 per 32x32x16): at 2.4 GHz the 1024 SIMDs deliver the 2.5 PF dense bf16 peak, so this is the
+      fraction of that peak the family's MFMAs would take at the peak clock -- for a bf16 GEMM family it
+      equals achieved TF/s / 2.5 PF (the fp8 MFMA counts its own cycles, 2x the FLOPs per cycle);
+  hbm = (FETCH_SIZE x 2 (gfx950 wide-read correction) + WRITE_SIZE) per step / traced wall per step
+      (FETCH_SIZE counts L2 -> fabric bytes, Infinity-Cache hits included: an upper bound of HBM reads).
 """
 from __future__ import annotations
 
@@ -25,8 +29,7 @@ import re
 import sys
 
 N_SIMD = 1024
-PEAK_CLK = 2.4
-STEPS = 3
+PEAK_CLK_GHZ = 2.4
 
 
 def family(n: str) -> str:
@@ -34,7 +37,8 @@ def family(n: str) -> str:
         return "gemm fp8"
     m = re.search(r"k_gemm(8|3)<(?:\d+, \d+, )?(true|false), (true|false)(?:, (\d+))?", n)
     if m:
-        amn, bmn, exp = m.group(2) == "true", m.group(3) == "true", int(m.group(4) or 0)
+        amn, bmn = m.group(2) == "true", m.group(3) == "true"
+        exp = int(m.group(4) or 0) if m.group(1) == "8" else 0   # k_gemm3's 5th parameter is its ring depth
         if exp & 4:
             return "gemm fwd gate|up + SwiGLU (roofline kernel)"
         if exp & 32:
@@ -56,60 +60,80 @@ def family(n: str) -> str:
         return "norms"
     if "k_adamw" in n:
         return "AdamW"
-    if "k_qkv" in n or "k_swiglu" in n or "k_act_bwd" in n:
-        return "qkv / activation (unfused)"
     if "k_colsum" in n:
         return "bias colsum"
-    return "other"
+    if "k_embed" in n or "k_image_src" in n or "k_patchify" in n:
+        return "embeddings / patchify"
+    if "k_qkv" in n or "k_swiglu" in n or "k_act_bwd" in n:
+        return "qkv / activation (unfused)"
+    if n.startswith("kd::") or "kd::(anonymous" in n or "_ZN2kd" in n:
+        return "other kd kernels"
+    return "torch (allocator fills, casts)"
 
 
-def load(root, pas):
-    """{dispatch id: {"name", "ns", counters...}} of one pass."""
+def load_pmc(root, pas):
     out = {}
     for f in glob.glob(f"{root}/{pas}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            d = out.setdefault(r["Dispatch_Id"], {"name": r["Kernel_Name"],
-                                                   "ns": float(r["End_Timestamp"]) - float(r["Start_Timestamp"])})
+            d = out.setdefault(r["Dispatch_Id"], {"name": r["Kernel_Name"], "t": int(r["Start_Timestamp"])})
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    return out
+    # the step window opens at the run's first KD kernel (model construction is not a step)
+    t0 = min((v["t"] for v in out.values() if family(v["name"]) != "torch (allocator fills, casts)"), default=0)
+    return {k: v for k, v in out.items() if v["t"] >= t0}
+
+
+def steps_of(names):
+    return max(1, sum(1 for n in names if "k_adamw" in n))
 
 
 def main():
-    root = sys.argv[1]
-    p1, p2, p3 = load(root, "p1"), load(root, "p2"), load(root, "p3")
-    fam = collections.defaultdict(lambda: collections.defaultdict(float))
-    for d in p3.values():
-        f = fam[family(d["name"])]
-        f["launches"] += 1
-        f["ns"] += d["ns"]
-        for k in ("GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES"):
-            f[k] += d.get(k, 0.0)
-    for src, key, mul in ((p1, "FETCH_SIZE", 2048.0), (p2, "WRITE_SIZE", 1024.0)):
-        for d in src.values():
-            f = fam[family(d["name"])]
-            f[key] += d.get(key, 0.0) * mul
-            f[key + "_ns"] += d["ns"]
-    tot_ns = sum(f["ns"] for f in fam.values())
+    root, trace = sys.argv[1], sys.argv[2]
+    wall = collections.defaultdict(float)
+    calls = collections.defaultdict(int)
+    tnames = []
+    started = False
+    for r in sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"])):
+        n = r["Kernel_Name"]
+        # the run's first KD kernel opens the step window: model construction (weight init) is not a step
+        started = started or family(n) not in ("torch (allocator fills, casts)",)
+        if not started:
+            continue
+        tnames.append(n)
+        f = family(n)
+        wall[f] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+        calls[f] += 1
+    t_steps = steps_of(tnames)
+    cnt = collections.defaultdict(lambda: collections.defaultdict(float))
+    p_steps = {}
+    for pas, keys in (("p1", ("FETCH_SIZE",)), ("p2", ("WRITE_SIZE",)),
+                      ("p3", ("GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES"))):
+        d = load_pmc(root, pas)
+        p_steps[pas] = steps_of([v["name"] for v in d.values()])
+        for v in d.values():
+            for k in keys:
+                cnt[family(v["name"])][k] += v.get(k, 0.0) / p_steps[pas]
+    tot = sum(wall.values()) / t_steps
+    mfma_all = sum(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for c in cnt.values())
     rows = {}
-    for name, f in sorted(fam.items(), key=lambda kv: -kv[1]["ns"]):
-        cyc = f["GRBM_GUI_ACTIVE"] / 8.0
-        util = f["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * cyc) if cyc else None
-        clk = cyc / f["ns"] if f["ns"] else None
-        fetch_gbs = f["FETCH_SIZE"] / f["FETCH_SIZE_ns"] if f.get("FETCH_SIZE_ns") else None
-        write_gbs = f["WRITE_SIZE"] / f["WRITE_SIZE_ns"] if f.get("WRITE_SIZE_ns") else None
-        rows[name] = dict(
-            launches_per_step=round(f["launches"] / STEPS, 1), ms_per_step=round(f["ns"] / STEPS / 1e6, 3),
-            share_of_serialized_step=round(f["ns"] / tot_ns, 4),
-            clock_ghz=round(clk, 3) if clk else None,
-            mfma_util=round(util, 4) if util is not None else None,
-            mfma_util_of_peak_at_2p4ghz=round(util * clk / PEAK_CLK, 4) if util is not None and clk else None,
-            sq_busy_per_cycle=round(f["SQ_BUSY_CYCLES"] / cyc, 3) if cyc else None,
-            wave_cycles_per_cycle=round(f["SQ_WAVE_CYCLES"] / cyc, 2) if cyc else None,
-            fetch_gb_per_step=round(f["FETCH_SIZE"] / STEPS / 1e9, 3), write_gb_per_step=round(f["WRITE_SIZE"] / STEPS / 1e9, 3),
-            hbm_gbs=round((fetch_gbs or 0) + (write_gbs or 0), 1),
-            hbm_frac_of_8tbs=round(((fetch_gbs or 0) + (write_gbs or 0)) / 8000.0, 4))
-    json.dump({"note": __doc__.strip().split("\n\n")[0], "method": __doc__.strip().split("\n\n", 2)[2],
-               "serialized_step_ms": round(tot_ns / STEPS / 1e6, 2), "families": rows}, sys.stdout, indent=1)
+    for f in sorted(wall, key=lambda k: -wall[k]):
+        ns = wall[f] / t_steps
+        c = cnt.get(f, {})
+        mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        fetch = c.get("FETCH_SIZE", 0.0) * 2048.0   # KB, x2
+        write = c.get("WRITE_SIZE", 0.0) * 1024.0
+        rows[f] = dict(launches_per_step=round(calls[f] / t_steps, 1), ms_per_step=round(ns / 1e6, 3),
+                       share_of_serialized_step=round(ns / 1e6 / (tot / 1e6), 4),
+                       mfma_util_vs_peak=round(mfma / (N_SIMD * PEAK_CLK_GHZ * ns), 4) if ns else None,
+                       fetch_gb_per_step=round(fetch / 1e9, 3), write_gb_per_step=round(write / 1e9, 3),
+                       hbm_gbs=round((fetch + write) / ns, 1) if ns else None,
+                       hbm_frac_of_8tbs=round((fetch + write) / ns / 8000.0, 4) if ns else None,
+                       sq_busy_per_wave_cycle=round(c["SQ_BUSY_CYCLES"] / c["SQ_WAVE_CYCLES"], 4)
+                       if c.get("SQ_WAVE_CYCLES") else None)
+    doc = __doc__.strip()
+    json.dump({"what": doc.split("\n\n")[0], "method": doc.split("\n\n", 2)[2],
+               "steps": {"trace": t_steps, **p_steps}, "serialized_step_ms": round(tot / 1e6, 2),
+               "step_mfma_util_vs_peak": round(mfma_all / (N_SIMD * PEAK_CLK_GHZ * tot), 4), "families": rows},
+              sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
