@@ -54,7 +54,10 @@ for s in $STEPS; do
             done ;;
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 2 --serial --no-teacher-rate --no-cpu-baseline --no-delta $BENCH_ARGS > $O/prof.log 2>&1 || fail prof $O/prof.log 20 ;;
     step)   timeout -k 10 300 rocprofv3 --kernel-trace -d $O/profstep -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-delta --no-timer --no-teacher-rate $BENCH_ARGS > $O/profstep.log 2>&1 || fail profstep $O/profstep.log 20
-            python3 tools/step_breakdown.py $(ls $O/profstep/*/run_results.db $O/profstep/run_results.db 2>/dev/null | head -1) 40 > $O/step_breakdown.txt 2>&1; head -45 $O/step_breakdown.txt ;;
+            DB=$(ls $O/profstep/*/run_results.db $O/profstep/run_results.db 2>/dev/null | head -1)
+            python3 tools/step_breakdown.py $DB 40 > $O/step_breakdown.txt 2>&1
+            python3 tools/step_phases.py $DB > $O/step_phases.txt 2>&1
+            python3 tools/step_timeline.py $DB 1.0 > $O/step_timeline.txt 2>&1; head -45 $O/step_breakdown.txt ;;
     blas)   OUT=$O bash tools/pmc_vs_blas.sh > $O/pmc_blas.log 2>&1 || fail pmc_vs_blas $O/pmc_blas.log 10
             cat $O/pmc_blas/summary.txt ;;
     pmc)    OUT=$O bash tools/pmc_bench.sh > $O/pmc_bench.log 2>&1 || fail pmc $O/pmc_bench.log 10 ;;
