@@ -26,6 +26,7 @@
  *    at load time (the Python binding refuses a mismatched library).
  *    ABI 6 -> 7: kd_gemm diagnostic variants (17-20, 22, 23, 25-28) are no longer accepted by
  *    the product library (A/B builds only); kd_loss err bit 4 is no longer set.
+ *    ABI 7 -> 8: kd_loss_params.s_stats appended; kd_loss_student_stats added.
  */
 #ifndef KDSTEP_H
 #define KDSTEP_H
@@ -54,7 +55,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 7
+#define KD_ABI_VERSION 8
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -111,6 +112,11 @@ typedef struct {
        the student's alone). */
     const float* s_row_stats;
     const float* t_row_stats;
+    /* optional (ABI 8): the student's statistics of THESE rows from kd_loss_student_stats (run
+       earlier, e.g. on the student's stream right after its lm_head, while the teacher finishes);
+       the loss then reads only the teacher's logits for its statistics. Bit-identical results.
+       Exclusive with s_row_stats. */
+    const float* s_stats;
 } kd_loss_params;
 
 /* loss_out (device float[4]): [0] KD term (mean, incl. T^2, unweighted)
@@ -131,6 +137,12 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t,
 /* Synchronises `stream` and reports a device-side error recorded in `workspace` by the
  * last kd_loss_fwd_bwd (KD_ERR_LABEL_RANGE), else KD_OK. */
 int kd_loss_check(const void* workspace, void* stream);
+/* The student half of kd_loss_fwd_bwd's per-row statistics (the log_softmax normalisers of
+ * DT:158-162 / LB:225-229 and of the HF causal-LM CE): stats_out fp32 [rows][4] =
+ * {max, sum exp((s - max)/T), sum exp(s - max), 0} over the first V_s columns of each row,
+ * 16-B aligned.  Hand it to kd_loss_fwd_bwd as params.s_stats with the same rows and T. */
+int kd_loss_student_stats(const void* student_logits, int64_t ld_s, int V_s, int rows, float temperature,
+                          float* stats_out, void* stream);
 
 /* ------------------------------------------------------------------ GEMM ---- */
 /* C[M,N] = epilogue(alpha * sum_k A[m,k] B[n,k]), bf16 operands, fp32 accumulation

@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("KDSTEP_LIB", _PKG / "libkdstep.so"))
 HEADER = _PKG.parent / "include" / "kdstep.h"
 
 KD_OK = 0
-ABI_VERSION = 7
+ABI_VERSION = 8
 STATUS_NAMES = {
     0: "KD_OK", 1: "KD_ERR_SHAPE", 2: "KD_ERR_DTYPE", 3: "KD_ERR_ALIGN", 4: "KD_ERR_ARCH",
     5: "KD_ERR_LABEL_RANGE", 6: "KD_ERR_LAUNCH", 7: "KD_ERR_ARG", 8: "KD_ERR_WORKSPACE",
@@ -45,6 +45,7 @@ class KdLossParams(C.Structure):
         ("dscale_given", C.c_int32),
         ("s_row_stats", C.c_void_p),
         ("t_row_stats", C.c_void_p),
+        ("s_stats", C.c_void_p),
     ]
 
 
@@ -132,6 +133,7 @@ SIGNATURES = {
     "kd_loss_fwd_bwd": (_i32, [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _i32, _i32, KdLossParams,
                                _vp, _vp, _i64, _vp, _sz, _vp]),
     "kd_loss_check": (_i32, [_vp, _vp]),
+    "kd_loss_student_stats": (_i32, [_vp, _i64, _i32, _i32, _f32, _vp, _vp]),
     "kd_gemm": (_i32, [C.POINTER(KdGemmDesc), _vp]),
     "kd_gemm_pretile_size": (_sz, [_i32, _i32, _i32]),
     "kd_gemm_pretile": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp]),

@@ -40,6 +40,11 @@ int kd_loss_fwd_bwd(const void* teacher_logits, int64_t ld_t, int V_t, const voi
 
 int kd_loss_check(const void* workspace, void* stream) { return kd::kd_loss_check_impl(workspace, stream); }
 
+int kd_loss_student_stats(const void* student_logits, int64_t ld_s, int V_s, int rows, float temperature,
+                          float* stats_out, void* stream) {
+    return kd::launch_kd_student_stats(student_logits, ld_s, V_s, rows, temperature, stats_out, stream);
+}
+
 int kd_gemm(const kd_gemm_desc* desc, void* stream) { return kd::gemm_timed(desc, stream); }
 size_t kd_gemm_pretile_size(int N, int K, int glu) { return kd::gemm_pretile_size(N, K, glu); }
 int kd_gemm_pretile(const void* W, int64_t ldw, int N, int K, int glu, void* out, void* stream) {

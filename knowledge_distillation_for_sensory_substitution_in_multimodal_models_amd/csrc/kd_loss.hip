@@ -106,11 +106,20 @@ __device__ __forceinline__ void report_label(int* err, int* err_ext, int bit, in
     }
 }
 
-// PART: the per-row max / sum-exp / top-2 come from the lm_head GEMMs' epilogue partials
-// (kd_gemm_desc.row_stats: [rows, ceil(V / 256), 8] per model, merged with the same lse_merge /
-// top2_push as the wave reductions below) instead of a pass over both logit tensors; the label
-// gathers, the CE and the LoCa override values are unchanged (a few single-element reads).
-template <bool PART>
+// Modes (RS_FULL: one pass over both logit tensors):
+//  RS_PART  the per-row max / sum-exp / top-2 come from the lm_head GEMMs' epilogue partials
+//           (kd_gemm_desc.row_stats: [rows, ceil(V / 256), 8] per model, merged with the same lse_merge /
+//           top2_push as the wave reductions below) instead of a pass over both logit tensors; the label
+//           gathers, the CE and the LoCa override values are unchanged (a few single-element reads).
+//  RS_SONLY the student's {max, sum exp at 1/T, sum exp at 1} only, into s_aux [rows][4]
+//           (kd_loss_student_stats: run on the student's stream right after its lm_head, beside the
+//           teacher's last layers); T_ must be null.
+//  RS_SPRE  the student's values read from s_aux (an RS_SONLY pass over the same rows): only the
+//           teacher's logits are read here.  RS_SONLY runs the student loop and the reductions of
+//           RS_FULL unchanged (the teacher's partials stay -inf / 0, which lse_merge skips), so the
+//           statistics -- and the loss -- are the same bits as one RS_FULL pass.
+enum { RS_FULL = 0, RS_PART = 1, RS_SONLY = 2, RS_SPRE = 3 };
+template <int MODE>
 __global__ void __launch_bounds__(NT)
 k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
             const bf16* __restrict__ S_, int64_t ld_s, int V_s,
@@ -118,11 +127,12 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
             int variant, float invT, float alpha, int want_tce,
             RowStats* __restrict__ stats, int* __restrict__ lab_last,
             int* __restrict__ klo_last, int* __restrict__ err, int* __restrict__ err_ext, int row_base,
-            const float* __restrict__ s_part, const float* __restrict__ t_part) {
+            const float* __restrict__ s_part, const float* __restrict__ t_part, float* __restrict__ s_aux) {
+    constexpr bool PART = MODE == RS_PART;
     __shared__ float sm[NW * 8];
     __shared__ int si[NW * 2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const bool has_t = (T_ != nullptr);
+    const bool has_t = MODE != RS_SONLY && (T_ != nullptr);
     for (int r = blockIdx.x; r < rows; r += gridDim.x) {
         const bf16* srow = S_ + (int64_t)r * ld_s;
         const bf16* trow = has_t ? T_ + (int64_t)r * ld_t : nullptr;
@@ -153,6 +163,7 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
         } else {
         // ---- student: max / sum-exp at T and at 1 (same max); RS_U chunks in flight per lane
         const bool t1 = invT == 1.f;   // T = 1 (LB): the two sums coincide, one exp per element
+        if (MODE != RS_SPRE)
         for (int v0 = tid * 8; v0 < V_s; v0 += NT * 8 * RS_U) {
             bf16x8 xs[RS_U];
 #pragma unroll
@@ -182,6 +193,13 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
         if (t1) zs1 = zs;
         // ---- teacher: max/sum over V_s at T, top-2 over V_s; max/sum over V_t at 1
         if (has_t) {
+            // thr: the largest lane second-best of this wave so far, a lower bound of the row's
+            // second-largest value (every lane's v2 is <= the row's top value's runner-up or ties
+            // it), refreshed per outer step.  A chunk whose max is below it cannot hold a top-2
+            // element, so once thr has risen (after a few hundred elements of random logits) the
+            // whole wave skips the per-element insertion instead of running it whenever any one of
+            // its 64 lanes has a candidate.  Elements equal to thr still go in (index tie-break).
+            float thr = -INFINITY;
             for (int v0 = tid * 8; v0 < V_t; v0 += NT * 8 * RS_U) {
                 bf16x8 xt[RS_U];
 #pragma unroll
@@ -222,13 +240,17 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
                             for (int j = 0; j < 8; ++j) zt += __expf((f[j] - mt) * invT);
                         }
                     }
-                    if (in_s) {
+                    if (in_s && cm >= thr) {
                         if (cm > v2 || (cm == v2 && v < i2)) {   // a chunk that can change the top-2
 #pragma unroll
                             for (int j = 0; j < 8; ++j) top2_push(f[j], v + j, v1, i1, v2, i2);
                         }
                     }
                 }
+                float t2 = v2;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) t2 = fmaxf(t2, __shfl_xor(t2, o, 64));
+                thr = t2;
             }
         }
         if (has_t && want_tce && t1 && mt != -INFINITY) zt *= __expf(mtf - mt);   // sum exp(t - mt) over V_s
@@ -261,6 +283,20 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
         __shared__ float sv2[NW];
         if (lane == 0) sv2[w] = v2;
         __syncthreads();
+        if (MODE == RS_SONLY) {
+            if (tid == 0) {
+                float Ms = sm[0], Zs = sm[1], Zs1 = sm[2];
+                for (int k = 1; k < NW; ++k) {
+                    float m1 = Ms, z1 = Zs1;
+                    lse_merge(Ms, Zs, sm[k * 8 + 0], sm[k * 8 + 1], invT);
+                    lse_merge(m1, z1, sm[k * 8 + 0], sm[k * 8 + 2], 1.f);
+                    Zs1 = z1;
+                }
+                *(f32x4*)(s_aux + (int64_t)r * 4) = f32x4{Ms, Zs, Zs1, 0.f};
+            }
+            __syncthreads();
+            continue;
+        }
         if (tid == 0) {
             float Ms = sm[0], Zs = sm[1], Zs1 = sm[2], Mt = sm[3], Zt = sm[4], Mtf = sm[5], Ztf = sm[6];
             float V1 = sm[7], V2 = sv2[0];
@@ -274,6 +310,10 @@ k_row_stats(const bf16* __restrict__ T_, int64_t ld_t, int V_t,
                 lse_merge(Mtf, Ztf, sm[k * 8 + 5], sm[k * 8 + 6], 1.f);
                 top2_push(sm[k * 8 + 7], si[k * 2 + 0], V1, I1, V2, I2);
                 top2_push(sv2[k], si[k * 2 + 1], V1, I1, V2, I2);
+            }
+            if (MODE == RS_SPRE) {   // the student's statistics from kd_loss_student_stats
+                const f32x4 a = *(const f32x4*)(s_aux + (int64_t)r * 4);
+                Ms = a[0]; Zs = a[1]; Zs1 = a[2];
             }
             RowStats st;
             st.ms = Ms; st.zs = Zs; st.zs1 = Zs1;
@@ -1077,17 +1117,24 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     const int rs_cap = std::max(1, ab_knob("KD_RS_GRID", 1 << 30));
     const int grid = std::min(rows, rs_cap);
     const bool part = p.s_row_stats != nullptr;
+    KD_CHECK_ARG(!(part && p.s_stats), "kd_loss: s_row_stats and s_stats are exclusive");
     if (part) {
         KD_CHECK_ARG(!T_ || p.t_row_stats, "kd_loss: s_row_stats without t_row_stats");
         KD_CHECK_ALIGN(p.s_row_stats, 16, "kd_loss: s_row_stats must be 16-B aligned");
         KD_CHECK_ALIGN(p.t_row_stats, 16, "kd_loss: t_row_stats must be 16-B aligned");
-        hipLaunchKernelGGL(k_row_stats<true>, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
+        hipLaunchKernelGGL(k_row_stats<RS_PART>, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
                            V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
-                           lab_last, klo_last, err, p.err_out, p.row_base, p.s_row_stats, p.t_row_stats);
+                           lab_last, klo_last, err, p.err_out, p.row_base, p.s_row_stats, p.t_row_stats, nullptr);
+    } else if (p.s_stats) {
+        KD_CHECK_ALIGN(p.s_stats, 16, "kd_loss: s_stats must be 16-B aligned");
+        hipLaunchKernelGGL(k_row_stats<RS_SPRE>, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
+                           V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
+                           lab_last, klo_last, err, p.err_out, p.row_base, nullptr, nullptr,
+                           const_cast<float*>(p.s_stats));
     } else {
-        hipLaunchKernelGGL(k_row_stats<false>, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
+        hipLaunchKernelGGL(k_row_stats<RS_FULL>, dim3(grid), dim3(NT), 0, stream, T_, ld_t, T_ ? V_t : 0, S_, ld_s,
                            V_s, labels, L, rows, variant, invT, p.alpha, (T_ && p.teacher_ce) ? 1 : 0, stats,
-                           lab_last, klo_last, err, p.err_out, p.row_base, nullptr, nullptr);
+                           lab_last, klo_last, err, p.err_out, p.row_base, nullptr, nullptr, nullptr);
     }
     KD_LAUNCH_CHECK("k_row_stats");
     if (variant == KD_LOSS_LOCA) {
@@ -1149,6 +1196,23 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(NT), 0, stream, stats, part_kl, rows, kl_scale,
                        p.kd_weight, p.ce_weight, p.out_scale, p.out_accumulate ? 1 : 0, loss_out);
     KD_LAUNCH_CHECK("k_finalize");
+    return KD_OK;
+}
+
+int launch_kd_student_stats(const void* student, int64_t ld_s, int V_s, int rows, float temperature, float* out,
+                            void* stream_) {
+    KD_CHECK_ARG(student && out, "kd_loss_student_stats: null pointer");
+    KD_CHECK_SHAPE(rows > 0 && V_s > 0, "kd_loss_student_stats: empty shape");
+    KD_CHECK_SHAPE(V_s % 8 == 0 && ld_s % 8 == 0 && ld_s >= V_s, "kd_loss_student_stats: V_s/ld_s must be multiples of 8");
+    KD_CHECK_ALIGN(student, 16, "kd_loss_student_stats: student logits must be 16-B aligned");
+    KD_CHECK_ALIGN(out, 16, "kd_loss_student_stats: out must be 16-B aligned");
+    KD_CHECK_ARG(temperature > 0.f, "kd_loss_student_stats: temperature must be > 0");
+    const int rs_cap = std::max(1, ab_knob("KD_RS_GRID", 1 << 30));
+    // the RS_FULL arguments the student loop reads; the label / LoCa tail is not run
+    hipLaunchKernelGGL(k_row_stats<RS_SONLY>, dim3(std::min(rows, rs_cap)), dim3(NT), 0, as_stream(stream_), nullptr,
+                       (int64_t)0, 0, (const bf16*)student, ld_s, V_s, nullptr, 1, rows, 0, 1.f / temperature, 0.f, 0,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, out);
+    KD_LAUNCH_CHECK("k_row_stats<student>");
     return KD_OK;
 }
 

@@ -9,6 +9,8 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
                    int V_s, const int64_t* labels, int B, int L, kd_loss_params p, float* loss_out,
                    void* dlogits, int64_t ld_d, void* ws, size_t ws_bytes, void* stream);
 size_t kd_loss_ws(int B, int L, int V);
+int launch_kd_student_stats(const void* student, int64_t ld_s, int V_s, int rows, float temperature, float* out,
+                            void* stream);
 int kd_loss_check_impl(const void* ws, void* stream);
 int launch_gemm(const kd_gemm_desc* d, void* stream);
 size_t gemm_workspace_size(const kd_gemm_desc* d);

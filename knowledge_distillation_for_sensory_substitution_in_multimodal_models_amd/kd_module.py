@@ -297,6 +297,9 @@ class _KDBase(_Base):
         # KD_FUSE_ROWSTATS=1: the lm_head epilogues emit the KD loss's row statistics.  Off by
         # default: measured slower (profiles/r03/row_stats_fusion_ab.txt)
         self.fuse_row_stats = os.environ.get("KD_FUSE_ROWSTATS", "0") == "1"
+        # the student's row statistics on the student stream ahead of the loss (kd_loss_student_stats;
+        # KD_STUDENT_STATS_EARLY=0 leaves them in the loss's own pass, for A/B)
+        self.student_stats_early = os.environ.get("KD_STUDENT_STATS_EARLY", "1") != "0"
         self.last_terms = None
         self.last_ntxent = None
         self.last_logits = None
@@ -428,6 +431,14 @@ class _KDBase(_Base):
                              want_post_ln=need_feats, want_logits=True, row_stats=(Vs_, 1.0 / T, False) if fuse else None)
             s_logits = sfwd.pop("logits")
             s_rst = sfwd.pop("row_stats", None)
+            # the student half of the loss's row statistics, on the student stream right after its
+            # lm_head: it finishes before the teacher forward (c1: ~7 ms of slack), so the loss,
+            # the one stretch of the step with nothing beside it, reads only the teacher's logits
+            # for its statistics (kd_loss_params.s_stats; bit-identical)
+            s_st = None
+            if s_rst is None and self.uses_teacher and self.student_stats_early:
+                s_st = ops.kd_loss_student_stats(s_logits, temperature=T)
+                s_st.record_stream(main)   # read by the loss on the caller's stream
         main.wait_stream(side)
         Vs = s_logits.shape[1]
         s3 = s_logits.view(B, L, Vs)
@@ -450,8 +461,9 @@ class _KDBase(_Base):
                                 dlogits_out=None if dlogits is None else dlogits[sl], err_out=self._errors.kd,
                                 row_base=g * G * L, dscale=dscale, dscale_given=g > 0,
                                 s_row_stats=None if s_rst is None else s_rst[rs],
-                                t_row_stats=None if (s_rst is None or t_rst is None) else t_rst[rs])
-        del s_rst, t_rst
+                                t_row_stats=None if (s_rst is None or t_rst is None) else t_rst[rs],
+                                s_stats=None if s_st is None else s_st[rs])
+        del s_rst, t_rst, s_st
         if self.keep_logits:
             self.last_logits = (s3, t3)
             self.last_post = (sfwd.get("post_ln"), t_post)

@@ -101,6 +101,27 @@ def _require(t: torch.Tensor, dtype, name: str):
 
 
 # ------------------------------------------------------------------ KD loss ----
+def kd_loss_student_stats(student_logits: torch.Tensor, temperature: float = 1.0,
+                          out: torch.Tensor | None = None) -> torch.Tensor:
+    """The student half of the KD loss's per-row statistics (include/kdstep.h
+    kd_loss_student_stats): fp32 [rows, 4] = {max, sum exp((s - max)/T), sum exp(s - max), 0}
+    of every row of student_logits [..., V_s] (bf16, rows uniformly strided).  For
+    kd_loss_fwd_bwd(s_stats=...) on the same rows and temperature."""
+    _require(student_logits, torch.bfloat16, "student_logits")
+    V_s = student_logits.shape[-1]
+    x = student_logits.reshape(-1, V_s)
+    if x.stride(1) != 1:
+        raise RuntimeError("student_logits: contiguous last dim expected")
+    rows = x.shape[0]
+    o = out if out is not None else torch.empty((rows, 4), dtype=torch.float32, device=x.device)
+    _require(o, torch.float32, "out")
+    if not o.is_contiguous() or o.numel() != rows * 4:
+        raise RuntimeError("out: expected a contiguous [rows, 4] fp32 tensor")
+    NV.call("kd_loss_student_stats", _ptr(x), x.stride(0), V_s, rows, float(temperature), _ptr(o), _stream())
+    return o
+
+
+
 VARIANTS = {"none": NV.KD_LOSS_NONE, "loca": NV.KD_LOSS_LOCA, "kl": NV.KD_LOSS_KL,
             "kl_logtarget": NV.KD_LOSS_KL_LOGTARGET}
 
@@ -113,7 +134,8 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
                     accumulate: bool = False, dlogits_out: torch.Tensor | None = None,
                     err_out: torch.Tensor | None = None, row_base: int = 0,
                     dscale: torch.Tensor | None = None, dscale_given: bool = False,
-                    s_row_stats: torch.Tensor | None = None, t_row_stats: torch.Tensor | None = None):
+                    s_row_stats: torch.Tensor | None = None, t_row_stats: torch.Tensor | None = None,
+                    s_stats: torch.Tensor | None = None):
     """Fused KD-loss forward + backward (include/kdstep.h kd_loss_fwd_bwd).
 
     student_logits [B, L, V_s] bf16 (last dim contiguous), teacher_logits [B, L, V_t] bf16,
@@ -129,6 +151,8 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
     stays exact in bf16).  s_row_stats / t_row_stats (fp32 [B*L, ceil(V / 256), 8], these rows):
     the lm_head GEMMs' row statistics (gemm(row_stats=...), modeling set_row_stats) in place of
     the loss's own pass over the logits (kd_loss_params.s_row_stats / t_row_stats).
+    s_stats (fp32 [B*L, 4], these rows, same temperature): kd_loss_student_stats' output, so the
+    loss reads only the teacher's logits for its statistics (kd_loss_params.s_stats; same bits).
     """
     B, L, V_s = student_logits.shape
     _require(student_logits, torch.bfloat16, "student_logits")
@@ -165,12 +189,16 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
                 raise RuntimeError(f"{nm}: expected a contiguous [B*L, ceil(V/256), 8] fp32 block of these rows")
     if (s_row_stats is None) != (t_row_stats is None) and teacher_logits is not None:
         raise RuntimeError("s_row_stats and t_row_stats: both or neither")
+    if s_stats is not None:
+        _require(s_stats, torch.float32, "s_stats")
+        if not s_stats.is_contiguous() or s_stats.numel() != B * L * 4:
+            raise RuntimeError("s_stats: expected a contiguous [B*L, 4] fp32 block of these rows (kd_loss_student_stats)")
     nbytes = NV.lib().kd_loss_workspace_size(B, L, V_s)
     ws = _workspace("kd_loss", nbytes, dev)
     prm = NV.KdLossParams(v, float(temperature), float(alpha), float(kd_weight), float(ce_weight),
                          float(grad_scale), float(clamp_min), 1 if teacher_ce else 0, float(out_scale),
                          1 if accumulate else 0, _ptr(err_out), int(row_base), _ptr(dscale),
-                         1 if dscale_given else 0, _ptr(s_row_stats), _ptr(t_row_stats))
+                         1 if dscale_given else 0, _ptr(s_row_stats), _ptr(t_row_stats), _ptr(s_stats))
     NV.call("kd_loss_fwd_bwd", _ptr(teacher_logits), ld_t, V_t, _ptr(student_logits),
            student_logits.stride(1), V_s, _ptr(labels), B, L, prm, _ptr(loss), _ptr(dl),
            V_s, _ptr(ws), ws.numel(), _stream())

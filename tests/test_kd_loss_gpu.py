@@ -252,3 +252,44 @@ def test_register_resident_loca_stand_in_is_bit_identical(B, L, V, T, dev, monke
     (l0, d0), (l1, d1) = out
     assert torch.equal(l0.cpu(), l1.cpu()), (l0, l1)
     assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+
+
+@pytest.mark.parametrize("variant,T,B,L,V", [("loca", 1.0, 2, 384, 151936), ("loca", 0.8, 1, 257, 151936),
+                                             ("kl", 0.8, 2, 64, 60000), ("kl_logtarget", 0.8, 2, 64, 60000),
+                                             ("loca", 1.0, 3, 7, 24)])
+def test_student_stats_ahead_is_bit_identical(variant, T, B, L, V, dev):
+    """kd_loss_student_stats (the student half of the row statistics, run ahead of the loss on
+    the student's stream) + kd_loss_fwd_bwd(s_stats=...) == kd_loss_fwd_bwd alone, bit for bit:
+    the student loop and its reductions are the same code, the teacher-only pass reads the
+    student's {max, sum exp} from s_stats.  Loss groups slice the stats with the rows."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(21)
+    s = (torch.randn(B, L, V, generator=g) * 2).to(dev, torch.bfloat16)
+    t = (torch.randn(B, L, V + 128, generator=g) * 2).to(dev, torch.bfloat16)
+    labels = torch.randint(0, V, (B, L), generator=g)
+    if variant != "loca":   # LoCa gathers at every label (DT:166): -100 only for the CE-only rows of KL
+        labels[:, -2:] = -100
+    labels = labels.to(dev)
+    l0, d0 = ops.kd_loss_fwd_bwd(s, t, labels, variant, temperature=T, check=True)
+    st = ops.kd_loss_student_stats(s, temperature=T)
+    l1, d1 = ops.kd_loss_fwd_bwd(s, t, labels, variant, temperature=T, check=True, s_stats=st)
+    torch.cuda.synchronize()
+    assert torch.equal(l0.cpu(), l1.cpu()), (l0, l1)
+    assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+    # the stats themselves: {max, sum exp((s-max)/T), sum exp(s-max)} of every row
+    sf = s.float().view(-1, V)
+    m = sf.max(-1).values
+    ref = torch.stack([m, torch.exp((sf - m[:, None]) / T).sum(-1), torch.exp(sf - m[:, None]).sum(-1)], -1)
+    assert torch.equal(st[:, 0], ref[:, 0])
+    assert torch.allclose(st[:, 1:3], ref[:, 1:], rtol=1e-5, atol=0)
+    if B > 1:   # one group per sample: the stats of the group's rows
+        loss = torch.zeros(4, dtype=torch.float32, device=dev)
+        loss2 = torch.zeros(4, dtype=torch.float32, device=dev)
+        for gi in range(B):
+            rs = slice(gi * L, (gi + 1) * L)
+            ops.kd_loss_fwd_bwd(s[gi:gi + 1], t[gi:gi + 1], labels[gi:gi + 1], variant, temperature=T,
+                                loss_out=loss, out_scale=1.0 / B, accumulate=gi > 0, want_grad=False)
+            ops.kd_loss_fwd_bwd(s[gi:gi + 1], t[gi:gi + 1], labels[gi:gi + 1], variant, temperature=T,
+                                loss_out=loss2, out_scale=1.0 / B, accumulate=gi > 0, want_grad=False,
+                                s_stats=st[rs])
+        assert torch.equal(loss.cpu(), loss2.cpu())
