@@ -263,7 +263,8 @@ GEOMETRY = (
 
 # the real widths at 2 layers per tower, bs 1, 336x336 (L = 1536): SigLIP hd 72, the teacher's
 # hd 128 with GQA 28/4 at width 3584, the student's 14/2 at 896, the real MLP widths
-REAL = (("lb", 0, "real_lb"), ("dt", 1, "real_dt1"), ("dt", 2, "real_dt2"), ("fb", 0, "real_fb"))
+REAL = (("lb", 0, "real_lb"), ("dt", 1, "real_dt1"), ("dt", 2, "real_dt2"), ("fb", 0, "real_fb"),
+        ("dt", 3, "real_dt3"), ("bd", 0, "real_bd"))
 
 
 def main_real(names):

@@ -16,7 +16,8 @@ GEOMETRY_KINDS = {"sun_lb": ("lb", 0), "sun_dt1": ("dt", 1), "mix_bd": ("bd", 0)
                   "mix_dt1": ("dt", 1)}
 ALL_KINDS = {**KINDS, **GEOMETRY_KINDS}
 # the real widths at 2 layers per tower (make_golden_model.REAL; bs 1, 336x336)
-REAL_KINDS = {"real_lb": ("lb", 0), "real_dt1": ("dt", 1), "real_dt2": ("dt", 2), "real_fb": ("fb", 0)}
+REAL_KINDS = {"real_lb": ("lb", 0), "real_dt1": ("dt", 1), "real_dt2": ("dt", 2), "real_fb": ("fb", 0),
+              "real_dt3": ("dt", 3), "real_bd": ("bd", 0)}
 EVERY_KIND = {**ALL_KINDS, **REAL_KINDS}
 GRAD_SAMPLE = 4096   # gradient entries recorded per parameter in the real-width fixtures
 

@@ -7,7 +7,8 @@ transformers with the same seeded weights —
     tiles, 2,929 image tokens, L = 2,980) at bs 1 for LoCa / DT phase 1, and a mixed,
     right-padded [336x336, 480x640] batch (-100 labels on the pads, NT-Xent over the 7 real
     tiles) for BD / FB / DT phase 1;
-  * the REAL widths at 2 layers per tower (real_*: bs 1, 336x336): SigLIP 1152/4304 with 16
+  * the REAL widths at 2 layers per tower (real_*: bs 1, 336x336; every module kind: LB, DT
+    phases 1-3, FB, BD): SigLIP 1152/4304 with 16
     heads of hd 72, the 7B's Qwen2 3584/18944 with GQA 28/4 at hd 128, the 0.5B's 896/4864
     with 14/2 at hd 64 — the shapes every kernel of the full-size step runs at.
 The HIP path stores bf16 with fp32 accumulation and fp32 residual streams; the reference
@@ -46,7 +47,7 @@ ATOL, RTOL = 1e-4, 1e-3   # north_star
 NTX_RTOL = 3e-3           # the NT-Xent term (1 / tau = 14.3 amplification of the feature error)
 # kinds whose gradient total norm meets the north-star 1e-3 (profiles/r04/parity.json)
 GRAD_NORTH_STAR = {"lb", "dt2", "dt3", "bd", "fb", "sun_lb", "mix_bd", "mix_fb", "mix_dt1", "real_lb", "real_dt1", "real_dt2",
-                   "real_fb"}
+                   "real_fb", "real_dt3", "real_bd"}
 
 
 def _near(got, ref, what, rtol=RTOL):

@@ -6,6 +6,8 @@ producing kernel leaves it); median of --iters calls.  Same jsonl rows as tune_g
 tools/fit_plan.py fits gemm.hip:plan_gemm to it.
     python tools/tune_gemm_cold.py tools/step_shapes_c1.json [top] [--iters 6]"""
 import json
+import os
+import re
 import sys
 from pathlib import Path
 
@@ -43,6 +45,8 @@ def cold_time(f, a):
 
 g = torch.Generator(device=dev).manual_seed(0)
 for sh in shapes:
+    if os.environ.get("TUNE_MATCH") and not re.search(os.environ["TUNE_MATCH"], sh):
+        continue
     parts = sh.split(":")
     kind, (M, N, K) = parts[0], map(int, parts[1].split("x"))
     if kind not in ("gemm_kk", "gemm_kn", "gemm_nn"):
@@ -59,10 +63,10 @@ for sh in shapes:
     ops.gemm(a, b, out=out, accumulate=acc)
     auto = cold_time(lambda: ops.gemm(a, b, out=out, accumulate=acc), a)
     res = {}
-    VARS = (5, 6, 7, 16)
+    VARS = tuple(int(v) for v in os.environ.get("TUNE_VARS", "5,6,7,16").split(","))
     for var in VARS:
         for sk in (1, 2, 3, 4, 6, 8, 12, 16):
-            if sk > 1 and (K // 32) // sk < 4:
+            if sk > 1 and (var == 1 or (K // 32) // sk < 4):
                 continue
             if sk > 1 and sk * M * N * 4 > ops.GEMM_SPLITK_WS:
                 continue
