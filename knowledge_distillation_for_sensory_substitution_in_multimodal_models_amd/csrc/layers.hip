@@ -734,7 +734,8 @@ __global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, con
 
 // ---------------------------------------------------------------- AdamW ----
 // torch.optim.AdamW semantics: p -= lr*wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
-// p -= lr * (m / (1-b1^t)) / (sqrt(v / (1-b2^t)) + eps).  Master fp32, working copy bf16.
+// p -= (lr / (1-b1^t)) * m / (sqrt(v) / sqrt(1-b2^t) + eps).  Master fp32, working copy bf16.
+template <int U, bool NTL, bool CW = false>
 __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const float* __restrict__ g, float* __restrict__ m,
                         float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
                         float bc1, float bc2, const float* __restrict__ gscale, const int32_t* __restrict__ skip,
@@ -745,12 +746,20 @@ __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const floa
     for (int j = 0; j < n_skip; ++j) bad |= skip[j];
     if (bad) return;
     const float gs = gscale ? *gscale : 1.f;
+    // torch.optim.AdamW's order (step_size = lr / bc1, denom = sqrt(v) / sqrt(bc2) + eps, p -=
+    // step_size * m / denom) with the two per-element IEEE divisions and the correctly rounded sqrt
+    // replaced by v_sqrt_f32, v_rcp_f32 and the host's reciprocal of sqrt(bc2): 55 -> ~14 VALU per
+    // parameter, which held the kernel below the HBM rate.  m and v are computed as before (same
+    // bits); the update term moves by a few ulp of itself, ~1e-3 of an ulp of p at lr 1e-3
+    // (tests/test_layers_gpu.py::test_adamw_matches_torch: p to 1e-6, the bf16 copy exactly)
+    const float step_size = lr / bc1, inv_bc2s = bc2;   // launch_adamw passes 1 / sqrt(bc2) as bc2
     auto step = [&](float& pi, float& mi, float& vi, float graw) {
         const float gi = graw * gs;
         pi = pi * (1.f - lr * wd);
         mi = b1 * mi + (1.f - b1) * gi;
         vi = b2 * vi + (1.f - b2) * gi * gi;
-        pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+        const float denom = fmaf(__builtin_amdgcn_sqrtf(vi), inv_bc2s, eps);
+        pi = fmaf(-step_size, mi * __builtin_amdgcn_rcpf(denom), pi);
     };
     // 4 parameters per thread and iteration: 16-B loads / stores of p, g, m, v, 8-B bf16 stores
     // (same per-element arithmetic as the scalar tail)
@@ -760,20 +769,29 @@ __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const floa
     int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // U chunks per thread and iteration, every load issued before the first store (a small grid
     // -- KD_ADAMW_GRID -- then still keeps 16 x 16 B in flight per lane)
-    constexpr int U = 4;
-    for (; i0 + (U - 1) * stride < n4; i0 += U * stride) {
+    auto ld = [](const float* a, int64_t i) {
+        if constexpr (NTL) return __builtin_nontemporal_load((const f32x4*)a + i);
+        else return *((const f32x4*)a + i);
+    };
+    // CW: each wave owns contiguous runs of U x 64 16-B chunks (U KiB of every tensor) instead of
+    // lane-strided chunks a grid apart
+    const int64_t wgl = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = stride >> 6;
+    const int lane = threadIdx.x & 63;
+    if (CW) i0 = wgl * 64 * U + lane;
+    const int64_t ustep = CW ? 64 : stride, istep = CW ? nw * 64 * U : U * stride;
+    for (; i0 + (U - 1) * ustep < n4; i0 += istep) {
         f32x4 pv[U], mv[U], vv[U], gv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            pv[u] = __builtin_nontemporal_load((const f32x4*)p + i);
-            mv[u] = __builtin_nontemporal_load((const f32x4*)m + i);
-            vv[u] = __builtin_nontemporal_load((const f32x4*)v + i);
-            gv[u] = __builtin_nontemporal_load((const f32x4*)g + i);
+            const int64_t i = i0 + u * ustep;
+            pv[u] = ld(p, i);
+            mv[u] = ld(m, i);
+            vv[u] = ld(v, i);
+            gv[u] = ld(g, i);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
+            const int64_t i = i0 + u * ustep;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float pe = pv[u][e], me = mv[u][e], ve = vv[u][e];
@@ -789,7 +807,7 @@ __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const floa
             __builtin_nontemporal_store(pbv, (bf16x4*)pb + i);
         }
     }
-    for (int64_t i = i0; i < n4; i += stride) {
+    for (int64_t i = i0; i < n4; i += ustep) {
         // every byte is touched once: non-temporal loads / stores (4.79 -> 4.65 ms for 894 M
         // parameters, tools/bench_adamw.py)
         f32x4 pv = __builtin_nontemporal_load((const f32x4*)p + i), mv = __builtin_nontemporal_load((const f32x4*)m + i);
@@ -1160,14 +1178,29 @@ int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t
                  float eps, float wd, int step, const float* gscale, const int32_t* skip, int n_skip, void* stream) {
     KD_CHECK_ARG(p && pb && g && m && v && step >= 1, "adamw: bad argument");
     KD_CHECK_ARG(n_skip >= 0 && n_skip <= 64 && (n_skip == 0 || skip), "adamw: bad skip words");
-    const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+    const float bc1 = 1.f - powf(b1, (float)step);
+    const float bc2 = (float)(1.0 / std::sqrt((double)(1.f - powf(b2, (float)step))));   // 1 / sqrt(bias correction 2)
     // KD_ADAMW_GRID (read per call): the workgroup count; default one 256-thread workgroup per 4 K
     // parameters up to 16384. A small grid leaves CUs to the GEMMs of the concurrent teacher forward
     // (a v8 GEMM workgroup needs a whole CU, so every CU holding AdamW waves is closed to it).
     int grid = grid_for(n, 256, 16384);
     if (const int cap = ab_knob("KD_ADAMW_GRID", 0); cap > 0) grid = std::min(grid, cap);
-    hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, as_stream(stream), p, (bf16*)pb, g, m, v, n,
-                       lr, b1, b2, eps, wd, bc1, bc2, gscale, skip, n_skip);
+    // eight 16-B chunks of each tensor in flight per lane (tools/bench_adamw.py, one box: 5.13-5.15 ms
+    // vs 5.22-5.28 with four; the CW build -- each wave on contiguous 8 KiB runs -- 5.08-5.16, not kept)
+#define KD_ADAMW_LAUNCH(U, NTL, CW)                                                                                   \
+    hipLaunchKernelGGL((k_adamw<U, NTL, CW>), dim3(grid), dim3(256), 0, as_stream(stream), p, (bf16*)pb, g, m, v, n, \
+                       lr, b1, b2, eps, wd, bc1, bc2, gscale, skip, n_skip)
+#ifdef KD_AB_BUILD
+    // KD_ADAMW_V: 1 = four chunks, temporal loads; 2 = two chunks; 3 = four; 4 = eight, contiguous per wave
+    const int av = ab_knob("KD_ADAMW_V", 0);
+    if (av == 1) KD_ADAMW_LAUNCH(4, false, false);
+    else if (av == 2) KD_ADAMW_LAUNCH(2, true, false);
+    else if (av == 3) KD_ADAMW_LAUNCH(4, true, false);
+    else if (av == 4) KD_ADAMW_LAUNCH(8, true, true);
+    else
+#endif
+    KD_ADAMW_LAUNCH(8, true, false);
+#undef KD_ADAMW_LAUNCH
     KD_LAUNCH_CHECK("k_adamw");
     return KD_OK;
 }
