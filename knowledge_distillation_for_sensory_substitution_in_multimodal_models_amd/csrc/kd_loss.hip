@@ -715,6 +715,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, u
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
+#ifdef KD_AB_BUILD
+// KD_RR_STAMPS=1 (A/B build): wave 0 of every workgroup adds its s_memtime cycles per phase of a row
+// (loads + pass A, block sums, hand-off, pass B + stores, rows) to rr_stamps[block][8]
+__device__ unsigned long long rr_stamps[4096 * 8];
+#define KD_RR_STAMP(k, v) do { if (stamp && wid == 0 && lane == 0) atomicAdd(&rr_stamps[blockIdx.x * 8 + (k)], (v)); } while (0)
+#else
+#define KD_RR_STAMP(k, v) do { } while (0)
+#endif
 template <bool T1, int RC>
 __global__ void __launch_bounds__(RR_NT, RC >= 5 ? 4 : 6)
 k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ S_, int64_t ld_s,
@@ -722,7 +730,10 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                     const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g,
                     const float* __restrict__ coefs, bf16* __restrict__ D_, int64_t ld_d,
                     float* __restrict__ part_kl, int nsl, int cps, int n_rg,
-                    unsigned long long* __restrict__ gran, uint32_t poll_ticks) {
+                    unsigned long long* __restrict__ gran, uint32_t poll_ticks, int stamp) {
+#ifndef KD_AB_BUILD
+    stamp = 0;   // the product build carries no stamps (every stamp branch folds away)
+#endif
     __shared__ unsigned long long smask[RR_MASK_W];
     __shared__ float red[2 * RR_NW];
     __shared__ float row_sums[2];
@@ -828,14 +839,18 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         }
     };
     // row r from registers (xt, xs)
-    auto row = [&](Set& xt, Set& xs, int r) {
+    auto row = [&](Set& xt, Set& xs, int r, uint64_t ts0) {
         const RowStats st = stats[r];
         R.cq = (st.mt * invT + logf(st.zt)) * KD_LOG2E;
         R.cs = (st.ms * invT + logf(st.zs)) * KD_LOG2E;
         f32x2 term2, sacc2;
         pass_a(xt, xs, c_lo, c_hi, mb, term2, sacc2);
+        uint64_t ts1 = 0;
+        if (stamp) { ts1 = __builtin_amdgcn_s_memtime(); KD_RR_STAMP(0, ts1 - ts0); }
         float tp, sp;
         block_sums(term2, sacc2, tp, sp);
+        uint64_t ts2 = 0;
+        if (stamp) { ts2 = __builtin_amdgcn_s_memtime(); KD_RR_STAMP(1, ts2 - ts1); }
         if (wid == 0) {
             int miss = 0;
             if (nsl > 1) {
@@ -863,6 +878,8 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         }
         __syncthreads();
         const int miss = miss_s;
+        uint64_t ts3 = 0;
+        if (stamp) { ts3 = __builtin_amdgcn_s_memtime(); KD_RR_STAMP(2, ts3 - ts2); }
         if (miss) {
             // a slice of this row is not running now (its workgroup is not resident beside this one:
             // other work holds CUs): compute its partials here with the same body and lane mapping, so
@@ -938,11 +955,18 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                 drow[labn] = (bf16)(g - R.cec);
             }
         }
+        if (stamp) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t ts4 = __builtin_amdgcn_s_memtime();
+            KD_RR_STAMP(3, ts4 - ts3);
+            KD_RR_STAMP(4, 1ull);
+        }
     };
     for (int r = rg; r < rows; r += n_rg) {
         Set xt, xs;
+        const uint64_t ts0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
         load(xt, xs, r, c_lo, c_hi);
-        row(xt, xs, r);
+        row(xt, xs, r, ts0);
     }
 }
 
@@ -1174,7 +1198,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
 #define KD_LAUNCH_RR(T1v, RCv)                                                                                   \
     hipLaunchKernelGGL((k_loss_grad_loca_rr<T1v, RCv>), dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s, \
                        V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg, gran,   \
-                       rr_poll_ticks())
+                       rr_poll_ticks(), ab_knob("KD_RR_STAMPS", 0))
         if (rc == 5) { if (invT == 1.f) KD_LAUNCH_RR(true, 5); else KD_LAUNCH_RR(false, 5); }
         else { if (invT == 1.f) KD_LAUNCH_RR(true, 3); else KD_LAUNCH_RR(false, 3); }
 #undef KD_LAUNCH_RR
@@ -1229,3 +1253,17 @@ int kd_loss_check_impl(const void* ws_, void* stream_) {
 }
 
 }  // namespace kd
+
+#ifdef KD_AB_BUILD
+// A/B build: read (and clear) k_loss_grad_loca_rr's per-workgroup phase stamps (KD_RR_STAMPS=1)
+extern "C" int kd_ab_rr_stamps(unsigned long long* host, int n, int clear) {
+    if (n > 4096 * 8) n = 4096 * 8;
+    if (hipDeviceSynchronize() != hipSuccess) return 6;
+    if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(kd::rr_stamps), (size_t)n * 8) != hipSuccess) return 6;
+    if (clear) {
+        static unsigned long long zeros[4096 * 8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(kd::rr_stamps), zeros, sizeof(zeros)) != hipSuccess) return 6;
+    }
+    return 0;
+}
+#endif
