@@ -738,7 +738,7 @@ __global__ void __launch_bounds__(NT) k_ntxent(const float* __restrict__ fs, con
 template <int U, bool NTL, bool CW = false>
 __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const float* __restrict__ g, float* __restrict__ m,
                         float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                        float bc1, float bc2, const float* __restrict__ gscale, const int32_t* __restrict__ skip,
+                        float bc1, float inv_bc2s, const float* __restrict__ gscale, const int32_t* __restrict__ skip,
                         int n_skip) {
     // a step whose batch raised a device error (the sticky error words of the step, see
     // kd_adamw) leaves every weight and moment untouched
@@ -752,7 +752,7 @@ __global__ void k_adamw(float* __restrict__ p, bf16* __restrict__ pb, const floa
     // parameter, which held the kernel below the HBM rate.  m and v are computed as before (same
     // bits); the update term moves by a few ulp of itself, ~1e-3 of an ulp of p at lr 1e-3
     // (tests/test_layers_gpu.py::test_adamw_matches_torch: p to 1e-6, the bf16 copy exactly)
-    const float step_size = lr / bc1, inv_bc2s = bc2;   // launch_adamw passes 1 / sqrt(bc2) as bc2
+    const float step_size = lr / bc1;   // inv_bc2s = 1 / sqrt(1 - b2^t), from the host
     auto step = [&](float& pi, float& mi, float& vi, float graw) {
         const float gi = graw * gs;
         pi = pi * (1.f - lr * wd);
@@ -1179,7 +1179,7 @@ int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t
     KD_CHECK_ARG(p && pb && g && m && v && step >= 1, "adamw: bad argument");
     KD_CHECK_ARG(n_skip >= 0 && n_skip <= 64 && (n_skip == 0 || skip), "adamw: bad skip words");
     const float bc1 = 1.f - powf(b1, (float)step);
-    const float bc2 = (float)(1.0 / std::sqrt((double)(1.f - powf(b2, (float)step))));   // 1 / sqrt(bias correction 2)
+    const float inv_bc2s = (float)(1.0 / std::sqrt((double)(1.f - powf(b2, (float)step))));   // 1 / sqrt(bias correction 2)
     // KD_ADAMW_GRID (read per call): the workgroup count; default one 256-thread workgroup per 4 K
     // parameters up to 16384. A small grid leaves CUs to the GEMMs of the concurrent teacher forward
     // (a v8 GEMM workgroup needs a whole CU, so every CU holding AdamW waves is closed to it).
@@ -1189,7 +1189,7 @@ int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t
     // vs 5.22-5.28 with four; the CW build -- each wave on contiguous 8 KiB runs -- 5.08-5.16, not kept)
 #define KD_ADAMW_LAUNCH(U, NTL, CW)                                                                                   \
     hipLaunchKernelGGL((k_adamw<U, NTL, CW>), dim3(grid), dim3(256), 0, as_stream(stream), p, (bf16*)pb, g, m, v, n, \
-                       lr, b1, b2, eps, wd, bc1, bc2, gscale, skip, n_skip)
+                       lr, b1, b2, eps, wd, bc1, inv_bc2s, gscale, skip, n_skip)
 #ifdef KD_AB_BUILD
     // KD_ADAMW_V: 1 = four chunks, temporal loads; 2 = two chunks; 3 = four; 4 = eight, contiguous per wave
     const int av = ab_knob("KD_ADAMW_V", 0);
