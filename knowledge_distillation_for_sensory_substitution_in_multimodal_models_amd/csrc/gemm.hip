@@ -71,6 +71,11 @@ struct GemmP {
     int sk_steps, sk_grid;
     float* sk_ws;
     int gm;                // tile rows per group of the grouped tile order (0: GM_GROUP)
+    // k-loop start stagger (v8, K % 32 == 0, K >= 2048): the tiles of row group j of ngrp start
+    // their K loop at stage j * nk / ngrp and wrap, so the XCDs (each a chunk of one group) stream
+    // different K stages at once while each XCD still shares its L2 (cold: teacher lm_head, q|k|v,
+    // o_proj, down_proj -4 %, gate|up -1 %; c1 step +0.7 %, profiles/r05/gemm_stagger.txt); 0 = off
+    int stagger;
 };
 
 // stream-K: the workgroup whose run [floor(tot w / G), floor(tot (w+1) / G)) holds step s
@@ -1208,6 +1213,18 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     const int m0 = tm * 256, n0 = tn * 256;
     const int K = p.K;
     const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
+    // staggered k start (GemmP.stagger): stage st of the loop reads K stage (st + rot) mod nk; the
+    // stages past the end (st >= nk) stay the zero-filled out-of-range DMAs they are unrotated. rot
+    // is a function of the tile ROW group alone (grp of ngrp, the grouped order's g rows each; a
+    // group is whole XCD chunks), so every launch over the same rows -- the SwiGLU build, pre-tiled
+    // B, the row-statistics build, the plain GEMM -- sums each output in the same order. Short K
+    // loops (nk < 64: the student's K = 896 lm_head measured 1-2 % slower rotated) start at 0.
+    int rot = 0;
+    if (p.stagger && nk_full == nk && nk >= 64) {
+        const int g = p.gm > 0 ? p.gm : GM_GROUP, ngrp = ((p.M + 255) / 256 + g - 1) / g;
+        rot = (int)(((int64_t)(tm / g) * nk) / ngrp);
+    }
+    auto kst = [&](int st) { return (rot == 0 || st >= nk) ? st : (st + rot >= nk ? st + rot - nk : st + rot); };
     const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (A_MN ? 0 : (int64_t)m0 * p.lda), A_MN ? 0u : rec_bytes(min(256, p.M - m0), p.lda));
     constexpr bool glu = !B_MN && (EXP & 4);   // gate rows [nb, nb+128) and up rows [I+nb, I+nb+128)
     const int nb = tn * 128;
@@ -1239,13 +1256,13 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
         uint32_t v = isA ? va[u & 3] : vb[u & 3];
         if (TB && !isA) {   // one contiguous KiB of stage st (zero-padded past K); past the last stage: zeros
-            int soff = st * (256 * BK2 * 2);
+            int soff = kst(st) * (256 * BK2 * 2);
             if (!FULL && st >= nkt) { v = OOB; soff = 0; }
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsBk, (lds_void_t*)dst, 16, v, soff, 0, 0);
             return;
         }
         if (!mn) {
-            int soff = HOT ? 0 : st * BK2 * 2;
+            int soff = HOT ? 0 : kst(st) * BK2 * 2;
             if (!FULL) {
                 const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
                 if (kleft < BK2) {                // zero the chunks at k >= K
@@ -1260,7 +1277,8 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
             const bf16* base = isA ? p.A + m0 : p.B + n0;
             const int64_t ld = isA ? p.lda : p.ldb;
             const int kv = FULL ? BK2 : max(0, min(BK2, K - st * BK2));
-            const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)(FULL ? st * BK2 : min(st * BK2, K)) * ld, rec_bytes(kv, ld));
+            const int ks = kst(st);
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)(FULL ? ks * BK2 : min(ks * BK2, K)) * ld, rec_bytes(kv, ld));
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)dst, 16, v, 0, 0, 0);
         }
     };
@@ -1274,7 +1292,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         const bool isA = u < 4;
         const int i = wid * 4 + (u & 3);
         uint32_t v = isA ? va[u & 3] : vb[u & 3];
-        int soff = st * BK2 * 2;
+        int soff = kst(st) * BK2 * 2;
         if (!FULL) {
             const int kleft = K - st * BK2;
             if (kleft < BK2) {
@@ -2705,6 +2723,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr;
     p.gm = 0;
     p.rst = nullptr; p.rst_nt = p.rst_vs = p.rst_top2 = 0; p.rst_inv_t = 1.f;
+    p.stagger = ab_knob("KD_GEMM_STAGGER", 1);
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->qkv || ((d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0))) &&

@@ -10,6 +10,10 @@ import pytest
 REPO = Path(__file__).resolve().parent.parent.parent
 AB_LIB = REPO / "tools" / "ab" / "libkdstep_ab.so"
 os.environ.setdefault("KDSTEP_LIB", str(AB_LIB))
+# v8's k-loop stagger (GemmP.stagger, on in the product) changes v8's summation order; the A/B
+# kernels (v9, v11, v12) have none, so their bit-exact comparisons run v8 unstaggered. The A/B
+# library reads the switch on every launch: test_v8_stagger_* turns it on where it compares.
+os.environ.setdefault("KD_GEMM_STAGGER", "0")
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tests"))
 sys.path.insert(0, str(REPO / "tests" / "golden"))

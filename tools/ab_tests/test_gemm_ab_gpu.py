@@ -57,3 +57,33 @@ def test_register_staged_v8_bitexact(M, N, K, dev):
         s16 = ops.gemm(a, w, act="swiglu", aux=g16, variant=16)
         s22 = ops.gemm(a, w, act="swiglu", aux=g22, variant=22)
         assert torch.equal(s22, s16) and torch.equal(g22, g16)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (6144, 1024, 3584), (3000, 1280, 1152), (2048, 768, 600)])
+def test_v8_stagger_matches_unstaggered(M, N, K, dev):
+    """The k-loop stagger (KD_GEMM_STAGGER, the product default) only rotates where each tile's
+    K loop starts: the same products, summed in another order -- equal to the unstaggered v8
+    within fp32 reordering (bf16 outputs: at most a few 1-ulp differences), bit-identical where
+    no tile rotates (one row group, K % 32 != 0 or K < 2048), and the same bits for the SwiGLU build's
+    aux, pre-tiled B and the plain GEMM under the stagger."""
+    import os
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=130)
+    w = _rand(N, K, dev=dev, seed=131, scale=0.05)
+    ref = ops.gemm(a, w, variant=16, split_k=1)
+    os.environ["KD_GEMM_STAGGER"] = "1"
+    try:
+        got = ops.gemm(a, w, variant=16, split_k=1)
+        if K % 32 or K < 2048:
+            assert torch.equal(got, ref)
+        d = (got.float() - ref.float()).abs()
+        assert d.max().item() <= 2 ** -6 * ref.float().abs().max().item()
+        assert (got != ref).float().mean().item() < 0.05
+        assert torch.equal(ops.gemm(a, w, b_pretiled=ops.pretile_b(w)), got)
+        if N % 256 == 0:
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            o = ops.gemm(a, w, act="swiglu", aux=aux)
+            assert torch.equal(aux, got)
+            assert torch.equal(o, ops.swiglu_fwd(got, N // 2))
+    finally:
+        os.environ["KD_GEMM_STAGGER"] = "0"
