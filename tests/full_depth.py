@@ -73,12 +73,14 @@ def row_index(L: int = 1536, n: int = N_ROWS):
     return torch.randperm(L, generator=g)[:n].sort().values
 
 
-def hip_step(dev, teacher_residual_f32: bool = False, keep_weights: bool = True):
+def hip_step(dev, teacher_residual_f32: bool = False, keep_weights: bool = True, teacher_fp8: bool | str = False):
     """One training_step + backward of LogitBasedKD at full size, bs 1.  Returns (results on
-    the host, teacher state_dict, student state_dict) -- the weights as fp32 host tensors."""
+    the host, teacher state_dict, student state_dict) -- the weights as fp32 host tensors.
+    teacher_fp8: the e4m3 teacher of BASELINE config c4 (a modeling.FP8_FAMILIES policy), on the
+    same (seeded) bf16 weights, quantised after the load."""
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import ops
-    m = K.LogitBasedKD(S_NAME, T_NAME, teacher_residual_f32=teacher_residual_f32)
+    m = K.LogitBasedKD(S_NAME, T_NAME, teacher_residual_f32=teacher_residual_f32, teacher_fp8=teacher_fp8)
     bc = batch_cpu()
     b = _to(bc, dev)
     m.keep_logits = True
@@ -213,9 +215,11 @@ def compare(hip: dict, ref: dict, W: torch.Tensor | None = None) -> dict:
     return out
 
 
-def measure(dev, floor: bool = False, teacher_stream_ab: bool = False) -> dict:
+def measure(dev, floor: bool = False, teacher_stream_ab: bool = False, teacher_fp8: str | None = None) -> dict:
     """The whole report: HIP (default teacher stream) vs the fp32 oracle; optionally the plain
-    bf16 oracle (floor) and the HIP step with the teacher's Qwen2 residual stream in fp32."""
+    bf16 oracle (floor), the HIP step with the teacher's Qwen2 residual stream in fp32, and the
+    HIP step with the fp8 (e4m3) teacher of config c4 (policy `teacher_fp8`) against the same fp32
+    reference -- the fp8 teacher's full-depth distance from the reference, not from the bf16 teacher."""
     t0 = time.time()
     _log("HIP step (teacher Qwen2 stream bf16, the default)")
     hip, tsd, ssd = hip_step(dev, teacher_residual_f32=False)
@@ -224,6 +228,10 @@ def measure(dev, floor: bool = False, teacher_stream_ab: bool = False) -> dict:
     if teacher_stream_ab:
         _log("HIP step (teacher Qwen2 stream fp32)")
         hip32, _, _ = hip_step(dev, teacher_residual_f32=True, keep_weights=False)
+    hip8 = None
+    if teacher_fp8:
+        _log(f"HIP step (fp8 e4m3 teacher, policy {teacher_fp8})")
+        hip8, _, _ = hip_step(dev, keep_weights=False, teacher_fp8=teacher_fp8)
     _log(f"fp32 oracle step on the same weights ({torch.get_num_threads()} threads)")
     ref = oracle_step(tsd, ssd, torch.float32)
     rep = {"config": "c1: LogitBasedKD (LoCa T = 1), bs 1, L 1536, 336x336, full depth (SigLIP 26 + Qwen2 28 / 24 layers)",
@@ -233,6 +241,10 @@ def measure(dev, floor: bool = False, teacher_stream_ab: bool = False) -> dict:
     if hip32 is not None:
         rep["hip_teacher_stream_f32"] = compare(hip32, ref, W)
         del hip32
+    if hip8 is not None:
+        rep["hip_teacher_fp8"] = compare(hip8, ref, W)
+        rep["hip_teacher_fp8"]["policy"] = teacher_fp8
+        del hip8
     if floor:
         _log("bf16 oracle step (the floor)")
         fl = oracle_step(tsd, ssd, torch.bfloat16)

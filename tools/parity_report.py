@@ -103,13 +103,16 @@ def main():
     ap.add_argument("--floor", action="store_true", help="--full-depth: also the plain-bf16 oracle (the floor)")
     ap.add_argument("--teacher-stream-ab", action="store_true",
                     help="--full-depth: also the HIP step with the teacher's Qwen2 residual stream in fp32")
+    ap.add_argument("--teacher-fp8", default=None, metavar="POLICY",
+                    help="--full-depth: also the HIP step with the fp8 (e4m3) teacher of c4 (e.g. lm_mlp)")
     ap.add_argument("kinds", nargs="*")
     a = ap.parse_args()
     import torch
     if a.full_depth:
         from full_depth import measure as fd_measure
-        rep = fd_measure(torch.device("cuda:0"), floor=a.floor, teacher_stream_ab=a.teacher_stream_ab)
-        for k in ("hip", "hip_teacher_stream_f32", "bf16_floor"):
+        rep = fd_measure(torch.device("cuda:0"), floor=a.floor, teacher_stream_ab=a.teacher_stream_ab,
+                         teacher_fp8=a.teacher_fp8)
+        for k in ("hip", "hip_teacher_stream_f32", "hip_teacher_fp8", "bf16_floor"):
             if k in rep:
                 r = {kk: vv for kk, vv in rep[k].items() if kk != "grad_params"}
                 print(k, json.dumps(r), flush=True)
