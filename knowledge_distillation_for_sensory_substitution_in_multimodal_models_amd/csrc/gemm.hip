@@ -801,10 +801,12 @@ __device__ __forceinline__ void epi_row_stats(const GemmP& p, const char* smem, 
 
 // HAS_ACT: the activation epilogue is instantiated for the forward (K-major x K-major) kernels
 // only; the launcher rejects an activation with MN-major operands or an fp32 output.
+// ST (diagnostic stamp builds): mk[0] = s_memtime after the bf16 LDS staging and its barrier,
+// mk[1] = after the flush's stores are issued (plain bf16 output only)
 template <int BM, int BN, int WM, int WN, int TM, int TN, int MT, int NT, int NTHR = NTH2, bool HAS_ACT = true,
-          bool RST = false, bool L32 = false>
+          bool RST = false, bool L32 = false, bool ST = false>
 __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int n0, int wm,
-                                          int wn, int lane, int tid) {
+                                          int wn, int lane, int tid, uint64_t* mk = nullptr) {
     const bool full = m0 + BM <= p.M && n0 + BN <= p.N;
     float alpha = p.alpha;
     if (p.alpha_dev) alpha *= *p.alpha_dev;
@@ -841,7 +843,9 @@ __device__ __forceinline__ void epilogue2(const GemmP& p, const f32x4 (&acc)[MT]
         if (HAS_ACT) epi_to_lds_act<TM, TN, MT, NT, false, L32>(p.act, acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         else epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS16, alpha, bcol, wm, wn, lane, 0, BM);
         __syncthreads();
+        if constexpr (ST) mk[0] = __builtin_amdgcn_s_memtime();
         epi_flush_sel<BM, BN, NTHR, false>(p, smem, RS16, p.C, p.ldc, m0, n0, tid, full, res, accum);
+        if constexpr (ST) mk[1] = __builtin_amdgcn_s_memtime();
         if constexpr (RST) epi_row_stats(p, smem, RS16, m0, n0, tid);
     } else {
 #pragma unroll
@@ -1421,15 +1425,17 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     else
 #endif
     if (!A_MN && !B_MN && glu) epilogue_glu<128, 128, 8, 8, NTH8, false, STAMP>(p, acc, smem, m0, nb, wm, wn, lane, tid, mk);
-    else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN, RSTATS>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+    else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, !A_MN && !B_MN, RSTATS, false, STAMP>(p, acc, smem, m0, n0, wm, wn, lane, tid, mk);
     if (STAMP) {
-        if (glu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         s_epi = te1 - te0;
         if (lane == 0) {
             uint32_t* o = stamps + ((int64_t)(blockIdx.y * p.gx + blockIdx.x) * 4 + wid) * 8;
-            // glu: o[1] = LDS staging (incl. the barrier), o[2] = the aux + silu * up pass
-            o[0] = (uint32_t)s_pro; o[1] = glu ? (uint32_t)(mk[0] - te0) : 0; o[2] = glu ? (uint32_t)(mk[1] - mk[0]) : 0;
+            // glu: o[1] = LDS staging (incl. the barrier), o[2] = the aux + silu * up pass;
+            // plain bf16 output: o[1] = LDS staging (incl. the barrier), o[2] = the flush's store
+            // issue, and the epilogue total o[5] includes the store drain (vmcnt(0)) after it
+            o[0] = (uint32_t)s_pro; o[1] = mk[0] ? (uint32_t)(mk[0] - te0) : 0; o[2] = mk[1] ? (uint32_t)(mk[1] - mk[0]) : 0;
             o[3] = (uint32_t)s_bar;
             o[4] = (uint32_t)s_units; o[5] = (uint32_t)s_epi; o[6] = (uint32_t)(te1 - ts0); o[7] = (uint32_t)nk;
             if (glu && wid == 0) {   // placement record per workgroup, past the per-wave block:

@@ -26,7 +26,7 @@ torch.cuda.synchronize()
 assert torch.equal(out, ref), "stamp build changed the result"
 blocks = ((M + 255) // 256) * ((N + 255) // 256)
 st = aux.view(-1).view(torch.int32)[: blocks * 4 * 8].view(blocks * 4, 8).cpu().double()
-names = ["prologue", "-", "-", "step sync", "units", "epilogue", "total"]
+names = ["prologue", "epi: LDS", "epi: store", "step sync", "units", "epilogue", "total"]
 tot = st[:, 6].mean().item()
 print(f"{M}x{N}x{K} {lay}: {blocks} blocks, {int(st[0, 7].item())} k-steps; mean cycles per wave")
 for i, n in enumerate(names):
