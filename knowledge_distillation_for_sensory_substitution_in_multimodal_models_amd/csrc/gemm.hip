@@ -2434,6 +2434,10 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     static const double fixed_c3[2][5] = {{5.253, 3.402, 3.414, 8.478, 5.888}, {5.885, 3.479, 3.398, 8.695, 8.442}};
     static const bool set3 = ab_knob("KD_PLAN_SET", 4) == 3;
     static const bool hybrid_on = ab_knob("KD_GEMM_HYBRID", 1) != 0;
+    // A/B: the cost model's split count capped (KD_SPLIT_CAP) and its partial-plane cost scaled
+    // (KD_SPLIT_PENALTY, percent) -- the model is fitted on isolated calls, the step runs two streams
+    static const int split_cap = ab_knob("KD_SPLIT_CAP", 32);
+    static const double split_pen = ab_knob("KD_SPLIT_PENALTY", 100) / 100.0;
     const double (&step_c)[2][5] = set3 ? step_c3 : step_c4;
     const double (&fixed_c)[2][5] = set3 ? fixed_c3 : fixed_c4;
     const double kBW = set3 ? 7.711e6 : 9.109e6;          // partial-plane bytes per microsecond
@@ -2462,9 +2466,10 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
             if (S > 1 && ((nk + kcs - 1) / kcs != S)) continue;          // empty trailing split
             if (S > 1 && d->split_k <= 1 && kcs < 8) continue;           // too little work per split
             if (S > 1 && (uint64_t)S * M * N * 4 > ws_cap) continue;
+            if (S > split_cap && d->split_k <= 0) continue;
             const int64_t waves = (tiles[v] * S + 255) / 256;
             double t = (double)waves * ((double)kcs * step[v] + fixed[v]);
-            if (S > 1) t += ((double)S * M * N * 8 + out_b) / kBW + kSplitLaunch;
+            if (S > 1) t += ((double)S * M * N * 8 * split_pen + out_b) / kBW + kSplitLaunch;
             if (d->split_k > 1 && S == d->split_k) t = -1;              // forced
             if (t < bt) { bt = t; best = GemmPlan{vcode[v], S, kcs * BK2, 0}; }
             // hybrid: whole waves unsplit, the tail tiles split S ways (model's choice only)
@@ -2473,7 +2478,7 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
                 const double tb = (double)tbm[v] * tbn[v];
                 double th = (double)(dp / 256) * ((double)nk * step[v] + fixed[v]) +
                             (double)((tail * S + 255) / 256) * ((double)kcs * step[v] + fixed[v]) +
-                            ((double)S * tail * tb * 8 + tail * tb * out_e) / kBW + 2 * kSplitLaunch;
+                            ((double)S * tail * tb * 8 * split_pen + tail * tb * out_e) / kBW + 2 * kSplitLaunch;
                 if (th < bt) { bt = th; best = GemmPlan{vcode[v], S, kcs * BK2, (int)dp}; }
             }
         }
