@@ -697,6 +697,12 @@ k_loss_grad_loca(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restri
 // other work holds CUs (a concurrent stream, a CU mask) the kernel slows down; it never waits on a
 // workgroup that is not running and never fails.
 // Same per-element arithmetic as k_loss_grad_loca; the row sums differ in fp32 order only.
+// Round 5: the LoCa override values of a slice's masked chunks (q and log2 q: one table for the whole
+// launch, a lane's chunks fixed) are copied once into an LDS image (<= ov_cap 64-B slots; a slice with
+// more reads the global table as before), so the per-row passes issue no override-table loads on the
+// in-order vector-memory counter (c1 loss 2361-2382 -> 2115-2156 us, the same bits); with them gone,
+// pass B loads chunk j of the row group's next row as soon as chunk j is computed (-1 %), the CE
+// one-hot then applied inside its chunk (the same arithmetic as the separate rewrite, the same bits).
 constexpr int RR_NT = 512, RR_NW = RR_NT / 64;
 constexpr int RR_C = 5;                                   // 16-B chunks of each tensor per lane per row (max)
 constexpr int RR_SLICE = RR_NT * RR_C;                    // max chunks per slice
@@ -730,10 +736,14 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                     const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g,
                     const float* __restrict__ coefs, bf16* __restrict__ D_, int64_t ld_d,
                     float* __restrict__ part_kl, int nsl, int cps, int n_rg,
-                    unsigned long long* __restrict__ gran, uint32_t poll_ticks, int stamp) {
+                    unsigned long long* __restrict__ gran, uint32_t poll_ticks, int stamp, int ov_cap, int pf) {
 #ifndef KD_AB_BUILD
     stamp = 0;   // the product build carries no stamps (every stamp branch folds away)
 #endif
+    // the slice's override values (q and log2 q of every overridden column of the lane's chunks), in
+    // LDS: ov_cap 64-B slots, one per chunk with a set mask byte, in (chunk j, wave, lane) order
+    extern __shared__ __attribute__((aligned(16))) f32x4 ov_img[];
+    __shared__ int wcnt[RC * RR_NW];
     __shared__ unsigned long long smask[RR_MASK_W];
     __shared__ float red[2 * RR_NW];
     __shared__ float row_sums[2];
@@ -757,12 +767,57 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
     __syncthreads();
     // the override mask is one table for the whole launch and the slice is fixed per
     // workgroup: a lane's RC mask bytes, once
+    // per chunk j a 12-bit field of mb: bit 0 = its mask byte is set, bits 1-11 = its override-image slot
     uint64_t mb = 0;
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
         const int c = c_lo + tid + j * RR_NT;
-        if (c < c_hi) mb |= ((smask[((c * 8) >> 6) - w_lo] >> ((c * 8) & 63)) & 0xffull) << (8 * j);
+        if (c < c_hi && ((smask[((c * 8) >> 6) - w_lo] >> ((c * 8) & 63)) & 0xffull)) mb |= 1ull << (12 * j);
     }
+    // the override image: the masked chunks' slots (base of this wave's run for chunk j + the lane's
+    // rank among the wave's masked lanes), filled once -- the table is one for the whole launch and a
+    // lane's chunks are fixed, so every row reads the same values.  With it the per-row passes issue
+    // no override-table loads on the vector-memory counter, which retires in order: the next row's
+    // chunks can be loaded during pass B without every table wait also waiting for them.  A slice
+    // with more masked chunks than ov_cap reads the table from global memory, as before.
+    {
+        uint64_t bal[RC];
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+            bal[j] = __ballot((mb >> (12 * j)) & 1u);
+            if (lane == 0) wcnt[j * RR_NW + wid] = __popcll(bal[j]);
+        }
+        __syncthreads();
+        int nmask = 0;
+#pragma unroll
+        for (int j = 0; j < RC; ++j)
+            for (int w = 0; w < RR_NW; ++w) {
+                if (w == wid && ((mb >> (12 * j)) & 1u)) {
+                    const int slot = nmask + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal[j] >> 32),
+                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bal[j], 0u));
+                    mb |= (uint64_t)(slot & 2047) << (12 * j + 1);
+                }
+                nmask += wcnt[j * RR_NW + w];
+            }
+        if (nmask > ov_cap) ov_cap = -1;   // uniform: every thread summed the same counts
+    }
+    const bool use_lds = ov_cap >= 0;
+    auto oslot = [&](int j) { return (int)((mb >> (12 * j + 1)) & 2047u); };
+    if (use_lds) {
+#pragma unroll
+        for (int j = 0; j < RC; ++j)
+            if ((mb >> (12 * j)) & 1u) {
+                const int v = (c_lo + tid + j * RR_NT) * 8;
+                f32x4* o = ov_img + 4 * oslot(j);
+                o[0] = *(const f32x4*)(ovr + v);
+                o[1] = *(const f32x4*)(ovr + v + 4);
+                o[2] = *(const f32x4*)(ovr + V + v);
+                o[3] = *(const f32x4*)(ovr + V + v + 4);
+            }
+        __syncthreads();
+    }
+    using LdsT = std::integral_constant<bool, true>;
+    using GlbT = std::integral_constant<bool, false>;
     LocaRow R;
     R.a = invT * KD_LOG2E;
     R.lcl = log2f(clamp_min);
@@ -786,7 +841,8 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
     // pass A (k_loss_grad_loca's arithmetic) over the chunks [lo, hi) held in (xt, xs), mask bytes mbx:
     // the lane's KD-term and S partials.  The ONE body both a slice's own partial and a stand-in's
     // recomputation of it run, so both give the same bits.
-    auto pass_a = [&](const Set& xt, const Set& xs, int lo, int hi, uint64_t mbx, f32x2& term2, f32x2& sacc2) {
+    auto pass_a = [&](const Set& xt, const Set& xs, int lo, int hi, uint64_t mbx, auto lds_tag, f32x2& term2, f32x2& sacc2) {
+        constexpr bool lds = decltype(lds_tag)::value;
         const f32x2 a2 = {R.a, R.a}, cq2 = {R.cq, R.cq}, cs2 = {R.cs, R.cs};
         term2 = f32x2{0.f, 0.f};
         sacc2 = f32x2{0.f, 0.f};
@@ -807,9 +863,15 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                 q[k] = ex2(lq[k]);
                 q[k + 1] = ex2(lq[k + 1]);
             }
-            if ((mbx >> (8 * j)) & 0xffu) {
-                const f32x4 o0 = *(const f32x4*)(ovr + v), o1 = *(const f32x4*)(ovr + v + 4);
-                const f32x4 l0 = *(const f32x4*)(ovr + V + v), l1 = *(const f32x4*)(ovr + V + v + 4);
+            if ((mbx >> (12 * j)) & 1u) {
+                f32x4 o0, o1, l0, l1;
+                if constexpr (lds) {
+                    const f32x4* o = ov_img + 4 * oslot(j);
+                    o0 = o[0]; o1 = o[1]; l0 = o[2]; l1 = o[3];
+                } else {
+                    o0 = *(const f32x4*)(ovr + v); o1 = *(const f32x4*)(ovr + v + 4);
+                    l0 = *(const f32x4*)(ovr + V + v); l1 = *(const f32x4*)(ovr + V + v + 4);
+                }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const float o = k < 4 ? o0[k] : o1[k - 4];
@@ -839,12 +901,16 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         }
     };
     // row r from registers (xt, xs)
-    auto row = [&](Set& xt, Set& xs, int r, uint64_t ts0) {
+    // row r from registers (xt, xs); returns true when pass B has already loaded row rn's chunks into them
+    // LDS (the override image is in use, a compile-time tag: one code path each, so neither carries
+    // the other's registers): the override values come from the image and pass B may prefetch
+    auto row = [&](Set& xt, Set& xs, int r, int rn, uint64_t ts0, auto lds_tag) -> bool {
+        constexpr bool LDS = decltype(lds_tag)::value;
         const RowStats st = stats[r];
         R.cq = (st.mt * invT + logf(st.zt)) * KD_LOG2E;
         R.cs = (st.ms * invT + logf(st.zs)) * KD_LOG2E;
         f32x2 term2, sacc2;
-        pass_a(xt, xs, c_lo, c_hi, mb, term2, sacc2);
+        pass_a(xt, xs, c_lo, c_hi, mb, lds_tag, term2, sacc2);
         uint64_t ts1 = 0;
         if (stamp) { ts1 = __builtin_amdgcn_s_memtime(); KD_RR_STAMP(0, ts1 - ts0); }
         float tp, sp;
@@ -892,10 +958,10 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
                     const int c = lo2 + tid + j * RR_NT;
-                    if (c < hi2) mb2 |= ((mask_g[(c * 8) >> 6] >> ((c * 8) & 63)) & 0xffull) << (8 * j);
+                    if (c < hi2 && ((mask_g[(c * 8) >> 6] >> ((c * 8) & 63)) & 0xffull)) mb2 |= 1ull << (12 * j);
                 }
                 load(xt, xs, r, lo2, hi2);
-                pass_a(xt, xs, lo2, hi2, mb2, term2, sacc2);
+                pass_a(xt, xs, lo2, hi2, mb2, GlbT{}, term2, sacc2);
                 float t2, s3;
                 block_sums(term2, sacc2, t2, s3);
                 if (tid == 0) { gv[2 * s2] = t2; gv[2 * s2 + 1] = s3; }
@@ -911,7 +977,7 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         }
         __syncthreads();
         const float Ssum = row_sums[1];
-        if (D_ == nullptr) return;
+        if (D_ == nullptr) return false;
         // ---- pass B from the registers
         R.cec = st.valid ? ce_coef : 0.f;
         R.K = kd_coef * Ssum + (T1 ? R.cec : 0.f);
@@ -919,6 +985,15 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
         R.c1 = (st.ms + logf(st.zs1)) * KD_LOG2E;
         bf16* drow = D_ + (int64_t)r * ld_d;
         const __amdgpu_buffer_rsrc_t rD = slice_rsrc(drow + c_lo * 8, (uint32_t)(c_hi - c_lo) * 16);
+        // pf: chunk j of row rn goes into (xt[j], xs[j]) as soon as chunk j of row r is computed; the
+        // CE one-hot is then applied inside its chunk (the same arithmetic as the rewrite below, so the
+        // same bits) instead of by a second store that would re-read the row's logits
+        const bool pre = LDS && pf && rn < rows;
+        const uint32_t nb = (uint32_t)(c_hi - c_lo) * 16;
+        const __amdgpu_buffer_rsrc_t rTn = slice_rsrc(T_ + (int64_t)(pre ? rn : r) * ld_t + c_lo * 8, nb);
+        const __amdgpu_buffer_rsrc_t rSn = slice_rsrc(S_ + (int64_t)(pre ? rn : r) * ld_s + c_lo * 8, nb);
+        const int labn = st.lab_next;
+        const int oh_c = (pre && st.valid) ? (labn >> 3) : -1, oh_k = labn & 7;
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
             const int c = c_lo + tid + j * RR_NT;
@@ -929,22 +1004,35 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
             bf16x8_to_f32(xs[j], sv);
 #pragma unroll
             for (int k = 0; k < 8; ++k) qk[k] = ex2(fmaf(t[k], R.a, -R.cqk));
-            if ((mb >> (8 * j)) & 0xffu) {
-                const f32x4 o0 = *(const f32x4*)(ovr + v), o1 = *(const f32x4*)(ovr + v + 4);
+            if ((mb >> (12 * j)) & 1u) {
+                f32x4 o0, o1;
+                if constexpr (LDS) {
+                    const f32x4* o = ov_img + 4 * oslot(j);
+                    o0 = o[0]; o1 = o[1];
+                } else {
+                    o0 = *(const f32x4*)(ovr + v); o1 = *(const f32x4*)(ovr + v + 4);
+                }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const float o = k < 4 ? o0[k] : o1[k - 4];
                     qk[k] = o == o ? o * kd_coef : qk[k];
                 }
             }
+            if (pre) {
+                xt[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rTn, vo, j * RR_NT * 16, 0));
+                xs[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rSn, vo, j * RR_NT * 16, 0));
+            }
             bf16x8 out;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) out[k] = (bf16)loca_grad<T1>(R, qk[k], sv[k]);
+            for (int k = 0; k < 8; ++k) {
+                float g = loca_grad<T1>(R, qk[k], sv[k]);
+                if (c == oh_c && k == oh_k) g -= R.cec;
+                out[k] = (bf16)g;
+            }
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out), rD, vo, j * RR_NT * 16, 0);
         }
         // the CE one-hot: the lane that wrote labn's chunk rewrites that element (program order)
-        const int labn = st.lab_next;
-        if (st.valid) {
+        if (st.valid && !pre) {
             const int c = labn >> 3;
             if (c >= c_lo && c < c_hi && (c - c_lo) % RR_NT == tid) {
                 const bf16* trow = T_ + (int64_t)r * ld_t;
@@ -961,13 +1049,19 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
             KD_RR_STAMP(3, ts4 - ts3);
             KD_RR_STAMP(4, 1ull);
         }
+        return pre;
     };
-    for (int r = rg; r < rows; r += n_rg) {
+    auto run = [&](auto lds_tag) {
         Set xt, xs;
-        const uint64_t ts0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-        load(xt, xs, r, c_lo, c_hi);
-        row(xt, xs, r, ts0);
-    }
+        bool have = false;
+        for (int r = rg; r < rows; r += n_rg) {
+            const uint64_t ts0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+            if (!have) load(xt, xs, r, c_lo, c_hi);
+            have = row(xt, xs, r, r + n_rg, ts0, lds_tag);
+        }
+    };
+    if (use_lds) run(LdsT{});
+    else run(GlbT{});
 }
 
 __global__ void k_finalize(const RowStats* __restrict__ stats, const float* __restrict__ part_kl,
@@ -1050,6 +1144,11 @@ k_loss_grad(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __restrict__ 
                             mask_g, kd_coef, ce_coef, D_, ld_d, part_kl, smask, red);
 }
 
+// LDS override-image slots of k_loss_grad_loca_rr<., rc> (64 B each): what leaves two (rc = 5) or three
+// (rc = 3) workgroups per CU their share of the 160 KB beside the kernel's static arrays
+inline int rr_ov_cap(int rc) { return rc >= 5 ? 1152 : 704; }
+inline size_t rr_smem(int rc) { return (size_t)rr_ov_cap(rc) * 64; }
+
 // resident k_loss_grad_loca_rr<., rc> workgroups on the current device (cached per device and rc):
 // CUs x min(occupancy answer, the workgroups per CU its __launch_bounds__ reserves registers for:
 // 2 at rc = 5, 3 at rc = 3) -- the occupancy API can answer one block high (MI355X_MICROARCH)
@@ -1062,7 +1161,7 @@ int rr_resident(int rc) {
         int cus = 0, nb = 0;
         const void* fn = rc >= 5 ? (const void*)k_loss_grad_loca_rr<true, 5> : (const void*)k_loss_grad_loca_rr<true, 3>;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, RR_NT, 0) != hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, RR_NT, rr_smem(rc)) != hipSuccess)
             cus = nb = 0;
         cache[dev][k] = cus * std::min(nb, cap) > 0 ? cus * std::min(nb, cap) : -1;
     }
@@ -1196,9 +1295,10 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
         if (nsl > 1 && hipMemsetAsync(gran, 0, (size_t)rows * nsl * 16, stream) != hipSuccess)
             return fail(KD_ERR_LAUNCH, "kd_loss: memset granules");
 #define KD_LAUNCH_RR(T1v, RCv)                                                                                   \
-    hipLaunchKernelGGL((k_loss_grad_loca_rr<T1v, RCv>), dim3(n_rg * nsl), dim3(RR_NT), 0, stream, T_, ld_t, S_, ld_s, \
-                       V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg, gran,   \
-                       rr_poll_ticks(), ab_knob("KD_RR_STAMPS", 0))
+    hipLaunchKernelGGL((k_loss_grad_loca_rr<T1v, RCv>), dim3(n_rg * nsl), dim3(RR_NT), rr_smem(RCv), stream, T_, ld_t,   \
+                       S_, ld_s, V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg, \
+                       gran, rr_poll_ticks(), ab_knob("KD_RR_STAMPS", 0), ab_knob("KD_RR_OV", 1) ? rr_ov_cap(RCv) : -1,   \
+                       ab_knob("KD_RR_PF", 1))
         if (rc == 5) { if (invT == 1.f) KD_LAUNCH_RR(true, 5); else KD_LAUNCH_RR(false, 5); }
         else { if (invT == 1.f) KD_LAUNCH_RR(true, 3); else KD_LAUNCH_RR(false, 3); }
 #undef KD_LAUNCH_RR

@@ -204,21 +204,35 @@ def test_loss_with_gemm_row_stats(variant, T, dev):
     assert bool((dd <= 2.0 ** -7 * d0.float().abs() + 1e-9).all()), dd.max().item()
 
 
+def _dense_labels(B, L, hi, g):
+    """B*L DISTINCT label ids in [0, hi): with hi one slice wide, that slice has more overridden
+    chunks than its LDS override image holds (k_loss_grad_loca_rr's ov_cap, 1152 at rc = 5), so it
+    reads the table from global memory while the other slices use their images."""
+    return torch.randperm(hi, generator=g)[:B * L].view(B, L)
+
+
 @pytest.mark.parametrize("B,L,V,T,ovr", [(2, 384, 151936, 1.0, True), (2, 384, 151936, 0.8, True),
-                                         (1, 200, 20480, 1.0, False), (3, 7, 24, 1.0, True)])
+                                         (1, 200, 20480, 1.0, False), (3, 7, 24, 1.0, True),
+                                         (2, 1536, 151936, 1.0, "dense"), (1, 2048, 151936, 0.8, "dense")])
 def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev, monkeypatch):
     """k_loss_grad_loca_rr (row slices held in registers, partials handed between the slices'
     workgroups) == k_loss_grad_loca (KD_LOSS_RR=0, two reads of every row) up to the fp32 order
     of the row sums: terms within 2e-6 relative, dlogits within one bf16 ulp.  Cases: the real
     vocab at T = 1 and 0.8 (8 slices), one slice (V = 20480), a vocab of 3 chunks; labels drawn
-    from a few ids so the LoCa override columns (DT:184-185) fall into several slices."""
+    from a few ids so the LoCa override columns (DT:184-185) fall into several slices; "dense":
+    3072 / 2048 distinct labels inside the first slice's 18,992 columns, more overridden chunks than
+    its LDS override image holds (the global-table path beside the other slices' images)."""
     ops = _ops()
     g = torch.Generator().manual_seed(5)
-    s = (torch.randn(B, L, V, generator=g) * 2).to(dev, torch.bfloat16)
-    t = (torch.randn(B, L, V + 128, generator=g) * 2).to(dev, torch.bfloat16)
-    hi = min(V, 4000) if ovr else V
-    labels = torch.randint(0, hi, (B, L), generator=g)
-    labels[:, ::3] = torch.randint(0, V, labels[:, ::3].shape, generator=g)
+    gd = torch.Generator(device=dev).manual_seed(5)
+    s = (torch.randn(B, L, V, generator=gd, device=dev) * 2).bfloat16()
+    t = (torch.randn(B, L, V + 128, generator=gd, device=dev) * 2).bfloat16()
+    if ovr == "dense":
+        labels = _dense_labels(B, L, 18992, g)
+    else:
+        hi = min(V, 4000) if ovr else V
+        labels = torch.randint(0, hi, (B, L), generator=g)
+        labels[:, ::3] = torch.randint(0, V, labels[:, ::3].shape, generator=g)
     labels = labels.to(dev)
     out = []
     for rr in ("0", "1"):
@@ -232,18 +246,22 @@ def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev, mo
     assert bool((dd <= 2.0 ** -7 * d0.float().abs() + 1e-12).all()), dd.max().item()
 
 
-@pytest.mark.parametrize("B,L,V,T", [(2, 384, 151936, 1.0), (1, 257, 151936, 0.8), (2, 64, 60000, 1.0)])
-def test_register_resident_loca_stand_in_is_bit_identical(B, L, V, T, dev, monkeypatch):
+@pytest.mark.parametrize("B,L,V,T,dense", [(2, 384, 151936, 1.0, False), (1, 257, 151936, 0.8, False),
+                                           (2, 64, 60000, 1.0, False), (2, 1536, 151936, 1.0, True)])
+def test_register_resident_loca_stand_in_is_bit_identical(B, L, V, T, dense, dev, monkeypatch):
     """Co-residency is not required by k_loss_grad_loca_rr: a slice whose partner slices have not
     handed over their pass-A partials within the poll budget computes them itself (same body, same
     lane mapping, same reduction order).  KD_LOSS_RR_POLL_US=0 forces that stand-in path for every
     absent partial of every row; the loss terms and dlogits must be the default path's bits, and no
-    error may be raised (the loss must never depend on workgroups being resident)."""
+    error may be raised (the loss must never depend on workgroups being resident).
+    dense: one slice overflows its LDS override image (global table) while the stand-ins read the
+    table from global memory for every slice they recompute."""
     ops = _ops()
     g = torch.Generator().manual_seed(11)
-    s = (torch.randn(B, L, V, generator=g) * 2).to(dev, torch.bfloat16)
-    t = (torch.randn(B, L, V + 128, generator=g) * 2).to(dev, torch.bfloat16)
-    labels = torch.randint(0, V, (B, L), generator=g).to(dev)
+    gd = torch.Generator(device=dev).manual_seed(11)
+    s = (torch.randn(B, L, V, generator=gd, device=dev) * 2).bfloat16()
+    t = (torch.randn(B, L, V + 128, generator=gd, device=dev) * 2).bfloat16()
+    labels = (_dense_labels(B, L, 18992, g) if dense else torch.randint(0, V, (B, L), generator=g)).to(dev)
     out = []
     for us in ("200", "0"):
         monkeypatch.setenv("KD_LOSS_RR_POLL_US", us)
