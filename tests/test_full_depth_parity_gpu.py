@@ -48,3 +48,31 @@ def test_c1_full_depth_matches_fp32_oracle(dev):
     # the fp32-output lm_head on the same hidden state: the bf16 rounding of the stored logits
     # is not where the raw-logit misses come from
     assert r["s_logits_rows_f32_out"]["frac_within"] >= r["s_logits_rows"]["frac_within"] - 0.01
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["dt1", "dt2", "dt3", "fb", "bd"])
+def test_every_module_full_depth_matches_fp32_oracle(name, dev):
+    """The other modules at FULL depth against the pinned fp32 oracle on the same weights
+    (tests/full_depth.py measure_kinds; profiles/r05/full_depth_kinds.json): the double-trouble
+    phases 1-3 (DT:250-260; phase 1 LM frozen, phase 2 ViT frozen), FeatureBasedKD (FB:161-165,
+    NT-Xent on the post-LN features) and the depth-student SFT baseline (BD:90-101), bs 1, L 1536.
+    Held: the total at north_star, every row's student logsumexp at north_star, the gradient total
+    norm within 1e-3, every trainable parameter's gradient within 1 % norm / cosine 0.999 except
+    the SigLIP k_proj.bias (exactly zero in exact arithmetic, tests/step_parity.py).
+    Measured: totals rel <= 4.1e-5, gradient norms rel <= 3.0e-4, worst other parameter cos 0.9997."""
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    from full_depth import measure_kinds
+    r = measure_kinds(dev, [name])[name]
+    for k, v in r["terms"].items():
+        assert v["ok"], (k, v)
+    assert r["s_lse"]["ok"], r["s_lse"]
+    assert r["grad_total_norm"]["ok"], r["grad_total_norm"]
+    for n, v in r["grad_params"].items():
+        if n.startswith("vision_tower.") and n.endswith("self_attn.k_proj.bias"):
+            # |g| (both ~0: softmax is invariant to a key bias) within 1e-2 of the layer's q_proj.bias gradient
+            gz = (v["norm_rel"] + 1.0) * v["ref_norm"] if v["ref_norm"] > 0 else v["norm_rel"]
+            qn = r["grad_params"][n.replace("k_proj.bias", "q_proj.bias")]["ref_norm"]
+            assert gz <= 1e-2 * qn, (n, gz, qn)
+            continue
+        assert abs(v["norm_rel"]) <= 1e-2 and v["cos"] >= 0.999, (n, v)

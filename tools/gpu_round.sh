@@ -9,6 +9,8 @@
 #            (tools/parity_report.py --full-depth) -> full_depth.json
 # fp8parity  c1 at full depth with the fp8 (e4m3, lm_mlp) teacher of c4 vs the same fp32 oracle
 #            -> full_depth_fp8.json
+# kindparity every other module (DT phases 1-3, FB, BD) at full depth vs the fp32 oracle
+#            (FULL_KINDS, default "dt1 dt2 dt3 fb bd") -> full_depth_kinds.json
 # parity     the reduced-depth fixtures' per-term / per-parameter report -> parity.json
 # ntx        tools/ntx_bias_study.py (NT-Xent-only bias gradients) -> ntx_bias.json
 # bench      bench.py (the driver's default line; BENCH_ARGS appended) -> bench.json
@@ -42,6 +44,8 @@ for s in $STEPS; do
             tail -2 $O/pytest_ab.log ;;
     fp8parity) timeout -k 10 900 python -u tools/parity_report.py --full-depth --teacher-fp8 lm_mlp \
                 --out $O/full_depth_fp8.json > $O/full_depth_fp8.log 2>&1 || fail fp8parity $O/full_depth_fp8.log ;;
+    kindparity) timeout -k 10 1100 python -u tools/parity_report.py --full-depth-kinds ${FULL_KINDS:-dt1 dt2 dt3 fb bd} \
+                --out $O/full_depth_kinds.json > $O/full_depth_kinds.log 2>&1 || fail kindparity $O/full_depth_kinds.log ;;
     fullparity) timeout -k 10 900 python -u tools/parity_report.py --full-depth --floor --teacher-stream-ab \
                 --out $O/full_depth.json > $O/full_depth.log 2>&1 || fail fullparity $O/full_depth.log ;;
     parity) timeout -k 10 600 python -u tools/parity_report.py --out $O/parity.json $PARITY_KINDS > $O/parity.log 2>&1 || fail parity $O/parity.log ;;

@@ -105,9 +105,21 @@ def main():
                     help="--full-depth: also the HIP step with the teacher's Qwen2 residual stream in fp32")
     ap.add_argument("--teacher-fp8", default=None, metavar="POLICY",
                     help="--full-depth: also the HIP step with the fp8 (e4m3) teacher of c4 (e.g. lm_mlp)")
+    ap.add_argument("--full-depth-kinds", nargs="+", default=None, metavar="KIND",
+                    help="each module kind (tests/full_depth.KINDS: lb dt1 dt2 dt3 fb bd) at full depth vs the fp32 oracle")
     ap.add_argument("kinds", nargs="*")
     a = ap.parse_args()
     import torch
+    if a.full_depth_kinds:
+        from full_depth import measure_kinds
+        rep = measure_kinds(torch.device("cuda:0"), a.full_depth_kinds)
+        for k in a.full_depth_kinds:
+            r = {kk: vv for kk, vv in rep[k].items() if kk != "grad_params"}
+            print(k, json.dumps(r)[:1500], flush=True)
+        if a.out:
+            Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+            Path(a.out).write_text(json.dumps(rep, indent=1))
+        return
     if a.full_depth:
         from full_depth import measure as fd_measure
         rep = fd_measure(torch.device("cuda:0"), floor=a.floor, teacher_stream_ab=a.teacher_stream_ab,
