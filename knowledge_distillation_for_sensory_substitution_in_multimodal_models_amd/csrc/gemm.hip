@@ -76,6 +76,7 @@ struct GemmP {
     // different K stages at once while each XCD still shares its L2 (cold: teacher lm_head, q|k|v,
     // o_proj, down_proj -4 %, gate|up -1 %; c1 step +0.7 %, profiles/r05/gemm_stagger.txt); 0 = off
     int stagger;
+    int stag_g;            // group height the stagger's row groups use (0: gm); v8n takes v8's, so both sum alike
 };
 
 // stream-K: the workgroup whose run [floor(tot w / G), floor(tot (w+1) / G)) holds step s
@@ -1225,7 +1226,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     // loops (nk < 64: the student's K = 896 lm_head measured 1-2 % slower rotated) start at 0.
     int rot = 0;
     if (p.stagger && nk_full == nk && nk >= 64) {
-        const int g = p.gm > 0 ? p.gm : GM_GROUP, ngrp = ((p.M + 255) / 256 + g - 1) / g;
+        const int g = p.stag_g > 0 ? p.stag_g : (p.gm > 0 ? p.gm : GM_GROUP), ngrp = ((p.M + 255) / 256 + g - 1) / g;
         rot = (int)(((int64_t)(tm / g) * nk) / ngrp);
     }
     auto kst = [&](int st) { return (rot == 0 || st >= nk) ? st : (st + rot >= nk ? st + rot - nk : st + rot); };
@@ -1448,6 +1449,170 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
         }
     }
 }
+
+#ifdef KD_AB_BUILD   // v8n: equal or slower than the plan on most of the step's shapes; A/B library only
+// =============================================================================
+// v8n: v8's arithmetic on a 256x128 tile at TWO workgroups per CU (round 5).  Four waves, each
+// 128 rows x 64 columns = 8x4 MFMA 16x16x32 tiles whose 128 accumulators stay in AGPRs (asm
+// MFMA, as v8), so a wave fits in half a SIMD's register file and a second workgroup is resident
+// beside the first: while one workgroup runs its prologue or its epilogue (on a K = 1152 tile of
+// v8 a quarter of the time, stamps), the other keeps the matrix pipe busy, and the half-size tile
+// halves the wave-quantisation loss of the sub-wave GEMMs (SigLIP, the student).  A 3-slot BK = 32
+// LDS-DMA ring (24 KB a slot: A 16 pieces, B 8 pieces of 1 KiB; 72 KB a workgroup with the
+// epilogue staging inside it): step t reads the fragments of stage t+1 and issues the DMA of
+// stage t+3 into the slot of stage t (its fragments are in registers since step t-1, every wave
+// past that step's barrier); the step ends with lgkmcnt(0), vmcnt(6) [stage t+2 landed: only
+// stage t+3's six pieces may be younger] and s_barrier.  Per step and wave: 32 MFMAs, 6 DMAs,
+// 12 fragment reads.  The same k32 MFMA sequence per output element as v8, the same k-loop
+// stagger (a function of the tile row), so C is v8's bit for bit.  K-major A and B, no q|k|v
+// scatter / SwiGLU / row statistics / pre-tiled B (the launcher routes those to v8).
+// =============================================================================
+constexpr int NS8N = 3;
+__device__ __forceinline__ void g8n_tile(GemmP p, int tm, int tn, char* smem) {
+    constexpr int SA = 256 * BK2 * 2, SB = 128 * BK2 * 2, SS = SA + SB;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int m0 = tm * 256, n0 = tn * 128;
+    const int K = p.K;
+    const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
+    int rot = 0;
+    if (p.stagger && nk_full == nk && nk >= 64) {
+        const int g = p.stag_g > 0 ? p.stag_g : (p.gm > 0 ? p.gm : GM_GROUP), ngrp = ((p.M + 255) / 256 + g - 1) / g;
+        rot = (int)(((int64_t)(tm / g) * nk) / ngrp);
+    }
+    auto kst = [&](int st) { return (rot == 0 || st >= nk) ? st : (st + rot >= nk ? st + rot - nk : st + rot); };
+    const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
+    const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(128, p.N - n0), p.ldb));
+    uint32_t va[4], vb[2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) va[u] = voff8<false>(wid * 4 + u, lane, p.lda, m0, p.M);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) vb[u] = voff8<false>(wid * 2 + u, lane, p.ldb, n0, p.N);
+    // DMA instruction u (0..3: A piece wid*4+u, 4..5: B piece wid*2+u-4) of stage st into slot sl
+    auto dma = [&](int st, int sl, int u, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        const bool isA = u < 4;
+        const int i = isA ? wid * 4 + u : wid * 2 + (u - 4);
+        char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
+        uint32_t v = isA ? va[u] : vb[u - 4];
+        int soff = kst(st) * BK2 * 2;
+        if (!FULL) {
+            const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
+            if (kleft < BK2) {
+                const int row = 16 * i + (lane >> 2);
+                const int gc = (lane & 3) ^ f4(row);
+                if (gc * 8 >= kleft) v = OOB;
+                if (kleft <= 0) soff = 0;
+            }
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsB, (lds_void_t*)dst, 16, v, soff, 0, 0);
+    };
+    using FullT = std::integral_constant<bool, true>;
+    using PartT = std::integral_constant<bool, false>;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int ra = wm * 128, cb = wn * 64;
+#pragma unroll
+    for (int st = 0; st < NS8N; ++st)
+#pragma unroll
+        for (int u = 0; u < 6; ++u) dma(st, st, u, PartT{});
+    wait_vm<12>();   // stage 0 landed (stages 1, 2 may stay in flight)
+    __builtin_amdgcn_s_barrier();
+    bf16x8 xa[8], xb[4], ya[8], yb[4];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xa[u] = frag2<256, false>(smem, ra + u * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xb[j] = frag2<128, false>(smem + SA, cb + j * 16, lane);
+#define KD_G8N_SYNC()                                      \
+    {                                                      \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        wait_vm<6>();                                      \
+        __builtin_amdgcn_s_barrier();                      \
+    }
+    KD_G8N_SYNC()
+    __builtin_amdgcn_sched_barrier(0);
+#define KD_SB __builtin_amdgcn_sched_barrier(0);
+    // unit u: the 4 MFMAs of A fragment u; DMA u (u < 6); next-stage fragment reads: units 0-3 two
+    // A fragments each, units 4-5 two B fragments each
+#define KD_G8N_STEP(SL, CA, CB, NA, NB, FT)                                                                  \
+    {                                                                                                         \
+        const int t_ = t + (SL);                                                                              \
+        const char* na_ = smem + (((SL) + 1) % NS8N) * SS;                                                    \
+        _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
+            mfma_agpr(acc[u][0], CB[0], CA[u]); KD_SB                                                         \
+            if (u < 6) dma(t_ + NS8N, (SL), u, FT{});                                                         \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][1], CB[1], CA[u]); KD_SB                                                         \
+            if (u < 4) NA[2 * u] = frag2<256, false>(na_, ra + 2 * u * 16, lane);                             \
+            else if (u < 6) NB[2 * (u - 4)] = frag2<128, false>(na_ + SA, cb + 2 * (u - 4) * 16, lane);       \
+            KD_SB                                                                                             \
+            mfma_agpr(acc[u][2], CB[2], CA[u]); KD_SB                                                         \
+            if (u < 4) NA[2 * u + 1] = frag2<256, false>(na_, ra + (2 * u + 1) * 16, lane);                   \
+            else if (u < 6) NB[2 * (u - 4) + 1] = frag2<128, false>(na_ + SA, cb + (2 * (u - 4) + 1) * 16, lane); \
+            if (u == 7) KD_G8N_SYNC()                                                                         \
+            KD_SB                                                                                             \
+            if (u == 7) mfma_agpr_last(acc[u][3], CB[3], CA[u], t_ + 1 == nk);                                \
+            else mfma_agpr(acc[u][3], CB[3], CA[u]);                                                          \
+            KD_SB                                                                                             \
+        }                                                                                                     \
+    }
+    // six steps per iteration: every slot index (t % 3) and fragment set (t % 2) is a constant
+    int t = 0;
+    for (; t + 6 + NS8N <= nk_full; t += 6) {   // every DMA of these steps lies inside K
+        KD_G8N_STEP(0, xa, xb, ya, yb, FullT)
+        KD_G8N_STEP(1, ya, yb, xa, xb, FullT)
+        KD_G8N_STEP(2, xa, xb, ya, yb, FullT)
+        t += 3;
+        KD_G8N_STEP(0, ya, yb, xa, xb, FullT)
+        KD_G8N_STEP(1, xa, xb, ya, yb, FullT)
+        KD_G8N_STEP(2, ya, yb, xa, xb, FullT)
+        t -= 3;
+    }
+    for (; t + 6 <= nk; t += 6) {
+        KD_G8N_STEP(0, xa, xb, ya, yb, PartT)
+        KD_G8N_STEP(1, ya, yb, xa, xb, PartT)
+        KD_G8N_STEP(2, xa, xb, ya, yb, PartT)
+        t += 3;
+        KD_G8N_STEP(0, ya, yb, xa, xb, PartT)
+        KD_G8N_STEP(1, xa, xb, ya, yb, PartT)
+        KD_G8N_STEP(2, ya, yb, xa, xb, PartT)
+        t -= 3;
+    }
+    const int rem = nk - t;
+    if (rem > 0) KD_G8N_STEP(0, xa, xb, ya, yb, PartT)
+    if (rem > 1) KD_G8N_STEP(1, ya, yb, xa, xb, PartT)
+    if (rem > 2) KD_G8N_STEP(2, xa, xb, ya, yb, PartT)
+    if (rem > 3) { t += 3; KD_G8N_STEP(0, ya, yb, xa, xb, PartT) t -= 3; }
+    if (rem > 4) { t += 3; KD_G8N_STEP(1, xa, xb, ya, yb, PartT) t -= 3; }
+#undef KD_G8N_STEP
+#undef KD_G8N_SYNC
+#undef KD_SB
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    epilogue2<256, 128, 2, 2, 128, 64, 8, 4, NTH8, true, false>(p, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+template <int EXP = 0>
+__global__ void __launch_bounds__(NTH8, 2) k_gemm8n(GemmP p_) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    GemmP p = p_;
+    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
+        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
+        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
+        p.A += k0;
+        p.B += k0;
+        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
+    }
+    int tm, tn;
+    tile_of(p.gx, (p.M + 255) / 256, (p.N + 127) / 128, tm, tn, p.tile0, p.gm);
+    g8n_tile(p, tm, tn, smem);
+}
+#endif  // KD_AB_BUILD
 
 #ifdef KD_AB_BUILD   // v11 / v12: measured slower than v8 in the step; tools' A/B library only
 // =============================================================================
@@ -2644,7 +2809,7 @@ static bool use_v12(int variant) {
 static bool variant_known(int v) {
     if ((v >= 0 && v <= 7) || v == 16 || v == 21 || v == 24) return true;
 #ifdef KD_AB_BUILD
-    if ((v >= 17 && v <= 20) || v == 22 || v == 23 || (v >= 26 && v <= 28)) return true;
+    if ((v >= 17 && v <= 20) || v == 22 || v == 23 || (v >= 26 && v <= 28) || v == 30) return true;
 #endif
     return false;
 }
@@ -2735,6 +2900,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     p.gm = 0;
     p.rst = nullptr; p.rst_nt = p.rst_vs = p.rst_top2 = 0; p.rst_inv_t = 1.f;
     p.stagger = ab_knob("KD_GEMM_STAGGER", 1);
+    p.stag_g = 0;
     hipStream_t st = as_stream(stream_);
     const bool amn = d->a_layout == KD_LAYOUT_MN_MAJOR, bmn = d->b_layout == KD_LAYOUT_MN_MAJOR;
     const bool c_ok16 = (d->qkv || ((d->ldc % 8 == 0) && ((uintptr_t)d->C % 16 == 0))) &&
@@ -2812,6 +2978,22 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         KD_LAUNCH_CHECK("k_gemm8 (b_pretiled)");
         return KD_OK;
     }
+#ifdef KD_AB_BUILD
+    if (d->variant == 30) {   // v8n (256x128, two workgroups per CU), forced; K-major operands, unsplit
+        KD_CHECK_ARG(!amn && !bmn && !d->qkv && !d->row_stats && !d->b_pretiled && !dact && d->act != KD_ACT_SWIGLU &&
+                     d->split_k <= 1 && d->N % 8 == 0 && c_ok16,
+                     "gemm variant 30 (v8n): K-major A and B, no q|k|v scatter / SwiGLU / backward activation / row "
+                     "statistics / split, N % 8 == 0");
+        GemmP q = p;
+        q.gm = pick_gm(ceil_div(d->M, 256), ceil_div(d->N, 128));
+        q.stag_g = pick_gm(ceil_div(d->M, 256), ceil_div(d->N, 256));   // v8's row groups: v8's bits
+        const dim3 grid(ceil_div(d->M, 256) * ceil_div(d->N, 128), 1);
+        q.gx = (int)grid.x; q.gy = 1; q.tile0 = 0;
+        hipLaunchKernelGGL((k_gemm8n<0>), grid, dim3(NTH8), (gemm2_lds<256, 128, NS8N>()), st, q);
+        KD_LAUNCH_CHECK("k_gemm8n");
+        return KD_OK;
+    }
+#endif
     const int force = d->variant;   // 0 auto, 1 v1 128x128, 2/5 v3 256x256, 3/6 v3 256x128, 4/7 v3 128x256,
                                     // 16 v8 256x256 (4 waves, AGPR accumulators), 17-19 v8 diagnostics, 22 v8 register-staged (negative result, kept for A/B)
     if (force != 1 && big_ok) {

@@ -362,5 +362,3 @@ def test_qkv_scatter_epilogue_equals_gemm_then_split(shape, variant, dev):
     torch.cuda.synchronize()
     for got, ref, n in ((q, q0, "q"), (k, k0, "k"), (v, v0, "v")):
         assert torch.equal(got, ref), f"{n}: {int((got != ref).sum())} elements differ"
-
-

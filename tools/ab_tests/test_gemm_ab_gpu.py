@@ -87,3 +87,35 @@ def test_v8_stagger_matches_unstaggered(M, N, K, dev):
             assert torch.equal(o, ops.swiglu_fwd(got, N // 2))
     finally:
         os.environ["KD_GEMM_STAGGER"] = "0"
+
+
+@pytest.mark.parametrize("M,N,K", [(5832, 4304, 1152), (5832, 1152, 4304), (300, 264, 96), (1100, 1040, 392),
+                                   (6144, 896, 4864), (2048, 640, 2304), (257, 136, 40)])
+def test_v8n_bitexact_vs_v8(M, N, K, dev):
+    """v8n (variant 30: 256x128 tiles, two workgroups per CU) runs v8's k32 MFMA sequence for every
+    output element with v8's k-loop stagger row groups, so C is v8's bit for bit -- plain and with
+    each epilogue it takes (bias + GELU-tanh + pre-activation aux, residual, fp32 accumulate);
+    partial tiles, K tails shorter than a stage and than the ring, K >= 2048 (stagger on).  The
+    reference is v8 over pre-tiled B (v8 at every size: a forced variant 16 runs v1 below 2^20
+    outputs), bit-identical to plain v8 (tests/test_gemm_pretiled_gpu.py)."""
+    import os
+    os.environ["KD_GEMM_STAGGER"] = "1"
+    try:
+        ops = _ops()
+        a = _rand(M, K, dev=dev, seed=140)
+        w = _rand(N, K, dev=dev, seed=141, scale=0.05)
+        pt = ops.pretile_b(w)
+        assert torch.equal(ops.gemm(a, w, variant=30), ops.gemm(a, w, b_pretiled=pt))
+        bias = _rand(N, dev=dev, seed=142)
+        res = _rand(M, N, dev=dev, seed=143)
+        ax = [torch.empty(M, N, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        o0 = ops.gemm(a, w, bias=bias, act="gelu_tanh", aux=ax[0], variant=30)
+        o1 = ops.gemm(a, w, bias=bias, act="gelu_tanh", aux=ax[1], b_pretiled=pt)
+        assert torch.equal(o0, o1) and torch.equal(ax[0], ax[1])
+        assert torch.equal(ops.gemm(a, w, residual=res, variant=30), ops.gemm(a, w, residual=res, b_pretiled=pt))
+        acc = [torch.full((M, N), 0.25, dtype=torch.float32, device=dev) for _ in range(2)]
+        ops.gemm(a, w, out=acc[0], accumulate=True, variant=30)
+        ops.gemm(a, w, out=acc[1], accumulate=True, b_pretiled=pt)
+        assert torch.equal(acc[0], acc[1])
+    finally:
+        os.environ["KD_GEMM_STAGGER"] = "0"

@@ -25,7 +25,7 @@ import tempfile
 from pathlib import Path
 
 LLVM = Path("/opt/rocm/lib/llvm/bin")
-KERNELS = re.compile(r"k_gemm8f8|k_gemm8I|k_gemm9I|k_gemm11I|k_gemm12I")
+KERNELS = re.compile(r"k_gemm8f8|k_gemm8I|k_gemm8nI|k_gemm9I|k_gemm11I|k_gemm12I")
 REQ = 19   # wait states before a non-XDL read of a 16-pass XDL result (the 8-pass ones need fewer)
 
 _AREG = re.compile(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b")
