@@ -192,20 +192,13 @@ typedef struct {
     int64_t ld_aux;
     int32_t residual_row_mod; /* >0: residual row index = m % residual_row_mod (SigLIP pos-emb) */
     int32_t variant;          /* 0 auto (cost model); forced (tests/tools): 1 128x128 4-wave; 2|5 / 3|6 / 4|7
-                                 256x256 / 256x128 / 128x256 8-wave; 16 256x256 4-wave (AGPR accumulators);
-                                 17-19 diagnostic builds of 16 (tools/stamp_gemm.py, tools/ablate_gemm.py);
-                                 20 256x256 8-wave ping-pong (two wave groups alternate on each SIMD);
-                                 21 stream-K on 16 (256 workgroups take equal runs of the tiles' k-steps,
-                                 shared tiles folded from fp32 partial planes; needs workspace);
-                                 22 16 with register staging instead of LDS-DMA (K-major operands;
-                                 measured slower, kept for A/B: tools/ab_gemm_rs.py);
-                                 23 the 256x256 4-wave tiles on 32x32x16 MFMAs (v11, K-major x K-major;
-                                 other layouts run 16); 24 = 16 forced even where the default is v11 / v12;
-                                 25 diagnostic build of 16 (whole-line DMA rows, WRONG results: timing only);
-                                 26 16 with whole-cache-line staging of K-major operands (v12, stage pairs;
-                                 K-major x K-major, other layouts run 16; bit-identical to 16);
-                                 27 26 without the odd-step barriers (A/B); 28 SwiGLU only: the stamp build
-                                 of 16 (per-wave cycle totals into the workspace, tools/stamp_glu.py) */
+                                 256x256 / 256x128 / 128x256 8-wave; 16 256x256 4-wave (v8, AGPR
+                                 accumulators); 24 = 16; 21 stream-K on 16 (256 workgroups take equal runs
+                                 of the tiles' k-steps, shared tiles folded from fp32 partial planes; needs
+                                 workspace).  The A/B library (csrc/build.py --ab) also accepts the
+                                 diagnostic / negative-result builds 17-20, 22, 23, 26-28 and 30 (v8n: 256x128
+                                 4-wave at two workgroups per CU, bit-identical to 16; tools/README.md);
+                                 this library rejects them. */
     int32_t split_k;          /* 0 auto (cost model, bounded by workspace); 1 off; >1 forced K splits */
     void* workspace;          /* optional fp32 split-K partials; NULL disables splitting */
     uint64_t workspace_bytes;

@@ -1450,7 +1450,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     }
 }
 
-#ifdef KD_AB_BUILD   // v8n: equal or slower than the plan on most of the step's shapes; A/B library only
+#ifdef KD_AB_BUILD   // v8n: no faster than the plan in the step; A/B library only
 // =============================================================================
 // v8n: v8's arithmetic on a 256x128 tile at TWO workgroups per CU (round 5).  Four waves, each
 // 128 rows x 64 columns = 8x4 MFMA 16x16x32 tiles whose 128 accumulators stay in AGPRs (asm
@@ -2979,11 +2979,16 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         return KD_OK;
     }
 #ifdef KD_AB_BUILD
-    if (d->variant == 30) {   // v8n (256x128, two workgroups per CU), forced; K-major operands, unsplit
-        KD_CHECK_ARG(!amn && !bmn && !d->qkv && !d->row_stats && !d->b_pretiled && !dact && d->act != KD_ACT_SWIGLU &&
-                     d->split_k <= 1 && d->N % 8 == 0 && c_ok16,
-                     "gemm variant 30 (v8n): K-major A and B, no q|k|v scatter / SwiGLU / backward activation / row "
-                     "statistics / split, N % 8 == 0");
+    // v8n (256x128, two workgroups per CU), forced (variant 30); K-major operands, unsplit.  As the
+    // auto choice for SigLIP's q|k|v scatter (62.5 vs 71.2 us alone, profiles/r05/v8n_qkv_ab.txt) the
+    // c1 step measured no faster (29.05-29.09 vs 29.08-29.13 samples/s), so the plan does not use it
+    if (d->variant == 30) {
+        // the q|k|v scatter takes 128-column tiles when a RoPE pair never straddles them (no RoPE, or
+        // 128 % head_dim == 0: a tile is whole heads)
+        KD_CHECK_ARG(!amn && !bmn && (!d->qkv || !d->qkv->cos_t || 128 % d->qkv->hd == 0) && !d->row_stats &&
+                     !d->b_pretiled && !dact && d->act != KD_ACT_SWIGLU && d->split_k <= 1 && d->N % 8 == 0 && c_ok16,
+                     "gemm variant 30 (v8n): K-major A and B, no SwiGLU / backward activation / row statistics / split, "
+                     "N % 8 == 0; a RoPE q|k|v scatter needs 128 % head_dim == 0");
         GemmP q = p;
         q.gm = pick_gm(ceil_div(d->M, 256), ceil_div(d->N, 128));
         q.stag_g = pick_gm(ceil_div(d->M, 256), ceil_div(d->N, 256));   // v8's row groups: v8's bits
@@ -3136,6 +3141,9 @@ int gemm_plan_query(const kd_gemm_desc* d, int32_t* var, int32_t* split, int32_t
                         ((uint64_t)d->M * d->N >= (1ull << 20) || (d->workspace && d->K >= 2048 && d->split_k != 1)) &&
                         (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0);
     if (d->act == KD_ACT_SWIGLU) { *var = 16; *split = 1; *dp = 0; return KD_OK; }
+#ifdef KD_AB_BUILD
+    if (d->variant == 30) { *var = 30; *split = 1; *dp = 0; return KD_OK; }   // v8n (launch_gemm)
+#endif
     if (d->variant == 1 || !big_ok) { *var = 1; *split = 1; *dp = 0; return KD_OK; }
     const GemmPlan pl = plan_gemm(d, d->workspace ? d->workspace_bytes : 0);
     *var = pl.var; *split = pl.split; *dp = pl.dp_tiles;

@@ -91,31 +91,57 @@ def test_v8_stagger_matches_unstaggered(M, N, K, dev):
 
 @pytest.mark.parametrize("M,N,K", [(5832, 4304, 1152), (5832, 1152, 4304), (300, 264, 96), (1100, 1040, 392),
                                    (6144, 896, 4864), (2048, 640, 2304), (257, 136, 40)])
-def test_v8n_bitexact_vs_v8(M, N, K, dev):
+def test_v8n_bitexact_vs_v8(M, N, K, dev, monkeypatch):
     """v8n (variant 30: 256x128 tiles, two workgroups per CU) runs v8's k32 MFMA sequence for every
     output element with v8's k-loop stagger row groups, so C is v8's bit for bit -- plain and with
     each epilogue it takes (bias + GELU-tanh + pre-activation aux, residual, fp32 accumulate);
     partial tiles, K tails shorter than a stage and than the ring, K >= 2048 (stagger on).  The
     reference is v8 over pre-tiled B (v8 at every size: a forced variant 16 runs v1 below 2^20
     outputs), bit-identical to plain v8 (tests/test_gemm_pretiled_gpu.py)."""
-    import os
-    os.environ["KD_GEMM_STAGGER"] = "1"
-    try:
-        ops = _ops()
-        a = _rand(M, K, dev=dev, seed=140)
-        w = _rand(N, K, dev=dev, seed=141, scale=0.05)
-        pt = ops.pretile_b(w)
-        assert torch.equal(ops.gemm(a, w, variant=30), ops.gemm(a, w, b_pretiled=pt))
-        bias = _rand(N, dev=dev, seed=142)
-        res = _rand(M, N, dev=dev, seed=143)
-        ax = [torch.empty(M, N, dtype=torch.bfloat16, device=dev) for _ in range(2)]
-        o0 = ops.gemm(a, w, bias=bias, act="gelu_tanh", aux=ax[0], variant=30)
-        o1 = ops.gemm(a, w, bias=bias, act="gelu_tanh", aux=ax[1], b_pretiled=pt)
-        assert torch.equal(o0, o1) and torch.equal(ax[0], ax[1])
-        assert torch.equal(ops.gemm(a, w, residual=res, variant=30), ops.gemm(a, w, residual=res, b_pretiled=pt))
-        acc = [torch.full((M, N), 0.25, dtype=torch.float32, device=dev) for _ in range(2)]
-        ops.gemm(a, w, out=acc[0], accumulate=True, variant=30)
-        ops.gemm(a, w, out=acc[1], accumulate=True, b_pretiled=pt)
-        assert torch.equal(acc[0], acc[1])
-    finally:
-        os.environ["KD_GEMM_STAGGER"] = "0"
+    monkeypatch.setenv("KD_GEMM_STAGGER", "1")   # the product default (the A/B suite runs v8 unstaggered)
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=140)
+    w = _rand(N, K, dev=dev, seed=141, scale=0.05)
+    pt = ops.pretile_b(w)
+    assert torch.equal(ops.gemm(a, w, variant=30), ops.gemm(a, w, b_pretiled=pt))
+    bias = _rand(N, dev=dev, seed=142)
+    res = _rand(M, N, dev=dev, seed=143)
+    ax = [torch.empty(M, N, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+    o0 = ops.gemm(a, w, bias=bias, act="gelu_tanh", aux=ax[0], variant=30)
+    o1 = ops.gemm(a, w, bias=bias, act="gelu_tanh", aux=ax[1], b_pretiled=pt)
+    assert torch.equal(o0, o1) and torch.equal(ax[0], ax[1])
+    assert torch.equal(ops.gemm(a, w, residual=res, variant=30), ops.gemm(a, w, residual=res, b_pretiled=pt))
+    acc = [torch.full((M, N), 0.25, dtype=torch.float32, device=dev) for _ in range(2)]
+    ops.gemm(a, w, out=acc[0], accumulate=True, variant=30)
+    ops.gemm(a, w, out=acc[1], accumulate=True, b_pretiled=pt)
+    assert torch.equal(acc[0], acc[1])
+
+
+@pytest.mark.parametrize("B,S,K,nq,nkv,hd,hdp,rope", [(4, 1536, 3584, 28, 4, 128, 128, True),
+                                                       (4, 1536, 896, 14, 2, 64, 64, True),
+                                                       (8, 729, 1152, 16, 16, 72, 96, False)])
+def test_v8n_qkv_scatter_bitexact_vs_v8(B, S, K, nq, nkv, hd, hdp, rope, dev, monkeypatch):
+    """v8n's q|k|v scatter epilogue (128-column tiles: whole heads with RoPE, any split without) writes
+    v8's head-major q / k / v bit for bit on the step's three attention-input shapes."""
+    monkeypatch.setenv("KD_GEMM_STAGGER", "1")   # the product default (the A/B suite runs v8 unstaggered)
+    ops = _ops()
+    g = torch.Generator(device=dev).manual_seed(3)
+    M, N = B * S, (nq + 2 * nkv) * hd
+    x = torch.randn(M, K, generator=g, device=dev).bfloat16()
+    w = (torch.randn(N, K, generator=g, device=dev) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, generator=g, device=dev).bfloat16()
+    cos = sin = None
+    if rope:
+        inv = 1.0 / (1e6 ** (torch.arange(0, hd, 2, dtype=torch.float32, device=dev) / hd))
+        fr = torch.arange(S, dtype=torch.float32, device=dev)[:, None] * inv[None]
+        cos, sin = fr.cos().contiguous(), fr.sin().contiguous()
+    outs = []
+    for v in (30, 24):
+        q = torch.full((B, nq, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)
+        k = torch.full((B, nkv, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)
+        vv = torch.full((B, nkv, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)
+        ops.gemm_qkv(x, w, bias, q, k, vv, S, nq, nkv, hd, hdp, cos, sin, variant=v)
+        outs.append((q, k, vv))
+    torch.cuda.synchronize()
+    for a, b, n in zip(outs[0], outs[1], "qkv"):
+        assert torch.equal(a, b), f"{n}: {int((a != b).sum())} elements differ"
