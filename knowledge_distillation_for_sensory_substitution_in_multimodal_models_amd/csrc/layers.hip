@@ -1180,11 +1180,22 @@ int launch_adamw(float* p, void* pb, const float* g, float* m, float* v, int64_t
     KD_CHECK_ARG(n_skip >= 0 && n_skip <= 64 && (n_skip == 0 || skip), "adamw: bad skip words");
     const float bc1 = 1.f - powf(b1, (float)step);
     const float inv_bc2s = (float)(1.0 / std::sqrt((double)(1.f - powf(b2, (float)step))));   // 1 / sqrt(bias correction 2)
-    // KD_ADAMW_GRID (read per call): the workgroup count; default one 256-thread workgroup per 4 K
-    // parameters up to 16384. A small grid leaves CUs to the GEMMs of the concurrent teacher forward
-    // (a v8 GEMM workgroup needs a whole CU, so every CU holding AdamW waves is closed to it).
-    int grid = grid_for(n, 256, 16384);
-    if (const int cap = ab_knob("KD_ADAMW_GRID", 0); cap > 0) grid = std::min(grid, cap);
+    // The workgroup count: two 256-thread workgroups per CU (512 on MI355X), grid-striding over the
+    // parameters.  Round 5: against the former 16384 (one per 4 K parameters) AdamW alone runs 4.97
+    // instead of 5.24 ms (5.4 vs 5.1 TB/s), and beside the next teacher forward the c1 step gains
+    // 0.4-0.8 % on three boxes (`profiles/r05/adamw_grid.txt`); 128 / 256 / 768 / 1024 measured
+    // slower.  KD_ADAMW_GRID (A/B library, read per call) overrides it.
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
+            cus = c;
+        else
+            cus = 256;
+    }
+    int grid = grid_for(n, 256, 2 * cus);
+    if (const int cap = ab_knob("KD_ADAMW_GRID", 0); cap > 0) grid = std::min(grid_for(n, 256, 16384), cap);
     // eight 16-B chunks of each tensor in flight per lane (tools/bench_adamw.py, one box: 5.13-5.15 ms
     // vs 5.22-5.28 with four; the CW build -- each wave on contiguous 8 KiB runs -- 5.08-5.16, not kept)
 #define KD_ADAMW_LAUNCH(U, NTL, CW)                                                                                   \
