@@ -2470,80 +2470,87 @@ __global__ void __launch_bounds__(256) k_quant_rows_f8(const bf16* __restrict__ 
 // GEMM launch); blockIdx.y takes a BM / gridDim.y row slab of its tile (one 4-column chunk
 // per thread: many blocks, every load of a block in flight at once), the S partial loads
 // of a chunk issued together.
-__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S, GemmP p, int BMr, int BNr) {
-    int tm, tn;
-    const int tiles_m = (p.M + BMr - 1) / BMr, tiles_n = (p.N + BNr - 1) / BNr;
-    tile_grouped(p.tile0 + (int)blockIdx.x, tiles_m, tiles_n, tm, tn, p.gm);
-    if (p.sk_steps > 0) {   // stream-K: this tile's piece count; a one-piece tile is already final
-        const int64_t tot = (int64_t)tiles_m * tiles_n * p.sk_steps;
-        const int64_t tb = (int64_t)(p.tile0 + (int)blockIdx.x) * p.sk_steps;
-        S = sk_wg_of(tb + p.sk_steps - 1, tot, p.sk_grid) - sk_wg_of(tb, tot, p.sk_grid) + 1;
-        if (S <= 1) return;
-    }
-    const int rows_per = BMr / p.gy;
-    const int r0 = tm * BMr + (int)blockIdx.y * rows_per;
-    const int r1 = min(r0 + rows_per, p.M);
-    const int c0 = tn * BNr, cw = min(BNr, p.N - c0);
-    const int c4 = cw / 4;   // N % 8 == 0 on this path
-    float alpha = p.alpha;
-    if (p.alpha_dev) alpha *= *p.alpha_dev;
-    for (int idx = threadIdx.x; idx < (r1 - r0) * c4; idx += 256) {
-        const int64_t row = r0 + idx / c4;
-        const int col = c0 + (idx % c4) * 4;
-        const float* src = ws + row * p.N + col;
-        f32x4 v = *(const f32x4*)src;
-        int s = 1;
-        for (; s + 3 < S; s += 4) {
-            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
-            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
-            const f32x4 c = *(const f32x4*)(src + (int64_t)(s + 2) * p.split_stride);
-            const f32x4 d = *(const f32x4*)(src + (int64_t)(s + 3) * p.split_stride);
-            v += a; v += b; v += c; v += d;
+__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int S0, GemmP p, int BMr, int BNr) {
+    // items (tile, row slab) = (p.gx tiles) x (p.gy slabs), strided over a 1-D grid of at most that many
+    // workgroups (the launch may cap it: KD_SK_REDUCE_GRID, A/B)
+    const int nitems = p.gx * p.gy;
+    for (int it = (int)blockIdx.x; it < nitems; it += (int)gridDim.x) {
+        const int bxi = it / p.gy, byi = it - bxi * p.gy;
+        int S = S0;
+        int tm, tn;
+        const int tiles_m = (p.M + BMr - 1) / BMr, tiles_n = (p.N + BNr - 1) / BNr;
+        tile_grouped(p.tile0 + bxi, tiles_m, tiles_n, tm, tn, p.gm);
+        if (p.sk_steps > 0) {   // stream-K: this tile's piece count; a one-piece tile is already final
+            const int64_t tot = (int64_t)tiles_m * tiles_n * p.sk_steps;
+            const int64_t tb = (int64_t)(p.tile0 + bxi) * p.sk_steps;
+            S = sk_wg_of(tb + p.sk_steps - 1, tot, p.sk_grid) - sk_wg_of(tb, tot, p.sk_grid) + 1;
+            if (S <= 1) continue;
         }
-        if (s + 1 < S) {   // same summation order, both loads in flight
-            const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
-            const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
-            v += a; v += b;
-            s += 2;
-        }
-        if (s < S) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
-            const int bc[4] = {col, col + 1, col + 2, col + 3};
-            load_bias<4>(p, bc, bv);
-        }
+        const int rows_per = BMr / p.gy;
+        const int r0 = tm * BMr + byi * rows_per;
+        const int r1 = min(r0 + rows_per, p.M);
+        const int c0 = tn * BNr, cw = min(BNr, p.N - c0);
+        const int c4 = cw / 4;   // N % 8 == 0 on this path
+        float alpha = p.alpha;
+        if (p.alpha_dev) alpha *= *p.alpha_dev;
+        for (int idx = threadIdx.x; idx < (r1 - r0) * c4; idx += 256) {
+            const int64_t row = r0 + idx / c4;
+            const int col = c0 + (idx % c4) * 4;
+            const float* src = ws + row * p.N + col;
+            f32x4 v = *(const f32x4*)src;
+            int s = 1;
+            for (; s + 3 < S; s += 4) {
+                const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
+                const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
+                const f32x4 c = *(const f32x4*)(src + (int64_t)(s + 2) * p.split_stride);
+                const f32x4 d = *(const f32x4*)(src + (int64_t)(s + 3) * p.split_stride);
+                v += a; v += b; v += c; v += d;
+            }
+            if (s + 1 < S) {   // same summation order, both loads in flight
+                const f32x4 a = *(const f32x4*)(src + (int64_t)s * p.split_stride);
+                const f32x4 b = *(const f32x4*)(src + (int64_t)(s + 1) * p.split_stride);
+                v += a; v += b;
+                s += 2;
+            }
+            if (s < S) v += *(const f32x4*)(src + (int64_t)s * p.split_stride);
+            float bv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (p.bias) {
+                const int bc[4] = {col, col + 1, col + 2, col + 3};
+                load_bias<4>(p, bc, bv);
+            }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            float x = v[e] * alpha;
-            if (p.bias) x += bv[e];
-            if (p.aux) p.aux[row * p.ld_aux + col + e] = (bf16)x;
-            v[e] = apply_act(x, p.act);
-        }
-        if (p.resid) {
-            const int64_t ro = (p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col;
-            if (p.res_f32) {
-                v += *(const f32x4*)((const float*)p.resid + ro);
+            for (int e = 0; e < 4; ++e) {
+                float x = v[e] * alpha;
+                if (p.bias) x += bv[e];
+                if (p.aux) p.aux[row * p.ld_aux + col + e] = (bf16)x;
+                v[e] = apply_act(x, p.act);
+            }
+            if (p.resid) {
+                const int64_t ro = (p.res_mod > 0 ? row % p.res_mod : row) * p.ldr + col;
+                if (p.res_f32) {
+                    v += *(const f32x4*)((const float*)p.resid + ro);
+                } else {
+                    const bf16x4 r = *(const bf16x4*)(p.resid + ro);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+                }
+            }
+            if (p.c_f32) {
+                float* dst = (float*)p.C + row * p.ldc + col;
+                if (p.accumulate) v += *(const f32x4*)dst;
+                *(f32x4*)dst = v;
             } else {
-                const bf16x4 r = *(const bf16x4*)(p.resid + ro);
+                bf16* dst = (bf16*)p.C + row * p.ldc + col;
+                bf16x4 o;
+                if (p.accumulate) {
+                    const bf16x4 c = *(const bf16x4*)dst;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+                    for (int e = 0; e < 4; ++e) v[e] += (float)c[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+                *(bf16x4*)dst = o;
             }
-        }
-        if (p.c_f32) {
-            float* dst = (float*)p.C + row * p.ldc + col;
-            if (p.accumulate) v += *(const f32x4*)dst;
-            *(f32x4*)dst = v;
-        } else {
-            bf16* dst = (bf16*)p.C + row * p.ldc + col;
-            bf16x4 o;
-            if (p.accumulate) {
-                const bf16x4 c = *(const bf16x4*)dst;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += (float)c[e];
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-            *(bf16x4*)dst = o;
         }
     }
 }
@@ -2806,6 +2813,13 @@ static bool use_v12(int variant) {
 // the variants kd_gemm accepts: 0 auto, 1 v1, 2-7 v3 tiles, 16 v8, 21 stream-K, 24 (= 16); the
 // tools' A/B library (KD_AB_BUILD: python csrc/build.py --ab) also the negative-result and
 // diagnostic builds 17-20, 22, 23, 26-28
+// workgroups of a split-K / stream-K fold launch over `items` (tile, row slab) items: one each, or
+// at most KD_SK_REDUCE_GRID (A/B: the fold runs beside the other stream's GEMMs)
+static unsigned reduce_grid(int items) {
+    const int cap = ab_knob("KD_SK_REDUCE_GRID", 0);
+    return (unsigned)(cap > 0 && cap < items ? cap : items);
+}
+
 static bool variant_known(int v) {
     if ((v >= 0 && v <= 7) || v == 16 || v == 21 || v == 24) return true;
 #ifdef KD_AB_BUILD
@@ -3021,7 +3035,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             else hipLaunchKernelGGL((k_gemm8<true, false, 0>), grid, dim3(NTH8), lds, st, q);
             KD_LAUNCH_CHECK("k_gemm8 (stream-K)");
             q.gx = tiles; q.gy = 256 * 256 / 1024;
-            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)tiles, (unsigned)q.gy), dim3(256), 0, st,
+            hipLaunchKernelGGL(k_splitk_reduce, dim3(reduce_grid(tiles * q.gy)), dim3(256), 0, st,
                                (const float*)d->workspace, 0, q, 256, 256);
             KD_LAUNCH_CHECK("k_splitk_reduce (stream-K)");
             return KD_OK;
@@ -3117,7 +3131,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         p.tile0 = pl.dp_tiles;
         p.gx = tiles - pl.dp_tiles; p.gy = tbm * tbn / 1024;
         // one float4 column chunk per thread: BM / (1024 / BN) row slabs of 1024 / BN rows per tile
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)(tiles - pl.dp_tiles), (unsigned)(tbm * tbn / 1024)), dim3(256), 0, st,
+        hipLaunchKernelGGL(k_splitk_reduce, dim3(reduce_grid(p.gx * p.gy)), dim3(256), 0, st,
                            (const float*)d->workspace, pl.split, p, tbm, tbn);
         KD_LAUNCH_CHECK("k_splitk_reduce");
         return KD_OK;
