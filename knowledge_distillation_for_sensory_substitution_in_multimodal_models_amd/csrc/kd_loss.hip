@@ -1331,7 +1331,8 @@ int launch_kd_student_stats(const void* student, int64_t ld_s, int V_s, int rows
     KD_CHECK_ALIGN(student, 16, "kd_loss_student_stats: student logits must be 16-B aligned");
     KD_CHECK_ALIGN(out, 16, "kd_loss_student_stats: out must be 16-B aligned");
     KD_CHECK_ARG(temperature > 0.f, "kd_loss_student_stats: temperature must be > 0");
-    const int rs_cap = std::max(1, ab_knob("KD_RS_GRID", 1 << 30));
+    // KD_SS_GRID (A/B): a cap on this launch's row-strided workgroups (it runs beside the teacher forward)
+    const int rs_cap = std::max(1, ab_knob("KD_SS_GRID", ab_knob("KD_RS_GRID", 1 << 30)));
     // the RS_FULL arguments the student loop reads; the label / LoCa tail is not run
     hipLaunchKernelGGL(k_row_stats<RS_SONLY>, dim3(std::min(rows, rs_cap)), dim3(NT), 0, as_stream(stream_), nullptr,
                        (int64_t)0, 0, (const bf16*)student, ld_s, V_s, nullptr, 1, rows, 0, 1.f / temperature, 0.f, 0,
