@@ -26,7 +26,12 @@
  *    at load time (the Python binding refuses a mismatched library).
  *    ABI 6 -> 7: kd_gemm diagnostic variants (17-20, 22, 23, 25-28) are no longer accepted by
  *    the product library (A/B builds only); kd_loss err bit 4 is no longer set.
+ *    ABI 6 -> 7 also changed kd_model_backward's dpost from a bf16 per-row gradient
+ *    [n_tiles*np, v_hidden] to an fp32 per-tile gradient [n_tiles, v_hidden] (same void*).
  *    ABI 7 -> 8: kd_loss_params.s_stats appended; kd_loss_student_stats added.
+ *    ABI 8 -> 9: kd_model_backward's on_layer_done also fires for the embeddings / projector
+ *    (KD_CB_EMBED_PROJECTOR) and after each SigLIP layer (KD_CB_VISION_LAYER(i), negative codes);
+ *    a callback written for ABI 8 must ignore layer < 0.
  */
 #ifndef KDSTEP_H
 #define KDSTEP_H
@@ -55,7 +60,7 @@ int kd_abi_version(void);                 /* returns KD_ABI_VERSION             
 const char* kd_last_error(void);          /* thread-local, never NULL                */
 int kd_device_is_gfx950(int device);      /* 1 if device `device` is gfx950, else 0  */
 
-#define KD_ABI_VERSION 8
+#define KD_ABI_VERSION 9
 
 /* ------------------------------------------------------------- KD losses ---- */
 /* Variants of the logit loss.  Each replaces one reference function:
@@ -562,9 +567,18 @@ int kd_model_forward(kd_model* m, const int64_t* ids, const void* pixels, int pi
  * gradients run on wgrad_stream beside the dgrad chain on `stream`; `stream` waits for
  * all of it before returning.  Work already queued on wgrad_stream (e.g. the caller's
  * lm_head wgrad into a tied embedding) is ordered before the embedding backward.
- * on_layer_done (optional) is called after each Qwen2 layer's backward is enqueued,
- * top-down (bucketed data-parallel all-reduce). */
+ * on_layer_done (optional) marks a part of the gradient final as soon as its backward is
+ * enqueued on `stream` / wgrad_stream (bucketed data-parallel all-reduce; a
+ * callback that launches a collective first makes its stream wait for wgrad_stream):
+ *   layer in [0, t_layers)      Qwen2 layer `layer`, top-down (after the final norm / lm_head);
+ *   KD_CB_EMBED_PROJECTOR (-1)  embed_tokens, image_newline and the projector (ABI 9; fired when
+ *                               the language model or the projector is trainable);
+ *   KD_CB_VISION_LAYER(i)       SigLIP layer i, top-down, with post_layernorm (ABI 9; trainable
+ *                               vision tower only).  The patch / position embeddings come last:
+ *                               they are final when kd_model_backward returns. */
 typedef void (*kd_layer_cb)(void* user, int layer);
+#define KD_CB_EMBED_PROJECTOR (-1)
+#define KD_CB_VISION_LAYER(i) (-2 - (i))
 size_t kd_model_backward_workspace_size(const kd_model* m, int B, int L, int n_tiles);
 int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids, const int32_t* src,
                       const float* rope_cos, const float* rope_sin, int B, int L, int n_tiles,

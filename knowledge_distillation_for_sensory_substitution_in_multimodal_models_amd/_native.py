@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("KDSTEP_LIB", _PKG / "libkdstep.so"))
 HEADER = _PKG.parent / "include" / "kdstep.h"
 
 KD_OK = 0
-ABI_VERSION = 8
+ABI_VERSION = 9
 STATUS_NAMES = {
     0: "KD_OK", 1: "KD_ERR_SHAPE", 2: "KD_ERR_DTYPE", 3: "KD_ERR_ALIGN", 4: "KD_ERR_ARCH",
     5: "KD_ERR_LABEL_RANGE", 6: "KD_ERR_LAUNCH", 7: "KD_ERR_ARG", 8: "KD_ERR_WORKSPACE",

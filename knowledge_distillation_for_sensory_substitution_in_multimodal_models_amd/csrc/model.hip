@@ -825,7 +825,7 @@ int lm_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, const float* cs
 }
 
 int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, const void* dpost, Lane& lane,
-                    hipStream_t s) {
+                    hipStream_t s, kd_layer_cb cb, void* user) {
     const Cfg& C = m->C;
     const kd_model_config& c = C.c;
     const int np = C.np(), D = c.v_hidden, Iv = c.v_inter, hdp = C.v_hdp(), hd = C.v_hd();
@@ -898,6 +898,10 @@ int vision_backward(kd_model* m, const FwdPlan& F, const BwdPlan& P, int NI, con
         KD_TRY(launch_norm_bwd(0, b.x, D, m->W(m->vis(i, VLN1W)), P.dhv, D, b.m1, b.r1, dx, D, 1,
                                gw ? m->G(m->vis(i, VLN1W)) : nullptr, gw ? m->G(m->vis(i, VLN1B)) : nullptr, 1, P.norm_ws,
                                P.norm_ws_bytes, NT, D, s, f32));
+        // layer i's gradients (and post_layernorm's) are enqueued: the caller may all-reduce them
+        // while the layers below run (ABI 9; the weight gradients are on the lane, which the
+        // callback joins before it launches a collective)
+        if (cb && gw) cb(user, KD_CB_VISION_LAYER(i));
     }
     if (gw) {   // patch embedding (im2col GEMM), its bias and the position embedding
         lane.begin();
@@ -1242,7 +1246,9 @@ int kd_model_backward(kd_model* m, const void* fwd_workspace, const int64_t* ids
         }
         if (need_vision) KD_TRY(gemm(s, P.splitk_main, NT, D, H, km(P.dz, H), mn(m->W(m->i_p1w), D), P.dxv, D, g0));
     }
-    if (need_vision) KD_TRY(vision_backward(m, F, P, NI, dpost, lane, s));
+    // embed_tokens, image_newline and the projector are final (ABI 9)
+    if (on_layer_done && (m->train_language || m->train_projector)) on_layer_done(user, KD_CB_EMBED_PROJECTOR);
+    if (need_vision) KD_TRY(vision_backward(m, F, P, NI, dpost, lane, s, on_layer_done, user));
     // the caller reads the grads (and reuses these buffers) after this: join the lane
     hipEvent_t done = m->event();
     (void)hipEventRecord(done, lane.lane);

@@ -3,7 +3,8 @@
 One process per GPU; the student's trainable gradient is one contiguous range of a flat
 fp32 buffer (modeling.ParamStore), so the all-reduce (mean over ranks) is a handful of
 large buckets, launched as soon as the backward has made a range final (LM layers
-top-down), overlapping the rest of the backward; RCCL over xGMI on GPUs (backend "nccl"),
+top-down, then embed_tokens / projector, then the SigLIP layers top-down: BackwardMarks),
+overlapping the rest of the backward; RCCL over xGMI on GPUs (backend "nccl"),
 gloo in the CPU tests.
 
 Gradient accumulation (the reference trains with accumulate_grad_batches=64, DT1T:70,
@@ -23,6 +24,52 @@ fp32 stays the default: the reference accumulates its 64 micro-batches' gradient
 and the collective overlaps the backward and the next teacher forward either way.
 """
 from __future__ import annotations
+
+import re
+
+# kd_model_backward's on_layer_done codes (include/kdstep.h, ABI 9): a Qwen2 layer index >= 0,
+# or one of these for the parts the backward finishes after the language model
+KD_CB_EMBED_PROJECTOR = -1
+
+
+def KD_CB_VISION_LAYER(i: int) -> int:
+    return -2 - i
+
+
+class BackwardMarks:
+    """Where the student gradient is final when kd_model_backward's callback fires.
+
+    Flat layout [vision (embeddings, layers 0..V-1, post_layernorm) | projector, image_newline |
+    language (embed_tokens, layers 0..N-1, norm)]; the backward finishes the language model top-down,
+    then embed_tokens / projector, then the SigLIP layers top-down, the patch / position embeddings
+    last.  first(code) is the flat offset from which everything up to the trainable range's top is
+    final after callback `code` (offsets: ParamStore.offsets, name -> (offset, numel))."""
+
+    def __init__(self, offsets: dict):
+        self.lm, self.vis = {}, {}
+        for name, (off, _) in offsets.items():
+            mt = re.match(r"language_model\.model\.layers\.(\d+)\.", name)
+            mv = re.match(r"vision_tower\.vision_model\.encoder\.layers\.(\d+)\.", name)
+            if mt:
+                i = int(mt.group(1))
+                self.lm[i] = min(off, self.lm.get(i, off))
+            elif mv:
+                i = int(mv.group(1))
+                self.vis[i] = min(off, self.vis.get(i, off))
+        self.proj = min(off for name, (off, _) in offsets.items()
+                        if name.startswith("multi_modal_projector.") or name == "image_newline")
+        self.embed = offsets["language_model.model.embed_tokens.weight"][0]
+
+    def first(self, code: int, train_language: bool, train_projector: bool, train_vision: bool):
+        """The flat offset, or None when `code` finishes nothing trainable."""
+        if code >= 0:
+            return self.lm[code] if train_language else None
+        if code == KD_CB_EMBED_PROJECTOR:
+            if train_projector:
+                return self.proj
+            return self.embed if train_language else None
+        i = -2 - code
+        return self.vis[i] if train_vision else None
 
 
 class GradSync:
@@ -44,13 +91,16 @@ class GradSync:
         self.world = dist.get_world_size()
         self.avg_in_collective = dist.get_backend() == "nccl"   # RCCL AVG; gloo has no AVG
         self.last_buckets = []   # element counts of the buckets of the last reducing backward
+        self.last_tail = 0       # elements of those launched only by end(), after the backward
         self._cur_buckets = []
+        self.top = None          # the trainable range's top (begin): nothing above it is reduced
 
     # -------------------------------------------------------------- backward ----
-    def begin(self, sync: bool):
+    def begin(self, sync: bool, top: int | None = None):
         self.wait()              # nothing in flight while this backward accumulates into grad
         self.active = bool(sync)
         self.hi = None
+        self.top = top
         self._cur_buckets = []
 
     def layer_done(self, first: int, before_launch=None):
@@ -58,7 +108,9 @@ class GradSync:
         if not self.active:
             return
         if self.hi is None:
-            self.hi = self.grad.numel()
+            self.hi = self.grad.numel() if self.top is None else self.top
+        if first >= self.hi:
+            return
         if (self.hi - first) * self.grad.element_size() >= self.bucket_bytes:
             if before_launch is not None:
                 before_launch()  # e.g. join the weight-gradient stream
@@ -69,6 +121,7 @@ class GradSync:
         """The backward is complete: reduce what is left of the trainable range [lo, hi)."""
         if self.active:
             top = hi if self.hi is None else min(hi, self.hi)
+            self.last_tail = max(0, top - lo)
             if top > lo:
                 self._launch(lo, top)
             self.unsynced = False

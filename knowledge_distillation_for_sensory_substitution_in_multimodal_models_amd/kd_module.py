@@ -32,7 +32,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .dp import GradSync
+from .dp import BackwardMarks, GradSync
 from .modeling import (STREAM_PRIORITY_HIGH, STUDENT_05B, TEACHER_7B, LlavaOnevisionModel, real_width_config,
                        tiny_config)
 
@@ -310,6 +310,7 @@ class _KDBase(_Base):
         import torch.distributed as dist
         self._dist = dist if (dist.is_available() and dist.is_initialized()) else None
         self._gsync = None
+        self._marks = None               # BackwardMarks of the student layout (first callback)
         if self._dist is not None:
             if self.uses_teacher:
                 # teacher weights broadcast once from rank 0, then read-only in every GPU's HBM
@@ -521,7 +522,7 @@ class _KDBase(_Base):
         sync = self._gsync is not None and self._no_sync_depth == 0 and \
             self._micro % self._accumulate() == 0
         if self._gsync is not None:
-            self._gsync.begin(sync)
+            self._gsync.begin(sync, top=self._trainable_range()[1])
         sf = ctx["sfwd"]
         hn = sf["hn"]
         W = s.lm_head_weight()
@@ -563,17 +564,21 @@ class _KDBase(_Base):
             self._no_sync_depth -= 1
 
     # ------------------------------------------------------- data parallel ----
-    def _on_layer_done(self, i):
-        """Bucketed all-reduce of LM grads as soon as the backward has made them final.
+    def _on_layer_done(self, code):
+        """Bucketed all-reduce of the student grads as soon as the backward has made them final
+        (kd_model_backward's callback, include/kdstep.h ABI 9).
 
         Flat layout [vision | projector | embed, layers 0..N-1, norm(, lm_head)]; the backward
-        finishes the tail first (lm_head, norm), then layers N-1..0, then embed / projector /
-        vision.  Everything from layer i's first parameter to the high-water mark is final
-        once layer i is done."""
+        finishes the tail first (lm_head, norm), then layers N-1..0 (code = the layer), then
+        embed / projector (KD_CB_EMBED_PROJECTOR), then the SigLIP layers top-down
+        (KD_CB_VISION_LAYER(i)), the patch / position embeddings last (GradSync.end).
+        Everything from the part's first parameter to the high-water mark is final."""
         s = self.student_model
-        if not s.train_language:
+        if self._marks is None:
+            self._marks = BackwardMarks(s.P.offsets)
+        first = self._marks.first(code, s.train_language, s.train_projector, s.train_vision)
+        if first is None:
             return
-        first = s.P.offsets[f"language_model.model.layers.{i}.self_attn.q_proj.weight"][0]
         lane = getattr(s, "wlane", None)
         self._gsync.layer_done(first, before_launch=lane.join if lane is not None else None)
 

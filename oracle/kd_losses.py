@@ -101,6 +101,53 @@ def loca_kd_term(teacher_logits, student_logits, labels, T: float, alpha: float 
     return (xlogx - q * torch.log(c_s)).mean() * (T ** 2)          # DT:188-192 (KAT 4)
 
 
+def loca_kd_term_rows(teacher_logits, student_logits, labels, T: float, alpha: float = 0.8,
+                      clamp_min: float = 1e-8, k=None, rows_per_chunk: int = 1024) -> float:
+    """loca_kd_term (DT:141-194) evaluated in row chunks (fp32 per chunk, fp64 sums) on any device,
+    for c4-size logits ([8, 1536, 152k]) where the whole-tensor restatement above would hold
+    several 7.5 GB temporaries.  `k` [B, L] replaces the LoCa second index topk(p_T, 2)[1]
+    (DT:170-171) -- with another teacher's index it splits a KD-term change into the part due to
+    the discrete override sets (KAT 1) and the part due to the probabilities themselves.
+    Same arithmetic as loca_kd_term (tests/test_oracle_golden.py)."""
+    V = student_logits.shape[-1]
+    B, L = labels.shape
+    dev = student_logits.device
+    if labels.min().item() < 0 or labels.max().item() >= V:       # KAT 2 (DT:166)
+        raise RuntimeError("index out of bounds: LoCa gathers the teacher prob at every label")
+    tf = teacher_logits[..., :V].reshape(B * L, V)
+    sf = student_logits.reshape(B * L, V)
+    lab = labels.reshape(-1).to(dev)
+    if k is None:
+        k = torch.cat([top2_second_index(_softmax_T(tf[r:r + rows_per_chunk].float(), T))
+                       for r in range(0, B * L, rows_per_chunk)])
+    kk = k.reshape(-1).to(dev)
+    X = torch.empty(B * L, dtype=torch.float32, device=dev)
+    Y = torch.empty_like(X)
+    for r in range(0, B * L, rows_per_chunk):                     # DT:158, :166-185 per row
+        p = _softmax_T(tf[r:r + rows_per_chunk].float(), T)
+        pg = p.gather(-1, lab[r:r + rows_per_chunk, None]).squeeze(-1)
+        pk = p.gather(-1, kk[r:r + rows_per_chunk, None]).squeeze(-1)
+        sc = alpha / (1.0 - pg + pk)
+        X[r:r + rows_per_chunk] = 1.0 - sc * (p.sum(-1) - pg)
+        Y[r:r + rows_per_chunk] = sc * pk
+    # KAT 1: one table of override values for the whole batch, labels first, klogits win
+    lab_last = torch.from_numpy(last_position_table(labels.cpu().numpy(), V)).to(dev)
+    klo_last = torch.from_numpy(last_position_table(kk.reshape(B, L).cpu().numpy(), V)).to(dev)
+    colv = torch.full((V,), float("nan"), dtype=torch.float32, device=dev)
+    m = lab_last >= 0
+    colv[m] = X[lab_last[m]]
+    m = klo_last >= 0
+    colv[m] = Y[klo_last[m]]
+    ov = ~torch.isnan(colv)
+    acc = 0.0
+    for r in range(0, B * L, rows_per_chunk):                     # DT:161-162, :188-192
+        q = torch.where(ov, colv, _softmax_T(tf[r:r + rows_per_chunk].float(), T))
+        c_s = torch.clamp(_softmax_T(sf[r:r + rows_per_chunk].float(), T), min=clamp_min)
+        xlogx = torch.where(q > 0, q * torch.log(torch.where(q > 0, q, torch.ones_like(q))), torch.zeros_like(q))
+        acc += float((xlogx - q * torch.log(c_s)).double().sum())
+    return acc / (B * L * V) * T * T
+
+
 def kl_mean_term(teacher_logits, student_logits, T: float):
     """kl_div(log_softmax(s/T), softmax(t/T), reduction='mean') * T^2 (DT:330-343)."""
     V = student_logits.shape[-1]

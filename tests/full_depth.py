@@ -170,15 +170,15 @@ def oracle_step(tsd, ssd, dtype=torch.float32):
 KINDS = {"lb": ("lb", 0), "dt1": ("dt", 1), "dt2": ("dt", 2), "dt3": ("dt", 3), "fb": ("fb", 0), "bd": ("bd", 0)}
 
 
-def _module(kind: str, phase: int):
+def _module(kind: str, phase: int, teacher_fp8: bool | str = False):
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd import kd_module as K
     if kind == "lb":
-        return K.LogitBasedKD(S_NAME, T_NAME)
+        return K.LogitBasedKD(S_NAME, T_NAME, teacher_fp8=teacher_fp8)
     if kind == "fb":
-        return K.FeatureBasedKD(S_NAME, T_NAME)
+        return K.FeatureBasedKD(S_NAME, T_NAME, teacher_fp8=teacher_fp8)
     if kind == "bd":
         return K.LlavaOnevisionModule(S_NAME)
-    m = K.OnlineKnowledgeDistillationLLavaOneVision(S_NAME, T_NAME, phase=phase)
+    m = K.OnlineKnowledgeDistillationLLavaOneVision(S_NAME, T_NAME, phase=phase, teacher_fp8=teacher_fp8)
     if phase == 1:
         m.freeze_student_language_layers()       # DT1T:105/111
     if phase == 2:
@@ -186,22 +186,29 @@ def _module(kind: str, phase: int):
     return m
 
 
-def hip_step_kind(dev, name: str):
+def hip_step_kind(dev, name: str, teacher_fp8: bool | str = False, detail: bool = False):
     """One training_step + backward of module `name` (KINDS: the reference's DT phases 1-3, LB, FB,
     BD) at full size, bs 1: the total, the student logits' per-row logsumexp, the trainable
-    parameters' gradients, and both models' weights (fp32 host tensors) for the oracle."""
+    parameters' gradients, and both models' weights (fp32 host tensors) for the oracle.
+    teacher_fp8: the e4m3 teacher (a modeling.FP8_FAMILIES policy; BASELINE config c4) on the same
+    seeded bf16 weights.  detail: also the fused kernel's KD term, student CE and teacher CE, and
+    the teacher logits' per-row logsumexp."""
     kind, phase = KINDS[name]
-    m = _module(kind, phase)
+    m = _module(kind, phase, teacher_fp8)
     b = _to(batch_cpu(), dev)
     m.keep_logits = True
     loss = m.training_step(b, 0)
     loss.backward()
     m.check_errors()
     torch.cuda.synchronize()
-    s3, _ = m.last_logits
+    s3, t3 = m.last_logits
     res = dict(terms=dict(total=float(loss.item())), s_lse=torch.logsumexp(s3[0].double(), -1).cpu())
+    if detail and t3 is not None:
+        kd, ce, tce, _ = m.last_terms.tolist()
+        res["terms"].update(kd_term=kd, student_ce=ce, teacher_ce=tce)
+        res["t_lse"] = torch.logsumexp(t3[0].double(), -1).cpu()
     m.last_logits = None
-    del s3
+    del s3, t3
     P = m.student_model.P
     g = P.grad
     grads = {}
@@ -219,10 +226,12 @@ def hip_step_kind(dev, name: str):
     return res, tsd, ssd
 
 
-def oracle_step_kind(tsd, ssd, name: str):
+def oracle_step_kind(tsd, ssd, name: str, detail: bool = False):
     """The pinned fp32 oracle's forward(batch) total of module `name` (oracle.model.kd_step_losses: DT:250-260,
     LB:164-165, FB:161-165, BD:90-101) on the same weights; the gradient of the trainable parameters (the
-    reference's freezes, tests/golden/model_fixtures.frozen) by autograd."""
+    reference's freezes, tests/golden/model_fixtures.frozen) by autograd.  detail: also the KD term of the
+    module's variant (LoCa DT:141-194 / KL DT:330-343 / log-target KL FB:205-219), the student and the
+    teacher CE, and the teacher logits' per-row logsumexp."""
     from oracle.model import OracleLlava, kd_step_losses
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import STUDENT_05B, TEACHER_7B
     kind, phase = KINDS[name]
@@ -243,6 +252,20 @@ def oracle_step_kind(tsd, ssd, name: str):
     res = dict(terms=dict(total=float(total.detach())),
                s_lse=torch.logsumexp(aux["s_logits"][0].detach().double(), -1),
                grads={k: v.grad for k, v in sw.items() if v.grad is not None})
+    if detail and teacher is not None:
+        from oracle import kd_losses as KL
+        s_l, t_l, labels = aux["s_logits"].detach(), aux["t_logits"], b["labels"]
+        h = KL.DT_HPARAMS if kind == "dt" else (KL.LB_HPARAMS if kind == "lb" else KL.FB_HPARAMS)
+        if kind == "fb":
+            kd = KL.kl_logtarget_term(t_l, s_l, h["T"])
+        elif (kind, phase) == ("dt", 1):
+            kd = KL.kl_mean_term(t_l, s_l, h["T"])
+        else:
+            kd = KL.loca_kd_term(t_l, s_l, labels, T=h["T"], alpha=h["alpha"])
+        res["terms"].update(kd_term=float(kd), student_ce=float(KL.causal_lm_ce(s_l, labels)),
+                            teacher_ce=float(KL.causal_lm_ce(t_l, labels)))
+        res["t_lse"] = torch.logsumexp(t_l[0].double(), -1)
+        del s_l, t_l, kd
     del total, aux, student, teacher
     gc.collect()
     return res
@@ -263,6 +286,30 @@ def measure_kinds(dev, names) -> dict:
         del hip, ref, tsd, ssd
         gc.collect()
     return rep
+
+
+C4_FP8_TOL = 1e-2   # the fp8 (e4m3) teacher's stated tolerance on the teacher-side terms
+
+
+def measure_c4(dev, policy: str = "lm_mlp") -> dict:
+    """BASELINE config c4's own module at full depth: double-trouble phase 3 (DT:257-260: 0.8 (LoCa
+    at T = 0.8 + CE) + 0.2 CE) with the fp8 (e4m3) teacher `policy`, bs 1, against the fp32 oracle
+    on the same (bf16-valued) weights -- the fp8 teacher's distance from the reference's fp32
+    teacher, measured on the configuration c4 runs."""
+    t0 = time.time()
+    _log(f"c4: HIP step (DT phase 3, fp8 teacher {policy})")
+    hip, tsd, ssd = hip_step_kind(dev, "dt3", teacher_fp8=policy, detail=True)
+    _log(f"c4: fp32 oracle step ({torch.get_num_threads()} threads)")
+    ref = oracle_step_kind(tsd, ssd, "dt3", detail=True)
+    del tsd, ssd
+    gc.collect()
+    r = compare(hip, ref, None)
+    r["config"] = (f"c4: DT phase 3 (LoCa T = 0.8), fp8 e4m3 teacher ({policy}), bs 1, L 1536, 336x336, full depth "
+                   "(SigLIP 26 + Qwen2 28 / 24 layers)")
+    r["tolerance"] = (f"north_star |d| <= {ATOL} + {RTOL} |ref| on the student CE, the total, every student lse row and "
+                      f"the gradient total norm; rel <= {C4_FP8_TOL} on the KD term and the teacher CE (the fp8 teacher)")
+    r["seconds"] = round(time.time() - t0, 1)
+    return r
 
 
 def compare(hip: dict, ref: dict, W: torch.Tensor | None = None) -> dict:

@@ -9,7 +9,7 @@ from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd im
 
 def test_library_loads_and_version():
     lib = N.lib()
-    assert lib.kd_abi_version() == N.ABI_VERSION == 8
+    assert lib.kd_abi_version() == N.ABI_VERSION == 9
     assert isinstance(lib.kd_last_error(), bytes)
 
 

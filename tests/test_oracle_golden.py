@@ -110,3 +110,24 @@ def test_oracle_kd_losses_match_reference(name):
     np.testing.assert_allclose(g.abs().sum(1).double().numpy(), exp["g_rowabs"], rtol=1e-4)
     idx = exp["g_samp_idx"]
     np.testing.assert_allclose(g[idx[:, 0], idx[:, 1]].numpy(), exp["g_samp_val"], rtol=1e-4, atol=1e-13)
+
+
+@pytest.mark.parametrize("name", [n for n in kd_fixture_names() if "loca" in n][:3])
+def test_chunked_loca_matches_reference(name):
+    """oracle.loca_kd_term_rows (row chunks, any device; the c4 fp8 KD-term split in bench.py /
+    tests/test_fp8_gpu.py) gives the reference's compute_loca_loss KD term; with its own second
+    index passed explicitly, the same value."""
+    meta, exp = load_kd_fixture(name)
+    t, s, labels = kd_inputs(meta, exp)
+    kd = O.loca_kd_term_rows(t, s, labels, T=meta["T"], alpha=meta["alpha"], rows_per_chunk=97)
+    assert kd == pytest.approx(float(exp["kd_term"]), rel=2e-5, abs=1e-12)
+    V = s.shape[-1]
+    k = O.top2_second_index(O._softmax_T(t[..., :V], meta["T"]))
+    assert O.loca_kd_term_rows(t, s, labels, T=meta["T"], alpha=meta["alpha"], k=k) == pytest.approx(kd, rel=1e-6)
+
+
+def test_chunked_loca_kat1():
+    k = KAT["kat1"]
+    kd = O.loca_kd_term_rows(torch.tensor(k["t"]), torch.tensor(k["s"]), torch.tensor(k["labels"]), T=k["T"],
+                             rows_per_chunk=1)
+    assert kd == pytest.approx(k["loss"], rel=1e-6)

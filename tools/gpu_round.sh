@@ -11,6 +11,9 @@
 #            -> full_depth_fp8.json
 # kindparity every other module (DT phases 1-3, FB, BD) at full depth vs the fp32 oracle
 #            (FULL_KINDS, default "dt1 dt2 dt3 fb bd") -> full_depth_kinds.json
+# c4parity   BASELINE c4 itself at full depth (DT phase 3 + fp8 lm_mlp teacher) vs the fp32 oracle -> c4_full_depth.json
+# fp8study   tools/fp8_c4_study.py: the c4 KD term's fp8-vs-bf16 move split into LoCa top-2 flips and smooth change,
+#            product library, then the A/B library with the GEMM k-loop stagger off -> fp8_c4*.json
 # parity     the reduced-depth fixtures' per-term / per-parameter report -> parity.json
 # ntx        tools/ntx_bias_study.py (NT-Xent-only bias gradients) -> ntx_bias.json
 # bench      bench.py (the driver's default line; BENCH_ARGS appended) -> bench.json
@@ -48,6 +51,12 @@ for s in $STEPS; do
                 --out $O/full_depth_kinds.json > $O/full_depth_kinds.log 2>&1 || fail kindparity $O/full_depth_kinds.log ;;
     fullparity) timeout -k 10 900 python -u tools/parity_report.py --full-depth --floor --teacher-stream-ab \
                 --out $O/full_depth.json > $O/full_depth.log 2>&1 || fail fullparity $O/full_depth.log ;;
+    c4parity) timeout -k 10 900 python -u tools/parity_report.py --c4-full-depth --out $O/c4_full_depth.json \
+                > $O/c4_full_depth.log 2>&1 || fail c4parity $O/c4_full_depth.log ;;
+    fp8study) timeout -k 10 600 python -u tools/fp8_c4_study.py --out $O/fp8_c4.json > /dev/null 2> $O/fp8_c4.log || fail fp8study $O/fp8_c4.log
+            KDSTEP_LIB=tools/ab/libkdstep_ab.so KD_GEMM_STAGGER=0 timeout -k 10 600 python -u tools/fp8_c4_study.py \
+                --out $O/fp8_c4_nostagger.json > /dev/null 2> $O/fp8_c4_nostagger.log || fail fp8study-nostagger $O/fp8_c4_nostagger.log
+            grep "seed" $O/fp8_c4.log $O/fp8_c4_nostagger.log ;;
     parity) timeout -k 10 600 python -u tools/parity_report.py --out $O/parity.json $PARITY_KINDS > $O/parity.log 2>&1 || fail parity $O/parity.log ;;
     ntx)    timeout -k 10 300 python -u tools/ntx_bias_study.py > $O/ntx_bias.json 2> $O/ntx_bias.err || fail ntx $O/ntx_bias.err ;;
     bench)  timeout -k 10 900 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err

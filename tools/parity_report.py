@@ -107,9 +107,19 @@ def main():
                     help="--full-depth: also the HIP step with the fp8 (e4m3) teacher of c4 (e.g. lm_mlp)")
     ap.add_argument("--full-depth-kinds", nargs="+", default=None, metavar="KIND",
                     help="each module kind (tests/full_depth.KINDS: lb dt1 dt2 dt3 fb bd) at full depth vs the fp32 oracle")
+    ap.add_argument("--c4-full-depth", action="store_true",
+                    help="BASELINE c4 itself at full depth: DT phase 3 + the fp8 lm_mlp teacher vs the fp32 oracle")
     ap.add_argument("kinds", nargs="*")
     a = ap.parse_args()
     import torch
+    if a.c4_full_depth:
+        from full_depth import measure_c4
+        rep = measure_c4(torch.device("cuda:0"))
+        print("c4", json.dumps({k: v for k, v in rep.items() if k != "grad_params"})[:3000], flush=True)
+        if a.out:
+            Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+            Path(a.out).write_text(json.dumps(rep, indent=1))
+        return
     if a.full_depth_kinds:
         from full_depth import measure_kinds
         rep = measure_kinds(torch.device("cuda:0"), a.full_depth_kinds)
