@@ -110,11 +110,12 @@ def host_cpu_info():
     return n, os.cpu_count(), model
 
 
-def _oracle_step_time(kind, phase, depth, dtype, batch):
-    """One oracle KD step (fwd + bwd) at `depth` layers of every tower, full widths."""
+def _oracle_models(kind, phase, depth, dtype, batch):
+    """The oracle's teacher and student at `depth` layers of every tower (None: full depth), full
+    widths, seeded N(0, 0.02) weights in `dtype`, and the batch in that dtype."""
     import torch
     from dataclasses import replace
-    from oracle.model import OracleLlava, kd_step_losses
+    from oracle.model import OracleLlava
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import (
         STUDENT_05B, TEACHER_7B, param_specs)
 
@@ -142,19 +143,43 @@ def _oracle_step_time(kind, phase, depth, dtype, batch):
     b = dict(batch)
     for k in ("rgb_pixel_values", "depth_pixel_values"):
         b[k] = b[k].to(dtype)
-    teacher, student = OracleLlava(tsd, tc), OracleLlava(ssd, sc)
-    t0 = time.perf_counter()
-    total, _ = kd_step_losses(kind, teacher, student, b, phase=phase)
-    total.float().backward()
-    return time.perf_counter() - t0
+    return OracleLlava(tsd, tc), OracleLlava(ssd, sc), ssd, b
+
+
+def _oracle_step_times(kind, phase, depth, dtype, batch, warmup=0, steps=1):
+    """Seconds of `steps` oracle KD steps (teacher fwd + student fwd + loss + student bwd) after
+    `warmup` untimed ones, on the same models (the gradients reset between steps, as zero_grad)."""
+    import torch
+    from oracle.model import kd_step_losses
+    teacher, student, ssd, b = _oracle_models(kind, phase, depth, dtype, batch)
+    out = []
+    for i in range(warmup + steps):
+        for v in ssd.values():
+            v.grad = None
+        t0 = time.perf_counter()
+        total, _ = kd_step_losses(kind, teacher, student, b, phase=phase)
+        total.float().backward()
+        dt = time.perf_counter() - t0
+        if i >= warmup:
+            out.append(dt)
+    del teacher, student, ssd, b
+    return out
+
+
+def _oracle_step_time(kind, phase, depth, dtype, batch):
+    """One oracle KD step (fwd + bwd) at `depth` layers of every tower, full widths."""
+    return _oracle_step_times(kind, phase, depth, dtype, batch)[0]
 
 
 def cpu_baseline(kind: str, phase: int, threads: int, full: bool = False):
-    """The oracle (CPU torch restatement of the reference's step, kind `port`) at bs=1,
-    L=1536, full widths, in fp32 and bf16.  full=True (default, ~1 min on 16 threads): one
-    full-depth step of each.  full=False (--cpu-extrapolate): depth 1 and 3 of every tower,
-    each timed twice (min), extrapolated to the full 26/28 + 26/24 layers by the per-layer
-    FLOP share of the depth 1 -> 3 delta."""
+    """The oracle (CPU torch restatement of the reference's step, kind `port`) at bs=1, L=1536,
+    full widths.  full=True (default): bf16 -- the GPU path's arithmetic type and BASELINE.md §2's
+    measured reference dtype -- as BASELINE.md §3 runs it: 1 warm-up + 3 timed full-depth steps, the
+    median (value); fp32 alongside as ONE full-depth step without a warm-up (4 fp32 steps would add
+    ~2 min to the default bench run; the sample stays bounded).  full=False (--cpu-extrapolate):
+    depth 1 and 3 of every tower, each timed twice (min), extrapolated to the full 26/28 + 26/24
+    layers by the per-layer FLOP share of the depth 1 -> 3 delta."""
+    import statistics
     import torch
     from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
     torch.set_num_threads(threads)
@@ -168,10 +193,15 @@ def cpu_baseline(kind: str, phase: int, threads: int, full: bool = False):
     tot = sum(parts.values())
     extra = {"t_vit": 25, "t_lm": 27, "s_vit": 25, "s_lm": 23}
     res = {}
-    for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
-        if full:   # one full-depth step (7B + 0.5B weights in host memory)
-            res[name] = dict(s_per_sample=round(_oracle_step_time(kind, phase, None, dt, batch), 2),
-                             measured="full depth")
+    for name, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+        if full:   # full-depth steps (7B + 0.5B weights in host memory)
+            if name == "bf16":
+                ts = _oracle_step_times(kind, phase, None, dt, batch, warmup=1, steps=3)
+                res[name] = dict(s_per_sample=round(statistics.median(ts), 2), steps_s=[round(t, 2) for t in ts],
+                                 measured="full depth, median of 3 steps after 1 warm-up")
+            else:
+                res[name] = dict(s_per_sample=round(_oracle_step_time(kind, phase, None, dt, batch), 2),
+                                 measured="full depth, one step, no warm-up")
             continue
         times = {}
         for d in (1, 3, 1, 3):
@@ -180,16 +210,17 @@ def cpu_baseline(kind: str, phase: int, threads: int, full: bool = False):
         t_full = times[1] + sum(delta * parts[k] / tot * extra[k] for k in parts)
         res[name] = dict(s_per_sample=round(t_full, 2), depth1_s=round(times[1], 2), depth3_s=round(times[3], 2))
     n, ncpu, model = host_cpu_info()
-    v = res["fp32"]["s_per_sample"]
-    return dict(value=round(1.0 / v, 5), unit="samples/s", cores=threads, kind="port",
-                cpu_model=model, machine_cpus=ncpu, bf16=dict(value=round(1.0 / res["bf16"]["s_per_sample"], 5), **res["bf16"]),
-                fp32=res["fp32"],
+    v = res["bf16"]["s_per_sample"]
+    return dict(value=round(1.0 / v, 5), unit="samples/s", cores=threads, kind="port", dtype="bf16",
+                cpu_model=model, machine_cpus=ncpu, bf16=res["bf16"],
+                fp32=dict(value=round(1.0 / res["fp32"]["s_per_sample"], 5), **res["fp32"]),
                 sample=(f"oracle (CPU torch restatement of the reference step, pinned to its fixtures) KD step, bs=1, "
                         f"L=1536, full widths, {threads} threads on {model}: "
-                        + ("one full-depth step" if full else
+                        + ("bf16 full depth, median of 3 steps after 1 warm-up (BASELINE.md §3); fp32 one full-depth "
+                           "step" if full else
                            "measured at depth 1 and 3 of every tower (min of 2 each), extrapolated to the full "
                            "26/28 + 26/24 layers by per-layer FLOP share")
-                        + f"; value = fp32 ({v:.1f} s/sample), bf16 alongside ({res['bf16']['s_per_sample']:.1f} s/sample)"))
+                        + f"; value = bf16 ({v:.1f} s/sample), fp32 alongside ({res['fp32']['s_per_sample']:.1f} s/sample)"))
 
 
 def kd_loss_delta(m, batch, variant_T):
@@ -436,12 +467,15 @@ def allreduce_cost(m, dist, dev, world):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms = float(t.item())
     nbytes = n * buf.element_size()
+    esz = buf.element_size()
     del buf
     return dict(buckets=len(gs.last_buckets), bytes=nbytes, dtype=str(dt_).replace("torch.", ""),
+                bytes_after_backward=int(getattr(gs, "last_tail", 0)) * esz,
                 standalone_ms=round(ms, 3),
                 ring_bus_GBps=round(2 * (world - 1) / world * nbytes / (ms * 1e-3) / 1e9, 1),
                 measured="the last reducing backward's buckets all-reduced (AVG) alone, after the timed region, "
-                         "max over ranks; in the step they overlap the backward and the next teacher forward")
+                         "max over ranks; in the step they overlap the backward and the next teacher forward, "
+                         "except bytes_after_backward (launched by GradSync.end once the backward is done)")
 
 
 def main():
@@ -457,8 +491,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-extrapolate", action="store_true",
-                    help="cpu_baseline: depth-1/3 runs extrapolated by per-layer FLOP share instead of one "
-                         "full-depth step (the default since round 2: 43 s fp32 + 15 s bf16 on 16 threads)")
+                    help="cpu_baseline: depth-1/3 runs extrapolated by per-layer FLOP share instead of the "
+                         "full-depth steps (default: bf16 1 warm-up + 3 timed, fp32 one step; ~1.7 min on 16 threads)")
     ap.add_argument("--no-timer", action="store_true", help="skip the serialized roofline pass (per-GEMM HIP events)")
     ap.add_argument("--no-delta", action="store_true", help="skip kd_loss_delta (the CPU oracle on this step's logits)")
     ap.add_argument("--serial", action="store_true",

@@ -29,7 +29,8 @@
  *    ABI 6 -> 7 also changed kd_model_backward's dpost from a bf16 per-row gradient
  *    [n_tiles*np, v_hidden] to an fp32 per-tile gradient [n_tiles, v_hidden] (same void*).
  *    ABI 7 -> 8: kd_loss_params.s_stats appended; kd_loss_student_stats added.
- *    ABI 8 -> 9: kd_model_backward's on_layer_done also fires for the embeddings / projector
+ *    ABI 8 -> 9: kd_loss_params.loca_path / rr_poll_us_p1 / standin_count appended (the library
+ *    reads no environment variable for the loss kernel any more); kd_model_backward's on_layer_done also fires for the embeddings / projector
  *    (KD_CB_EMBED_PROJECTOR) and after each SigLIP layer (KD_CB_VISION_LAYER(i), negative codes);
  *    a callback written for ABI 8 must ignore layer < 0.
  */
@@ -122,6 +123,17 @@ typedef struct {
        the loss then reads only the teacher's logits for its statistics. Bit-identical results.
        Exclusive with s_row_stats. */
     const float* s_stats;
+    /* optional (ABI 9): the LoCa kernel (0 = the product default).  loca_path 0: register-resident
+       row slices (k_loss_grad_loca_rr) where they fit, 1: the two-read k_loss_grad_loca (same terms up
+       to the fp32 order of the row sums).  rr_poll_us_p1: the register-resident kernel's poll budget
+       for a partner slice's partials, in microseconds + 1 (0 = the default 200 us; 1 = no wait: every
+       partner partial recomputed by the waiting slice itself, which must give the same bits). */
+    int32_t loca_path;
+    int32_t rr_poll_us_p1;
+    /* optional (ABI 9): device int32, += the number of partner partials the register-resident kernel
+       recomputed because the partner slice was not running within the poll budget (0 on an idle or
+       evenly shared GPU; the fallback only slows the step down, this shows when it fires) */
+    int32_t* standin_count;
 } kd_loss_params;
 
 /* loss_out (device float[4]): [0] KD term (mean, incl. T^2, unweighted)

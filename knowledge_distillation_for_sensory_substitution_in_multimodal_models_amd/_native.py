@@ -46,6 +46,9 @@ class KdLossParams(C.Structure):
         ("s_row_stats", C.c_void_p),
         ("t_row_stats", C.c_void_p),
         ("s_stats", C.c_void_p),
+        ("loca_path", C.c_int32),
+        ("rr_poll_us_p1", C.c_int32),
+        ("standin_count", C.c_void_p),
     ]
 
 

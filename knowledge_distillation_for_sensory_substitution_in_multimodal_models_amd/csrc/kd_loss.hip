@@ -736,7 +736,8 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
                     const float* __restrict__ ovr, const unsigned long long* __restrict__ mask_g,
                     const float* __restrict__ coefs, bf16* __restrict__ D_, int64_t ld_d,
                     float* __restrict__ part_kl, int nsl, int cps, int n_rg,
-                    unsigned long long* __restrict__ gran, uint32_t poll_ticks, int stamp, int ov_cap, int pf) {
+                    unsigned long long* __restrict__ gran, uint32_t poll_ticks, int stamp, int ov_cap, int pf,
+                    int* __restrict__ standin_count) {
 #ifndef KD_AB_BUILD
     stamp = 0;   // the product build carries no stamps (every stamp branch folds away)
 #endif
@@ -950,7 +951,8 @@ k_loss_grad_loca_rr(const bf16* __restrict__ T_, int64_t ld_t, const bf16* __res
             // a slice of this row is not running now (its workgroup is not resident beside this one:
             // other work holds CUs): compute its partials here with the same body and lane mapping, so
             // they are the bits it stores itself, then restore this slice's chunks.  Progress never
-            // depends on co-residency.
+            // depends on co-residency; kd_loss_params.standin_count shows when this path runs.
+            if (standin_count != nullptr && tid == 0) atomicAdd(standin_count, __popc((unsigned)miss));
             for (int s2 = 0; s2 < nsl; ++s2) {
                 if (!((miss >> s2) & 1)) continue;
                 const int lo2 = s2 * cps, hi2 = min(V >> 3, lo2 + cps);
@@ -1175,18 +1177,11 @@ int rr_chunks() {
 
 // poll budget of a slice waiting for its row's other slices, in ticks of the 100 MHz real-time
 // clock: 200 us by default (co-resident slices of a row arrive microseconds apart); after it the
-// slice computes the absent partials itself.  KD_LOSS_RR_POLL_US (read per call; tests: 0 = every
+// slice computes the absent partials itself.  kd_loss_params.rr_poll_us_p1 (tests: 1 = no wait, every
 // slice recomputes every other slice's partials, which must give the same bits)
-uint32_t rr_poll_ticks() {
-    const char* e = std::getenv("KD_LOSS_RR_POLL_US");
-    const long us = e ? std::atol(e) : 200;
-    return (uint32_t)std::min<long>(std::max<long>(us, 0) * 100, 100000000L);
-}
-
-// KD_LOSS_RR=0: the two-read k_loss_grad_loca (A/B; read at every call, so a test can switch)
-bool rr_enabled() {
-    const char* e = std::getenv("KD_LOSS_RR");
-    return e == nullptr || std::atoi(e) != 0;
+uint32_t rr_poll_ticks(int32_t us_p1) {
+    const long us = us_p1 > 0 ? (long)us_p1 - 1 : 200;
+    return (uint32_t)std::min<long>(us * 100, 100000000L);
 }
 
 }  // namespace
@@ -1285,7 +1280,7 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
     const int rc = rr_chunks();
     const int nsl = rr_nsl(V_s, rc);
     const int resident = rr_resident(rc);
-    if (loca_fast && rr_enabled() && nsl <= RR_MAX_SL && resident >= 2 * nsl) {
+    if (loca_fast && p.loca_path == 0 && nsl <= RR_MAX_SL && resident >= 2 * nsl) {
         // register-resident slices (k_loss_grad_loca_rr): resident / nsl row groups of nsl workgroups,
         // sized so that all of them fit at once on an idle GPU; a slice whose partner is not running
         // (other work holds CUs) stands in for it after the poll budget, so nothing depends on that
@@ -1297,8 +1292,8 @@ int launch_kd_loss(const void* teacher, int64_t ld_t, int V_t, const void* stude
 #define KD_LAUNCH_RR(T1v, RCv)                                                                                   \
     hipLaunchKernelGGL((k_loss_grad_loca_rr<T1v, RCv>), dim3(n_rg * nsl), dim3(RR_NT), rr_smem(RCv), stream, T_, ld_t,   \
                        S_, ld_s, V_s, rows, invT, p.clamp_min, stats, ovr, mask, coefs, D_, ld_d, part_kl, nsl, cps, n_rg, \
-                       gran, rr_poll_ticks(), ab_knob("KD_RR_STAMPS", 0), ab_knob("KD_RR_OV", 1) ? rr_ov_cap(RCv) : -1,   \
-                       ab_knob("KD_RR_PF", 1))
+                       gran, rr_poll_ticks(p.rr_poll_us_p1), ab_knob("KD_RR_STAMPS", 0),                          \
+                       ab_knob("KD_RR_OV", 1) ? rr_ov_cap(RCv) : -1, ab_knob("KD_RR_PF", 1), p.standin_count)
         if (rc == 5) { if (invT == 1.f) KD_LAUNCH_RR(true, 5); else KD_LAUNCH_RR(false, 5); }
         else { if (invT == 1.f) KD_LAUNCH_RR(true, 3); else KD_LAUNCH_RR(false, 3); }
 #undef KD_LAUNCH_RR

@@ -23,14 +23,11 @@ import torch
 
 from . import ops
 
-import os
 
 EOS_TOKEN_IDS = (151645,)   # <|im_end|>: generation_config.eos_token_id of the -ov-hf chat checkpoints
 
 
-def _fuse_norm_default() -> bool:
-    """RMSNorm fused into the decode GEMVs unless KD_DECODE_FUSE_NORM=0 (A/B knob; read per call)."""
-    return os.environ.get("KD_DECODE_FUSE_NORM", "1") != "0"
+FUSE_NORM_DEFAULT = True   # RMSNorm fused into the decode GEMVs (tools/bench_generate.py passes fuse_norm for A/B)
 
 
 @torch.no_grad()
@@ -40,9 +37,9 @@ def generate(model, input_ids: torch.Tensor, pixel_values: torch.Tensor, image_s
              graph: bool = True, fuse_norm: bool | None = None):
     """-> int64 [1, L + n_new] on the device (and the bf16 logits row of every step if
     return_logits).  `temperature` is accepted for signature parity and ignored (greedy).
-    fuse_norm: RMSNorm fused into the q|k|v and gate|up GEMVs (default: KD_DECODE_FUSE_NORM)."""
+    fuse_norm: RMSNorm fused into the q|k|v and gate|up GEMVs (default: FUSE_NORM_DEFAULT)."""
     del temperature, pad_token_id   # greedy, batch of one: no padding of finished rows
-    FUSE_NORM = _fuse_norm_default() if fuse_norm is None else bool(fuse_norm)
+    FUSE_NORM = FUSE_NORM_DEFAULT if fuse_norm is None else bool(fuse_norm)
     if input_ids.dim() != 2 or input_ids.shape[0] != 1:
         raise ValueError("generate: batch size 1 (as evaluate_onevision.py runs it)")
     T, P = model.cfg.text, model.P

@@ -26,7 +26,6 @@ from __future__ import annotations
 import contextlib
 import inspect
 
-import os
 
 import torch
 import torch.nn as nn
@@ -294,12 +293,15 @@ class _KDBase(_Base):
         self._errors = _ErrorWatch(dev)
         self._errors.bind(self.student_model, self.teacher_model)
         self.keep_logits = False         # tests: keep the step's logits in last_logits
-        # KD_FUSE_ROWSTATS=1: the lm_head epilogues emit the KD loss's row statistics.  Off by
-        # default: measured slower (profiles/r03/row_stats_fusion_ab.txt)
-        self.fuse_row_stats = os.environ.get("KD_FUSE_ROWSTATS", "0") == "1"
+        # fuse_row_stats: the lm_head epilogues emit the KD loss's row statistics.  Off by default:
+        # measured slower (profiles/r03/row_stats_fusion_ab.txt); tests / tools set the attribute
+        self.fuse_row_stats = False
         # the student's row statistics on the student stream ahead of the loss (kd_loss_student_stats;
-        # KD_STUDENT_STATS_EARLY=0 leaves them in the loss's own pass, for A/B)
-        self.student_stats_early = os.environ.get("KD_STUDENT_STATS_EARLY", "1") != "0"
+        # False leaves them in the loss's own pass, for A/B)
+        self.student_stats_early = True
+        # kd_loss_params.standin_count: partner partials the register-resident LoCa kernel recomputed
+        # (its fallback when a row's slices are not co-resident; bench.py reports it)
+        self.loss_standins = torch.zeros(1, dtype=torch.int32, device=dev)
         self.last_terms = None
         self.last_ntxent = None
         self.last_logits = None
@@ -419,7 +421,7 @@ class _KDBase(_Base):
             side.wait_event(self._opt_done)
             self._opt_pending = False
         # the lm_head epilogues emit the loss's per-row softmax statistics (kd_gemm_desc.row_stats)
-        # so the loss does not read both logit tensors once more just for them (KD_FUSE_ROWSTATS=1;
+        # so the loss does not read both logit tensors once more just for them (fuse_row_stats;
         # default: the loss's own pass)
         Vs_ = s.cfg.text.vocab
         fuse = self.fuse_row_stats
@@ -463,7 +465,7 @@ class _KDBase(_Base):
                                 row_base=g * G * L, dscale=dscale, dscale_given=g > 0,
                                 s_row_stats=None if s_rst is None else s_rst[rs],
                                 t_row_stats=None if (s_rst is None or t_rst is None) else t_rst[rs],
-                                s_stats=None if s_st is None else s_st[rs])
+                                s_stats=None if s_st is None else s_st[rs], standin_count=self.loss_standins)
         del s_rst, t_rst, s_st
         if self.keep_logits:
             self.last_logits = (s3, t3)

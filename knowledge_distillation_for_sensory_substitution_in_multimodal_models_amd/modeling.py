@@ -19,7 +19,6 @@ a trainable model) in the transformers-4.45 state_dict order and names
 from __future__ import annotations
 
 import ctypes as C
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -343,7 +342,7 @@ def rope_tables(seq: int, hd: int, theta: float, device):
 
 
 # priority of the training step's streams (lower = higher; 0 = default)
-STREAM_PRIORITY_HIGH = int(os.environ.get("KD_STREAM_PRIORITY", "-1"))
+STREAM_PRIORITY_HIGH = -1   # the student chain's stream priority (DESIGN §3 Streams: measured best)
 
 
 class WgradLane:
@@ -665,6 +664,13 @@ class LlavaOnevisionModel:
         if "ws" not in fwd:
             raise RuntimeError("backward needs a forward run with save=True")
         B, L, tiles = fwd["shape"]
+        if dpost is not None:
+            # ABI 7: the gradient of each tile's MEAN post_ln feature, fp32 [tiles, v_hidden] (the
+            # bf16 per-row gradient of ABI <= 6 would be read as the wrong type and shape)
+            if dpost.dtype != torch.float32 or not dpost.is_contiguous() or \
+                    tuple(dpost.shape) != (tiles, self.cfg.vision.hidden):
+                raise RuntimeError(f"backward: dpost must be a contiguous fp32 [{tiles}, {self.cfg.vision.hidden}] "
+                                   f"tile gradient, got {tuple(dpost.shape)} {dpost.dtype}")
         cos, sin = self._rope_for(L)
         nb = NV.lib().kd_model_backward_workspace_size(self._h, B, L, tiles)
         ws = self._workspace(("bwd", B, L, tiles), nb)

@@ -135,7 +135,8 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
                     err_out: torch.Tensor | None = None, row_base: int = 0,
                     dscale: torch.Tensor | None = None, dscale_given: bool = False,
                     s_row_stats: torch.Tensor | None = None, t_row_stats: torch.Tensor | None = None,
-                    s_stats: torch.Tensor | None = None):
+                    s_stats: torch.Tensor | None = None, loca_path: str = "auto", rr_poll_us: int | None = None,
+                    standin_count: torch.Tensor | None = None):
     """Fused KD-loss forward + backward (include/kdstep.h kd_loss_fwd_bwd).
 
     student_logits [B, L, V_s] bf16 (last dim contiguous), teacher_logits [B, L, V_t] bf16,
@@ -153,6 +154,10 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
     the loss's own pass over the logits (kd_loss_params.s_row_stats / t_row_stats).
     s_stats (fp32 [B*L, 4], these rows, same temperature): kd_loss_student_stats' output, so the
     loss reads only the teacher's logits for its statistics (kd_loss_params.s_stats; same bits).
+    loca_path "auto" (the register-resident slices where they fit) or "two_read" (k_loss_grad_loca);
+    rr_poll_us: the register-resident kernel's partner poll budget (None = 200 us; 0 = every partner
+    partial recomputed by the waiting slice); standin_count (device int32 [1]) += the partials that
+    were recomputed (kd_loss_params.loca_path / rr_poll_us_p1 / standin_count).
     """
     B, L, V_s = student_logits.shape
     _require(student_logits, torch.bfloat16, "student_logits")
@@ -198,7 +203,11 @@ def kd_loss_fwd_bwd(student_logits: torch.Tensor, teacher_logits: torch.Tensor |
     prm = NV.KdLossParams(v, float(temperature), float(alpha), float(kd_weight), float(ce_weight),
                          float(grad_scale), float(clamp_min), 1 if teacher_ce else 0, float(out_scale),
                          1 if accumulate else 0, _ptr(err_out), int(row_base), _ptr(dscale),
-                         1 if dscale_given else 0, _ptr(s_row_stats), _ptr(t_row_stats), _ptr(s_stats))
+                         1 if dscale_given else 0, _ptr(s_row_stats), _ptr(t_row_stats), _ptr(s_stats),
+                         {"auto": 0, "two_read": 1}[loca_path], 0 if rr_poll_us is None else int(rr_poll_us) + 1,
+                         _ptr(standin_count))
+    if standin_count is not None:
+        _require(standin_count, torch.int32, "standin_count")
     NV.call("kd_loss_fwd_bwd", _ptr(teacher_logits), ld_t, V_t, _ptr(student_logits),
            student_logits.stride(1), V_s, _ptr(labels), B, L, prm, _ptr(loss), _ptr(dl),
            V_s, _ptr(ws), ws.numel(), _stream())

@@ -84,6 +84,7 @@ def _allreduce_rank(rank, world, port, q):
 
     class _GS:
         last_buckets = [1 << 16, 1 << 15, 1000]
+        last_tail = 1000
         comm_dtype = None
 
     class _M:
@@ -115,7 +116,9 @@ def test_allreduce_cost_schema_gloo():
     a, b = res[0], res[1]
     n = (1 << 16) + (1 << 15) + 1000
     for r in (a, b):
-        assert set(r) == {"buckets", "bytes", "dtype", "standalone_ms", "ring_bus_GBps", "measured"}
+        assert set(r) == {"buckets", "bytes", "dtype", "bytes_after_backward", "standalone_ms", "ring_bus_GBps",
+                          "measured"}
+        assert r["bytes_after_backward"] == 4000
         assert r["buckets"] == 3 and r["bytes"] == 4 * n and r["dtype"] == "float32"
         assert r["standalone_ms"] > 0
         bw = 2 * (2 - 1) / 2 * r["bytes"] / (r["standalone_ms"] * 1e-3) / 1e9

@@ -214,9 +214,9 @@ def _dense_labels(B, L, hi, g):
 @pytest.mark.parametrize("B,L,V,T,ovr", [(2, 384, 151936, 1.0, True), (2, 384, 151936, 0.8, True),
                                          (1, 200, 20480, 1.0, False), (3, 7, 24, 1.0, True),
                                          (2, 1536, 151936, 1.0, "dense"), (1, 2048, 151936, 0.8, "dense")])
-def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev, monkeypatch):
+def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev):
     """k_loss_grad_loca_rr (row slices held in registers, partials handed between the slices'
-    workgroups) == k_loss_grad_loca (KD_LOSS_RR=0, two reads of every row) up to the fp32 order
+    workgroups) == k_loss_grad_loca (loca_path="two_read", two reads of every row) up to the fp32 order
     of the row sums: terms within 2e-6 relative, dlogits within one bf16 ulp.  Cases: the real
     vocab at T = 1 and 0.8 (8 slices), one slice (V = 20480), a vocab of 3 chunks; labels drawn
     from a few ids so the LoCa override columns (DT:184-185) fall into several slices; "dense":
@@ -235,9 +235,8 @@ def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev, mo
         labels[:, ::3] = torch.randint(0, V, labels[:, ::3].shape, generator=g)
     labels = labels.to(dev)
     out = []
-    for rr in ("0", "1"):
-        monkeypatch.setenv("KD_LOSS_RR", rr)
-        out.append(ops.kd_loss_fwd_bwd(s, t, labels, "loca", temperature=T, check=True))
+    for path in ("two_read", "auto"):
+        out.append(ops.kd_loss_fwd_bwd(s, t, labels, "loca", temperature=T, check=True, loca_path=path))
     torch.cuda.synchronize()
     (l0, d0), (l1, d1) = out
     a, b = l0.cpu().double(), l1.cpu().double()
@@ -248,11 +247,11 @@ def test_register_resident_loca_matches_two_read_kernel(B, L, V, T, ovr, dev, mo
 
 @pytest.mark.parametrize("B,L,V,T,dense", [(2, 384, 151936, 1.0, False), (1, 257, 151936, 0.8, False),
                                            (2, 64, 60000, 1.0, False), (2, 1536, 151936, 1.0, True)])
-def test_register_resident_loca_stand_in_is_bit_identical(B, L, V, T, dense, dev, monkeypatch):
+def test_register_resident_loca_stand_in_is_bit_identical(B, L, V, T, dense, dev):
     """Co-residency is not required by k_loss_grad_loca_rr: a slice whose partner slices have not
     handed over their pass-A partials within the poll budget computes them itself (same body, same
-    lane mapping, same reduction order).  KD_LOSS_RR_POLL_US=0 forces that stand-in path for every
-    absent partial of every row; the loss terms and dlogits must be the default path's bits, and no
+    lane mapping, same reduction order).  rr_poll_us=0 forces that stand-in path for every
+    absent partial of every row (kd_loss_params.standin_count counts them); the loss terms and dlogits must be the default path's bits, and no
     error may be raised (the loss must never depend on workgroups being resident).
     dense: one slice overflows its LDS override image (global table) while the stand-ins read the
     table from global memory for every slice they recompute."""
@@ -263,13 +262,26 @@ def test_register_resident_loca_stand_in_is_bit_identical(B, L, V, T, dense, dev
     t = (torch.randn(B, L, V + 128, generator=gd, device=dev) * 2).bfloat16()
     labels = (_dense_labels(B, L, 18992, g) if dense else torch.randint(0, V, (B, L), generator=g)).to(dev)
     out = []
-    for us in ("200", "0"):
-        monkeypatch.setenv("KD_LOSS_RR_POLL_US", us)
-        out.append(ops.kd_loss_fwd_bwd(s, t, labels, "loca", temperature=T, check=True))
+    counts = []
+    for us in (None, 0):
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        out.append(ops.kd_loss_fwd_bwd(s, t, labels, "loca", temperature=T, check=True, rr_poll_us=us,
+                                       standin_count=cnt))
+        counts.append(cnt)
     torch.cuda.synchronize()
     (l0, d0), (l1, d1) = out
     assert torch.equal(l0.cpu(), l1.cpu()), (l0, l1)
     assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+    # the counter shows the fallback: none on an idle GPU (a row's slices are co-resident and arrive
+    # microseconds apart); with no poll budget every partner partial not yet stored when a slice looks
+    # is recomputed -- at least the first arriver's nsl - 1 per row, at most nsl (nsl - 1) per row
+    nsl = -(-(V // 8) // 2560)      # slices of <= 2560 16-B chunks
+    assert int(counts[0].item()) == 0, counts[0].item()
+    n = int(counts[1].item())
+    if nsl > 1:
+        assert B * L * (nsl - 1) <= n <= B * L * nsl * (nsl - 1), (n, nsl)
+    else:
+        assert n == 0
 
 
 @pytest.mark.parametrize("variant,T,B,L,V", [("loca", 1.0, 2, 384, 151936), ("loca", 0.8, 1, 257, 151936),

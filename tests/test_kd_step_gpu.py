@@ -103,7 +103,7 @@ def test_training_step_matches_reference(name, dev):
 
 @pytest.mark.parametrize("name", ["lb", "dt2"])
 def test_fused_row_stats_step_matches(name, dev):
-    """KD_FUSE_ROWSTATS=1 (the lm_head epilogues emit the loss's row statistics): every loss
+    """fuse_row_stats (the lm_head epilogues emit the loss's row statistics): every loss
     term at the north-star tolerance against the reference and within 1e-6 |ref| of the
     default path's (the same statistics, merged per 256-column tile instead of per row)."""
     meta, exp = load(name)
