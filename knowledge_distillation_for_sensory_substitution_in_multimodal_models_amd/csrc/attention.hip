@@ -136,218 +136,7 @@ __device__ __forceinline__ bf16x4 tr_read_off(uint32_t addr) {
 }
 
 #ifdef KD_AB_BUILD   // the round-2 16x16x32 forward (forced variant 16): the tools' A/B library only
-// NQ query sub-tiles of 16 rows per wave (workgroup = 4 waves x 16·NQ rows): every K
-// fragment (b128) and V^T fragment (tr_b16) read from LDS feeds NQ MFMAs, so LDS bytes
-// per FLOP drop by NQ (at NQ = 1 the kernel was bound by its LDS reads: one 64-key tile =
-// 32 KiB of fragment reads per wave for a 16 x 64 block of scores).
-template <int HDP, bool CAUSAL, int NQ>
-__global__ void __launch_bounds__(256, 2) k_attn_fwd(AttnP p) {
-    constexpr int RB = Geo<HDP>::RB, KS = Geo<HDP>::KSTEPS, DT = Geo<HDP>::DT;
-    constexpr int TILE = 64 * RB;
-    // HDP 96 holds hd <= 80 (SigLIP: 72): the QK^T products take two 32-deep MFMA steps and
-    // one 16-deep step (v_mfma_f32_16x16x16_bf16) over dims [64, 80) instead of a third
-    // 32-deep step over zero padding
-    constexpr bool HALF = HDP == 96;
-    constexpr int KSF = HALF ? KS - 1 : KS;
-    constexpr int QBLK = 64 * NQ;   // query rows per workgroup
-    extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][K TILE | V TILE]
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int g = lane >> 4, li = lane & 15;
-    const int nqb = (p.S + QBLK - 1) / QBLK;
-    // grid (H, B, query blocks): every head's longest causal block is dispatched first, the
-    // shortest fill the tail
-    int h, b, zb;
-    gqa_xcd_map(p.H, p.HKV, p.B, h, b, zb);
-    const int qb = CAUSAL ? (nqb - 1 - zb) : zb;
-    const int kvh = h / (p.H / p.HKV);
-    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
-    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    int myq[NQ];
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) myq[j] = qb * QBLK + wid * 16 * NQ + j * 16 + li;
-
-    bf16x8 qf[NQ][KS];
-    bf16x4 qh[NQ];
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) {
-#pragma unroll
-        for (int kk = 0; kk < KSF; ++kk) {
-            if (myq[j] < p.S) qf[j][kk] = *(const bf16x8*)(Q + (int64_t)myq[j] * HDP + kk * 32 + 8 * g);
-            else qf[j][kk] = (bf16x8){};
-        }
-        if (HALF) qh[j] = myq[j] < p.S ? *(const bf16x4*)(Q + (int64_t)myq[j] * HDP + KSF * 32 + 4 * g) : (bf16x4){};
-    }
-    f32x4 o[NQ][DT];
-#pragma unroll
-    for (int j = 0; j < NQ; ++j)
-#pragma unroll
-        for (int d = 0; d < DT; ++d) o[j][d] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float m[NQ], l[NQ];
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
-
-    const int nkv_all = (p.S + 63) / 64;
-    const int nkv = CAUSAL ? min((qb + 1) * QBLK / 64, nkv_all) : nkv_all;
-    stage_kv<HDP, false>(smem, K, 0, p.S, wid, lane);
-    stage_kv<HDP, true>(smem + TILE, V, 0, p.S, wid, lane);
-    // per-lane LDS byte offsets of the fragment reads: the swizzles depend on the lane only,
-    // so the buffer, the key tile kt and the 32-key step ks are immediate offsets of the
-    // ds_read instructions in the tile loop (unrolled by two: even tiles read buffer 0)
-    int koff[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) koff[kk] = li * RB + (((kk * 4 + g) ^ swK<RB>(li)) << 4);
-    // the 16-deep step's A fragment: row li, dims 32 KSF + 4g + [0, 4) = 8 B of chunk 4 KSF + g/2
-    const int khoff = li * RB + (((KSF * 4 + (g >> 1)) ^ swK<RB>(li)) << 4) + (g & 1) * 8;
-    uint32_t vaddr[DT];
-    {
-        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-        const int r = 4 * g + (li >> 2);
-#pragma unroll
-        for (int d = 0; d < DT; ++d) {
-            const int dc = d * 16 + 4 * (li & 3);
-            vaddr[d] = sbase + TILE + r * RB + ((((dc >> 3) ^ swV<RB>(r))) << 4) + ((dc & 4) << 1);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    auto tile = [&](const int t, auto buf_c) {
-        constexpr int BUF = decltype(buf_c)::value;
-        if (t + 1 < nkv) {
-            char* nb = smem + (BUF ^ 1) * 2 * TILE;
-            stage_kv<HDP, false>(nb, K, (t + 1) * 64, p.S, wid, lane);
-            stage_kv<HDP, true>(nb + TILE, V, (t + 1) * 64, p.S, wid, lane);
-        }
-        const char* kt_l = smem + BUF * 2 * TILE;
-        // ---- S^T tiles: rows = keys 16kt + 4g + r, col = the lane's query of sub-tile j
-        f32x4 sc[NQ][4];
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) sc[j][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int kk = 0; kk < KSF; ++kk) {
-                const bf16x8 kf = *(const bf16x8*)(kt_l + koff[kk] + kt * 16 * RB);
-#pragma unroll
-                for (int j = 0; j < NQ; ++j)
-                    sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[j][kk], sc[j][kt], 0, 0, 0);
-            }
-            if (HALF) {
-                const bf16x4 kh = *(const bf16x4*)(kt_l + khoff + kt * 16 * RB);
-#pragma unroll
-                for (int j = 0; j < NQ; ++j)
-                    sc[j][kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kh, qh[j], sc[j][kt], 0, 0, 0);
-            }
-        }
-        // ---- online softmax in the log2 domain. The mask is applied only on tiles that
-        // cross the causal diagonal or the sequence end (wave-uniform test); the scale is
-        // folded into the exponent's fma; v_exp_f32 directly (exp2f adds range handling).
-        // Lazy rescale: the exponent reference m only moves when the tile's max exceeds it
-        // by more than 8 (P <= 2^8 otherwise, exact in fp32 accumulation and bf16 range), so
-        // the O rescale (8·DT multiplies per sub-tile) runs on a few tiles per row only.
-        const int key0 = t * 64 + 4 * g;
-        bf16x8 pf[NQ][2];
-#pragma unroll
-        for (int j = 0; j < NQ; ++j) {
-            const int qlo = qb * QBLK + wid * 16 * NQ + j * 16;   // first query of this sub-tile
-            if (t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qlo)) {
-#pragma unroll
-                for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int key = key0 + 16 * kt + r;
-                        if (key >= p.S || (CAUSAL && key > myq[j])) sc[j][kt][r] = -INFINITY;
-                    }
-            }
-            float mt = -INFINITY;
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sc[j][kt][r]);
-            mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-            const float mts = mt * p.scale_log2;   // scale > 0: max commutes
-            const bool move = mts > m[j] + 8.f;   // also the first tile with a finite score (m = -inf)
-            if (__ballot(move)) {
-                const float mn = move ? mts : m[j];
-                const float alpha = __builtin_amdgcn_exp2f(m[j] - mn);   // m = -inf: 0 (O, l are 0)
-                l[j] *= alpha;
-#pragma unroll
-                for (int d = 0; d < DT; ++d) o[j][d] *= alpha;
-                m[j] = mn;
-            }
-            const float mref = (m[j] == -INFINITY) ? 0.f : m[j];
-            float ls = 0.f;
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][kt][r], p.scale_log2, -mref));
-                    sc[j][kt][r] = e;
-                    ls += e;
-                }
-            l[j] += ls;
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) { pf[j][ks][r] = (bf16)sc[j][2 * ks][r]; pf[j][ks][4 + r] = (bf16)sc[j][2 * ks + 1][r]; }
-        }
-        // ---- O^T += V^T P^T, two 32-key steps; each V^T fragment feeds the NQ sub-tiles
-        auto pv = [&](auto ks_c) {
-            constexpr int KS_ = decltype(ks_c)::value;
-            constexpr int OFF0 = BUF * 2 * TILE + (32 * KS_) * RB, OFF1 = OFF0 + 16 * RB;
-            bf16x4 v0[DT], v1[DT];
-#pragma unroll
-            for (int d = 0; d < DT; ++d) {
-                v0[d] = tr_read_off<OFF0>(vaddr[d]);
-                v1[d] = tr_read_off<OFF1>(vaddr[d]);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int d = 0; d < DT; ++d) {
-                bf16x8 vf;
-                vf[0] = v0[d][0]; vf[1] = v0[d][1]; vf[2] = v0[d][2]; vf[3] = v0[d][3];
-                vf[4] = v1[d][0]; vf[5] = v1[d][1]; vf[6] = v1[d][2]; vf[7] = v1[d][3];
-#pragma unroll
-                for (int j = 0; j < NQ; ++j) o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[j][KS_], o[j][d], 0, 0, 0);
-            }
-        };
-        pv(std::integral_constant<int, 0>{});
-        pv(std::integral_constant<int, 1>{});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    };
-    int t = 0;
-    for (; t + 1 < nkv; t += 2) {
-        tile(t, std::integral_constant<int, 0>{});
-        tile(t + 1, std::integral_constant<int, 1>{});
-    }
-    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) {
-        float lj = l[j];
-        lj += __shfl_xor(lj, 16, 64);
-        lj += __shfl_xor(lj, 32, 64);
-        if (myq[j] < p.S) {
-            const float inv = 1.f / lj;
-            bf16* orow = p.o + (((int64_t)b * p.S + myq[j]) * p.H + h) * p.hd;
-#pragma unroll
-            for (int d = 0; d < DT; ++d) {
-                const int dd = d * 16 + 4 * g;
-                if (dd < p.hd) {
-                    bf16x4 w;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[j][d][r] * inv);
-                    *(bf16x4*)(orow + dd) = w;
-                }
-            }
-            if (g == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq[j]] = (m[j] + log2f(lj)) * 0.6931471805599453f;
-        }
-    }
-}
-
+#include "attention_fwd16.inc"   // tools/ab/attention_fwd16.inc: the round-2 16x16x32 attention forward (forced variant 16)
 #endif  // KD_AB_BUILD
 
 // ------------------------------------------------------- forward, 32x32x16 MFMAs ----
@@ -708,491 +497,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 3) k_attn_fwd32(AttnP p
 }
 
 #ifdef KD_AB_BUILD   // k_attn_fwd64 / k_attn_fwd32p: measured slower; A/B library only
-// k_attn_fwd64: k_attn_fwd32's arithmetic with TWO 32-row query blocks per wave (workgroup = 4 waves
-// x 64 rows = 256 query rows), one wave per SIMD (up to 512 registers: O of both blocks, 2 x ND x 16,
-// beside their scores). Every K fragment (ds_read_b128) and every V^T fragment (ds_read_b64_tr_b16)
-// read from LDS feeds both blocks' MFMAs, so LDS reads and their issue slots per MFMA halve -- at one
-// block per wave a tile's ~4.5 softmax VALU + 1.5 LDS reads per MFMA exceed the ~5 fillers a 32x32x16
-// MFMA gap hides (MI355X_MICROARCH constants). Per query row the operations and their order are
-// k_attn_fwd32's (same max, lazy rescale, exps, sum chains, PV MFMA order), so O and lse are
-// bit-identical to it. Causal: a wave's two blocks end on the same 64-key tile (its first row is a
-// multiple of 64), so neither computes a tile the other skips. Forced variant 64 (KD_ATTN_FWD_V=64).
-template <int HDP, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) k_attn_fwd64(AttnP p) {
-    constexpr int QB = 256;
-    constexpr int RB = Geo<HDP>::RB;
-    constexpr int TILE = 64 * RB;
-    constexpr int KS = HDP == 96 ? 5 : HDP / 16;
-    constexpr int ND = HDP == 64 ? 2 : (HDP == 96 ? 3 : 4);
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int r32 = lane & 31, hf = lane >> 5;
-    const int nqb = (p.S + QB - 1) / QB;
-    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
-    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
-    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
-    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const int q0 = qb * QB + wid * 64;   // block j: rows q0 + 32 j + [0, 32)
-    bf16x8 qf[2][KS];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int myq = q0 + 32 * j + r32;
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk)
-            qf[j][kk] = myq < p.S ? *(const bf16x8*)(Q + (int64_t)myq * HDP + kk * 16 + 8 * hf) : (bf16x8){};
-    }
-    f32x16 o[2][ND];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int d = 0; d < ND; ++d)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o[j][d][i] = 0.f;
-    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-    const int nkv_all = (p.S + 63) / 64;
-    const int nkv = CAUSAL ? min(((qb + 1) * QB + 63) / 64, nkv_all) : nkv_all;
-    const int nkv_w = CAUSAL ? min(nkv, (q0 + 63) / 64 + 1) : nkv;   // both blocks: the same last tile
-    stage_kv32<HDP, false>(smem, K, 0, p.S, wid, lane);
-    stage_kv32<HDP, true>(smem + TILE, V, 0, p.S, wid, lane);
-    uint32_t koff[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-        koff[kk] = (uint32_t)(uintptr_t)smem + r32 * RB + (((2 * kk + hf) ^ swK<RB>(r32)) << 4);
-    uint32_t vaddr[ND];
-    {
-        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-        const int row = 4 * hf + ((lane >> 2) & 3);
-#pragma unroll
-        for (int d = 0; d < ND; ++d) {
-            const int col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            vaddr[d] = sbase + TILE + row * RB + ((((col >> 3) ^ swV32<RB>(row))) << 4) + ((col & 4) << 1);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    auto tile = [&](const int t, auto buf_c) {
-        constexpr int BUF = decltype(buf_c)::value;
-        if (t + 1 < nkv) {
-            char* nb = smem + (BUF ^ 1) * 2 * TILE;
-            stage_kv32<HDP, false>(nb, K, (t + 1) * 64, p.S, wid, lane);
-            stage_kv32<HDP, true>(nb + TILE, V, (t + 1) * 64, p.S, wid, lane);
-        }
-        if (t < nkv_w) {
-            f32x16 sc[2][2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) sc[j][kt][i] = 0.f;
-            // S^T = K Q^T for both blocks: each K fragment feeds two MFMAs
-            u32x4 ka[KS], kb[KS];
-#pragma unroll
-            for (int kk = 0; kk < KS; ++kk)
-                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ka[kk]) : "v"(koff[kk]), "i"(BUF * 2 * TILE));
-#pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
-                asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ka[kk]) : "i"(KS - 1) : "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                sc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ka[kk]), qf[0][kk], sc[0][0], 0, 0, 0);
-                sc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ka[kk]), qf[1][kk], sc[1][0], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kb[kk]) : "v"(koff[kk]), "i"(BUF * 2 * TILE + 32 * RB));
-            }
-#pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
-                asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(kb[kk]) : "i"(KS - 1 - kk) : "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                sc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kb[kk]), qf[0][kk], sc[0][1], 0, 0, 0);
-                sc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kb[kk]), qf[1][kk], sc[1][1], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            bf16x8 pf[2][4];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int qj = q0 + 32 * j, myq = qj + r32;
-                if (t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > qj)) {
-#pragma unroll
-                    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const int key = t * 64 + 32 * kt + 8 * (i >> 2) + 4 * hf + (i & 3);
-                            if (key >= p.S || (CAUSAL && key > myq)) sc[j][kt][i] = -INFINITY;
-                        }
-                }
-                float mt = -INFINITY;
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sc[j][kt][i]);
-                mt = half_max(mt);
-                const float mts = mt * p.scale_log2;
-                const bool move = mts > m[j] + 8.f;
-                if (__ballot(move)) {
-                    const float mn = move ? mts : m[j];
-                    const float alpha = __builtin_amdgcn_exp2f(m[j] - mn);
-                    l[j] *= alpha;
-#pragma unroll
-                    for (int d = 0; d < ND; ++d) o[j][d] *= alpha;
-                    m[j] = mn;
-                }
-                const float mref = (m[j] == -INFINITY) ? 0.f : m[j];
-                float ls[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][kt][i], p.scale_log2, -mref));
-                        sc[j][kt][i] = e;
-                        ls[i & 3] += e;
-                    }
-                l[j] += (ls[0] + ls[1]) + (ls[2] + ls[3]);
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) pf[j][s4][e] = (bf16)sc[j][s4 >> 1][8 * (s4 & 1) + e];
-            }
-            // O^T += V^T P^T for both blocks: each V^T fragment feeds two MFMAs
-            u32x2 vr[2][8];
-#define KD_F64_RD(D, SET)                                                                                        \
-    _Pragma("unroll") for (int s4 = 0; s4 < 4; ++s4) {                                                           \
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[SET][2 * s4]) : "v"(vaddr[D]), "i"(BUF * 2 * TILE + (16 * s4) * RB));     \
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[SET][2 * s4 + 1]) : "v"(vaddr[D]), "i"(BUF * 2 * TILE + (16 * s4 + 8) * RB)); \
-    }
-#define KD_F64_MM(D, SET)                                                                                        \
-    _Pragma("unroll") for (int s4 = 0; s4 < 4; ++s4) {                                                           \
-        const bf16x8 vf = cat4(__builtin_bit_cast(bf16x4, vr[SET][2 * s4]), __builtin_bit_cast(bf16x4, vr[SET][2 * s4 + 1])); \
-        o[0][D] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][s4], o[0][D], 0, 0, 0);                       \
-        o[1][D] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1][s4], o[1][D], 0, 0, 0);                       \
-    }
-#define KD_F64_WAIT(N, SET) wait_lgkm_def8<N>(vr[SET]); __builtin_amdgcn_sched_barrier(0);
-            KD_F64_RD(0, 0)
-            KD_F64_RD(1, 1)
-            KD_F64_WAIT(8, 0)
-            KD_F64_MM(0, 0)
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (ND > 2) { KD_F64_RD(2, 0) KD_F64_WAIT(8, 1) }
-            else { KD_F64_WAIT(0, 1) }
-            KD_F64_MM(1, 1)
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (ND > 2) {
-                if constexpr (ND > 3) { KD_F64_RD(3, 1) KD_F64_WAIT(8, 0) }
-                else { KD_F64_WAIT(0, 0) }
-                KD_F64_MM(2, 0)
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (ND > 3) {
-                    KD_F64_WAIT(0, 1)
-                    KD_F64_MM(3, 1)
-                }
-            }
-#undef KD_F64_RD
-#undef KD_F64_MM
-#undef KD_F64_WAIT
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    };
-    int t = 0;
-    for (; t + 1 < nkv; t += 2) {
-        tile(t, std::integral_constant<int, 0>{});
-        tile(t + 1, std::integral_constant<int, 1>{});
-    }
-    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const float lj = half_sum(l[j]);
-        const int myq = q0 + 32 * j + r32;
-        if (myq < p.S) {
-            const float inv = 1.f / lj;
-            bf16* orow = p.o + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
-#pragma unroll
-            for (int d = 0; d < ND; ++d)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int dd = 32 * d + 8 * g + 4 * hf;
-                    if (dd < p.hd) {
-                        bf16x4 w;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[j][d][4 * g + r] * inv);
-                        *(bf16x4*)(orow + dd) = w;
-                    }
-                }
-            if (hf == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq] = (m[j] + log2f(lj)) * 0.6931471805599453f;
-        }
-    }
-}
-
-// k_attn_fwd32 software-pipelined at 32-key sub-tile granularity. In k_attn_fwd32 every step
-// of a tile waits on the previous one (QK^T -> max -> exp -> PV), and with two waves per SIMD
-// the waves spent ~half their lifetime stalled on those dependencies (SQ_WAIT_INST_ANY), the
-// matrix pipe 34% busy. Here, per sub-tile u (32 keys; S(u) already computed):
-//   phase A: the QK^T MFMAs of sub-tile u+1, and between them the row max / rescale test /
-//            exps of sub-tile u and the transposed V reads of PV(u)
-//   phase B: the PV(u) MFMAs, and between them the bf16 packing of P(u), the row-sum adds and
-//            the K fragment reads of sub-tile u+2
-// Every LDS read is inline asm and every group is pinned by sched_barrier, so the instruction
-// stream is the one written here. Rule for the asm reads (the round-2 fault class): a register
-// an asm read is still filling never crosses a basic-block boundary, and the s_waitcnt that
-// retires it names it as an in/out operand, so no compiler copy of it can be placed before
-// the wait (a PHI copy at a branch merge did exactly that in a first version: wrong outputs
-// whenever a workgroup had one K/V tile). Hence the V^T reads of PV(u) are issued only after
-// phase A's rescale branch and retired at the start of phase B, and the K reads of sub-tile
-// u + 2 are retired at the end of phase B. The K image is read two
-// sub-tiles ahead: tile t+1's K must have landed while tile t is processed, so the K ring is
-// filled one tile ahead of the V ring (LDS: K slots [0, 2 TILE), V slots [2 TILE, 4 TILE)).
-// The causal per-wave skip is per sub-tile (a wave stops at its diagonal sub-tile).
-// LDS reads with an immediate offset (asm: not tracked by the compiler's lgkmcnt; the caller
-// waits). Functions, not asm in the generic lambdas below (clang rejects captured asm operands
-// there).
-template <int OFF> __device__ __forceinline__ void lds_b128(u32x4& dst, uint32_t addr) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
-}
-template <int OFF> __device__ __forceinline__ void lds_tr16(u32x2& dst, uint32_t addr) {
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
-}
-
-// s_waitcnt lgkmcnt(0) that the compiler sees as (re)defining the N registers of r: no use or
-// copy of them can be scheduled before it (asm reads are invisible to its own lgkmcnt tracking)
-template <int N, typename T> __device__ __forceinline__ void wait_lgkm0_def(T (&r)[N]) {
-    static_assert(N <= 16, "wait_lgkm0_def: at most 16 registers");
-    if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) :: "memory");
-    else if constexpr (N == 5) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) :: "memory");
-    else if constexpr (N == 8)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]) :: "memory");
-    else if constexpr (N == 12)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
-                     "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]) :: "memory");
-    else if constexpr (N == 16)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
-                     "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15]) :: "memory");
-    else static_assert(N == 4, "wait_lgkm0_def: unsupported count");
-}
-
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_(F&& f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F> __device__ __forceinline__ void static_for(F&& f) {
-    static_for_(f, std::make_integer_sequence<int, N>{});
-}
-
-template <int HDP, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2) k_attn_fwd32p(AttnP p) {
-    constexpr int RB = Geo<HDP>::RB;
-    constexpr int TILE = 64 * RB;
-    constexpr int KS = HDP == 96 ? 5 : HDP / 16;               // 16-deep QK^T steps
-    constexpr int ND = HDP == 64 ? 2 : (HDP == 96 ? 3 : 4);    // 32-dim O^T tiles
-    constexpr int NV = 4 * ND;                                 // V^T reads per sub-tile
-    constexpr int VPS = (NV + KS - 3) / (KS - 2);              // V^T reads per phase-A slot 2..KS-1
-    static_assert(KS <= 2 * ND, "phase B issues one K read per PV MFMA");
-    static_assert(NV <= 16 && KS <= 16, "at most 16 LDS reads in flight (as k_attn_fwd: issue stalls at the counter limit)");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int r32 = lane & 31, hf = lane >> 5;
-    const int nqb = (p.S + 127) / 128;
-    const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.z) : (int)blockIdx.z;
-    const int h = blockIdx.x, b = blockIdx.y, kvh = h / (p.H / p.HKV);
-    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
-    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
-    const int q0 = qb * 128 + wid * 32;
-    const int myq = q0 + r32;
-
-    bf16x8 qf[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-        qf[kk] = myq < p.S ? *(const bf16x8*)(Q + (int64_t)myq * HDP + kk * 16 + 8 * hf) : (bf16x8){};
-    f32x16 o[ND];
-#pragma unroll
-    for (int d = 0; d < ND; ++d)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
-    float m = -INFINITY, l = 0.f;
-
-    const int nkv_all = (p.S + 63) / 64;
-    const int nkv = CAUSAL ? min((qb + 1) * 2, nkv_all) : nkv_all;
-    const int nsub_all = (p.S + 31) / 32;
-    const int nsub_w = CAUSAL ? min(nsub_all, q0 / 32 + 1) : nsub_all;   // the wave's sub-tiles
-
-    const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-    uint32_t koff[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) koff[kk] = sbase + r32 * RB + (((2 * kk + hf) ^ swK<RB>(r32)) << 4);
-    uint32_t vaddr[ND];
-    {
-        const int row = 4 * hf + ((lane >> 2) & 3);
-#pragma unroll
-        for (int d = 0; d < ND; ++d) {
-            const int col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            vaddr[d] = sbase + 2 * TILE + row * RB + ((((col >> 3) ^ swV32<RB>(row))) << 4) + ((col & 4) << 1);
-        }
-    }
-    // K(0) -> K slot 0, V(0) -> V slot 0, K(1) -> K slot 1
-    stage_kv32<HDP, false>(smem, K, 0, p.S, wid, lane);
-    stage_kv32<HDP, true>(smem + 2 * TILE, V, 0, p.S, wid, lane);
-    if (nkv > 1) stage_kv32<HDP, false>(smem + TILE, K, 64, p.S, wid, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    u32x4 kf[KS];   // K fragments of the sub-tile whose QK^T runs next
-    f32x16 sc;      // S^T of the current sub-tile (raw scores, then exps)
-    auto kread = [&](auto kk_c, auto off_c) {
-        constexpr int KK = decltype(kk_c)::value, OFF = decltype(off_c)::value;
-        lds_b128<OFF>(kf[KK], koff[KK]);
-    };
-#define KD_WAIT(N) asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(N) : "memory")
-#define KD_SB __builtin_amdgcn_sched_barrier(0)
-    // prologue: S(0) from K(0) rows 0-31, then the reads of K(0) rows 32-63 (sub-tile 1)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sc[i] = 0.f;
-    static_for<KS>([&](auto kk_c) { kread(kk_c, std::integral_constant<int, 0>{}); });
-    KD_WAIT(0);
-    KD_SB;
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[kk]), qf[kk], sc, 0, 0, 0);
-    KD_SB;
-    static_for<KS>([&](auto kk_c) { kread(kk_c, std::integral_constant<int, 32 * RB>{}); });
-    wait_lgkm0_def<KS>(kf);
-    __syncthreads();   // every wave's K(0) reads are done before K(2) overwrites slot 0
-
-    // one 32-key sub-tile u = 2t + H2: V(t) in V slot BUF; its successor's K fragments are in
-    // kf (in flight); the K of sub-tile u + 2 is K(t+1) in slot BUF ^ 1
-    auto sub = [&](const int u, auto buf_c, auto h2_c) {
-        constexpr int BUF = decltype(buf_c)::value, H2 = decltype(h2_c)::value;
-        constexpr int VOFF = BUF * TILE + H2 * 32 * RB;
-        constexpr int KNEXT = (BUF ^ 1) * TILE + H2 * 32 * RB;
-        f32x16 sn;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sn[i] = 0.f;
-        u32x2 vr[NV];   // read vi: k-step vi / (2 ND), dims tile (vi / 2) % ND, key half vi & 1
-        auto vread = [&](auto vi_c) {
-            constexpr int VI = decltype(vi_c)::value;
-            constexpr int S_ = VI / (2 * ND), D_ = (VI / 2) % ND, HS = VI & 1;
-            lds_tr16<VOFF + (16 * S_ + 8 * HS) * RB>(vr[VI], vaddr[D_]);
-        };
-        const bool diag = (32 * u + 31 >= p.S) || (CAUSAL && 32 * u + 31 > q0);
-        float mt = -INFINITY, mref = 0.f;
-        float ls[4] = {0.f, 0.f, 0.f, 0.f};
-        // ---- phase A: QK^T(u+1) || V^T reads of PV(u) || max, rescale, exps of S(u)
-        static_for<KS>([&](auto kk_c) {
-            constexpr int KKc = decltype(kk_c)::value;
-            KD_SB;
-            // pin the MFMA between this slot's wait and the next slot (the DAG scheduler otherwise
-            // sinks all but the first two to the end of phase A): its operand passes through an
-            // empty volatile asm here, and its result through one at the end of the slot
-            asm volatile("" : "+v"(kf[KKc]));
-            sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[KKc]), qf[KKc], sn, 0, 0, 0);
-            KD_SB;
-            static_for<VPS>([&](auto j_c) {
-                constexpr int VI = VPS * (KKc - 2) + decltype(j_c)::value;
-                if constexpr (KKc >= 2 && VI < NV) vread(std::integral_constant<int, VI>{});
-            });
-            if constexpr (KKc == 0) {
-                if (diag) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int key = 32 * u + 8 * (i >> 2) + 4 * hf + (i & 3);
-                        if (key >= p.S || (CAUSAL && key > myq)) sc[i] = -INFINITY;
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 8; ++i) mt = fmaxf(mt, sc[i]);
-            } else if constexpr (KKc == 1) {
-#pragma unroll
-                for (int i = 8; i < 16; ++i) mt = fmaxf(mt, sc[i]);
-                mt = half_max(mt);
-                // lazy rescale (k_attn_fwd): the reference max moves only by more than 8
-                const float mts = mt * p.scale_log2;
-                const bool move = mts > m + 8.f;
-                if (__ballot(move)) {
-                    const float mn = move ? mts : m;
-                    const float alpha = __builtin_amdgcn_exp2f(m - mn);
-                    l *= alpha;
-#pragma unroll
-                    for (int d = 0; d < ND; ++d) o[d] *= alpha;
-                    m = mn;
-                }
-                mref = (m == -INFINITY) ? 0.f : m;
-            } else {
-                constexpr int E0 = (KKc - 2) * 16 / (KS - 2), E1 = (KKc - 1) * 16 / (KS - 2);
-#pragma unroll
-                for (int i = E0; i < E1; ++i) {
-                    const float e = __builtin_amdgcn_exp2f(fmaf(sc[i], p.scale_log2, -mref));
-                    sc[i] = e;
-                    ls[i & 3] += e;
-                }
-            }
-            KD_SB;
-            asm volatile("" :: "v"(sn));
-        });
-        // ---- phase B: PV(u) || P(u) packing, row sums, K reads of sub-tile u + 2
-        KD_SB;
-        wait_lgkm0_def<NV>(vr);
-        KD_SB;
-        bf16x8 pf[2];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[0][j] = (bf16)sc[j];
-        static_for<2 * ND>([&](auto j_c) {
-            constexpr int J = decltype(j_c)::value, S_ = J / ND, D_ = J % ND;
-            KD_SB;
-            const bf16x8 vf = cat4(__builtin_bit_cast(bf16x4, vr[2 * J]), __builtin_bit_cast(bf16x4, vr[2 * J + 1]));
-            o[D_] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[S_], o[D_], 0, 0, 0);
-            KD_SB;
-            if constexpr (J < KS) kread(std::integral_constant<int, J>{}, std::integral_constant<int, KNEXT>{});
-            if constexpr (J == 0) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pf[1][j] = (bf16)sc[8 + j];
-            }
-            if constexpr (J == 1) l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
-        });
-        KD_SB;
-        wait_lgkm0_def<KS>(kf);
-        KD_SB;
-        sc = sn;
-    };
-    auto tile = [&](const int t, auto buf_c) {
-        constexpr int BUF = decltype(buf_c)::value;
-        // K(t+2) -> K slot BUF (K(t) was last read in tile t-1), V(t+1) -> V slot BUF ^ 1
-        if (t + 2 < nkv) stage_kv32<HDP, false>(smem + BUF * TILE, K, (t + 2) * 64, p.S, wid, lane);
-        if (t + 1 < nkv) stage_kv32<HDP, true>(smem + 2 * TILE + (BUF ^ 1) * TILE, V, (t + 1) * 64, p.S, wid, lane);
-        if (2 * t < nsub_w) sub(2 * t, buf_c, std::integral_constant<int, 0>{});
-        if (2 * t + 1 < nsub_w) sub(2 * t + 1, buf_c, std::integral_constant<int, 1>{});
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __syncthreads();
-    };
-#undef KD_WAIT
-#undef KD_SB
-    int t = 0;
-    for (; t + 1 < nkv; t += 2) {
-        tile(t, std::integral_constant<int, 0>{});
-        tile(t + 1, std::integral_constant<int, 1>{});
-    }
-    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
-    l = half_sum(l);
-    if (myq < p.S) {
-        const float inv = 1.f / l;
-        bf16* orow = p.o + (((int64_t)b * p.S + myq) * p.H + h) * p.hd;
-#pragma unroll
-        for (int d = 0; d < ND; ++d)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int dd = 32 * d + 8 * g + 4 * hf;
-                if (dd < p.hd) {
-                    bf16x4 w;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[d][4 * g + r] * inv);
-                    *(bf16x4*)(orow + dd) = w;
-                }
-            }
-        if (hf == 0 && p.lse) p.lse[((int64_t)b * p.H + h) * p.S + myq] = (m + log2f(l)) * 0.6931471805599453f;
-    }
-}
-
+#include "attention_fwd64_fwd32p.inc"   // tools/ab/attention_fwd64_fwd32p.inc: k_attn_fwd64 / k_attn_fwd32p and the other forward / backward A/B variants
 #endif  // KD_AB_BUILD
 
 // ------------------------------------------------------------------ backward ----

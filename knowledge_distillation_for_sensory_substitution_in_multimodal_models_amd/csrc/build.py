@@ -37,16 +37,19 @@ def _sources():
     return sorted(HERE.glob("*.hip"))
 
 
-def _deps_mtime():
+def _deps_mtime(ab: bool = False):
     hdrs = list(HERE.glob("*.h")) + list((REPO / "include").glob("*.h")) + [Path(__file__)]
+    if ab:
+        hdrs += list(AB_LIB.parent.glob("*.inc"))
     return max(p.stat().st_mtime for p in hdrs)
 
 
 def _compile(src: Path, ab: bool = False) -> Path:
     obj = (AB_OBJ_DIR if ab else OBJ_DIR) / (src.stem + ".o")
-    if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, _deps_mtime()):
+    if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, _deps_mtime(ab)):
         return obj
-    cmd = [HIPCC, *CFLAGS, *(["-DKD_AB_BUILD"] if ab else []), "-c", str(src), "-o", str(obj)]
+    # the A/B-only kernel bodies live in tools/ab/*.inc, included inside the sources' KD_AB_BUILD blocks
+    cmd = [HIPCC, *CFLAGS, *(["-DKD_AB_BUILD", f"-I{AB_LIB.parent}"] if ab else []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")

@@ -63,13 +63,17 @@ struct GemmP {
     float* rst;
     int rst_nt, rst_vs, rst_top2;
     float rst_inv_t;
-    // stream-K (v8): the launch's sk_grid workgroups split the tiles' sk_steps-deep K loops
-    // evenly (one workgroup's run may cover the end of one tile and the start of the next);
-    // a tile covered by several workgroups gets fp32 partial planes in sk_ws (plane stride
-    // split_stride, plane = the workgroup's piece index in that tile), folded by
-    // k_splitk_reduce. 0 = off.
+    // stream-K (v8, variant 21, round 6): the first sk_dp linear tiles (whole waves) run as plain
+    // data-parallel tiles, then the launch's sk_grid workgroups split the remaining tiles'
+    // sk_steps-deep K loops evenly (one workgroup's run may cover the end of one tile and the start
+    // of the next).  A tile covered by several runs is folded INSIDE the launch: every piece stores
+    // its fp32 accumulators (fragment-native layout) to its run's slot in sk_ws, then takes a ticket
+    // from sk_cnt[tile]; the last arriver sums the pieces in piece order and runs the full epilogue
+    // (no fold launch, no partial-plane round trip for the last piece).  0 = off.
     int sk_steps, sk_grid;
     float* sk_ws;
+    int sk_dp;
+    int* sk_cnt;
     int gm;                // tile rows per group of the grouped tile order (0: GM_GROUP)
     // k-loop start stagger (v8, K % 32 == 0, K >= 2048): the tiles of row group j of ngrp start
     // their K loop at stage j * nk / ngrp and wrap, so the XCDs (each a chunk of one group) stream
@@ -964,45 +968,7 @@ __device__ __forceinline__ void epilogue_glu(const GemmP& p, const f32x4 (&acc)[
     if (ST) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); mk[1] = __builtin_amdgcn_s_memtime(); }
 }
 #ifdef KD_AB_BUILD
-
-// the round-4 SwiGLU epilogue before the packed rewrite (EXP bit 512 / KD_GLU_EPI_V0=1: A/B only)
-template <int TM, int TN, int MT, int NT, int NTHR, bool L32 = false>
-__device__ __forceinline__ void epilogue_glu_v0(const GemmP& p, const f32x4 (&acc)[MT][NT], char* smem, int m0, int nb, int wm,
-                                             int wn, int lane, int tid) {
-    float alpha = p.alpha;
-    if (p.alpha_dev) alpha *= *p.alpha_dev;
-    f32x4 bcol[NT];
-#pragma unroll
-    for (int j = 0; j < NT; ++j) bcol[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    constexpr int RS = 256 * 2 + 16;
-    epi_to_lds<KD_ACT_NONE, TM, TN, MT, NT, false, L32>(acc, smem, RS, alpha, bcol, wm, wn, lane, 0, 256);
-    __syncthreads();
-    const int I = p.glu;
-    const bool full = m0 + 256 <= p.M;
-    if (p.aux) {
-#pragma unroll 4
-        for (int idx = tid; idx < 256 * 32; idx += NTHR) {
-            const int lr = idx >> 5, c = idx & 31, row = m0 + lr;
-            if (!full && row >= p.M) continue;
-            const int col = c < 16 ? nb + c * 8 : I + nb + (c - 16) * 8;
-            *(bf16x8*)(p.aux + (int64_t)row * p.ld_aux + col) = *(const bf16x8*)(smem + lr * RS + c * 16);
-        }
-    }
-#pragma unroll 4
-    for (int idx = tid; idx < 256 * 16; idx += NTHR) {
-        const int lr = idx >> 4, c = idx & 15, row = m0 + lr;
-        if (!full && row >= p.M) continue;
-        const bf16x8 g = *(const bf16x8*)(smem + lr * RS + c * 16);
-        const bf16x8 u = *(const bf16x8*)(smem + lr * RS + 256 + c * 16);
-        bf16x8 o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float gf = (float)g[e];
-            o[e] = (bf16)(silu_fast(gf) * (float)u[e]);
-        }
-        *(bf16x8*)((bf16*)p.C + (int64_t)row * p.ldc + nb + c * 8) = o;
-    }
-}
+#include "gemm_glu_epi_v0.inc"   // tools/ab/gemm_glu_epi_v0.inc: the round-4 SwiGLU epilogue (KD_GLU_EPI_V0)
 #endif  // KD_AB_BUILD
 
 // =============================================================================
@@ -1185,8 +1151,82 @@ __device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, i
 // forward shape of the step (gate|up+SwiGLU 1291 -> 1379 us, lm_head 5320 -> 5808 us): the DMA
 // issue is not what holds v8 below hipBLASLt's MFMA-busy fraction. Kept as a forced variant only.
 // one 256x256 output tile over p's K range (the whole K, a split-K plane or a stream-K piece)
+// the in-launch fold of a stream-K tile shared by several runs (GemmP.sk_*): piece `piece` of `np`
+// of SK tile `t` (first k-step tb of the SK range's tot steps over G runs; run wf holds piece 0)
+struct SkFold {
+    float* part; int* cnt;
+    int64_t tot, tb;
+    int G, wf, piece, np, t;
+};
+constexpr int SK_TILE_F32 = 256 * 256;   // one partial tile: 4 waves x 64 accumulator quads x 64 lanes x 4
+// a run's partial slots: 0 = its first piece (its range starts inside that tile), 1 = its last
+__device__ __forceinline__ float* sk_slot(const SkFold& f, int w) {
+    const int64_t s0 = f.tot * w / f.G;
+    return f.part + ((int64_t)w * 2 + (s0 >= f.tb ? 0 : 1)) * SK_TILE_F32;
+}
+// after a piece's main loop: publish its accumulators, take the tile's ticket; the last arriver
+// folds every piece in piece order (x0 + x1 + ...: the same sum whichever piece arrives last) into
+// acc and returns true (it then runs the epilogue), the others return false.  Guideline 16 counter
+// form: plain 16-B stores, every wave drains, barrier, one lane's agent-scope release + ticket;
+// the last arriver's agent-scope acquire before any wave reads another piece.
+__device__ __forceinline__ bool sk_fold_tile(const SkFold& f, f32x4 (&acc)[8][8], int tid, int lane, int wid,
+                                          char* smem) {
+    const int64_t lo = ((int64_t)wid * 64 * 64 + lane) * 4;   // + a * 256: quad a of this lane
+    float* mine = sk_slot(f, f.wf + f.piece) + lo;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *(f32x4*)(mine + (i * 8 + j) * 256) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;   // the staging array (the one __shared__ object): free after the loop
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(f.cnt + f.t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == f.np - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        flag[0] = last;
+    }
+    __syncthreads();
+    const int last = flag[0];
+    __syncthreads();   // the epilogue restages through the same LDS
+    if (!last) return false;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {   // 16 quads at a time: 64 VGPRs of loads in flight
+        f32x4 v[16];
+        if (f.piece == 0) {
+#pragma unroll
+            for (int a = 0; a < 16; ++a) v[a] = acc[(h * 16 + a) / 8][(h * 16 + a) % 8];
+        } else {
+            const float* src = sk_slot(f, f.wf) + lo;
+#pragma unroll
+            for (int a = 0; a < 16; ++a) v[a] = *(const f32x4*)(src + (h * 16 + a) * 256);
+        }
+        for (int pc = 1; pc < f.np; ++pc) {
+            if (pc == f.piece) {
+#pragma unroll
+                for (int a = 0; a < 16; ++a) v[a] += acc[(h * 16 + a) / 8][(h * 16 + a) % 8];
+            } else {
+                const float* src = sk_slot(f, f.wf + pc) + lo;
+                f32x4 x[16];
+#pragma unroll
+                for (int a = 0; a < 16; ++a) x[a] = *(const f32x4*)(src + (h * 16 + a) * 256);
+#pragma unroll
+                for (int a = 0; a < 16; ++a) v[a] += x[a];
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 16; ++a) acc[(h * 16 + a) / 8][(h * 16 + a) % 8] = v[a];
+    }
+    return true;
+}
+
 template <bool A_MN, bool B_MN, int EXP>
-__device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
+__device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem, const SkFold* fold = nullptr) {
     constexpr bool STAMP = EXP & 1, NODMA = EXP & 2, HOT = EXP & 64;
     constexpr bool RS = (EXP & 8) && !A_MN && !B_MN;
     // bit 5: the epilogue also writes the tile's row statistics (kd_gemm_desc.row_stats, the
@@ -1421,6 +1461,9 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
     uint64_t te0 = 0;
     if (STAMP) { te0 = __builtin_amdgcn_s_memtime(); s_units += te0 - tprev; }
     __syncthreads();
+    if constexpr ((EXP & 1024) != 0) {   // stream-K build: a published piece ends here
+        if (fold != nullptr && !sk_fold_tile(*fold, acc, tid, lane, wid, smem)) return;
+    }
 #ifdef KD_AB_BUILD
     if constexpr (!A_MN && !B_MN && (EXP & 512)) epilogue_glu_v0<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
     else
@@ -1451,576 +1494,53 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem) {
 }
 
 #ifdef KD_AB_BUILD   // v8n: no faster than the plan in the step; A/B library only
-// =============================================================================
-// v8n: v8's arithmetic on a 256x128 tile at TWO workgroups per CU (round 5).  Four waves, each
-// 128 rows x 64 columns = 8x4 MFMA 16x16x32 tiles whose 128 accumulators stay in AGPRs (asm
-// MFMA, as v8), so a wave fits in half a SIMD's register file and a second workgroup is resident
-// beside the first: while one workgroup runs its prologue or its epilogue (on a K = 1152 tile of
-// v8 a quarter of the time, stamps), the other keeps the matrix pipe busy, and the half-size tile
-// halves the wave-quantisation loss of the sub-wave GEMMs (SigLIP, the student).  A 3-slot BK = 32
-// LDS-DMA ring (24 KB a slot: A 16 pieces, B 8 pieces of 1 KiB; 72 KB a workgroup with the
-// epilogue staging inside it): step t reads the fragments of stage t+1 and issues the DMA of
-// stage t+3 into the slot of stage t (its fragments are in registers since step t-1, every wave
-// past that step's barrier); the step ends with lgkmcnt(0), vmcnt(6) [stage t+2 landed: only
-// stage t+3's six pieces may be younger] and s_barrier.  Per step and wave: 32 MFMAs, 6 DMAs,
-// 12 fragment reads.  The same k32 MFMA sequence per output element as v8, the same k-loop
-// stagger (a function of the tile row), so C is v8's bit for bit.  K-major A and B, no q|k|v
-// scatter / SwiGLU / row statistics / pre-tiled B (the launcher routes those to v8).
-// =============================================================================
-constexpr int NS8N = 3;
-__device__ __forceinline__ void g8n_tile(GemmP p, int tm, int tn, char* smem) {
-    constexpr int SA = 256 * BK2 * 2, SB = 128 * BK2 * 2, SS = SA + SB;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 1, wn = wid & 1;
-    const int m0 = tm * 256, n0 = tn * 128;
-    const int K = p.K;
-    const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
-    int rot = 0;
-    if (p.stagger && nk_full == nk && nk >= 64) {
-        const int g = p.stag_g > 0 ? p.stag_g : (p.gm > 0 ? p.gm : GM_GROUP), ngrp = ((p.M + 255) / 256 + g - 1) / g;
-        rot = (int)(((int64_t)(tm / g) * nk) / ngrp);
-    }
-    auto kst = [&](int st) { return (rot == 0 || st >= nk) ? st : (st + rot >= nk ? st + rot - nk : st + rot); };
-    const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
-    const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(128, p.N - n0), p.ldb));
-    uint32_t va[4], vb[2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) va[u] = voff8<false>(wid * 4 + u, lane, p.lda, m0, p.M);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) vb[u] = voff8<false>(wid * 2 + u, lane, p.ldb, n0, p.N);
-    // DMA instruction u (0..3: A piece wid*4+u, 4..5: B piece wid*2+u-4) of stage st into slot sl
-    auto dma = [&](int st, int sl, int u, auto full_tag) {
-        constexpr bool FULL = decltype(full_tag)::value;
-        const bool isA = u < 4;
-        const int i = isA ? wid * 4 + u : wid * 2 + (u - 4);
-        char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
-        uint32_t v = isA ? va[u] : vb[u - 4];
-        int soff = kst(st) * BK2 * 2;
-        if (!FULL) {
-            const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
-            if (kleft < BK2) {
-                const int row = 16 * i + (lane >> 2);
-                const int gc = (lane & 3) ^ f4(row);
-                if (gc * 8 >= kleft) v = OOB;
-                if (kleft <= 0) soff = 0;
-            }
-        }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsB, (lds_void_t*)dst, 16, v, soff, 0, 0);
-    };
-    using FullT = std::integral_constant<bool, true>;
-    using PartT = std::integral_constant<bool, false>;
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int ra = wm * 128, cb = wn * 64;
-#pragma unroll
-    for (int st = 0; st < NS8N; ++st)
-#pragma unroll
-        for (int u = 0; u < 6; ++u) dma(st, st, u, PartT{});
-    wait_vm<12>();   // stage 0 landed (stages 1, 2 may stay in flight)
-    __builtin_amdgcn_s_barrier();
-    bf16x8 xa[8], xb[4], ya[8], yb[4];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) xa[u] = frag2<256, false>(smem, ra + u * 16, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) xb[j] = frag2<128, false>(smem + SA, cb + j * 16, lane);
-#define KD_G8N_SYNC()                                      \
-    {                                                      \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-        wait_vm<6>();                                      \
-        __builtin_amdgcn_s_barrier();                      \
-    }
-    KD_G8N_SYNC()
-    __builtin_amdgcn_sched_barrier(0);
-#define KD_SB __builtin_amdgcn_sched_barrier(0);
-    // unit u: the 4 MFMAs of A fragment u; DMA u (u < 6); next-stage fragment reads: units 0-3 two
-    // A fragments each, units 4-5 two B fragments each
-#define KD_G8N_STEP(SL, CA, CB, NA, NB, FT)                                                                  \
-    {                                                                                                         \
-        const int t_ = t + (SL);                                                                              \
-        const char* na_ = smem + (((SL) + 1) % NS8N) * SS;                                                    \
-        _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
-            mfma_agpr(acc[u][0], CB[0], CA[u]); KD_SB                                                         \
-            if (u < 6) dma(t_ + NS8N, (SL), u, FT{});                                                         \
-            KD_SB                                                                                             \
-            mfma_agpr(acc[u][1], CB[1], CA[u]); KD_SB                                                         \
-            if (u < 4) NA[2 * u] = frag2<256, false>(na_, ra + 2 * u * 16, lane);                             \
-            else if (u < 6) NB[2 * (u - 4)] = frag2<128, false>(na_ + SA, cb + 2 * (u - 4) * 16, lane);       \
-            KD_SB                                                                                             \
-            mfma_agpr(acc[u][2], CB[2], CA[u]); KD_SB                                                         \
-            if (u < 4) NA[2 * u + 1] = frag2<256, false>(na_, ra + (2 * u + 1) * 16, lane);                   \
-            else if (u < 6) NB[2 * (u - 4) + 1] = frag2<128, false>(na_ + SA, cb + (2 * (u - 4) + 1) * 16, lane); \
-            if (u == 7) KD_G8N_SYNC()                                                                         \
-            KD_SB                                                                                             \
-            if (u == 7) mfma_agpr_last(acc[u][3], CB[3], CA[u], t_ + 1 == nk);                                \
-            else mfma_agpr(acc[u][3], CB[3], CA[u]);                                                          \
-            KD_SB                                                                                             \
-        }                                                                                                     \
-    }
-    // six steps per iteration: every slot index (t % 3) and fragment set (t % 2) is a constant
-    int t = 0;
-    for (; t + 6 + NS8N <= nk_full; t += 6) {   // every DMA of these steps lies inside K
-        KD_G8N_STEP(0, xa, xb, ya, yb, FullT)
-        KD_G8N_STEP(1, ya, yb, xa, xb, FullT)
-        KD_G8N_STEP(2, xa, xb, ya, yb, FullT)
-        t += 3;
-        KD_G8N_STEP(0, ya, yb, xa, xb, FullT)
-        KD_G8N_STEP(1, xa, xb, ya, yb, FullT)
-        KD_G8N_STEP(2, ya, yb, xa, xb, FullT)
-        t -= 3;
-    }
-    for (; t + 6 <= nk; t += 6) {
-        KD_G8N_STEP(0, xa, xb, ya, yb, PartT)
-        KD_G8N_STEP(1, ya, yb, xa, xb, PartT)
-        KD_G8N_STEP(2, xa, xb, ya, yb, PartT)
-        t += 3;
-        KD_G8N_STEP(0, ya, yb, xa, xb, PartT)
-        KD_G8N_STEP(1, xa, xb, ya, yb, PartT)
-        KD_G8N_STEP(2, ya, yb, xa, xb, PartT)
-        t -= 3;
-    }
-    const int rem = nk - t;
-    if (rem > 0) KD_G8N_STEP(0, xa, xb, ya, yb, PartT)
-    if (rem > 1) KD_G8N_STEP(1, ya, yb, xa, xb, PartT)
-    if (rem > 2) KD_G8N_STEP(2, xa, xb, ya, yb, PartT)
-    if (rem > 3) { t += 3; KD_G8N_STEP(0, ya, yb, xa, xb, PartT) t -= 3; }
-    if (rem > 4) { t += 3; KD_G8N_STEP(1, xa, xb, ya, yb, PartT) t -= 3; }
-#undef KD_G8N_STEP
-#undef KD_G8N_SYNC
-#undef KD_SB
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    epilogue2<256, 128, 2, 2, 128, 64, 8, 4, NTH8, true, false>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-}
-
-template <int EXP = 0>
-__global__ void __launch_bounds__(NTH8, 2) k_gemm8n(GemmP p_) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    GemmP p = p_;
-    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += k0;
-        p.B += k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
-    int tm, tn;
-    tile_of(p.gx, (p.M + 255) / 256, (p.N + 127) / 128, tm, tn, p.tile0, p.gm);
-    g8n_tile(p, tm, tn, smem);
-}
+#include "gemm_v8n.inc"   // tools/ab/gemm_v8n.inc: v8n (256x128 tiles, two workgroups per CU, forced variant 30)
 #endif  // KD_AB_BUILD
 
 #ifdef KD_AB_BUILD   // v11 / v12: measured slower than v8 in the step; tools' A/B library only
-// =============================================================================
-// v11: v8's tile, ring, DMA and barriers (256x256, four waves of 128x128, the 4-slot BK = 32
-// LDS-DMA ring, three stages in flight) on 32x32x16 MFMAs, K-major x K-major operands (every
-// forward GEMM of the step).  Why: with one wave per SIMD a 16x16x32 MFMA holds the SIMD's
-// vector issue for 8 of its 16 cycles, so a k-step's 64 MFMAs leave 512 issue cycles for its
-// 8 LDS-DMA pieces (~60 cycles each among MFMAs) and 16 fragment reads, and v8's step measures
-// ~1,240 cycles against 1,024 of MFMA; a 32x32x16 MFMA holds issue for 8 of its 32 cycles, so
-// the same step (32 MFMAs of 32 cycles) has 768 free issue cycles.  Per step and wave: 8 units
-// of 4 MFMAs (unit q: k-half h = q >> 2, row block bi = q & 3, column blocks 0..3), each unit
-// carrying one DMA piece of stage t+4 and two fragment reads of stage t+1 (A block q >> 1,
-// k-half q & 1, and the same for B).  Fragments: lane l reads row (l & 31), 16-B chunk
-// 2h + (l >> 5) of the [rows][32 k] image (v8's swizzle f4 is conflict-free for this read:
-// every 16-lane ds_read_b128 group covers the 16 (row & 3, chunk) slots once).  Accumulators:
-// f32x16 [4][4] in AGPRs (C^T blocks), viewed as f32x4 [4][16] by the L32 epilogue.
-// =============================================================================
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-
-__device__ __forceinline__ void mfma32_agpr(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-
-// the tile's last MFMA with its result-latency drain in the same asm statement (mfma_agpr_last;
-// 64 wait states >= the 32x32x16's 16-pass latency with margin)
-__device__ __forceinline__ void mfma32_agpr_last(f32x16& acc, const bf16x8& a, const bf16x8& b, int last) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0\n\t"
-                 "s_cmp_eq_u32 %3, 0\n\t"
-                 "s_cbranch_scc1 .Lkd_mfma32_nodrain%=\n\t"
-                 "s_nop 15\n\t"
-                 "s_nop 15\n\t"
-                 "s_nop 15\n\t"
-                 "s_nop 15\n"
-                 ".Lkd_mfma32_nodrain%=:"
-                 : "+a"(acc) : "v"(a), "v"(b), "s"(__builtin_amdgcn_readfirstlane(last)) : "scc");
-}
-
-// 32x32x16 operand fragment (K-major [rows][32 k] stage image): rows rb..rb+31, k-half h
-__device__ __forceinline__ bf16x8 frag32(const char* tile, int rb, int h, int lane) {
-    const int r = rb + (lane & 31);
-    const int c = 2 * h + (lane >> 5);
-    return *(const bf16x8*)(tile + r * 64 + ((c ^ f4(r)) << 4));
-}
-
-// EXP bits as v8: 4 = the fused SwiGLU build, 32 = the lm_head row-statistics build
-template <int EXP>
-__device__ __forceinline__ void g11_tile(GemmP p, int tm, int tn, char* smem) {
-    constexpr bool RSTATS = EXP & 32;
-    constexpr bool glu = EXP & 4;
-    constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 1, wn = wid & 1;
-    const int m0 = tm * 256, n0 = tn * 256;
-    const int K = p.K;
-    const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
-    const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
-    const int nb = tn * 128;
-    const __amdgpu_buffer_rsrc_t rsBk = glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
-                                            : make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
-    uint32_t va[4], vb[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        va[u] = voff8<false>(wid * 4 + u, lane, p.lda, m0, p.M);
-        vb[u] = voff8<false>(wid * 4 + u, lane, p.ldb, n0, p.N);
-        if (glu) {   // tile row r -> weight row (r < 128 ? nb + r : I + nb + r - 128); same LDS swizzle
-            const int row = 16 * (wid * 4 + u) + (lane >> 2);
-            const int gc = (lane & 3) ^ f4(row);
-            const int wrow = row < 128 ? nb + row : p.glu + nb + row - 128;
-            vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
-        }
-    }
-    // one DMA instruction (u: 0..3 operand A, 4..7 operand B) of stage st into slot sl
-    auto dma = [&](int st, int sl, int u, auto full_tag) {
-        constexpr bool FULL = decltype(full_tag)::value;
-        const bool isA = u < 4;
-        const int i = wid * 4 + (u & 3);
-        char* dst = smem + sl * SS + (isA ? 0 : SA) + i * 1024;
-        uint32_t v = isA ? va[u & 3] : vb[u & 3];
-        int soff = st * BK2 * 2;
-        if (!FULL) {
-            const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
-            if (kleft < BK2) {                // zero the chunks at k >= K
-                const int row = 16 * i + (lane >> 2);
-                const int gc = (lane & 3) ^ f4(row);
-                if (gc * 8 >= kleft) v = OOB;
-                if (kleft <= 0) soff = 0;
-            }
-        }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, v, soff, 0, 0);
-    };
-    using FullT = std::integral_constant<bool, true>;
-    using PartT = std::integral_constant<bool, false>;
-    f32x16 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){};
-    const int ra = wm * 128, cb = wn * 128;
-#pragma unroll
-    for (int st = 0; st < NS8; ++st)
-#pragma unroll
-        for (int u = 0; u < 8; ++u) dma(st, st, u, PartT{});
-    wait_vm<24>();   // stage 0 landed (stages 1..3 may stay in flight)
-    __builtin_amdgcn_s_barrier();
-    // fragment sets: index 2 * block + k-half
-    bf16x8 xa[8], xb[8], ya[8], yb[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        xa[q] = frag32(smem, ra + (q >> 1) * 32, q & 1, lane);
-        xb[q] = frag32(smem + SA, cb + (q >> 1) * 32, q & 1, lane);
-    }
-#define KD_G11_SYNC()                                      \
-    {                                                      \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-        wait_vm<16>();                                     \
-        __builtin_amdgcn_s_barrier();                      \
-    }
-    KD_G11_SYNC()
-    __builtin_amdgcn_sched_barrier(0);
-#define KD_SB __builtin_amdgcn_sched_barrier(0);
-#define KD_G11_STEP(SL, CA, CB, NA, NB, FT)                                                                  \
-    {                                                                                                         \
-        const int t_ = t + (SL);                                                                              \
-        const char* na_ = smem + (((SL) + 1) % NS8) * SS;                                                     \
-        _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                       \
-            const int h_ = q >> 2, bi_ = q & 3;                                                               \
-            mfma32_agpr(acc[bi_][0], CB[0 + h_], CA[2 * bi_ + h_]); KD_SB                                     \
-            dma(t_ + NS8, (SL), q, FT{});                                                                     \
-            KD_SB                                                                                             \
-            mfma32_agpr(acc[bi_][1], CB[2 + h_], CA[2 * bi_ + h_]); KD_SB                                     \
-            NA[q] = frag32(na_, ra + (q >> 1) * 32, q & 1, lane);                                             \
-            KD_SB                                                                                             \
-            mfma32_agpr(acc[bi_][2], CB[4 + h_], CA[2 * bi_ + h_]); KD_SB                                     \
-            NB[q] = frag32(na_ + SA, cb + (q >> 1) * 32, q & 1, lane);                                        \
-            if (q == 7) KD_G11_SYNC()                                                                         \
-            KD_SB                                                                                             \
-            if (q == 7) mfma32_agpr_last(acc[bi_][3], CB[6 + h_], CA[2 * bi_ + h_], t_ + 1 == nk);            \
-            else mfma32_agpr(acc[bi_][3], CB[6 + h_], CA[2 * bi_ + h_]);                                      \
-            KD_SB                                                                                             \
-        }                                                                                                     \
-    }
-    int t = 0;
-    for (; t + 2 * NS8 <= nk_full; t += NS8) {   // every DMA of these steps lies inside K
-        KD_G11_STEP(0, xa, xb, ya, yb, FullT)
-        KD_G11_STEP(1, ya, yb, xa, xb, FullT)
-        KD_G11_STEP(2, xa, xb, ya, yb, FullT)
-        KD_G11_STEP(3, ya, yb, xa, xb, FullT)
-    }
-    for (; t + NS8 <= nk; t += NS8) {
-        KD_G11_STEP(0, xa, xb, ya, yb, PartT)
-        KD_G11_STEP(1, ya, yb, xa, xb, PartT)
-        KD_G11_STEP(2, xa, xb, ya, yb, PartT)
-        KD_G11_STEP(3, ya, yb, xa, xb, PartT)
-    }
-    const int rem = nk - t;
-    if (rem > 0) KD_G11_STEP(0, xa, xb, ya, yb, PartT)
-    if (rem > 1) KD_G11_STEP(1, ya, yb, xa, xb, PartT)
-    if (rem > 2) KD_G11_STEP(2, xa, xb, ya, yb, PartT)
-#undef KD_G11_STEP
-#undef KD_G11_SYNC
-#undef KD_SB
-    // drain the ring (out-of-range DMAs still write LDS) and the MFMA pipe before the
-    // accumulators are read back (asm MFMAs are invisible to the hazard recognizer)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    const f32x4 (&acc4)[4][16] = *reinterpret_cast<const f32x4(*)[4][16]>(&acc);
-    if (glu) epilogue_glu<128, 128, 4, 16, NTH8, true>(p, acc4, smem, m0, nb, wm, wn, lane, tid);
-    else epilogue2<256, 256, 2, 2, 128, 128, 4, 16, NTH8, true, RSTATS, true>(p, acc4, smem, m0, n0, wm, wn, lane, tid);
-}
-
-template <int EXP = 0>
-__global__ void __launch_bounds__(NTH8, 1) k_gemm11(GemmP p_) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tiles_m = (p_.M + 255) / 256, tiles_n = (p_.N + 255) / 256;
-    GemmP p = p_;
-    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += k0;
-        p.B += k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
-    int tm, tn;
-    tile_of(p.gx, tiles_m, tiles_n, tm, tn, p.tile0, p.gm);
-    g11_tile<EXP>(p, tm, tn, smem);
-}
-
-// =============================================================================
-// v12: v8 (256x256 tile, four waves of 128x128 on 16x16x32 MFMAs, AGPR accumulators, the same
-// 128 KiB of ring) with WHOLE-CACHE-LINE staging of K-major operands.  v8's K-major DMA
-// instruction covers 16 rows x 64 B (one BK = 32 stage), half of a 128-B line per row; the
-// diagnostic build that reads 8 rows x 128 B per instruction instead (same instructions and
-// bytes, forced variant 25) ran 8-10 % faster on the big forward shapes (profiles/r04, the
-// hipBLASLt kernel stages BK = 64 for the same reason).  Here the ring holds two PAIRS of
-// stages (stages 2q, 2q+1 = 64 k): a pair image is [256 rows][128 B] per operand (k 0..63 of
-// each row, 16-B chunk c at physical chunk c ^ swp(row), swp(r) = (r >> 1) & 7: every
-// 16-lane group of a ds_read_b128 fragment read covers the 16 (row & 1, chunk) bank slots once),
-// filled by instructions of 8 rows x 128 B (lane l: row 8i + (l >> 3), logical chunk
-// (l & 7) ^ swp(row) -> lane-linear LDS position).  Compute stays per BK = 32 stage (64 MFMAs
-// per step, fragments of stage t+1 read during step t).  Pair q (in pair slot q % 2) can only be
-// refilled once stage 2q-3 is in registers, so pair q is issued in the odd step 2q-3, 16 DMA
-// instructions per wave (two per unit), and must land by the end of step 2q-2: step ends wait
-// vmcnt(0) after even steps and vmcnt(16) after odd ones.
-// =============================================================================
-__device__ __forceinline__ int swp(int r) { return (r >> 1) & 7; }
-
-// 16x16x32 operand fragment of stage half h (k 32h..32h+31) from a pair image [rows][128 B]
-__device__ __forceinline__ bf16x8 frag_pair(const char* img, int rb, int h, int lane) {
-    const int r = rb + (lane & 15);
-    const int c = 4 * h + (lane >> 4);
-    return *(const bf16x8*)(img + r * 128 + ((c ^ swp(r)) << 4));
-}
-
-template <int EXP>
-__device__ __forceinline__ void g12_tile(GemmP p, int tm, int tn, char* smem) {
-    constexpr bool RSTATS = EXP & 32;
-    constexpr bool glu = EXP & 4;
-    // EXP & 256 (forced variant 27): no barrier at the end of odd steps.  The only cross-wave
-    // hazards are per PAIR: RAW (pair q, issued in step 2q-3, is first read in step 2q-1: every
-    // wave's vmcnt(0) + the barrier at the end of EVEN step 2q-2) and WAR (pair q+2 overwrites
-    // pair q's slot in odd step 2q+1, after every wave's last read of pair q in step 2q: the
-    // lgkmcnt(0) + barrier at the end of even step 2q); the odd-step barrier guards nothing.
-    constexpr bool NOB = EXP & 256;
-    constexpr int PA = 256 * 128;       // one operand's pair image (32 KiB)
-    constexpr int PS = 2 * PA;          // a pair slot (64 KiB); two of them
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 1, wn = wid & 1;
-    const int m0 = tm * 256, n0 = tn * 256;
-    const int K = p.K;
-    const int nk = (K + BK2 - 1) / BK2, nk_full = K / BK2;
-    const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A + (int64_t)m0 * p.lda, rec_bytes(min(256, p.M - m0), p.lda));
-    const int nb = tn * 128;
-    const __amdgpu_buffer_rsrc_t rsB = glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
-                                           : make_rsrc(p.B + (int64_t)n0 * p.ldb, rec_bytes(min(256, p.N - n0), p.ldb));
-    // wave w fills rows 64w .. 64w + 63 of each operand: instruction j (0..7) rows 64w + 8j + (l >> 3);
-    // the lane's swizzled chunk depends on j only through j & 1, the row step goes to soffset
-    const int rlo = 64 * wid + (lane >> 3);
-    const int brow = glu ? (wid < 2 ? nb : p.glu + nb - 128) : 0;   // weight row of tile row 0 of this wave's half
-    uint32_t va[2], vb[2];
-    int gcl[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        const int gc = (lane & 7) ^ swp(rlo + 8 * e);
-        gcl[e] = gc;
-        va[e] = (uint32_t)((int64_t)rlo * p.lda * 2 + gc * 16);
-        vb[e] = (uint32_t)((int64_t)(brow + rlo) * p.ldb * 2 + gc * 16);
-    }
-    // instruction j of operand (isA) of pair q into pair slot ps
-    auto dma = [&](int q, int ps, int j, bool isA, auto full_tag) {
-        constexpr bool FULL = decltype(full_tag)::value;
-        char* dst = smem + ps * PS + (isA ? 0 : PA) + (wid * 8 + j) * 1024;
-        uint32_t v = isA ? va[j & 1] : vb[j & 1];
-        const int64_t ld = isA ? p.lda : p.ldb;
-        int kq = q * 64;
-        if (!FULL) {
-            const int kleft = K - kq;     // valid k of this pair (<= 0: past the end)
-            if (gcl[j & 1] * 8 >= kleft) v = OOB;
-            if (kleft <= 0) kq = 0;
-        }
-        const int soff = __builtin_amdgcn_readfirstlane((int)(8 * j * ld * 2 + kq * 2));
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsB, (lds_void_t*)dst, 16, v, soff, 0, 0);
-    };
-    using FullT = std::integral_constant<bool, true>;
-    using PartT = std::integral_constant<bool, false>;
-    f32x4 acc[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int ra = wm * 128, cb = wn * 128;
-    // prologue: pairs 0 and 1 (stages 0..3) into pair slots 0 and 1; pair 0 landed
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            dma(q, q, j, true, PartT{});
-            dma(q, q, j, false, PartT{});
-        }
-    wait_vm<16>();
-    __builtin_amdgcn_s_barrier();
-    bf16x8 xa[8], xb[8], ya[8], yb[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        xa[u] = frag_pair(smem, ra + u * 16, 0, lane);
-        xb[u] = frag_pair(smem + PA, cb + u * 16, 0, lane);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#define KD_G12_SYNC(ODD)                                   \
-    if (!(NOB && (ODD))) {                                 \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-        if (ODD) wait_vm<16>();                            \
-        else wait_vm<0>();                                 \
-        __builtin_amdgcn_s_barrier();                      \
-    }
-#define KD_SB __builtin_amdgcn_sched_barrier(0);
-    // step t + SL (SL = 0..3 of a group of four; t % 4 == 0): stage t+SL is in registers (CA, CB);
-    // stage t+SL+1 is read from pair slot ((SL+1) >> 1) & 1, half (SL+1) & 1; odd SL issue pair
-    // (t+SL+3)/2 into pair slot ((SL+3) >> 1) & 1
-#define KD_G12_STEP(SL, CA, CB, NA, NB, FT)                                                                  \
-    {                                                                                                         \
-        const int t_ = t + (SL);                                                                              \
-        const char* na_ = smem + ((((SL) + 1) >> 1) & 1) * PS;                                                \
-        constexpr int nh_ = ((SL) + 1) & 1;                                                                   \
-        constexpr bool odd_ = (SL) & 1;                                                                       \
-        const int q_ = (t_ + 3) >> 1;                                                                         \
-        constexpr int qs_ = (((SL) + 3) >> 1) & 1;                                                            \
-        _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                       \
-            mfma_agpr(acc[u][0], CB[0], CA[u]); KD_SB                                                         \
-            if (odd_) dma(q_, qs_, u, true, FT{});                                                            \
-            KD_SB                                                                                             \
-            mfma_agpr(acc[u][1], CB[1], CA[u]); KD_SB                                                         \
-            if (u < 4) NA[2 * u] = frag_pair(na_, ra + 2 * u * 16, nh_, lane);                                \
-            KD_SB                                                                                             \
-            mfma_agpr(acc[u][2], CB[2], CA[u]); mfma_agpr(acc[u][3], CB[3], CA[u]); KD_SB                     \
-            if (u < 4) NB[2 * u] = frag_pair(na_ + PA, cb + 2 * u * 16, nh_, lane);                           \
-            KD_SB                                                                                             \
-            mfma_agpr(acc[u][4], CB[4], CA[u]); KD_SB                                                         \
-            if (odd_) dma(q_, qs_, u, false, FT{});                                                           \
-            KD_SB                                                                                             \
-            mfma_agpr(acc[u][5], CB[5], CA[u]); KD_SB                                                         \
-            if (u < 4) NA[2 * u + 1] = frag_pair(na_, ra + (2 * u + 1) * 16, nh_, lane);                      \
-            KD_SB                                                                                             \
-            mfma_agpr(acc[u][6], CB[6], CA[u]); KD_SB                                                         \
-            if (u < 4) NB[2 * u + 1] = frag_pair(na_ + PA, cb + (2 * u + 1) * 16, nh_, lane);                 \
-            if (u == 7) KD_G12_SYNC(odd_)                                                                     \
-            KD_SB                                                                                             \
-            if (u == 7) mfma_agpr_last(acc[u][7], CB[7], CA[u], t_ + 1 == nk);                                \
-            else mfma_agpr(acc[u][7], CB[7], CA[u]);                                                          \
-            KD_SB                                                                                             \
-        }                                                                                                     \
-    }
-    int t = 0;
-    for (; t + 8 <= nk_full; t += 4) {   // every pair these steps issue (up to stage t + 7) lies inside K
-        KD_G12_STEP(0, xa, xb, ya, yb, FullT)
-        KD_G12_STEP(1, ya, yb, xa, xb, FullT)
-        KD_G12_STEP(2, xa, xb, ya, yb, FullT)
-        KD_G12_STEP(3, ya, yb, xa, xb, FullT)
-    }
-    for (; t + 4 <= nk; t += 4) {
-        KD_G12_STEP(0, xa, xb, ya, yb, PartT)
-        KD_G12_STEP(1, ya, yb, xa, xb, PartT)
-        KD_G12_STEP(2, xa, xb, ya, yb, PartT)
-        KD_G12_STEP(3, ya, yb, xa, xb, PartT)
-    }
-    const int rem = nk - t;
-    if (rem > 0) KD_G12_STEP(0, xa, xb, ya, yb, PartT)
-    if (rem > 1) KD_G12_STEP(1, ya, yb, xa, xb, PartT)
-    if (rem > 2) KD_G12_STEP(2, xa, xb, ya, yb, PartT)
-#undef KD_G12_STEP
-#undef KD_G12_SYNC
-#undef KD_SB
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    if (glu) epilogue_glu<128, 128, 8, 8, NTH8>(p, acc, smem, m0, nb, wm, wn, lane, tid);
-    else epilogue2<256, 256, 2, 2, 128, 128, 8, 8, NTH8, true, RSTATS>(p, acc, smem, m0, n0, wm, wn, lane, tid);
-}
-
-template <int EXP = 0>
-__global__ void __launch_bounds__(NTH8, 1) k_gemm12(GemmP p_) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tiles_m = (p_.M + 255) / 256, tiles_n = (p_.N + 255) / 256;
-    GemmP p = p_;
-    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += k0;
-        p.B += k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
-    int tm, tn;
-    tile_of(p.gx, tiles_m, tiles_n, tm, tn, p.tile0, p.gm);
-    g12_tile<EXP>(p, tm, tn, smem);
-}
-
+#include "gemm_v11_v12.inc"   // tools/ab/gemm_v11_v12.inc: v11 (32x32x16 MFMAs) and v12 (whole-line staging)
 #endif  // KD_AB_BUILD
 
 template <bool A_MN, bool B_MN, int EXP = 0>
 __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tiles_m = (p_.M + 255) / 256, tiles_n = (p_.N + 255) / 256;
-    if (p_.sk_steps > 0) {   // stream-K: this workgroup's run of the tiles' k-steps
-        const int nkt = p_.sk_steps, G = p_.sk_grid, w = blockIdx.x;
-        const int64_t tot = (int64_t)tiles_m * tiles_n * nkt;
-        int64_t s0 = tot * w / G;
-        const int64_t s1 = tot * (w + 1) / G;
-        while (s0 < s1) {
-            const int t = (int)(s0 / nkt);
-            const int64_t tb = (int64_t)t * nkt, e = min(s1, tb + nkt);
-            const int wf = sk_wg_of(tb, tot, G), wl = sk_wg_of(tb + nkt - 1, tot, G);
+    if constexpr ((EXP & 1024) != 0) {   // the stream-K build (variant 21): data-parallel whole waves, then runs
+        const int nkt = p_.sk_steps, G = p_.sk_grid;
+        const bool dp = (int)blockIdx.x < p_.sk_dp;
+        // run w of workgroup i (sk_dp % 8 == 0, so workgroup i sits on XCD i % 8): the runs of one XCD
+        // are consecutive, i.e. a contiguous stretch of the grouped tile order (L2-shared panels)
+        const int i = (int)blockIdx.x - p_.sk_dp;
+        const int q8 = G / 8, r8 = G % 8, x = i % 8;
+        const int w = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + i / 8;
+        const int64_t tot = (int64_t)(tiles_m * tiles_n - p_.sk_dp) * nkt;
+        int64_t s0 = dp ? 0 : tot * w / G;
+        const int64_t s1 = dp ? 1 : tot * (w + 1) / G;
+        while (s0 < s1) {   // ONE g8_tile call site (one inlined copy of the tile body)
             GemmP q = p_;
-            const int64_t k0 = (s0 - tb) * BK2;
-            q.K = (int)min((int64_t)p_.K - k0, (e - s0) * BK2);
-            q.A += A_MN ? k0 * q.lda : k0;
-            q.B += B_MN ? k0 * q.ldb : k0;
-            if (wl > wf) {   // a piece of a shared tile: plain fp32 partial plane
-                q.C = p_.sk_ws + (int64_t)(w - wf) * p_.split_stride;
-                q.ldc = p_.N; q.c_f32 = 1; q.accumulate = 0; q.alpha = 1.f; q.alpha_dev = nullptr;
-                q.bias = nullptr; q.aux = nullptr; q.resid = nullptr; q.act = KD_ACT_NONE;
-            }
             int tm, tn;
-            tile_grouped(t, tiles_m, tiles_n, tm, tn, p_.gm);
-            g8_tile<A_MN, B_MN, EXP>(q, tm, tn, smem);
+            int64_t e = s1;
+            SkFold f;
+            const SkFold* fp = nullptr;
+            if (dp) {
+                tile_of(p_.sk_dp, tiles_m, tiles_n, tm, tn, 0, p_.gm);
+            } else {
+                const int t = (int)(s0 / nkt);
+                const int64_t tb = (int64_t)t * nkt;
+                e = min(s1, tb + nkt);
+                const int wf = sk_wg_of(tb, tot, G), wl = sk_wg_of(tb + nkt - 1, tot, G);
+                const int64_t k0 = (s0 - tb) * BK2;
+                q.K = (int)min((int64_t)p_.K - k0, (e - s0) * BK2);
+                q.A += A_MN ? k0 * q.lda : k0;
+                q.B += B_MN ? k0 * q.ldb : k0;
+                tile_grouped(p_.sk_dp + t, tiles_m, tiles_n, tm, tn, p_.gm);
+                if (wl > wf) {   // a piece of a shared tile: folded in this launch by its last arriver
+                    q.stagger = 0;
+                    f = SkFold{p_.sk_ws, p_.sk_cnt, tot, tb, G, wf, w - wf, wl - wf + 1, t};
+                    fp = &f;
+                }
+            }
+            g8_tile<A_MN, B_MN, EXP>(q, tm, tn, smem, fp);
             s0 = e;
             __syncthreads();   // the next piece's DMA refills the LDS the epilogue staged through
         }
@@ -2040,135 +1560,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
 }
 
 #ifdef KD_AB_BUILD   // v9: equal speed to v8 on the step's shapes, not in the plan; A/B library only
-// =============================================================================
-// v9: 256x256 tile, EIGHT waves in two groups that ping-pong on every SIMD. Group g
-// (waves 4g..4g+3, one per SIMD) owns rows 128g..128g+127; wave 4g+c owns columns
-// 64c..64c+63, 8x4 MFMA 16x16x32 tiles whose accumulators stay in the AGPR file (asm
-// MFMA, as v8). Same 4-slot BK=32 LDS-DMA ring and stage images as v3/v8.
-// Group 1 runs one barrier behind group 0, so between consecutive barriers one group
-// issues its LDS reads and DMA while the other owns the SIMD's MFMA pipe (s_setprio 1):
-//   K-tile t, per wave: [reads of slot t%4 (12 fragments) ; DMA of K-tile t+3 (4 of the
-//   32 1-KiB wave-instructions) ; vmcnt(8) ; lgkmcnt(0)] barrier [32 MFMA] barrier
-// Barrier intervals: group 0 reads K-tile t in interval 2t, group 1 in 2t+1.
-// RAW: K-tile t+1's DMA is retired by every wave's vmcnt(8) in its load phase of K-tile t
-//   (issued then: t+1, t+2, t+3), before barrier 2t+1 (g0) / 2t+2 (g1); its first reader
-//   (g0) starts after barrier 2t+2.
-// WAR: K-tile t+3 goes into the slot of K-tile t-1, whose reads every wave retired
-//   (lgkmcnt 0) before barrier 2t (g1's is the later one); the DMA is issued in interval
-//   2t (g0) / 2t+1 (g1). Past the last K-tile the DMAs still run (all lanes out of range:
-//   zero-fill, no memory traffic) so the counts stay uniform.
-// =============================================================================
-constexpr int NTH9 = 512;
-
-template <bool A_MN, bool B_MN>
-__global__ void __launch_bounds__(NTH9, 1) k_gemm9(GemmP p_) {
-    GemmP p = p_;
-    if (p.gy > 1) {   // split-K: this grid row owns K range [k0, k0 + kchunk) -> fp32 partial plane
-        const int64_t k0 = (int64_t)blockIdx.y * p.kchunk;
-        p.K = (int)min((int64_t)p.K - k0, p.kchunk);
-        p.A += A_MN ? k0 * p.lda : k0;
-        p.B += B_MN ? k0 * p.ldb : k0;
-        p.C = (float*)p.C + (int64_t)blockIdx.y * p.split_stride;
-    }
-    constexpr int SA = 256 * BK2 * 2, SS = 2 * SA;   // 16 KiB per operand, 32 KiB per slot
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wid >> 2, wc = wid & 3;
-    int tm, tn;
-    tile_of(p.gx, (p.M + 255) / 256, (p.N + 255) / 256, tm, tn, p.tile0, p.gm);
-    const int m0 = tm * 256, n0 = tn * 256;
-    const int K = p.K;
-    const int nk = (K + BK2 - 1) / BK2;
-    const __amdgpu_buffer_rsrc_t rsAk = make_rsrc(p.A + (A_MN ? 0 : (int64_t)m0 * p.lda), A_MN ? 0u : rec_bytes(min(256, p.M - m0), p.lda));
-    const bool glu = !B_MN && p.glu != 0;   // gate rows [nb, nb+128) and up rows [I+nb, I+nb+128)
-    const int nb = tn * 128;
-    const __amdgpu_buffer_rsrc_t rsBk =
-        glu ? make_rsrc(p.B, rec_bytes(p.N, p.ldb))
-            : make_rsrc(p.B + (B_MN ? 0 : (int64_t)n0 * p.ldb), B_MN ? 0u : rec_bytes(min(256, p.N - n0), p.ldb));
-    // this wave's DMA share of a K-tile: A and B wave-instructions 2*wid, 2*wid+1 (of 16 each)
-    uint32_t va[2], vb[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        va[u] = voff8<A_MN>(wid * 2 + u, lane, p.lda, m0, p.M);
-        vb[u] = voff8<B_MN>(wid * 2 + u, lane, p.ldb, n0, p.N);
-        if (glu) {
-            const int row = 16 * (wid * 2 + u) + (lane >> 2);
-            const int gc = (lane & 3) ^ f4(row);
-            const int wrow = row < 128 ? nb + row : p.glu + nb + row - 128;
-            vb[u] = (uint32_t)((int64_t)wrow * p.ldb * 2 + gc * 16);
-        }
-    }
-    auto dma = [&](int st, int u) {   // u: 0,1 operand A; 2,3 operand B
-        const bool isA = u < 2;
-        const bool mn = isA ? A_MN : B_MN;
-        const int i = wid * 2 + (u & 1);
-        char* dst = smem + (st & 3) * SS + (isA ? 0 : SA) + i * 1024;
-        uint32_t v = isA ? va[u & 1] : vb[u & 1];
-        if (!mn) {
-            int soff = st * BK2 * 2;
-            const int kleft = K - st * BK2;   // valid k of this stage (<= 0: past the end)
-            if (kleft < BK2) {
-                const int row = 16 * i + (lane >> 2);
-                const int gc = (lane & 3) ^ f4(row);
-                if (gc * 8 >= kleft) v = OOB;
-                if (kleft <= 0) soff = 0;
-            }
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsAk : rsBk, (lds_void_t*)dst, 16, v, soff, 0, 0);
-        } else {
-            const bf16* base = isA ? p.A + m0 : p.B + n0;
-            const int64_t ld = isA ? p.lda : p.ldb;
-            const int kv = max(0, min(BK2, K - st * BK2));
-            const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)min(st * BK2, K) * ld, rec_bytes(kv, ld));
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)dst, 16, v, 0, 0, 0);
-        }
-    };
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int ra = grp * 128, cb = wc * 64;
-#pragma unroll
-    for (int st = 0; st < 3; ++st)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) dma(st, u);
-    wait_vm<8>();   // K-tile 0 landed (1 and 2 stay in flight)
-    __builtin_amdgcn_s_barrier();
-    if (grp == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
-    __builtin_amdgcn_sched_barrier(0);
-    for (int t = 0; t < nk; ++t) {
-        const char* sl = smem + (t & 3) * SS;
-        bf16x8 fa[8], fb[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = frag2<256, B_MN>(sl + SA, cb + j * 16, lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) fa[i] = frag2<256, A_MN>(sl, ra + i * 16, lane);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) dma(t + 3, u);
-        wait_vm<8>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (i == 7 && j == 3) mfma_agpr_last(acc[i][j], fb[j], fa[i], t + 1 == nk);
-                else mfma_agpr(acc[i][j], fb[j], fa[i]);
-            }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (grp == 0) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    if (!A_MN && !B_MN && glu) epilogue_glu<128, 64, 8, 4, NTH9>(p, acc, smem, m0, nb, grp, wc, lane, tid);
-    else epilogue2<256, 256, 2, 4, 128, 64, 8, 4, NTH9, !A_MN && !B_MN>(p, acc, smem, m0, n0, grp, wc, lane, tid);
-}
+#include "gemm_v9.inc"   // tools/ab/gemm_v9.inc: v9 (eight-wave ping-pong)
 #endif  // KD_AB_BUILD
 
 
@@ -2476,16 +1868,10 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
     const int nitems = p.gx * p.gy;
     for (int it = (int)blockIdx.x; it < nitems; it += (int)gridDim.x) {
         const int bxi = it / p.gy, byi = it - bxi * p.gy;
-        int S = S0;
+        const int S = S0;
         int tm, tn;
         const int tiles_m = (p.M + BMr - 1) / BMr, tiles_n = (p.N + BNr - 1) / BNr;
         tile_grouped(p.tile0 + bxi, tiles_m, tiles_n, tm, tn, p.gm);
-        if (p.sk_steps > 0) {   // stream-K: this tile's piece count; a one-piece tile is already final
-            const int64_t tot = (int64_t)tiles_m * tiles_n * p.sk_steps;
-            const int64_t tb = (int64_t)(p.tile0 + bxi) * p.sk_steps;
-            S = sk_wg_of(tb + p.sk_steps - 1, tot, p.sk_grid) - sk_wg_of(tb, tot, p.sk_grid) + 1;
-            if (S <= 1) continue;
-        }
         const int rows_per = BMr / p.gy;
         const int r0 = tm * BMr + byi * rows_per;
         const int r1 = min(r0 + rows_per, p.M);
@@ -2571,10 +1957,17 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
 struct GemmPlan { int var; int split; int64_t kchunk; int dp_tiles; };
 constexpr int SK_GRID = 256;   // stream-K workgroups: one per CU
 
-// stream-K pieces: at most this many workgroups share one tile (the workspace's planes)
-inline int sk_max_pieces(int64_t tiles, int64_t nk, int G) {
-    const int64_t per = tiles * nk / G;   // >= 1 k-step per workgroup (callers ensure tot >= G)
-    return (int)((nk - 1) / per + 2);
+// stream-K workspace: one int ticket per run tile (a 256-B block, zeroed per launch), then two
+// 256 KB partial-tile slots per run (its first and its last piece)
+inline size_t sk_cnt_bytes(int64_t sk_tiles) { return (size_t)((sk_tiles * 4 + 255) / 256) * 256; }
+inline size_t sk_workspace_bytes(int64_t sk_tiles) {
+    return sk_cnt_bytes(sk_tiles) + (size_t)SK_GRID * 2 * 256 * 256 * 4;
+}
+// data-parallel tiles ahead of the runs: whole waves, all but the last (so every run holds more than
+// one tile's worth of k-steps when there are several waves: "DP + two-tile stream-K")
+inline int64_t sk_dp_tiles(int64_t tiles, int64_t nk) {
+    (void)nk;
+    return tiles >= 2 * SK_GRID ? (tiles / SK_GRID - 1) * SK_GRID : 0;
 }
 
 #ifdef KD_AB_BUILD
@@ -2655,23 +2048,17 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
             }
         }
     }
-    // stream-K on v8 (forced variant 21 only): SK_GRID workgroups take equal runs of the tiles'
-    // k-steps (runs cross tile boundaries); tiles shared by several runs fold fp32 partial
-    // planes. Measured slower than the split-K / hybrid plans on every backward shape of the
-    // step (1152x1152x5832 wgrad 71 vs 39 us, 6144x896x9728 dgrad 155 vs 149 us, down_proj
-    // 1020 vs 710 us): a run accumulates one tile over a contiguous K range, so the ~32
-    // workgroups of an XCD no longer share A / B k-slices in L2 (each tile's panels are
-    // fetched once per piece), and a sub-wave tile count makes every tile a shared one.
-    const int64_t tot = t256 * nk;
-    if (d->variant == 21 && d->split_k <= 0 && tot >= 2 * SK_GRID) {
-        const int64_t per = (tot + SK_GRID - 1) / SK_GRID;
-        const int pieces = sk_max_pieces(t256, nk, SK_GRID);
-        const double segs = 1.0 + (double)((per + nk - 1) / nk);
-        const double t_sk = (double)per * step[3] + segs * fixed[3] +
-                            ((double)(t256 + SK_GRID) * 65536.0 * 8.0 + out_b) / kBW;
-        if ((uint64_t)pieces * M * N * 4 <= ws_cap) {
-            bt = t_sk;
-            best = GemmPlan{21, pieces, d->K, 0};
+    // stream-K on v8 (variant 21): all but the last whole wave of tiles data-parallel, then SK_GRID
+    // workgroups take equal runs of the remaining tiles' k-steps (runs cross tile boundaries); a
+    // tile shared by several runs is folded inside the launch by its last-arriving piece (round 6).
+    // The round-2 build (every tile in runs, fp32 partial planes folded by a second launch) measured
+    // slower than the split-K / hybrid plans on every backward shape of the step (1152x1152x5832
+    // wgrad 71 vs 39 us, 6144x896x9728 dgrad 155 vs 149 us, down_proj 1020 vs 710 us).
+    if (d->variant == 21 && d->split_k <= 1) {   // (split_k 1: the fused dact / q|k|v epilogues; not a K split)
+        const int64_t dp = sk_dp_tiles(t256, nk);
+        if ((t256 - dp) * nk >= 2 * SK_GRID && sk_workspace_bytes(t256 - dp) <= ws_cap) {
+            bt = 0;
+            best = GemmPlan{21, 1, d->K, (int)dp};
         }
     }
     return best;
@@ -2828,6 +2215,24 @@ static bool variant_known(int v) {
     return false;
 }
 
+// stream-K launch setup over `tiles` 256 x 256 tiles: the data-parallel prefix, the run grid, the
+// tickets (zeroed by a memset node ahead of every launch: Guideline 16) and the partial-tile slots
+static bool sk_fits(int64_t tiles, int64_t nk, const kd_gemm_desc* d) {
+    const int64_t dp = sk_dp_tiles(tiles, nk);
+    return (tiles - dp) * nk >= 2 * SK_GRID && d->workspace && d->workspace_bytes >= sk_workspace_bytes(tiles - dp);
+}
+static int sk_setup(GemmP& q, int64_t tiles, const kd_gemm_desc* d, hipStream_t st) {
+    const int64_t dp = sk_dp_tiles(tiles, ceil_div(d->K, BK2));
+    KD_CHECK_ARG(d->workspace && d->workspace_bytes >= sk_workspace_bytes(tiles - dp), "gemm: stream-K workspace too small");
+    q.sk_steps = ceil_div(d->K, BK2); q.sk_grid = SK_GRID; q.sk_dp = (int)dp;
+    q.sk_cnt = (int*)d->workspace;
+    q.sk_ws = (float*)((char*)d->workspace + sk_cnt_bytes(tiles - dp));
+    q.gx = (int)dp + SK_GRID; q.gy = 1; q.tile0 = 0;
+    if (hipMemsetAsync(q.sk_cnt, 0, sk_cnt_bytes(tiles - dp), st) != hipSuccess)
+        return fail(KD_ERR_LAUNCH, "gemm: stream-K ticket memset");
+    return KD_OK;
+}
+
 int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_ARG(d != nullptr, "gemm: null descriptor");
     KD_CHECK_ARG(d->A && d->B && (d->C || d->qkv), "gemm: null operand");
@@ -2850,7 +2255,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     if (dact) {
         const int64_t w = d->act == KD_ACT_DSWIGLU ? 2 * (int64_t)d->N : d->N;
         KD_CHECK_ARG(d->aux && d->c_dtype == KD_DTYPE_BF16 && !d->bias && !d->residual && !d->accumulate && d->split_k <= 1 &&
-                     d->variant != 1 && d->variant != 21,
+                     d->variant != 1,
                      "gemm backward activation: aux (forward pre-activation), bf16 C, no bias / residual / accumulate / split-K");
         KD_CHECK_SHAPE(d->N % 8 == 0 && d->ldc >= w && d->ld_aux >= w && d->ldc % 8 == 0 && d->ld_aux % 8 == 0 &&
                        (uintptr_t)d->aux % 16 == 0, "gemm backward activation: ldc / ld_aux >= N (2N for dswiglu), 16-B rows");
@@ -2910,7 +2315,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     }
     p.kchunk = d->K; p.split_stride = 0; p.glu = 0; p.tile0 = 0;
     p.sa = p.sb = nullptr; p.gx = 0; p.gy = 1;
-    p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr;
+    p.sk_steps = 0; p.sk_grid = 0; p.sk_ws = nullptr; p.sk_dp = 0; p.sk_cnt = nullptr;
     p.gm = 0;
     p.rst = nullptr; p.rst_nt = p.rst_vs = p.rst_top2 = 0; p.rst_inv_t = 1.f;
     p.stagger = ab_knob("KD_GEMM_STAGGER", 1);
@@ -2924,7 +2329,7 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
                         (!amn || d->M % 8 == 0) && (!bmn || d->N % 8 == 0) &&
                         (uint64_t)BK2 * (amn ? d->lda : 0) * 2 < 0x7FFFFFFFull;
     KD_CHECK_ARG(!dact || big_ok, "gemm backward activation: needs the tiled kernels (M, N >= 128, M*N >= 2^20)");
-    KD_CHECK_ARG(!d->qkv || (big_ok && d->variant != 1 && d->variant != 21),
+    KD_CHECK_ARG(!d->qkv || (big_ok && d->variant != 1),
                  "gemm qkv: needs the tiled kernels (M, N >= 128, M*N >= 2^20)");
     kd_gemm_desc d1;
     if ((dact || d->qkv) && d->split_k != 1) {   // the fused backward activation / q|k|v scatter are never split-K
@@ -2978,6 +2383,10 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         else
 #endif
         if (d->b_pretiled) hipLaunchKernelGGL((k_gemm8<false, false, 4 | 256>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        else if (d->variant == 21 && sk_fits(grid.x, ceil_div(d->K, BK2), d)) {   // stream-K (v8 SwiGLU build)
+            if (const int rc = sk_setup(pk, grid.x, d, st); rc != KD_OK) return rc;
+            hipLaunchKernelGGL((k_gemm8<false, false, 4 | 1024>), dim3(pk.gx), dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
+        }
         else hipLaunchKernelGGL((k_gemm8<false, false, 4>), grid, dim3(NTH8), (gemm2_lds<256, 256>()), st, pk);
         KD_LAUNCH_CHECK("k_gemm<swiglu>");
         return KD_OK;
@@ -3020,24 +2429,16 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
         const int tbm = pl.var == 4 ? 128 : 256, tbn = pl.var == 3 ? 128 : 256;
         const int tiles = ceil_div(d->M, tbm) * ceil_div(d->N, tbn);
         p.gm = pick_gm(ceil_div(d->M, tbm), ceil_div(d->N, tbn));
-        if (pl.var == 21) {   // stream-K (v8), then the fold of the shared tiles
-            KD_CHECK_ARG(d->workspace && d->workspace_bytes >= (uint64_t)pl.split * d->M * d->N * 4,
-                         "gemm: stream-K workspace too small");
+        if (pl.var == 21) {   // stream-K (v8): whole waves data-parallel, the rest in runs, folded in-launch
             GemmP q = p;
-            q.sk_steps = ceil_div(d->K, BK2); q.sk_grid = SK_GRID; q.sk_ws = (float*)d->workspace;
-            q.split_stride = (int64_t)d->M * d->N;
-            q.gx = SK_GRID; q.gy = 1; q.tile0 = 0;
+            if (const int rc = sk_setup(q, tiles, d, st); rc != KD_OK) return rc;
             const size_t lds = gemm2_lds<256, 256>();
-            const dim3 grid(SK_GRID);
-            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, 0>), grid, dim3(NTH8), lds, st, q);
-            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, 0>), grid, dim3(NTH8), lds, st, q);
-            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, 0>), grid, dim3(NTH8), lds, st, q);
-            else hipLaunchKernelGGL((k_gemm8<true, false, 0>), grid, dim3(NTH8), lds, st, q);
+            const dim3 grid(q.gx);
+            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, 1024>), grid, dim3(NTH8), lds, st, q);
+            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, 1024>), grid, dim3(NTH8), lds, st, q);
+            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, 1024>), grid, dim3(NTH8), lds, st, q);
+            else hipLaunchKernelGGL((k_gemm8<true, false, 1024>), grid, dim3(NTH8), lds, st, q);
             KD_LAUNCH_CHECK("k_gemm8 (stream-K)");
-            q.gx = tiles; q.gy = 256 * 256 / 1024;
-            hipLaunchKernelGGL(k_splitk_reduce, dim3(reduce_grid(tiles * q.gy)), dim3(256), 0, st,
-                               (const float*)d->workspace, 0, q, 256, 256);
-            KD_LAUNCH_CHECK("k_splitk_reduce (stream-K)");
             return KD_OK;
         }
         // one launch of the planned kernel over linear tiles [q.tile0, q.tile0 + nt), gy K splits
@@ -3167,6 +2568,7 @@ int gemm_plan_query(const kd_gemm_desc* d, int32_t* var, int32_t* split, int32_t
 size_t gemm_workspace_size(const kd_gemm_desc* d) {
     if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->variant == 1 || d->act == KD_ACT_SWIGLU) return 0;
     const GemmPlan pl = plan_gemm(d, ~0ull);
+    if (pl.var == 21) return sk_workspace_bytes((int64_t)ceil_div(d->M, 256) * ceil_div(d->N, 256) - pl.dp_tiles);
     return pl.split > 1 ? (size_t)pl.split * d->M * d->N * 4 : 0;
 }
 

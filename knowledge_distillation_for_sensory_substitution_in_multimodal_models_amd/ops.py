@@ -259,7 +259,7 @@ def _gemm_desc(a, b, out, bias, act, residual, aux, alpha, alpha_dev, accumulate
     d.act = ACTS[act]
     d.variant = int(variant)
     d.split_k = int(split_k)
-    if split_k != 1:
+    if split_k != 1 or variant == 21:   # split-K partial planes / stream-K tickets + partial tiles
         ws = _workspace(("gemm_splitk", _stream()), GEMM_SPLITK_WS, a.device)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     if residual is not None:

@@ -288,6 +288,80 @@ def measure_kinds(dev, names) -> dict:
     return rep
 
 
+def _rel_l2(a, b) -> float:
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float((a - b).norm() / b.norm())
+
+
+def measure_depth_profile(dev, vision_depths=(1, 4, 8, 13, 17, 21, 26), text_depths=(1, 4, 8, 12, 16, 20, 24)) -> dict:
+    """Where along the student's towers the final hidden state's error against the fp32 oracle is
+    added (DT:232-240): the 0.5B student of c1 (seeded weights, one 336x336
+    sample) cut to `dv` SigLIP and `dt` Qwen2 layers -- the same weights, so the cut model's
+    outputs ARE the full model's hidden states at that depth, passed through the final norm --
+    on the HIP path (bf16 GEMMs, fp32 residual streams) and through the fp32 oracle.
+      vision[dv]: rel-L2 of the post-LN hook output (post_layernorm of SigLIP layer dv's output)
+      text[dt]:   rel-L2 of hn = norm(Qwen2 layer dt's output), with the full 26-layer SigLIP
+    and, as the yardstick, one bf16 rounding of the oracle's own tensor (the floor of any bf16
+    output).  The projector sits between them (text[1] - vision[26])."""
+    from dataclasses import replace
+    from oracle.model import OracleLlava
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.modeling import (
+        STUDENT_05B, LlavaOnevisionModel)
+    full = LlavaOnevisionModel(STUDENT_05B, dev, trainable=True, seed=2)
+    sd = {k: v.detach().float().cpu() for k, v in full.P.state_dict().items() if k != "language_model.lm_head.weight"}
+    del full
+    gc.collect()
+    torch.cuda.empty_cache()
+    bc = batch_cpu()
+    b = _to(bc, dev)
+    bo = dict(bc)
+    for k in ("rgb_pixel_values", "depth_pixel_values"):
+        bo[k] = bo[k].float()
+
+    def keep(cfg):
+        Vl, Tl = cfg.vision.layers, cfg.text.layers
+        out = {}
+        for k, v in sd.items():
+            if ".encoder.layers." in k and int(k.split(".encoder.layers.")[1].split(".")[0]) >= Vl:
+                continue
+            if "language_model.model.layers." in k and int(k.split("language_model.model.layers.")[1].split(".")[0]) >= Tl:
+                continue
+            out[k] = v
+        return out
+
+    def one(dv, dt):
+        cfg = replace(STUDENT_05B, vision=replace(STUDENT_05B.vision, layers=dv),
+                      text=replace(STUDENT_05B.text, layers=dt))
+        w = keep(cfg)
+        m = LlavaOnevisionModel(cfg, dev, trainable=True)
+        m.P.load_state_dict({k: v.to(dev) for k, v in w.items()}, strict=False)
+        f = m.forward(b["depth_input_ids"], b["depth_pixel_values"], b["image_sizes"], want_post_ln=True)
+        torch.cuda.synchronize()
+        hn, post = f["hn"].float().cpu(), f["post_ln"].float().cpu()
+        del f, m
+        torch.cuda.empty_cache()
+        o = OracleLlava(w, cfg)
+        with torch.no_grad():
+            _, opost = o(bo["depth_input_ids"], bo["depth_pixel_values"], bo["image_sizes"])
+        ohn = o.last_hn[0]
+        opost = opost.reshape(post.shape)
+        return dict(hn=_rel_l2(hn, ohn), hn_floor=_rel_l2(ohn.bfloat16(), ohn),
+                    post_ln=_rel_l2(post, opost), post_ln_floor=_rel_l2(opost.bfloat16(), opost))
+
+    rep = {"config": "c1 student (0.5B: SigLIP 26 + Qwen2 24), seeded weights, bs 1, L 1536, 336x336; HIP vs the fp32 "
+                     "oracle on the same weights, the models cut to the listed depths",
+           "vision": {}, "text": {}}
+    for dv in vision_depths:
+        _log(f"depth profile: SigLIP {dv}")
+        r = one(dv, 1)
+        rep["vision"][str(dv)] = dict(post_ln_rel_l2=r["post_ln"], floor=r["post_ln_floor"])
+    for dt in text_depths:
+        _log(f"depth profile: Qwen2 {dt}")
+        r = one(STUDENT_05B.vision.layers, dt)
+        rep["text"][str(dt)] = dict(hn_rel_l2=r["hn"], floor=r["hn_floor"])
+    return rep
+
+
 C4_FP8_TOL = 1e-2   # the fp8 (e4m3) teacher's stated tolerance on the teacher-side terms (DESIGN §4)
 
 

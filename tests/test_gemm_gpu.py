@@ -93,7 +93,7 @@ def test_epilogue_bias_act_residual_aux_accumulate(dev):
     assert (out - 0.5 * (a.float() @ w.float().t())).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("variant,split_k", [(1, 1), (5, 1), (6, 1), (7, 1), (16, 1), (16, 3), (0, 0)])
+@pytest.mark.parametrize("variant,split_k", [(1, 1), (5, 1), (6, 1), (7, 1), (16, 1), (16, 3), (0, 0), (21, 0)])
 def test_fp32_residual_stream(variant, split_k, dev):
     """C (fp32) = A B^T + bias + residual (fp32): the fp32 residual stream's epilogue (o_proj /
     fc2 / down_proj with kd_model_set_residual_f32) in every kernel and through the split-K
@@ -181,11 +181,13 @@ def test_splitk_all_layouts(split, variant, M, N, K, dev):
     assert (acc - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize("M,N,K", [(1152, 1152, 5832), (1000, 904, 4296), (6144, 5632, 256)])
+@pytest.mark.parametrize("M,N,K", [(1152, 1152, 5832), (1000, 904, 4296), (6144, 5632, 256), (6144, 4608, 3584),
+                                   (5832, 1152, 4304)])
 def test_stream_k_all_layouts(M, N, K, dev):
-    """Stream-K (variant 21): 256 workgroups take equal runs of the tiles' k-steps; shared
-    tiles are folded from fp32 partial planes, tiles a single run covers get the epilogue
-    directly (the 528-tile case). Ragged M / N / K tails; every operand layout; fp32 +=."""
+    """Stream-K (variant 21): all but the last whole wave of 256 x 256 tiles run data-parallel (the
+    528- and 432-tile cases), then 256 workgroups take equal runs of the remaining tiles' k-steps;
+    a tile shared by several runs is folded inside the launch by its last-arriving piece, tiles a
+    single run covers get the epilogue directly. Ragged M / N / K tails; every operand layout; fp32 +=."""
     ops = _ops()
     a = _rand(M, K, dev=dev, seed=60)
     w = _rand(N, K, dev=dev, seed=61, scale=0.05)
@@ -221,6 +223,31 @@ def test_stream_k_epilogue(dev):
     ref = o.float() + a.float() @ w.float().t()
     ops.gemm(a, w, out=o, accumulate=True, variant=21)
     _check(o, ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(6144, 3584, 3584), (1458, 1152, 4304), (6144, 896, 4864)])
+def test_stream_k_fold_is_deterministic(M, N, K, dev):
+    """The in-launch fold sums a shared tile's pieces in piece order whichever piece arrives last:
+    repeated launches (with another stream's GEMM competing for the CUs in the second round) give
+    the same bits; and the result matches the fp32 reference."""
+    ops = _ops()
+    a = _rand(M, K, dev=dev, seed=70)
+    w = _rand(N, K, dev=dev, seed=71, scale=0.05)
+    ref = ops.gemm(a, w, variant=21)
+    _check(ref, a.float() @ w.float().t())
+    for _ in range(3):
+        assert torch.equal(ops.gemm(a, w, variant=21), ref)
+    side = torch.cuda.Stream(device=dev)
+    x = _rand(4096, 4096, dev=dev, seed=72)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(4):
+            y = x @ x
+    out = ops.gemm(a, w, variant=21)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    del y
 
 
 def test_splitk_epilogue(dev):
@@ -308,7 +335,7 @@ def test_swiglu_epilogue_bitexact(M, I, K, dev):
     _check(a, torch.nn.functional.silu(g[:, :I]) * g[:, I:])
 
 
-@pytest.mark.parametrize("variant", [0, 5, 6, 7, 16])
+@pytest.mark.parametrize("variant", [0, 5, 6, 7, 16, 21])
 @pytest.mark.parametrize("M, N, K", [(1100, 1040, 392), (6144 // 2, 4864, 896), (5832 // 4, 4304, 1152)])
 def test_fused_backward_activation(variant, M, N, K, dev):
     """KD_ACT_DGELU_TANH / KD_ACT_DSWIGLU: the dgrad GEMM with the activation backward in its
@@ -317,7 +344,7 @@ def test_fused_backward_activation(variant, M, N, K, dev):
     ops = _ops()
     dy = _rand(M, K, dev=dev, seed=41)
     w = _rand(K, N, dev=dev, seed=42, scale=K ** -0.5)
-    v = ops.gemm(dy, w.t(), variant=variant, split_k=1)
+    v = ops.gemm(dy, w.t(), variant=variant, split_k=1 if variant != 21 else 0)
     pre = _rand(M, N, dev=dev, seed=43)
     out = ops.gemm(dy, w.t(), act="dgelu_tanh", aux=pre, variant=variant)
     assert torch.equal(out, ops.act_bwd(pre, v, "gelu_tanh"))
@@ -332,8 +359,8 @@ def test_fused_backward_activation(variant, M, N, K, dev):
 
 
 @pytest.mark.parametrize("shape,variant", [
-    ("teacher", 0), ("teacher", 16), ("teacher", 6), ("student", 0), ("student", 5), ("student", 7),
-    ("siglip", 0), ("siglip", 16), ("siglip", 6)])
+    ("teacher", 0), ("teacher", 16), ("teacher", 6), ("teacher", 21), ("student", 0), ("student", 5), ("student", 7),
+    ("siglip", 0), ("siglip", 16), ("siglip", 6), ("siglip", 21)])
 def test_qkv_scatter_epilogue_equals_gemm_then_split(shape, variant, dev):
     """The fused q|k|v projection (kd_qkv_scatter epilogue: bias, bf16 rounding, head-major
     scatter, RoPE on q / k, zeroed padding) equals the plain GEMM followed by k_qkv_split bit
@@ -353,7 +380,7 @@ def test_qkv_scatter_epilogue_equals_gemm_then_split(shape, variant, dev):
         inv = 1.0 / (1e6 ** (torch.arange(0, hd, 2, dtype=torch.float32) / hd))
         f = torch.arange(S, dtype=torch.float32)[:, None] * inv[None]
         cos, sin = f.cos().to(dev).contiguous(), f.sin().to(dev).contiguous()
-    qkv = ops.gemm(x, w, bias=bias, variant=variant, split_k=1)
+    qkv = ops.gemm(x, w, bias=bias, variant=variant, split_k=1 if variant != 21 else 0)
     q0, k0, v0 = ops.qkv_split(qkv, B, S, nq, nkv, hd, hdp, cos, sin)
     q = torch.full((B, nq, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)   # garbage: the padding must be zeroed
     k = torch.full((B, nkv, S, hdp), 7.0, dtype=torch.bfloat16, device=dev)
@@ -362,3 +389,19 @@ def test_qkv_scatter_epilogue_equals_gemm_then_split(shape, variant, dev):
     torch.cuda.synchronize()
     for got, ref, n in ((q, q0, "q"), (k, k0, "k"), (v, v0, "v")):
         assert torch.equal(got, ref), f"{n}: {int((got != ref).sum())} elements differ"
+
+
+@pytest.mark.parametrize("M,I,K", [(6144, 4864, 896), (2048, 3584, 1536)])
+def test_stream_k_swiglu_matches_plain_stream_k(M, I, K, dev):
+    """The SwiGLU build on stream-K (variant 21: 912 / 224 gate|up tiles, a data-parallel prefix
+    and runs folded in-launch): silu(gate) * up of the pre-activations the plain stream-K GEMM
+    of the same gathered tiles produces, and the aux output equals that GEMM bit for bit."""
+    ops = _ops()
+    h = _rand(M, K, dev=dev, seed=81)
+    w = _rand(2 * I, K, dev=dev, seed=82, scale=K ** -0.5)
+    aux = torch.empty(M, 2 * I, dtype=torch.bfloat16, device=dev)
+    a = ops.gemm(h, w, act="swiglu", aux=aux, variant=21)
+    g = (h.float() @ w.float().t())
+    _check(aux, g)
+    _check(a, torch.nn.functional.silu(aux.float()[:, :I]) * aux.float()[:, I:])
+    assert torch.equal(ops.gemm(h, w, act="swiglu", aux=aux, variant=21), a)   # deterministic

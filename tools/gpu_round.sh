@@ -12,6 +12,7 @@
 # kindparity every other module (DT phases 1-3, FB, BD) at full depth vs the fp32 oracle
 #            (FULL_KINDS, default "dt1 dt2 dt3 fb bd") -> full_depth_kinds.json
 # c4parity   BASELINE c4 itself at full depth (DT phase 3 + fp8 lm_mlp teacher) vs the fp32 oracle -> c4_full_depth.json
+# hnprofile  the student's hidden-state error vs the fp32 oracle at SigLIP / Qwen2 depths -> depth_profile.json
 # fp8study   tools/fp8_c4_study.py: the c4 KD term's fp8-vs-bf16 move split into LoCa top-2 flips and smooth change,
 #            product library, then the A/B library with the GEMM k-loop stagger off -> fp8_c4*.json
 # parity     the reduced-depth fixtures' per-term / per-parameter report -> parity.json
@@ -53,6 +54,8 @@ for s in $STEPS; do
                 --out $O/full_depth.json > $O/full_depth.log 2>&1 || fail fullparity $O/full_depth.log ;;
     c4parity) timeout -k 10 900 python -u tools/parity_report.py --c4-full-depth --out $O/c4_full_depth.json \
                 > $O/c4_full_depth.log 2>&1 || fail c4parity $O/c4_full_depth.log ;;
+    hnprofile) timeout -k 10 900 python -u tools/parity_report.py --depth-profile --out $O/depth_profile.json \
+                > $O/depth_profile.log 2>&1 || fail hnprofile $O/depth_profile.log ;;
     fp8study) timeout -k 10 600 python -u tools/fp8_c4_study.py --out $O/fp8_c4.json > /dev/null 2> $O/fp8_c4.log || fail fp8study $O/fp8_c4.log
             KDSTEP_LIB=tools/ab/libkdstep_ab.so KD_GEMM_STAGGER=0 timeout -k 10 600 python -u tools/fp8_c4_study.py \
                 --out $O/fp8_c4_nostagger.json > /dev/null 2> $O/fp8_c4_nostagger.log || fail fp8study-nostagger $O/fp8_c4_nostagger.log

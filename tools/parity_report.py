@@ -109,9 +109,19 @@ def main():
                     help="each module kind (tests/full_depth.KINDS: lb dt1 dt2 dt3 fb bd) at full depth vs the fp32 oracle")
     ap.add_argument("--c4-full-depth", action="store_true",
                     help="BASELINE c4 itself at full depth: DT phase 3 + the fp8 lm_mlp teacher vs the fp32 oracle")
+    ap.add_argument("--depth-profile", action="store_true",
+                    help="the student's hidden-state error vs the fp32 oracle along both towers (tests/full_depth.py)")
     ap.add_argument("kinds", nargs="*")
     a = ap.parse_args()
     import torch
+    if a.depth_profile:
+        from full_depth import measure_depth_profile
+        rep = measure_depth_profile(torch.device("cuda:0"))
+        print(json.dumps(rep, indent=1), flush=True)
+        if a.out:
+            Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+            Path(a.out).write_text(json.dumps(rep, indent=1))
+        return
     if a.c4_full_depth:
         from full_depth import measure_c4
         rep = measure_c4(torch.device("cuda:0"))
