@@ -109,6 +109,8 @@ def main():
                     help="each module kind (tests/full_depth.KINDS: lb dt1 dt2 dt3 fb bd) at full depth vs the fp32 oracle")
     ap.add_argument("--c4-full-depth", action="store_true",
                     help="BASELINE c4 itself at full depth: DT phase 3 + the fp8 lm_mlp teacher vs the fp32 oracle")
+    ap.add_argument("--image", default=None, metavar="HxW",
+                    help="--full-depth on this image size (e.g. 480x640: SUNRGBD geometry, 5 tiles, L 2980)")
     ap.add_argument("--depth-profile", action="store_true",
                     help="the student's hidden-state error vs the fp32 oracle along both towers (tests/full_depth.py)")
     ap.add_argument("kinds", nargs="*")
@@ -141,9 +143,12 @@ def main():
             Path(a.out).write_text(json.dumps(rep, indent=1))
         return
     if a.full_depth:
-        from full_depth import measure as fd_measure
-        rep = fd_measure(torch.device("cuda:0"), floor=a.floor, teacher_stream_ab=a.teacher_stream_ab,
-                         teacher_fp8=a.teacher_fp8)
+        from full_depth import geometry, measure as fd_measure
+        hw = tuple(int(v) for v in a.image.split("x")) if a.image else (336, 336)
+        with geometry(hw):
+            rep = fd_measure(torch.device("cuda:0"), floor=a.floor, teacher_stream_ab=a.teacher_stream_ab,
+                             teacher_fp8=a.teacher_fp8)
+        rep["image"] = list(hw)
         for k in ("hip", "hip_teacher_stream_f32", "hip_teacher_fp8", "bf16_floor"):
             if k in rep:
                 r = {kk: vv for kk, vv in rep[k].items() if kk != "grad_params"}
