@@ -637,7 +637,7 @@ def main():
     fwd12 = ops.TIMER.summary("gemm_kk_swiglu", where=lambda M, N, K: not v8_shape(M, N, K))
     fwd8 = ops.TIMER.summary("gemm_f8_swiglu")
     traffic = None   # PMC HBM bytes per launch of that kernel (tools/pmc_bench.sh -> profiles/)
-    for rd in ("r05", "r04", "r03", "r02", "r01"):
+    for rd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         tpath = REPO / "profiles" / rd / "pmc_traffic.json"
         if tpath.exists():
             fg = json.load(open(tpath)).get("roofline_kernel")
@@ -646,10 +646,11 @@ def main():
                 break
     # the step-wide MFMA utilisation per kernel family (tools/pmc_step.py over the serialized step)
     step_pmc = None
-    spath = REPO / "profiles" / "r05" / "pmc_step.json"
-    if spath.exists():
+    spath = next((REPO / "profiles" / rd / "pmc_step.json" for rd in ("r06", "r05")
+                  if (REPO / "profiles" / rd / "pmc_step.json").exists()), None)
+    if spath is not None:
         sp = json.load(open(spath))
-        step_pmc = dict(source="profiles/r05/pmc_step.json", serialized_step_ms=sp["serialized_step_ms"],
+        step_pmc = dict(source=str(spath.relative_to(REPO)), serialized_step_ms=sp["serialized_step_ms"],
                         step_mfma_util_vs_peak=sp.get("step_mfma_util_vs_peak"),
                         families={k: dict(ms=v["ms_per_step"], mfma=v["mfma_util_vs_peak"], hbm_gbs=v["hbm_gbs"])
                                   for k, v in list(sp["families"].items())[:10]})

@@ -1153,14 +1153,19 @@ __device__ __forceinline__ uint32_t voff8(int i, int lane, int64_t ld, int r0, i
 // one 256x256 output tile over p's K range (the whole K, a split-K plane or a stream-K piece)
 // the in-launch fold of a stream-K tile shared by several runs (GemmP.sk_*): piece `piece` of `np`
 // of SK tile `t` (first k-step tb of the SK range's tot steps over G runs; run wf holds piece 0)
+// (split-K with the in-launch fold, variant 32: tot = 0, the tile's S splits are pieces wf = 0 .. np - 1
+// with slots split_base + piece)
 struct SkFold {
     float* part; int* cnt;
     int64_t tot, tb;
     int G, wf, piece, np, t;
+    int64_t split_base;
 };
 constexpr int SK_TILE_F32 = 256 * 256;   // one partial tile: 4 waves x 64 accumulator quads x 64 lanes x 4
-// a run's partial slots: 0 = its first piece (its range starts inside that tile), 1 = its last
+// a run's partial slots: 0 = its first piece (its range starts inside that tile), 1 = its last; in
+// split mode the tile's S consecutive slots
 __device__ __forceinline__ float* sk_slot(const SkFold& f, int w) {
+    if (f.tot == 0) return f.part + (f.split_base + w) * SK_TILE_F32;
     const int64_t s0 = f.tot * w / f.G;
     return f.part + ((int64_t)w * 2 + (s0 >= f.tb ? 0 : 1)) * SK_TILE_F32;
 }
@@ -1461,7 +1466,7 @@ __device__ __forceinline__ void g8_tile(GemmP p, int tm, int tn, char* smem, con
     uint64_t te0 = 0;
     if (STAMP) { te0 = __builtin_amdgcn_s_memtime(); s_units += te0 - tprev; }
     __syncthreads();
-    if constexpr ((EXP & 1024) != 0) {   // stream-K build: a published piece ends here
+    if constexpr ((EXP & (1024 | 2048)) != 0) {   // stream-K / split-K fold builds: a published piece ends here
         if (fold != nullptr && !sk_fold_tile(*fold, acc, tid, lane, wid, smem)) return;
     }
 #ifdef KD_AB_BUILD
@@ -1536,7 +1541,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
                 tile_grouped(p_.sk_dp + t, tiles_m, tiles_n, tm, tn, p_.gm);
                 if (wl > wf) {   // a piece of a shared tile: folded in this launch by its last arriver
                     q.stagger = 0;
-                    f = SkFold{p_.sk_ws, p_.sk_cnt, tot, tb, G, wf, w - wf, wl - wf + 1, t};
+                    f = SkFold{p_.sk_ws, p_.sk_cnt, tot, tb, G, wf, w - wf, wl - wf + 1, t, 0};
                     fp = &f;
                 }
             }
@@ -1544,6 +1549,24 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
             s0 = e;
             __syncthreads();   // the next piece's DMA refills the LDS the epilogue staged through
         }
+        return;
+    }
+    if constexpr ((EXP & 2048) != 0) {   // split-K with the in-launch fold (variant 32): no partial planes,
+        // no reduce launch -- split blockIdx.y publishes its accumulators, the tile's last arriver sums the
+        // S pieces in split order and runs the full epilogue
+        GemmP q = p_;
+        const int64_t k0 = (int64_t)blockIdx.y * q.kchunk;
+        q.K = (int)min((int64_t)q.K - k0, q.kchunk);
+        q.A += A_MN ? k0 * q.lda : k0;
+        q.B += B_MN ? k0 * q.ldb : k0;
+        q.stagger = 0;
+        int tm, tn;
+        tile_of(q.gx, tiles_m, tiles_n, tm, tn, q.tile0, q.gm);
+        // this launch's tile index (tile_of's remap without the first-tile offset): tickets and slots
+        const int b = blockIdx.x, q8 = q.gx / 8, r8 = q.gx % 8, x = b % 8;
+        const int lt = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + b / 8;
+        const SkFold f{q.sk_ws, q.sk_cnt, 0, 0, 1, 0, (int)blockIdx.y, q.gy, lt, (int64_t)lt * q.gy};
+        g8_tile<A_MN, B_MN, EXP>(q, tm, tn, smem, &f);
         return;
     }
     GemmP p = p_;
@@ -2208,7 +2231,7 @@ static unsigned reduce_grid(int items) {
 }
 
 static bool variant_known(int v) {
-    if ((v >= 0 && v <= 7) || v == 16 || v == 21 || v == 24) return true;
+    if ((v >= 0 && v <= 7) || v == 16 || v == 21 || v == 24 || v == 32) return true;
 #ifdef KD_AB_BUILD
     if ((v >= 17 && v <= 20) || v == 22 || v == 23 || (v >= 26 && v <= 28) || v == 30) return true;
 #endif
@@ -2521,6 +2544,24 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
             p.tile0 = 0;
             launch_tiles(p, pl.dp_tiles, 1);
             KD_LAUNCH_CHECK("k_gemm (whole waves)");
+        }
+        if (force == 32 && pl.var == 16) {   // v8 split tiles folded in-launch (no planes, no reduce launch)
+            const int nt = tiles - pl.dp_tiles;
+            const size_t cnt_b = sk_cnt_bytes(nt);
+            KD_CHECK_ARG(d->workspace_bytes >= cnt_b + (size_t)nt * pl.split * SK_TILE_F32 * 4,
+                         "gemm: split-K fold workspace too small");
+            GemmP q = p;
+            q.kchunk = pl.kchunk; q.tile0 = pl.dp_tiles; q.gx = nt; q.gy = pl.split;
+            q.sk_cnt = (int*)d->workspace; q.sk_ws = (float*)((char*)d->workspace + cnt_b);
+            if (hipMemsetAsync(q.sk_cnt, 0, cnt_b, st) != hipSuccess) return fail(KD_ERR_LAUNCH, "gemm: split-K ticket memset");
+            const dim3 grid((unsigned)nt, (unsigned)pl.split);
+            const size_t lds = gemm2_lds<256, 256>();
+            if (!amn && !bmn) hipLaunchKernelGGL((k_gemm8<false, false, 2048>), grid, dim3(NTH8), lds, st, q);
+            else if (!amn && bmn) hipLaunchKernelGGL((k_gemm8<false, true, 2048>), grid, dim3(NTH8), lds, st, q);
+            else if (amn && bmn) hipLaunchKernelGGL((k_gemm8<true, true, 2048>), grid, dim3(NTH8), lds, st, q);
+            else hipLaunchKernelGGL((k_gemm8<true, false, 2048>), grid, dim3(NTH8), lds, st, q);
+            KD_LAUNCH_CHECK("k_gemm8 (split-K fold)");
+            return KD_OK;
         }
         GemmP pk = p;   // the split tiles write plain fp32 partial planes
         pk.C = d->workspace; pk.ldc = d->N; pk.c_f32 = 1; pk.accumulate = 0; pk.alpha = 1.f;

@@ -93,7 +93,7 @@ def test_epilogue_bias_act_residual_aux_accumulate(dev):
     assert (out - 0.5 * (a.float() @ w.float().t())).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("variant,split_k", [(1, 1), (5, 1), (6, 1), (7, 1), (16, 1), (16, 3), (0, 0), (21, 0)])
+@pytest.mark.parametrize("variant,split_k", [(1, 1), (5, 1), (6, 1), (7, 1), (16, 1), (16, 3), (0, 0), (21, 0), (32, 3)])
 def test_fp32_residual_stream(variant, split_k, dev):
     """C (fp32) = A B^T + bias + residual (fp32): the fp32 residual stream's epilogue (o_proj /
     fc2 / down_proj with kd_model_set_residual_f32) in every kernel and through the split-K
@@ -162,11 +162,11 @@ def test_variant_epilogue(variant, dev):
 
 
 @pytest.mark.parametrize("split", [2, 3, 7])
-@pytest.mark.parametrize("variant", [0, 6, 7, 16])
+@pytest.mark.parametrize("variant", [0, 6, 7, 16, 32])
 @pytest.mark.parametrize("M,N,K", [(520, 384, 2248), (1152, 1152, 5832)])
 def test_splitk_all_layouts(split, variant, M, N, K, dev):
-    """Forced K splits (fp32 partial planes + reduce) in every operand layout; K is not a
-    multiple of split*32, so the last split is ragged."""
+    """Forced K splits (fp32 partial planes + reduce; variant 32: v8 with the in-launch fold) in
+    every operand layout; K is not a multiple of split*32, so the last split is ragged."""
     ops = _ops()
     a = _rand(M, K, dev=dev, seed=50)
     w = _rand(N, K, dev=dev, seed=51, scale=0.05)
@@ -405,3 +405,20 @@ def test_stream_k_swiglu_matches_plain_stream_k(M, I, K, dev):
     _check(aux, g)
     _check(a, torch.nn.functional.silu(aux.float()[:, :I]) * aux.float()[:, I:])
     assert torch.equal(ops.gemm(h, w, act="swiglu", aux=aux, variant=21), a)   # deterministic
+
+
+@pytest.mark.parametrize("M,N,K,split", [(896, 896, 6144, 8), (1152, 4304, 5832, 3), (6144, 3584, 3584, 0)])
+def test_splitk_fold_equals_reduce(M, N, K, split, dev):
+    """Variant 32 (v8 split-K folded in-launch by each tile's last-arriving split) sums the S pieces
+    in split order like the reduce launch (x0 + x1 + ...): the same fp32 sums, and the same result
+    through the whole epilogue (fp32 += here; split 0: the cost model's plan, the hybrid tail).
+    Deterministic whichever split arrives last."""
+    ops = _ops()
+    a = _rand(K, M, dev=dev, seed=91)
+    b = _rand(K, N, dev=dev, seed=92, scale=0.05)
+    ref = torch.ones(M, N, dtype=torch.float32, device=dev)
+    ops.gemm(a.t(), b.t(), out=ref, accumulate=True, variant=16, split_k=split)
+    for _ in range(2):
+        got = torch.ones(M, N, dtype=torch.float32, device=dev)
+        ops.gemm(a.t(), b.t(), out=got, accumulate=True, variant=32, split_k=split)
+        assert torch.equal(got, ref), float((got - ref).abs().max())

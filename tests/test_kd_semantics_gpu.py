@@ -335,3 +335,63 @@ def test_rccl_world1_steps_equal_local(comm, tmp_path):
                MASTER_PORT=str(29900 + os.getpid() % 90))
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "rccl ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+class _RecordingDist:
+    """A stand-in process group for GradSync (one rank, nothing on the wire): records where in
+    the student backward each bucket is launched -- by kd_model_backward's per-part callbacks
+    (include/kdstep.h ABI 9) or by GradSync.end after the backward."""
+
+    class ReduceOp:
+        AVG, SUM = "avg", "sum"
+
+    class _Work:
+        def wait(self):
+            pass
+
+    def __init__(self):
+        self.launched = []
+
+    def get_world_size(self):
+        return 1
+
+    def get_backend(self):
+        return "nccl"
+
+    def all_reduce(self, t, op=None, async_op=False):
+        self.launched.append(int(t.numel()))
+        return self._Work()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("phase", [3, 2])
+def test_vit_gradient_buckets_launch_during_the_backward(phase, dev):
+    """BASELINE c4 (DT phase 3, every student tower trainable) / c3 (phase 2, ViT frozen) at the real
+    widths and full depth, bs 1: the data-parallel buckets are launched as kd_model_backward makes
+    each part of the flat gradient final -- the Qwen2 layers, then embed_tokens / projector, then the
+    SigLIP layers -- so what GradSync.end launches after the backward (grad_allreduce
+    .bytes_after_backward in bench.py) is at most one 256 MB bucket plus the SigLIP patch / position
+    embeddings (round 5 launched the whole ViT + projector + embed_tokens, 2.15 GB, there).
+    Every trainable element is reduced exactly once."""
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.dp import GradSync
+    from knowledge_distillation_for_sensory_substitution_in_multimodal_models_amd.data import synthetic_batch
+    K = _K()
+    m = K.OnlineKnowledgeDistillationLLavaOneVision("llava-hf/llava-onevision-qwen2-0.5b-ov-hf",
+                                                    "llava-hf/llava-onevision-qwen2-7b-ov-hf", phase=phase)
+    if phase == 2:
+        m.freeze_student_vision_layers()
+    rec = _RecordingDist()
+    m._gsync = GradSync(rec, m.student_model.P.grad)
+    loss = m.training_step(synthetic_batch(1, dev, L=1536, seed=0), 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    gs = m._gsync
+    lo, hi = m._trainable_range()
+    assert sum(gs.last_buckets) == hi - lo                          # the trainable range, once
+    tail_bytes = gs.last_tail * 4
+    emb = m.student_model.P.regions["vision"][0]
+    vis_embed = min(off for n, (off, _) in m.student_model.P.offsets.items()
+                    if ".encoder.layers.0." in n) - emb              # patch + position embeddings
+    assert tail_bytes <= gs.bucket_bytes + 4 * vis_embed, tail_bytes
+    assert tail_bytes <= 0.6e9
+    assert len(gs.last_buckets) >= (8 if phase == 3 else 5), gs.last_buckets

@@ -29,7 +29,7 @@
 # blas       PMC clock / MFMA-busy / FETCH of kd_gemm vs hipBLASLt on the big shapes (tools/pmc_vs_blas.sh)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 O=gpurun_out/$ROUND
 mkdir -p $O
 STEPS=${STEPS:-"tests parity bench prof"}
