@@ -85,6 +85,12 @@ def build(cfg, dev, teacher_fp8=False, grad_comm_dtype=None, teacher_residual_f3
     return m, opt
 
 
+def _progress(msg: str) -> None:
+    """A progress line on stderr (stdout carries the one JSON line): long phases -- the CPU
+    baseline's full-depth oracle steps -- would otherwise be silent for minutes."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def host_cpu_info():
     """(threads usable by this process, machine CPU count, CPU model): the process's
     affinity capped by its cgroup CPU quota (a GPU box shares its host; OMP_NUM_THREADS
@@ -151,6 +157,7 @@ def _oracle_step_times(kind, phase, depth, dtype, batch, warmup=0, steps=1):
     `warmup` untimed ones, on the same models (the gradients reset between steps, as zero_grad)."""
     import torch
     from oracle.model import kd_step_losses
+    _progress(f"cpu_baseline: building the oracle models ({str(dtype).replace('torch.', '')}, depth {depth or 'full'})")
     teacher, student, ssd, b = _oracle_models(kind, phase, depth, dtype, batch)
     out = []
     for i in range(warmup + steps):
@@ -160,6 +167,8 @@ def _oracle_step_times(kind, phase, depth, dtype, batch, warmup=0, steps=1):
         total, _ = kd_step_losses(kind, teacher, student, b, phase=phase)
         total.float().backward()
         dt = time.perf_counter() - t0
+        _progress(f"cpu_baseline {str(dtype).replace('torch.', '')} depth {depth or 'full'} step {i + 1}/"
+                  f"{warmup + steps}{' (warm-up)' if i < warmup else ''}: {dt:.2f} s")
         if i >= warmup:
             out.append(dt)
     del teacher, student, ssd, b
@@ -567,6 +576,7 @@ def main():
     hp = torch.cuda.Stream(device=dev, priority=int(os.environ.get("KD_MAIN_STREAM_PRIORITY", "0")))
     hp.wait_stream(torch.cuda.current_stream())
     torch.cuda.set_stream(hp)
+    _progress(f"{a.config}: model built, {a.warmup} warm-up + {a.steps} timed steps")
     for i in range(a.warmup):
         loss = step(i)
     torch.cuda.synchronize()
@@ -732,6 +742,7 @@ def main():
                 out["kd_loss_delta"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = host_cpu_info()[0]
+        _progress(f"timed region done ({value:.3f} samples/s); cpu_baseline on {threads} threads")
         try:
             out["cpu_baseline"] = cpu_baseline(cfg["kind"], cfg["phase"], threads, full=not a.cpu_extrapolate)
         except Exception as e:  # report, never hide

@@ -11,6 +11,8 @@
 #            -> full_depth_fp8.json
 # kindparity every other module (DT phases 1-3, FB, BD) at full depth vs the fp32 oracle
 #            (FULL_KINDS, default "dt1 dt2 dt3 fb bd") -> full_depth_kinds.json
+# sunparity  c1 at full depth on the SUNRGBD 480x640 geometry (5 tiles, L 2980) vs the fp32 oracle -> full_depth_sunrgbd.json
+# sunbench   bench.py --image 480x640 (the c1 line at SUNRGBD geometry) -> bench_c1_sunrgbd.json
 # c4parity   BASELINE c4 itself at full depth (DT phase 3 + fp8 lm_mlp teacher) vs the fp32 oracle -> c4_full_depth.json
 # hnprofile  the student's hidden-state error vs the fp32 oracle at SigLIP / Qwen2 depths -> depth_profile.json
 # fp8study   tools/fp8_c4_study.py: the c4 KD term's fp8-vs-bf16 move split into LoCa top-2 flips and smooth change,
@@ -52,6 +54,10 @@ for s in $STEPS; do
                 --out $O/full_depth_kinds.json > $O/full_depth_kinds.log 2>&1 || fail kindparity $O/full_depth_kinds.log ;;
     fullparity) timeout -k 10 900 python -u tools/parity_report.py --full-depth --floor --teacher-stream-ab \
                 --out $O/full_depth.json > $O/full_depth.log 2>&1 || fail fullparity $O/full_depth.log ;;
+    sunparity) timeout -k 10 900 python -u tools/parity_report.py --full-depth --image 480x640 \
+                --out $O/full_depth_sunrgbd.json > $O/full_depth_sunrgbd.log 2>&1 || fail sunparity $O/full_depth_sunrgbd.log ;;
+    sunbench) timeout -k 10 600 python -u bench.py --image 480x640 --no-cpu-baseline > $O/bench_c1_sunrgbd.json 2> $O/bench_sun.err || fail sunbench $O/bench_sun.err
+            tail -1 $O/bench_c1_sunrgbd.json | cut -c1-240 ;;
     c4parity) timeout -k 10 900 python -u tools/parity_report.py --c4-full-depth --out $O/c4_full_depth.json \
                 > $O/c4_full_depth.log 2>&1 || fail c4parity $O/c4_full_depth.log ;;
     hnprofile) timeout -k 10 900 python -u tools/parity_report.py --depth-profile --out $O/depth_profile.json \
