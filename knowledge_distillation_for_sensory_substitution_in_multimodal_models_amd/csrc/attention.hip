@@ -876,7 +876,8 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dkdv2(AttnBwdP p) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int qh0 = q0 + 32 * ks;
-            if (CAUSAL && qh0 + 31 < kw0) continue;
+            // no key of this wave (past the sequence end) or no query at or past one (causal): P = 0
+            if (kw0 >= p.S || (CAUSAL && qh0 + 31 < kw0)) continue;
             // S, dP for query rows qh0 + 16qs' + 4g + r (qs' = 0, 1) and both key sub-tiles
             f32x4 s[2][2], dp[2][2];
 #pragma unroll
@@ -1280,6 +1281,457 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
         }
 }
 
+
+// ------------------------------------------------------ backward, 32x32x16 MFMAs ----
+// The 16x16x32 backward above is bound by vector issue (an MFMA of 16 cycles holds the SIMD's
+// issue for 8 of them, and every 16x16 tile carries its own LDS fragment reads and softmax
+// VALU): ~0.17 of the MFMA peak. These two kernels compute the same products with 32x32x16
+// MFMAs (issue held 8 of 32 cycles, half the LDS bytes per FLOP), the forward's layout tricks
+// reused:
+//   k_attn_bwd_dq32: per wave 32 queries (query on the lane). S^T = K Q^T and dP^T = V dO^T
+//     (A = K / V rows from LDS, B = the wave's Q / dO rows in registers), dS^T in the same
+//     registers, then dQ^T += K^T dS^T with the dS^T accumulator as the B operand (keys in the
+//     forward's permuted order, K^T by ds_read_b64_tr_b16 in that order).
+//   k_attn_bwd_dkdv32: per wave 32 keys (key on the lane). S = Q K^T and dP = dO V^T (A = Q /
+//     dO rows from LDS, B = the wave's K / V rows in registers), then dV^T += dO^T P and
+//     dK^T += Q^T dS with P / dS as the B operand (queries permuted the same way).
+// One LDS image per tile serves both read directions (swQ below); all LDS reads in the loops
+// are asm with counted lgkmcnt waits (a compiler-visible LDS read beside the in-flight LDS-DMA
+// of the next tile is preceded by vmcnt(0)).
+
+// swQ: chunk swizzle of an image read by rows (ds_read_b128: a 16-lane group reads one chunk
+// of 16 rows whose indices cover every residue mod 16) AND by the 32x32 transposed reads (a
+// 32-lane half reads 4 consecutive rows x 64 B). A bijection of the row's low 4 bits (RB 256)
+// or bits 1-3 (RB 128, two rows per 256-B bank line) onto the chunk index -- row reads
+// conflict-free -- whose top bits (RB 256: chunk bits 2-3 from row bits 0-1; RB 128: chunk bit 2
+// from row bit 1, beside the row parity) put 4 consecutive rows in 4 different 64-B bank blocks.
+template <int RB> __device__ __forceinline__ int swQ(int r) {
+    return RB == 256 ? (((r & 3) << 2) | ((r >> 2) & 3)) : ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
+}
+
+// 64 rows x ncols of a row-strided bf16 matrix (ld elements per row) -> swQ image [64][RB];
+// rows >= S and columns >= ncols land as zeros (out-of-range buffer offsets)
+template <int HDP>
+__device__ __forceinline__ void stage_q32(char* lds, const bf16* base, int64_t ld, int ncols, int row0, int S, int wid,
+                                          int lane) {
+    constexpr int RB = Geo<HDP>::RB, ROWS_PER = 1024 / RB, CH = RB / 16, NINSTR = 64 / ROWS_PER;
+    const int rows_valid = min(64, S - row0);
+    const uint32_t bytes = rows_valid <= 0 ? 0u : (uint32_t)(((int64_t)(rows_valid - 1) * ld + ncols) * 2);
+    auto rs = rsrc(base + (int64_t)(rows_valid <= 0 ? 0 : row0) * ld, bytes);
+#pragma unroll
+    for (int s = 0; s < NINSTR / 4; ++s) {
+        const int i = wid * (NINSTR / 4) + s;
+        const int r = i * ROWS_PER + lane / CH;
+        const int gc = (lane % CH) ^ swQ<RB>(r);
+        const uint32_t voff = (gc * 8 < ncols && r < rows_valid) ? (uint32_t)((r * ld + gc * 8) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(lds + i * 1024), 16, voff, 0, 0, 0);
+    }
+}
+
+// LDS reads at a per-lane address + an immediate offset (`off` must fold to a constant once the
+// caller is inlined and unrolled)
+__device__ __forceinline__ u32x4 ds_b128(uint32_t addr, const int off) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+    return v;
+}
+__device__ __forceinline__ u32x2 ds_tr(uint32_t addr, const int off) {
+    u32x2 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+    return v;
+}
+// s_waitcnt lgkmcnt(N) naming the register it retires (no compiler copy above the wait)
+template <int N, typename T> __device__ __forceinline__ void wait_lgkm(T& r) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(r) : "i"(N) : "memory");
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) { (f(std::integral_constant<int, I>{}), ...); }
+template <int N, typename F> __device__ __forceinline__ void sfor(F&& f) { sfor_impl(f, std::make_integer_sequence<int, N>{}); }
+
+// two KS-step MFMA chains, A rows read from LDS, B in registers:
+//   c0 += A(rows at a + OFF0) . b0,  c1 += A(rows at a + OFF1) . b1   (16-deep steps kk = 0 .. KS-1)
+// every read issued one MFMA ahead of its use; `a[kk]` is the lane's byte address of step kk.
+// INIT: c0 / c1 start from i0 / i1 (4 x 4 dwords each, LDS reads the caller issued before this
+// call), retired by the first fragment wait, which names them (LDS returns in order)
+// FILL(std::integral_constant<int, m>) runs after the m-th MFMA (m = 0 .. 2 KS - 1) is issued: VALU
+// work of an earlier tile placed in the MFMA gaps (sched_barrier-fenced, so it stays there).
+struct NoFill {
+    template <typename T> __device__ __forceinline__ void operator()(T) const {}
+};
+template <int KS, int OFF0, int OFF1, bool INIT = false, typename FILL = NoFill>
+__device__ __forceinline__ void chain2(f32x16& c0, f32x16& c1, const uint32_t (&a)[KS], const bf16x8 (&b0)[KS],
+                                       const bf16x8 (&b1)[KS], u32x4 (&i0)[4], u32x4 (&i1)[4], FILL fill = FILL{}) {
+    u32x4 x0[KS], x1[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) x0[kk] = ds_b128(a[kk], OFF0);
+    sfor<KS>([&](auto kc) {
+        constexpr int kk = decltype(kc)::value;
+        // in flight after x0[kk]: x0[kk + 1 ..] and x1[.. kk - 1]
+        if constexpr (INIT && kk == 0) {
+            asm volatile("s_waitcnt lgkmcnt(%9)"
+                         : "+v"(x0[0]), "+v"(i0[0]), "+v"(i0[1]), "+v"(i0[2]), "+v"(i0[3]), "+v"(i1[0]), "+v"(i1[1]),
+                           "+v"(i1[2]), "+v"(i1[3])
+                         : "i"(KS - 1)
+                         : "memory");
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    c0[4 * g + r] = __uint_as_float(i0[g][r]);
+                    c1[4 * g + r] = __uint_as_float(i1[g][r]);
+                }
+        } else {
+            wait_lgkm<KS - 1>(x0[kk]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x0[kk]), b0[kk], c0, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        x1[kk] = ds_b128(a[kk], OFF1);
+        fill(std::integral_constant<int, kk>{});
+        __builtin_amdgcn_sched_barrier(0);
+    });
+    sfor<KS>([&](auto kc) {
+        constexpr int kk = decltype(kc)::value;
+        wait_lgkm<KS - 1 - kk>(x1[kk]);
+        __builtin_amdgcn_sched_barrier(0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x1[kk]), b1[kk], c1, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        fill(std::integral_constant<int, KS + kk>{});
+        __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// s_waitcnt lgkmcnt(M), then every register of `r` named (no use of them above the wait): the M
+// LDS reads issued after r's last are left in flight
+template <int M, int N> __device__ __forceinline__ void wait_lgkm_n(u32x2 (&r)[N]) {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(M) : "memory");
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(r[i]));
+}
+// plain f32 subtract / multiply as single instructions (the compiler's SLP pass would pair them
+// into v_pk_* ops, which cost more than two single ops beside MFMAs)
+__device__ __forceinline__ float f32_sub(float a, float b) {
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float f32_mul(float a, float b) {
+    float r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// s_waitcnt lgkmcnt(0), then every register of `r` named (no use of them above the wait)
+template <int N> __device__ __forceinline__ void wait_lgkm0_all(u32x2 (&r)[N]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(r[i]));
+}
+
+// per-lane byte addresses of the 32x32 transposed reads (the forward's V^T pattern): lane reads
+// rows 4 hf + ((lane >> 2) & 3) (x = 0) and + 8 (x = 1), 4 columns at 32 D + 16 ((lane >> 4) & 1)
+// + 4 (lane & 3); further rows (16 s, 32 ks) are immediates (swQ reads only row bits 0-3)
+template <int HDP, int ND>
+__device__ __forceinline__ void tr_addrs32(uint32_t (&ta)[ND][2], uint32_t base, int lane) {
+    constexpr int RB = Geo<HDP>::RB;
+    const int row = 4 * (lane >> 5) + ((lane >> 2) & 3);
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            const int r = row + 8 * x;
+            const int col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            ta[d][x] = base + r * RB + ((((col >> 3) ^ swQ<RB>(r))) << 4) + ((col & 4) << 1);
+        }
+}
+
+// dQ for 128 query rows of one head (4 waves x 32 queries), K / V tiles of 64 keys double-
+// buffered by LDS-DMA; also writes delta = rowsum(dO * O) for the dK / dV kernel (launched after)
+// DIAG (A/B library timing diagnostics only; wrong results): 1 = no K/V staging after the first tile
+// (compute + barriers alone), 2 = staging without the end-of-tile vmcnt / barrier wait, 3 = neither
+// staging nor waits (compute alone), 4 = as 3 with every tile taking the edge path
+// PIPE: interior tiles software-pipelined (softmax in the MFMA gaps; 182 / 236 VGPRs at hd 64 / 96).
+// The product runs it at two workgroups per CU; the unpipelined build (163 VGPRs at hd 64: three per CU)
+// measured equal at hd 96 and 4 % slower at hd 64 (A/B: KD_ATTN_BWD_V=3).
+template <int HDP, bool CAUSAL, int OCC = 2, int DIAG = 0, bool PIPE = true>
+__global__ void __launch_bounds__(256, OCC) k_attn_bwd_dq32(AttnBwdP p) {
+    constexpr int RB = Geo<HDP>::RB, TILE = 64 * RB;
+    constexpr int KS = HDP == 96 ? 5 : HDP / 16;              // 16-deep steps (hd <= 16 KS)
+    constexpr int ND = HDP == 64 ? 2 : (HDP == 96 ? 3 : 4);   // 32-dim dQ^T tiles
+    extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][K TILE | V TILE], swQ images
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r32 = lane & 31, hf = lane >> 5;
+    const int nqb = (p.S + 127) / 128;
+    int h, b, zb;
+    gqa_xcd_map(p.H, p.HKV, p.B, h, b, zb);
+    const int qb = CAUSAL ? (nqb - 1 - zb) : zb;
+    const int kvh = h / (p.H / p.HKV);
+    const bf16* Q = p.q + ((int64_t)(b * p.H + h) * p.S) * HDP;
+    const bf16* K = p.k + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const bf16* V = p.v + ((int64_t)(b * p.HKV + kvh) * p.S) * HDP;
+    const int q0 = qb * 128 + wid * 32;   // the wave's first query (uniform)
+    const int myq = q0 + r32;
+    const bool qok = myq < p.S;
+
+    // the lane's Q and dO chunks (the B operands), delta = rowsum(dO * O) over both lane halves
+    bf16x8 qf[KS], df[KS];
+    float dsum = 0.f;
+    {
+        const int64_t orow = (((int64_t)b * p.S + (qok ? myq : 0)) * p.H + h) * p.hd;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            const int d0 = 16 * kk + 8 * hf;
+            qf[kk] = qok ? *(const bf16x8*)(Q + (int64_t)myq * HDP + d0) : (bf16x8){};
+            const bool in = qok && d0 < p.hd;
+            df[kk] = in ? *(const bf16x8*)(p.dO + orow + d0) : (bf16x8){};
+            const bf16x8 of = in ? *(const bf16x8*)(p.o + orow + d0) : (bf16x8){};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dsum = __builtin_fmaf((float)df[kk][e], (float)of[e], dsum);
+        }
+    }
+    dsum = half_sum(dsum);
+    const float dl = qok ? dsum : 0.f;
+    if (qok && hf == 0) p.delta[((int64_t)b * p.H + h) * p.S + myq] = dsum;
+    const float lse2 = qok ? p.lse[((int64_t)b * p.H + h) * p.S + myq] * 1.4426950408889634f : 0.f;
+
+    f32x16 acc[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[d][i] = 0.f;
+
+    const int nkv_all = (p.S + 63) / 64;
+    const int nkv = CAUSAL ? min((qb * 128 + 127) / 64 + 1, nkv_all) : nkv_all;
+    // tiles with a key <= the wave's last query (none for a wave past the sequence end)
+    const int nkv_w = q0 >= p.S ? 0 : (CAUSAL ? min(nkv, (q0 + 31) / 64 + 1) : nkv);
+    stage_q32<HDP>(smem, K, HDP, HDP, 0, p.S, wid, lane);
+    stage_q32<HDP>(smem + TILE, V, HDP, HDP, 0, p.S, wid, lane);
+    const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+    uint32_t ra[KS];   // row reads: row r32 (+ 32 kt), chunk 2 kk + hf
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) ra[kk] = sbase + r32 * RB + (((2 * kk + hf) ^ swQ<RB>(r32)) << 4);
+    uint32_t ta[ND][2];
+    tr_addrs32<HDP, ND>(ta, sbase, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    auto tile = [&](const int t, auto buf_c) {
+        constexpr int BUF = decltype(buf_c)::value;
+        constexpr int KO = BUF * 2 * TILE, VO = KO + TILE;
+        if (DIAG != 1 && DIAG != 3 && DIAG != 4 && t + 1 < nkv) {
+            char* nb = smem + (BUF ^ 1) * 2 * TILE;
+            stage_q32<HDP>(nb, K, HDP, HDP, (t + 1) * 64, p.S, wid, lane);
+            stage_q32<HDP>(nb + TILE, V, HDP, HDP, (t + 1) * 64, p.S, wid, lane);
+        }
+        const bool edge = DIAG == 4 || t * 64 + 63 >= p.S || (CAUSAL && t * 64 + 63 > q0);   // a key past S or a query
+        if (PIPE && t < nkv_w && !edge) {
+            // interior tile, software-pipelined: the softmax of keys 0-31 runs in the MFMA gaps of
+            // keys 32-63's S^T / dP^T chains, that of keys 32-63 in the gaps of dQ's first two key steps
+            f32x16 sc[2], dp[2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { sc[kt][i] = 0.f; dp[kt][i] = 0.f; }
+            u32x4 nz[4];
+            bf16x8 dsf[4];
+            // dS^T elements [I0, I0 + N) of sub-tile KT, staged so no result is used by the next
+            // instruction (fma .. exp .. sub .. mul), single-lane f32 ops (no packed pairs beside MFMAs)
+            auto sm = [&](auto kt_c, auto i0_c, auto n_c) {
+                constexpr int KT = decltype(kt_c)::value, I0 = decltype(i0_c)::value, N = decltype(n_c)::value;
+                if constexpr (N > 0) {
+                    float x[N], y[N];
+                    sfor<N>([&](auto j) { x[j] = fmaf(sc[KT][I0 + j], p.scale_log2, -lse2); });
+                    sfor<N>([&](auto j) { x[j] = __builtin_amdgcn_exp2f(x[j]); });
+                    sfor<N>([&](auto j) { y[j] = f32_sub(dp[KT][I0 + j], dl); });
+                    sfor<N>([&](auto j) {
+                        constexpr int i = I0 + decltype(j)::value;
+                        dsf[2 * KT + (i >> 3)][i & 7] = (bf16)f32_mul(x[j], y[j]);
+                    });
+                }
+            };
+            // slot m of n slots gets elements [lo(m), lo(m + 1)) of `cnt` starting at `base`
+            auto part = [&](auto kt_c, auto base_c, auto cnt_c, auto n_c, auto m_c) {
+                constexpr int base = decltype(base_c)::value, cnt = decltype(cnt_c)::value;
+                constexpr int n = decltype(n_c)::value, m = decltype(m_c)::value;
+                constexpr int lo = base + cnt * m / n, hi = base + cnt * (m + 1) / n;
+                sm(kt_c, std::integral_constant<int, lo>{}, std::integral_constant<int, hi - lo>{});
+            };
+            using I0c = std::integral_constant<int, 0>;
+            using I1c = std::integral_constant<int, 1>;
+            chain2<KS, KO, VO>(sc[0], dp[0], ra, qf, df, nz, nz);   // keys 0-31: S^T = K Q^T, dP^T = V dO^T
+            // keys 32-63, sub-tile 0's softmax in MFMA gaps 2 .. 2 KS - 1 (dP^T of keys 0-31 lands first)
+            chain2<KS, KO + 32 * RB, VO + 32 * RB, false>(sc[1], dp[1], ra, qf, df, nz, nz, [&](auto m_c) {
+                constexpr int m = decltype(m_c)::value;
+                if constexpr (m >= 2)
+                    part(I0c{}, I0c{}, std::integral_constant<int, 16>{}, std::integral_constant<int, 2 * KS - 2>{},
+                         std::integral_constant<int, m - 2>{});
+            });
+            // dQ^T += K^T dS^T: key steps 0-1 (keys 0-31) beside sub-tile 1's first 8 elements, key step 2
+            // beside its last 8, then key step 3; every K^T read issued before the first of these MFMAs
+            u32x2 kc[ND * 4], kd[ND * 4];
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    kc[4 * d + 2 * s] = ds_tr(ta[d][0], KO + 16 * s * RB);
+                    kc[4 * d + 2 * s + 1] = ds_tr(ta[d][1], KO + 16 * s * RB);
+                }
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    kd[4 * d + 2 * s] = ds_tr(ta[d][0], KO + 16 * (s + 2) * RB);
+                    kd[4 * d + 2 * s + 1] = ds_tr(ta[d][1], KO + 16 * (s + 2) * RB);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            wait_lgkm_n<ND * 4>(kc);   // the kd reads (issued after) may still be in flight
+            __builtin_amdgcn_sched_barrier(0);
+            sfor<2 * ND>([&](auto m_c) {
+                constexpr int m = decltype(m_c)::value, d = m >> 1, s = m & 1;
+                acc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    cat4(__builtin_bit_cast(bf16x4, kc[4 * d + 2 * s]), __builtin_bit_cast(bf16x4, kc[4 * d + 2 * s + 1])),
+                    dsf[s], acc[d], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                part(I1c{}, I0c{}, std::integral_constant<int, 8>{}, std::integral_constant<int, 2 * ND>{}, m_c);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            wait_lgkm0_all(kd);
+            __builtin_amdgcn_sched_barrier(0);
+            sfor<ND>([&](auto d_c) {
+                constexpr int d = decltype(d_c)::value;
+                acc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    cat4(__builtin_bit_cast(bf16x4, kd[4 * d]), __builtin_bit_cast(bf16x4, kd[4 * d + 1])), dsf[2], acc[d], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                part(I1c{}, std::integral_constant<int, 8>{}, std::integral_constant<int, 8>{}, std::integral_constant<int, ND>{}, d_c);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+                acc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    cat4(__builtin_bit_cast(bf16x4, kd[4 * d + 2]), __builtin_bit_cast(bf16x4, kd[4 * d + 3])), dsf[3], acc[d], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        } else if (t < nkv_w) {
+            f32x16 sc[2], dp[2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { sc[kt][i] = 0.f; dp[kt][i] = 0.f; }
+            u32x4 nz[4];
+            chain2<KS, KO, KO + 32 * RB>(sc[0], sc[1], ra, qf, qf, nz, nz);   // S^T = K Q^T (two 32-key sub-tiles)
+            chain2<KS, VO, VO + 32 * RB>(dp[0], dp[1], ra, df, df, nz, nz);   // dP^T = V dO^T
+            if (edge) {
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int key = t * 64 + 32 * kt + 8 * (i >> 2) + 4 * hf + (i & 3);
+                        if (key >= p.S || (CAUSAL && key > myq)) sc[kt][i] = -INFINITY;
+                    }
+            }
+            // dS^T = P (dP - delta), P = 2^(s scale_log2 - lse2); packed to bf16 in the forward's
+            // permuted key order (k-step s: registers 8 (s & 1) .. + 7 of sub-tile s >> 1)
+            bf16x8 dsf[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int kt = s >> 1, i = 8 * (s & 1) + j;
+                    const float pe = __builtin_amdgcn_exp2f(fmaf(sc[kt][i], p.scale_log2, -lse2));
+                    dsf[s][j] = (bf16)(pe * (dp[kt][i] - dl));
+                }
+            // dQ^T += K^T dS^T: per 32-dim tile 8 transposed K reads (4 key steps x rows +0 / +8)
+            u32x2 kr[2][8];
+#define KD_DQ_RD(D, SET)                                                              \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                   \
+        kr[SET][2 * s] = ds_tr(ta[D][0], KO + 16 * s * RB);                           \
+        kr[SET][2 * s + 1] = ds_tr(ta[D][1], KO + 16 * s * RB);                       \
+    }
+#define KD_DQ_MM(D, SET)                                                                                           \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                                                \
+        const bf16x8 kv = cat4(__builtin_bit_cast(bf16x4, kr[SET][2 * s]), __builtin_bit_cast(bf16x4, kr[SET][2 * s + 1])); \
+        acc[D] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kv, dsf[s], acc[D], 0, 0, 0);                           \
+    }
+#define KD_DQ_WAIT(N, SET) wait_lgkm_def8<N>(kr[SET]); __builtin_amdgcn_sched_barrier(0);
+            KD_DQ_RD(0, 0)
+            KD_DQ_RD(1, 1)
+            KD_DQ_WAIT(8, 0)
+            KD_DQ_MM(0, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ND > 2) { KD_DQ_RD(2, 0) KD_DQ_WAIT(8, 1) }
+            else { KD_DQ_WAIT(0, 1) }
+            KD_DQ_MM(1, 1)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ND > 2) {
+                if constexpr (ND > 3) { KD_DQ_RD(3, 1) KD_DQ_WAIT(8, 0) }
+                else { KD_DQ_WAIT(0, 0) }
+                KD_DQ_MM(2, 0)
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (ND > 3) {
+                    KD_DQ_WAIT(0, 1)
+                    KD_DQ_MM(3, 1)
+                }
+            }
+#undef KD_DQ_RD
+#undef KD_DQ_MM
+#undef KD_DQ_WAIT
+        }
+        if (DIAG < 2) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    };
+    int t = 0;
+    for (; t + 1 < nkv; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        tile(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nkv) tile(t, std::integral_constant<int, 0>{});
+
+    // lane = query myq, register 4 g + r of tile D = dim 32 D + 8 g + 4 hf + r
+    if (qok) {
+        if (p.dqkv) {   // the merged row: (bf16) of the scaled fp32 value, as kd_qkv_merge rounds it
+            f32x16 v[ND];
+#pragma unroll
+            for (int d = 0; d < ND; ++d) v[d] = acc[d] * p.scale;
+            if (p.rcos) {   // RoPE transpose (hd == HDP, hd % 32 == 0): columns c, c + hd/2 are tiles D, D + ND/2
+                const int hh = p.hd / 2;
+                const float* cr = p.rcos + (int64_t)myq * hh;
+                const float* sr = p.rsin + (int64_t)myq * hh;
+#pragma unroll
+                for (int d = 0; d < ND / 2; ++d)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int c = 32 * d + 8 * (i >> 2) + 4 * hf + (i & 3);
+                        float y1, y2;
+                        rope_t(v[d][i], v[d + ND / 2][i], cr[c], sr[c], y1, y2);
+                        v[d][i] = y1; v[d + ND / 2][i] = y2;
+                    }
+            }
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    put_qkv4(p, b, myq, h, 32 * d + 8 * g + 4 * hf,
+                             (bf16x4){(bf16)v[d][4 * g], (bf16)v[d][4 * g + 1], (bf16)v[d][4 * g + 2], (bf16)v[d][4 * g + 3]});
+        } else {
+            float* dQr = p.dq + ((int64_t)(b * p.H + h) * p.S + myq) * HDP;
+#pragma unroll
+            for (int d = 0; d < ND; ++d)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    *(f32x4*)(dQr + 32 * d + 8 * g + 4 * hf) =
+                        (f32x4){acc[d][4 * g], acc[d][4 * g + 1], acc[d][4 * g + 2], acc[d][4 * g + 3]} * p.scale;
+        }
+    }
+}
+
+#ifdef KD_AB_BUILD
+#include "attention_bwd_dkdv32.inc"   // tools/ab/attention_bwd_dkdv32.inc: the 32x32x16 dK / dV kernel (KD_ATTN_BWD_V=32)
+#endif  // KD_AB_BUILD
+
 }  // namespace
 
 #ifdef KD_AB_BUILD
@@ -1374,6 +1826,43 @@ void launch_dkdv(bool kv16, dim3 grid, size_t smem, hipStream_t st, const AttnBw
     }
 }
 
+// dQ (+ delta) by the 32x32x16 k_attn_bwd_dq32 (head dims 64 / 96). A/B library: `diag` 1 = the
+// unpipelined build (hd 64: three workgroups per CU), 2-5 = its DIAG builds 1-4
+template <int HD, bool C>
+int launch_dq32(int diag, dim3 grid_q, size_t smem_q, hipStream_t st, const AttnBwdP& p) {
+    if constexpr (HD == 128) {
+        (void)diag; (void)grid_q; (void)smem_q; (void)st; (void)p;
+        return fail(KD_ERR_SHAPE, "attn_bwd: no 32x32 dQ kernel for head dim 128");
+    } else {
+#ifdef KD_AB_BUILD
+        if (diag == 1) hipLaunchKernelGGL((k_attn_bwd_dq32<HD, C, HD == 64 ? 3 : 2, 0, false>), grid_q, dim3(256), smem_q, st, p);
+        else if (diag == 2) hipLaunchKernelGGL((k_attn_bwd_dq32<HD, C, 2, 1>), grid_q, dim3(256), smem_q, st, p);
+        else if (diag == 3) hipLaunchKernelGGL((k_attn_bwd_dq32<HD, C, 2, 2>), grid_q, dim3(256), smem_q, st, p);
+        else if (diag == 4) hipLaunchKernelGGL((k_attn_bwd_dq32<HD, C, 2, 3>), grid_q, dim3(256), smem_q, st, p);
+        else if (diag == 5) hipLaunchKernelGGL((k_attn_bwd_dq32<HD, C, 2, 4>), grid_q, dim3(256), smem_q, st, p);
+        else
+#endif
+        hipLaunchKernelGGL((k_attn_bwd_dq32<HD, C>), grid_q, dim3(256), smem_q, st, p);
+        (void)diag;
+        KD_LAUNCH_CHECK("k_attn_bwd_dq32");
+        return KD_OK;
+    }
+}
+
+#ifdef KD_AB_BUILD
+template <int HD, bool C>
+int launch_dkdv32(dim3 grid, size_t smem_kv, hipStream_t st, const AttnBwdP& p) {
+    if constexpr (HD == 128) {
+        (void)grid; (void)smem_kv; (void)st; (void)p;
+        return fail(KD_ERR_SHAPE, "attn_bwd: no 32x32 dK / dV kernel for head dim 128");
+    } else {
+        hipLaunchKernelGGL((k_attn_bwd_dkdv32<HD, C>), grid, dim3(256), smem_kv, st, p);
+        KD_LAUNCH_CHECK("k_attn_bwd_dkdv32");
+        return KD_OK;
+    }
+}
+#endif  // KD_AB_BUILD
+
 size_t attn_bwd_workspace_size(const kd_attn_bwd_desc* d) {
     if (!d || d->HKV <= 0 || d->H == d->HKV) return 0;
     return (size_t)2 * d->B * d->H * d->S * d->hdp * 4;
@@ -1407,32 +1896,55 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
                d->dq, (bf16*)d->dk, (bf16*)d->dv, dkp, dvp, d->B, d->H, d->HKV, d->S, d->hd, (float)sc,
                (float)(sc * 1.4426950408889634), (bf16*)d->dqkv, d->ld_qkv, d->cos_t, d->sin_t};
 #ifdef KD_AB_BUILD
-    // dK / dV: two 16-key sub-tiles per wave by default; KD_ATTN_BWD_V=16 selects the one-sub-tile
-    // kernel, KD_ATTN_DQ_NQ=1 one query sub-tile per dQ wave (A/B; read per call)
+    // head dims 64 / 96 (A/B; read per call): unset / 0 = the product pair (k_attn_bwd_dq32 +
+    // k_attn_bwd_dkdv2); 2 = the round-6 16x16x32 pair (k_attn_bwd_dq + k_attn_bwd_dkdv2); 16 = the
+    // one-sub-tile dK / dV kernel; 32 = k_attn_bwd_dq32 + k_attn_bwd_dkdv32; 3 / 5-8 = dq32 unpipelined
+    // (hd 64: three workgroups per CU) / its DIAG builds 1-4 (timing only). KD_ATTN_DQ_NQ=1: one query sub-tile per
+    // 16x16 dQ wave
     const char* bve = std::getenv("KD_ATTN_BWD_V");
-    const bool kv16 = bve && std::atoi(bve) == 16;
+    const int bv = bve ? std::atoi(bve) : 0;
+    const bool kv16 = bv == 16, dq32 = bv != 2 && bv != 16, kv32 = bv == 32;
+    const int diag = bv == 3 ? 1 : (bv >= 5 && bv <= 8 ? bv - 3 : 0);
     static const int nq_dq = [] { const char* e = std::getenv("KD_ATTN_DQ_NQ"); return (e && e[0] == '1') ? 1 : 2; }();
 #else
-    constexpr bool kv16 = false;
-    constexpr int nq_dq = 2;
+    constexpr bool kv16 = false, dq32 = true;
+    constexpr int diag = 0, nq_dq = 2;
 #endif
     dim3 grid(d->H, d->B, kv16 ? (d->S + 63) / 64 : (d->S + 127) / 128);
-    dim3 grid_q(d->H, d->B, (d->S + 64 * nq_dq - 1) / (64 * nq_dq));
+    const int qrows = dq32 ? 128 : 64 * nq_dq;   // query rows per dQ workgroup
+    dim3 grid_q(d->H, d->B, (d->S + qrows - 1) / qrows);
     const int rb = d->hdp == 64 ? 128 : 256;
     const size_t smem_kv = 2 * (2 * 64 * rb + 512);
     const size_t smem_q = 2 * 2 * 64 * rb;
+#ifdef KD_AB_BUILD
+#define KD_AB_KV32(HD, C)                                                                     \
+    if (HD != 128 && kv32) {                                                                  \
+        const int rc = launch_dkdv32<HD, C>(grid, smem_kv, st, p);                            \
+        if (rc != KD_OK) return rc;                                                           \
+        break;                                                                                \
+    }
+#else
+#define KD_AB_KV32(HD, C)
+#endif
 #define LAUNCH(HD, C)                                                                         \
     do {                                                                                      \
-        if (nq_dq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p); \
-        else launch_dq1<HD, C>(grid_q, smem_q, st, p);                                                   \
-        KD_LAUNCH_CHECK("k_attn_bwd_dq");                                                     \
-        launch_dkdv<HD, C>(kv16, grid, smem_kv, st, p);                                     \
+        if (HD != 128 && dq32) {                                                              \
+            const int rc = launch_dq32<HD, C>(diag, grid_q, smem_q, st, p);                   \
+            if (rc != KD_OK) return rc;                                                       \
+        } else {                                                                              \
+            if (nq_dq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p); \
+            else launch_dq1<HD, C>(grid_q, smem_q, st, p);                                    \
+            KD_LAUNCH_CHECK("k_attn_bwd_dq");                                                 \
+        }                                                                                     \
+        KD_AB_KV32(HD, C)                                                                     \
+        launch_dkdv<HD, C>(kv16, grid, smem_kv, st, p);                                       \
         KD_LAUNCH_CHECK("k_attn_bwd_dkdv");                                                   \
     } while (0)
     if (d->hdp == 64) { if (d->causal) LAUNCH(64, true); else LAUNCH(64, false); }
     else if (d->hdp == 96) { if (d->causal) LAUNCH(96, true); else LAUNCH(96, false); }
     else { if (d->causal) LAUNCH(128, true); else LAUNCH(128, false); }
 #undef LAUNCH
+#undef KD_AB_KV32
     if (need) {
         const int dcols = 16 * (d->hdp == 64 ? 4 : (d->hdp == 96 ? 5 : 8));
         const int64_t work = (int64_t)d->B * d->HKV * d->S * dcols / 4;
