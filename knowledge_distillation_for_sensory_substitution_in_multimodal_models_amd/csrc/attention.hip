@@ -1457,6 +1457,8 @@ __device__ __forceinline__ void tr_addrs32(uint32_t (&ta)[ND][2], uint32_t base,
 // measured equal at hd 96 and 4 % slower at hd 64 (A/B: KD_ATTN_BWD_V=3).
 template <int HDP, bool CAUSAL, int OCC = 2, int DIAG = 0, bool PIPE = true>
 __global__ void __launch_bounds__(256, OCC) k_attn_bwd_dq32(AttnBwdP p) {
+    // hd 128 would need lgkmcnt(16) below (the counter holds 15) and more VGPRs than two waves allow
+    static_assert(HDP == 64 || HDP == 96, "k_attn_bwd_dq32: head dims 64 / 96");
     constexpr int RB = Geo<HDP>::RB, TILE = 64 * RB;
     constexpr int KS = HDP == 96 ? 5 : HDP / 16;              // 16-deep steps (hd <= 16 KS)
     constexpr int ND = HDP == 64 ? 2 : (HDP == 96 ? 3 : 4);   // 32-dim dQ^T tiles
