@@ -69,7 +69,9 @@ def build(verbose: bool = False, jobs: int | None = None, ab: bool = False) -> P
         if not ab:
             _try_c_host(verbose)
         return lib
-    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(lib)]
+    # the A/B library also links hipBLASLt (tools/ab/gemm_blas.inc); the product library links no BLAS
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(lib),
+           *(["-L/opt/rocm/lib", "-lhipblaslt"] if ab else [])]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")

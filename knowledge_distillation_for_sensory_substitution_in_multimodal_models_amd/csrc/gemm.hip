@@ -23,6 +23,9 @@
 
 #include <cstring>
 #include <type_traits>
+#ifdef KD_AB_BUILD
+#include <hipblaslt/hipblaslt.h>   // tools/ab/gemm_blas.inc (KD_GEMM_BLAS): the A/B library only
+#endif
 
 namespace kd {
 namespace {
@@ -1584,6 +1587,7 @@ __global__ void __launch_bounds__(NTH8, 1) k_gemm8(GemmP p_) {
 
 #ifdef KD_AB_BUILD   // v9: equal speed to v8 on the step's shapes, not in the plan; A/B library only
 #include "gemm_v9.inc"   // tools/ab/gemm_v9.inc: v9 (eight-wave ping-pong)
+#include "gemm_blas.inc"   // tools/ab/gemm_blas.inc: plain GEMMs through hipBLASLt (KD_GEMM_BLAS)
 #endif  // KD_AB_BUILD
 
 
@@ -2309,6 +2313,12 @@ int launch_gemm(const kd_gemm_desc* d, void* stream_) {
     KD_CHECK_SHAPE(!d->aux || d->ld_aux >= d->N, "gemm: ld_aux < N");
     KD_CHECK_SHAPE((uint64_t)256 * d->lda * 2 < 0x7FFFFFFFull && (uint64_t)256 * d->ldb * 2 < 0x7FFFFFFFull,
                    "gemm: leading dimension too large for 31-bit buffer records");
+#ifdef KD_AB_BUILD
+    {
+        const int bl = ab_knob("KD_GEMM_BLAS", 0);
+        if (bl && blas_eligible(d) && (bl == 1 || blas_wins(d))) return blas_gemm(d, as_stream(stream_));
+    }
+#endif
     GemmP p;
     p.A = (const bf16*)d->A; p.B = (const bf16*)d->B; p.C = d->C;
     p.bias = d->bias; p.resid = (const bf16*)d->residual; p.aux = (bf16*)d->aux; p.alpha_dev = d->alpha_dev;
