@@ -1851,6 +1851,26 @@ int launch_dq32(int diag, dim3 grid_q, size_t smem_q, hipStream_t st, const Attn
     }
 }
 
+// dQ by the 16x16x32 k_attn_bwd_dq: head dim 128 in the product (no 32x32 build there; the teacher
+// runs no backward in the step), every head dim in the A/B library (the round-6 pair, KD_ATTN_BWD_V=2)
+template <int HD, bool C>
+int launch_dq16(int nq, dim3 grid_q, size_t smem_q, hipStream_t st, const AttnBwdP& p) {
+#ifdef KD_AB_BUILD
+    constexpr bool avail = true;
+#else
+    constexpr bool avail = HD == 128;
+#endif
+    if constexpr (!avail) {
+        (void)nq; (void)grid_q; (void)smem_q; (void)st; (void)p;
+        return fail(KD_ERR_SHAPE, "attn_bwd: the 16x16 dQ kernel runs head dim 128 only (k_attn_bwd_dq32 below)");
+    } else {
+        if (nq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p);
+        else launch_dq1<HD, C>(grid_q, smem_q, st, p);
+        KD_LAUNCH_CHECK("k_attn_bwd_dq");
+        return KD_OK;
+    }
+}
+
 #ifdef KD_AB_BUILD
 template <int HD, bool C>
 int launch_dkdv32(dim3 grid, size_t smem_kv, hipStream_t st, const AttnBwdP& p) {
@@ -1934,9 +1954,8 @@ int launch_attn_bwd(const kd_attn_bwd_desc* d, void* stream_) {
             const int rc = launch_dq32<HD, C>(diag, grid_q, smem_q, st, p);                   \
             if (rc != KD_OK) return rc;                                                       \
         } else {                                                                              \
-            if (nq_dq == 2) hipLaunchKernelGGL((k_attn_bwd_dq<HD, C, 2>), grid_q, dim3(256), smem_q, st, p); \
-            else launch_dq1<HD, C>(grid_q, smem_q, st, p);                                    \
-            KD_LAUNCH_CHECK("k_attn_bwd_dq");                                                 \
+            const int rc = launch_dq16<HD, C>(nq_dq, grid_q, smem_q, st, p);                  \
+            if (rc != KD_OK) return rc;                                                       \
         }                                                                                     \
         KD_AB_KV32(HD, C)                                                                     \
         launch_dkdv<HD, C>(kv16, grid, smem_kv, st, p);                                       \
