@@ -1283,18 +1283,19 @@ __global__ void __launch_bounds__(256, 2) k_attn_bwd_dq(AttnBwdP p) {
 
 
 // ------------------------------------------------------ backward, 32x32x16 MFMAs ----
-// The 16x16x32 backward above is bound by vector issue (an MFMA of 16 cycles holds the SIMD's
-// issue for 8 of them, and every 16x16 tile carries its own LDS fragment reads and softmax
-// VALU): ~0.17 of the MFMA peak. These two kernels compute the same products with 32x32x16
-// MFMAs (issue held 8 of 32 cycles, half the LDS bytes per FLOP), the forward's layout tricks
-// reused:
-//   k_attn_bwd_dq32: per wave 32 queries (query on the lane). S^T = K Q^T and dP^T = V dO^T
-//     (A = K / V rows from LDS, B = the wave's Q / dO rows in registers), dS^T in the same
-//     registers, then dQ^T += K^T dS^T with the dS^T accumulator as the B operand (keys in the
-//     forward's permuted order, K^T by ds_read_b64_tr_b16 in that order).
-//   k_attn_bwd_dkdv32: per wave 32 keys (key on the lane). S = Q K^T and dP = dO V^T (A = Q /
-//     dO rows from LDS, B = the wave's K / V rows in registers), then dV^T += dO^T P and
+// The 16x16x32 backward above runs at ~0.17 of the MFMA peak (an MFMA of 16 cycles holds the
+// SIMD's issue for 8 of them, and every 16x16 tile carries its own LDS fragment reads). The same
+// products on 32x32x16 MFMAs (issue held 8 of 32 cycles, half the LDS bytes per FLOP), with the
+// forward's layout tricks:
+//   k_attn_bwd_dq32 (product, head dims 64 / 96): per wave 32 queries (query on the lane).
+//     S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = the wave's Q / dO rows in
+//     registers), dS^T in the same registers, then dQ^T += K^T dS^T with the dS^T accumulator as
+//     the B operand (keys in the forward's permuted order, K^T by ds_read_b64_tr_b16 in that order).
+//   k_attn_bwd_dkdv32 (A/B library only, tools/ab/attention_bwd_dkdv32.inc: slower than
+//     k_attn_bwd_dkdv2 at hd 96): per wave 32 keys (key on the lane), dV^T += dO^T P and
 //     dK^T += Q^T dS with P / dS as the B operand (queries permuted the same way).
+// Measured bound of dq32 (DESIGN.md §3 Attention, timing builds): the grid (1.44 rounds of
+// two-per-SIMD waves at SigLIP's 729 queries) and the per-wave chain, not memory or VALU issue.
 // One LDS image per tile serves both read directions (swQ below); all LDS reads in the loops
 // are asm with counted lgkmcnt waits (a compiler-visible LDS read beside the in-flight LDS-DMA
 // of the next tile is preceded by vmcnt(0)).
