@@ -139,3 +139,28 @@ def test_attn_bwd_direct_dqkv_gqa_bitexact(B, H, HKV, S, hd, rope, dev):
     out = torch.full_like(ref, 3.0)
     ops.attn_bwd(q, k, v, o, do, lse, hd, True, dqkv=out, cos=cos, sin=sin)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("B,H,HKV,S,hd,hdp,causal", [CASES[1], CASES[3], (1, 14, 2, 1536, 64, 64, True)])
+def test_attn_bwd_is_deterministic(B, H, HKV, S, hd, hdp, causal, dev):
+    """The backward has no atomics (dQ per query block, dK / dV per key block, the GQA partials summed
+    in a fixed order): two calls on the same inputs give the same bits, including the fused q|k|v
+    gradient with RoPE."""
+    ops = _ops()
+    q, k, v = _inputs(B, H, HKV, S, hd, hdp, dev, seed=9)
+    o, lse = ops.attn_fwd(q, k, v, hd, causal)
+    g = torch.Generator(device=dev).manual_seed(10)
+    do = torch.randn(B, S, H, hd, device=dev, generator=g).bfloat16()
+    a = [t.clone() for t in ops.attn_bwd(q, k, v, o, do, lse, hd, causal)]
+    b = ops.attn_bwd(q, k, v, o, do, lse, hd, causal)
+    sl = (Ellipsis, slice(0, hd))
+    for x, y in zip(a, b):
+        assert torch.equal(x[sl], y[sl])
+    if H != HKV and hd == hdp:
+        ang = torch.rand(S, hd // 2, device=dev, generator=g) * 6.0
+        cos, sin = torch.cos(ang).contiguous(), torch.sin(ang).contiguous()
+        w = B * S, (H + 2 * HKV) * hd
+        o1, o2 = torch.zeros(w, dtype=torch.bfloat16, device=dev), torch.ones(w, dtype=torch.bfloat16, device=dev)
+        ops.attn_bwd(q, k, v, o, do, lse, hd, causal, dqkv=o1, cos=cos, sin=sin)
+        ops.attn_bwd(q, k, v, o, do, lse, hd, causal, dqkv=o2, cos=cos, sin=sin)
+        assert torch.equal(o1, o2)
