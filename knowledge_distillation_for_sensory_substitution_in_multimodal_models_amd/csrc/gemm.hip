@@ -2026,13 +2026,9 @@ GemmPlan plan_gemm(const kd_gemm_desc* d, uint64_t ws_cap) {
     static const double fixed_c3[2][5] = {{5.253, 3.402, 3.414, 8.478, 5.888}, {5.885, 3.479, 3.398, 8.695, 8.442}};
     static const bool set3 = ab_knob("KD_PLAN_SET", 4) == 3;
     static const bool hybrid_on = ab_knob("KD_GEMM_HYBRID", 1) != 0;
-    // The cost model's split count is capped at 2 (A/B: KD_SPLIT_CAP) and its partial-plane cost
-    // scaled (A/B: KD_SPLIT_PENALTY, percent): the model is fitted on isolated calls, where 3-9 splits
-    // win, but the step runs two streams that already fill a GEMM's idle CUs, so there the extra
-    // planes and reduce bytes cost more than the splits gain: capped at 2 the c1 step ran +0.5-0.7 %
-    // (interleaved A/B on two boxes: 29.20-29.31 vs 29.04-29.07 and 28.04-28.08 vs 27.91-27.94
-    // samples/s; cap 3 / 4 in between, no split -1.5 %; profiles/r06/split_cap_ab.txt)
-    static const int split_cap = ab_knob("KD_SPLIT_CAP", 2);
+    // A/B: the cost model's split count capped (KD_SPLIT_CAP) and its partial-plane cost scaled
+    // (KD_SPLIT_PENALTY, percent) -- the model is fitted on isolated calls, the step runs two streams
+    static const int split_cap = ab_knob("KD_SPLIT_CAP", 32);
     static const double split_pen = ab_knob("KD_SPLIT_PENALTY", 100) / 100.0;
     const double (&step_c)[2][5] = set3 ? step_c3 : step_c4;
     const double (&fixed_c)[2][5] = set3 ? fixed_c3 : fixed_c4;

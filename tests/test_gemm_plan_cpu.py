@@ -28,17 +28,8 @@ def _plan(M, N, K, lay="kk", f32=False, acc=False, ws=None):
 
 
 def test_teacher_down_proj_hybrid():
-    # 336 tiles of 256x256: one whole wave unsplit, the 80-tile tail split (2 ways: the plan's
-    # split cap, gemm.hip plan_gemm)
-    assert _plan(6144, 3584, 18944) == (16, 2, 256)
-
-
-def test_split_count_capped_at_two():
-    # the cost model alone picks 5-9 splits for the small weight gradients; the step measured
-    # faster with at most 2 (gemm.hip plan_gemm); a forced split_k is not capped
-    for shape in [(1152, 1152, 5832, "nn", True, True), (896, 896, 6144, "nn", True, True),
-                  (6144, 896, 151936, "kn"), (1152, 4304, 5832, "nn", True, True)]:
-        assert _plan(*shape)[1] <= 2, shape
+    # 336 tiles of 256x256: one whole wave unsplit, the 80-tile tail split 3 ways
+    assert _plan(6144, 3584, 18944) == (16, 3, 256)
 
 
 def test_siglip_qkv_not_split():
